@@ -1,0 +1,239 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY.  Captures golden vectors from the *reference itself*.
+
+Run in the build container (``python oracle/make_golden.py``): it imports the reference
+hot path from ``/root/reference`` (read-only; offline stubs for the three import-time-only
+modules ``ot``/``unidecode``/``inflect`` and a bypass of ``model/__init__.py``, per
+SURVEY.md §8c), runs it on CPU in fp32 with dropout disabled, and writes small ``.npz``
+fixtures to ``tests/golden/``.  Only data leaves this script; the reference never travels
+to the GPU box.
+
+Fixtures:
+  g1_lr.npz        LengthRegulator known-answer tests (int and float durations, cropping)
+  g2_round.npz     inference duration rounding (half-to-even)
+  g3_bucket.npz    bucketize KATs and the 255-entry pitch/energy bins
+  g4_ops.npz       per-module fwd outputs / input grads / weight-grad checksums
+  g5_step_*.npz    3-step training trajectories (losses, eloss, grad norm, lr, output sums)
+"""
+import importlib
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF = "/root/reference"
+OUT = os.path.join(REPO, "tests", "golden")
+sys.path.insert(0, REPO)
+
+
+def import_reference():
+    sys.path.insert(0, REF)
+    sys.dont_write_bytecode = True
+    for n in ("ot", "unidecode", "inflect"):
+        sys.modules.setdefault(n, types.ModuleType(n))
+    sys.modules["unidecode"].unidecode = lambda s: s
+    sys.modules["inflect"].engine = lambda: None
+    pkg = types.ModuleType("model")
+    pkg.__path__ = [os.path.join(REF, "model")]
+    sys.modules["model"] = pkg
+    fs2 = importlib.import_module("model.fastspeech2")
+    loss = importlib.import_module("model.loss")
+    mods = importlib.import_module("model.modules")
+    layers = importlib.import_module("transformer.Layers")
+    return fs2, loss, mods, layers
+
+
+def no_dropout():
+    torch.nn.functional.dropout = lambda x, p=0.5, training=True, inplace=False: x
+
+
+PKG = importlib.import_module("mid-attribute-speaker-generation_amd")
+
+
+def seeded(module, prefix=""):
+    sd = module.state_dict()
+    new = PKG.seeded.seeded_state_dict((prefix + k, v.shape) for k, v in sd.items())
+    with torch.no_grad():
+        for k, v in sd.items():
+            if prefix + k in new:
+                v.copy_(torch.from_numpy(new[prefix + k]))
+    return module
+
+
+def probe_idx(n, k=16, seed=0):
+    return np.random.default_rng(seed + n).integers(0, n, size=k)
+
+
+def grad_summary(module, prefix):
+    out = {}
+    for name, p in module.named_parameters():
+        if p.grad is None:
+            continue
+        g = p.grad.detach().reshape(-1).double().numpy()
+        idx = probe_idx(g.size)
+        out[f"{prefix}{name}.gsum"] = np.array([g.sum(), np.abs(g).sum()])
+        out[f"{prefix}{name}.gprobe"] = g[idx].astype(np.float32)
+    return out
+
+
+def g1_g2_g3(mods):
+    LR = mods.LengthRegulator()
+    x = torch.arange(24, dtype=torch.float32).view(2, 4, 3)
+    res = {"x": x.numpy()}
+    d_int = torch.tensor([[1, 0, 2, 3], [2, 2, 0, 0]])
+    d_flt = torch.tensor([[1.7, -1.0, 2.2, 0.0], [0.49, 2.5, 3.0, 1.0]])
+    for name, d, ml in (("int", d_int, None), ("flt", d_flt, None), ("crop", d_int, 4),
+                        ("pad", d_int, 9)):
+        o, ln = LR(x, d, ml)
+        res[f"d_{name}"] = d.numpy()
+        res[f"out_{name}"] = o.numpy()
+        res[f"len_{name}"] = ln.numpy()
+        res[f"maxlen_{name}"] = np.array(-1 if ml is None else ml)
+    rng = np.random.default_rng(1)
+    d_rand = rng.integers(-2, 6, size=(5, 11))
+    xr = torch.from_numpy(rng.standard_normal((5, 11, 7)).astype(np.float32))
+    o, ln = LR(xr, torch.from_numpy(d_rand), None)
+    res.update(d_rand=d_rand, x_rand=xr.numpy(), out_rand=o.numpy(), len_rand=ln.numpy())
+    np.savez_compressed(os.path.join(OUT, "g1_lr.npz"), **res)
+
+    # G2: exp(log(d+1)) - 1 -> round (half to even) -> clamp at 0 (modules.py:132-135)
+    d = torch.tensor([1.5, 2.5, 3.5, 0.2, 0.5, -0.7, 7.49])
+    logd = torch.log(d + 1)
+    r = torch.clamp(torch.round(torch.exp(logd) - 1) * 1.0, min=0)
+    np.savez_compressed(os.path.join(OUT, "g2_round.npz"), log_d=logd.numpy(), rounded=r.numpy())
+
+    # G3: bucketize (modules.py:84,96) incl. bins built from stats.json
+    cfg = PKG.config.config_dir("JVS-VCTK")
+    pp, mc, tc, path = PKG.config.load_configs(cfg)
+    va = mods.VarianceAdaptor(pp, mc, path)
+    v = torch.tensor([-2.0, -1.0, -0.5, 0.0, 1.0, 2.0])
+    bins = torch.tensor([-1.0, 0.0, 1.0])
+    vr = torch.from_numpy(np.random.default_rng(3).standard_normal(4096).astype(np.float32) * 4)
+    edge = va.pitch_bins.detach()[::17].clone()
+    np.savez_compressed(
+        os.path.join(OUT, "g3_bucket.npz"), v=v.numpy(), bins=bins.numpy(),
+        idx=torch.bucketize(v, bins).numpy(),
+        pitch_bins=va.pitch_bins.detach().numpy(), energy_bins=va.energy_bins.detach().numpy(),
+        v_rand=vr.numpy(), pitch_idx=torch.bucketize(vr, va.pitch_bins).numpy(),
+        energy_idx=torch.bucketize(vr, va.energy_bins).numpy(),
+        v_edge=edge.numpy(), edge_idx=torch.bucketize(edge, va.pitch_bins).numpy())
+
+
+def g4(fs2, loss_mod, mods, layers):
+    torch.manual_seed(0)
+    rng = np.random.default_rng(4)
+    res = {}
+    pp, mc, tc, path = PKG.config.load_configs("JVS-VCTK")
+
+    # FFT block (decoder-sized), B=3 T=24, lengths 24/17/9
+    blk = seeded(layers.FFTBlock(256, 2, 128, 128, 1024, [9, 1], dropout=0.2), "fft.")
+    B, T = 3, 24
+    lens = torch.tensor([24, 17, 9])
+    pad = torch.arange(T)[None] >= lens[:, None]
+    x = torch.from_numpy(rng.standard_normal((B, T, 256)).astype(np.float32)).requires_grad_()
+    y, _ = blk(x, mask=pad, slf_attn_mask=pad[:, None, :].expand(-1, T, -1))
+    gy = torch.from_numpy(rng.standard_normal((B, T, 256)).astype(np.float32))
+    y.backward(gy)
+    res.update({"fft.x": x.detach().numpy(), "fft.lens": lens.numpy(), "fft.y": y.detach().numpy(),
+                "fft.gy": gy.numpy(), "fft.gx": x.grad.numpy()})
+    res.update(grad_summary(blk, "fft."))
+
+    # Variance predictor, B=3 T=20 (padding rows nonzero on purpose)
+    vp = seeded(mods.VariancePredictor(mc), "vp.")
+    B, T = 3, 20
+    lens = torch.tensor([20, 13, 5])
+    pad = torch.arange(T)[None] >= lens[:, None]
+    x = torch.from_numpy(rng.standard_normal((B, T, 256)).astype(np.float32)).requires_grad_()
+    y = vp(x, pad)
+    gy = torch.from_numpy(rng.standard_normal((B, T)).astype(np.float32))
+    y.backward(gy)
+    res.update({"vp.x": x.detach().numpy(), "vp.lens": lens.numpy(), "vp.y": y.detach().numpy(),
+                "vp.gy": gy.numpy(), "vp.gx": x.grad.numpy()})
+    res.update(grad_summary(vp, "vp."))
+
+    # PostNet (train mode: batch statistics), B=2 T=40
+    pn = seeded(layers.PostNet(), "pn.")
+    pn.train()
+    x = torch.from_numpy(rng.standard_normal((2, 40, 80)).astype(np.float32)).requires_grad_()
+    y = pn(x)
+    gy = torch.from_numpy(rng.standard_normal((2, 40, 80)).astype(np.float32))
+    y.backward(gy)
+    res.update({"pn.x": x.detach().numpy(), "pn.y": y.detach().numpy(), "pn.gy": gy.numpy(),
+                "pn.gx": x.grad.numpy()})
+    res.update(grad_summary(pn, "pn."))
+    for i in range(5):
+        res[f"pn.running_mean{i}"] = pn.convolutions[i][1].running_mean.numpy()
+        res[f"pn.running_var{i}"] = pn.convolutions[i][1].running_var.numpy()
+
+    # GMM head + SpeakerMetaEncLoss, B=6
+    enc = seeded(fs2.SpeakerMetaEncoder(pp, mc), "senc.")
+    meta = torch.from_numpy(np.concatenate([np.eye(2)[[0, 1, 1, 0, 0, 1]],
+                                            np.eye(2)[[1, 1, 0, 0, 1, 0]]], 1).astype(np.float32))
+    e = torch.from_numpy(rng.standard_normal((6, 256)).astype(np.float32) * 0.5)
+    gmm = enc(meta)
+    el = loss_mod.SpeakerMetaEncLoss(pp, mc)(e, gmm)
+    (-el).backward()
+    res.update({"gmm.meta": meta.numpy(), "gmm.e": e.numpy(), "gmm.eloss": np.array(float(el)),
+                "gmm.logp": gmm.log_prob(e).detach().numpy(),
+                "gmm.pi": gmm.mixture_distribution.probs.detach().numpy(),
+                "gmm.mu": gmm.component_distribution.base_dist.loc.detach().numpy(),
+                "gmm.sigma": gmm.component_distribution.base_dist.scale.detach().numpy()})
+    for name, p in enc.named_parameters():
+        res[f"gmm.{name}.grad"] = p.grad.numpy()
+    np.savez_compressed(os.path.join(OUT, "g4_ops.npz"), **res)
+
+
+def g5(fs2, loss_mod, B, Ts, steps=3, seed=0):
+    from model.optimizer import ScheduledOptim
+    pp, mc, tc, path = PKG.config.load_configs("JVS-VCTK")
+    torch.manual_seed(0)
+    model = fs2.FastSpeech2(pp, mc, path)
+    seeded(model)
+    model.train()
+    opt = ScheduledOptim(model, tc, mc, 0)
+    Loss = loss_mod.FastSpeech2Loss(pp, mc)
+    eLoss = loss_mod.SpeakerMetaEncLoss(pp, mc)
+    res = {"B": np.array(B), "Ts": np.array(Ts), "seed": np.array(seed)}
+    batch = PKG.data.to_device(PKG.data.syn_batch(B, Ts, seed=seed), "cpu")
+    res["pos_enc_probe"] = model.encoder.position_enc.detach()[0, ::97, ::31].numpy()
+    for s in range(steps):
+        output = model(*(batch[2:12]), accents=batch[13], speaker_meta=batch[12])
+        losses = Loss(batch[:12], output[:-2])
+        losses[0].backward()
+        eloss = eLoss(output[-1], output[-2])
+        (-eloss).backward()
+        gn = torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+        opt.step_and_update_lr()
+        opt.zero_grad()
+        res[f"s{s}.losses"] = np.array([float(l) for l in losses])
+        res[f"s{s}.eloss"] = np.array(float(eloss))
+        res[f"s{s}.gnorm"] = np.array(float(gn))
+        res[f"s{s}.lr"] = np.array(opt._optimizer.param_groups[0]["lr"])
+        o, po = output[0].detach().double(), output[1].detach().double()
+        res[f"s{s}.out_sum"] = np.array([o.sum(), o.abs().sum(), po.sum(), po.abs().sum()])
+        res[f"s{s}.out_probe"] = output[1].detach()[:, ::37, ::7].numpy()
+        res[f"s{s}.pred_probe"] = np.stack([output[2].detach().numpy(), output[3].detach().numpy(),
+                                            output[4].detach().numpy()])
+        res[f"s{s}.mel_lens"] = output[9].numpy()
+    res["final_probe"] = torch.cat([p.detach().reshape(-1)[:64] for p in model.parameters()
+                                    if p.requires_grad]).numpy()
+    np.savez_compressed(os.path.join(OUT, f"g5_step_b{B}_t{Ts}.npz"), **res)
+    print("g5", B, Ts, res["s0.losses"], res["s2.losses"])
+
+
+def main():
+    os.makedirs(OUT, exist_ok=True)
+    fs2, loss_mod, mods, layers = import_reference()
+    no_dropout()
+    torch.set_num_threads(8)
+    g1_g2_g3(mods)
+    g4(fs2, loss_mod, mods, layers)
+    sizes = [(3, 16), (8, 32)] + ([(48, 128)] if "--full" in sys.argv else [])
+    for B, Ts in sizes:
+        g5(fs2, loss_mod, B, Ts)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,166 @@
+"""Pin the CPU oracle against golden vectors captured from the reference (oracle/make_golden.py).
+
+These run on CPU only; they establish that ``oracle/`` restates the reference before any
+HIP result is compared with it.
+"""
+import importlib
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_golden
+from oracle import fs2_cpu, index_math
+
+PKG = importlib.import_module("mid-attribute-speaker-generation_amd")
+
+
+def test_g1_length_regulator_kats():
+    g = load_golden("g1_lr.npz")
+    for name in ("int", "flt", "crop", "pad"):
+        ml = int(g[f"maxlen_{name}"])
+        out, ln = index_math.length_regulate(g["x"], g[f"d_{name}"], None if ml < 0 else ml)
+        np.testing.assert_array_equal(out, g[f"out_{name}"])
+        np.testing.assert_array_equal(ln, g[f"len_{name}"])
+    out, ln = index_math.length_regulate(g["x_rand"], g["d_rand"])
+    np.testing.assert_array_equal(out, g["out_rand"])
+    np.testing.assert_array_equal(ln, g["len_rand"])
+    # the survey's hand-checked maps
+    src, ln = index_math.lr_source_map(g["d_int"])
+    assert src.tolist() == [[0, 2, 2, 3, 3, 3], [0, 0, 1, 1, -1, -1]] and ln.tolist() == [6, 4]
+    src, ln = index_math.lr_source_map(g["d_flt"])
+    assert src.tolist() == [[0, 2, 2, -1, -1, -1], [1, 1, 2, 2, 2, 3]] and ln.tolist() == [3, 6]
+
+
+def test_g1_torch_oracle_matches():
+    g = load_golden("g1_lr.npz")
+    for name in ("int", "flt", "crop", "pad"):
+        ml = int(g[f"maxlen_{name}"])
+        out, ln = fs2_cpu.length_regulate(torch.from_numpy(g["x"]), torch.from_numpy(g[f"d_{name}"]),
+                                          None if ml < 0 else ml)
+        np.testing.assert_array_equal(out.numpy(), g[f"out_{name}"])
+        np.testing.assert_array_equal(ln.numpy(), g[f"len_{name}"])
+
+
+def test_g2_rounding():
+    g = load_golden("g2_round.npz")
+    np.testing.assert_array_equal(index_math.inference_durations(g["log_d"]), g["rounded"])
+
+
+def test_g3_bucketize():
+    g = load_golden("g3_bucket.npz")
+    np.testing.assert_array_equal(index_math.bucketize(g["v"], g["bins"]), g["idx"])
+    np.testing.assert_array_equal(index_math.bucketize(g["v_rand"], g["pitch_bins"]), g["pitch_idx"])
+    np.testing.assert_array_equal(index_math.bucketize(g["v_rand"], g["energy_bins"]), g["energy_idx"])
+    np.testing.assert_array_equal(index_math.bucketize(g["v_edge"], g["pitch_bins"]), g["edge_idx"])
+    m, _ = fs2_cpu.build("JVS-VCTK")
+    np.testing.assert_array_equal(m.variance_adaptor.pitch_bins.detach().numpy(), g["pitch_bins"])
+    np.testing.assert_array_equal(m.variance_adaptor.energy_bins.detach().numpy(), g["energy_bins"])
+
+
+def _seed(module, prefix):
+    sd = module.state_dict()
+    new = PKG.seeded.seeded_state_dict((prefix + k, v.shape) for k, v in sd.items())
+    with torch.no_grad():
+        for k, v in sd.items():
+            if prefix + k in new:
+                v.copy_(torch.from_numpy(new[prefix + k]))
+    return module
+
+
+def _check_grads(module, prefix, g, rtol=1e-4):
+    for name, p in module.named_parameters():
+        key = f"{prefix}{name}"
+        if f"{key}.gsum" not in g:
+            continue
+        gg = p.grad.detach().reshape(-1).double().numpy()
+        idx = np.random.default_rng(gg.size).integers(0, gg.size, size=16)
+        s = g[f"{key}.gsum"]
+        np.testing.assert_allclose([gg.sum(), np.abs(gg).sum()], s, rtol=rtol, atol=1e-5 * s[1] + 1e-7)
+        np.testing.assert_allclose(gg[idx], g[f"{key}.gprobe"], rtol=rtol, atol=1e-6)
+
+
+@pytest.fixture
+def no_dropout():
+    fs2_cpu.DROPOUT["enabled"] = False
+    yield
+    fs2_cpu.DROPOUT["enabled"] = True
+
+
+def test_g4_fft_block(no_dropout):
+    g = load_golden("g4_ops.npz")
+    blk = _seed(fs2_cpu.FFTBlock(256, 2, 1024, [9, 1], 0.2), "fft.")
+    x = torch.from_numpy(g["fft.x"]).requires_grad_()
+    T = x.shape[1]
+    pad = torch.arange(T)[None] >= torch.from_numpy(g["fft.lens"])[:, None]
+    y = blk(x, pad)
+    np.testing.assert_allclose(y.detach().numpy(), g["fft.y"], rtol=1e-5, atol=1e-5)
+    y.backward(torch.from_numpy(g["fft.gy"]))
+    np.testing.assert_allclose(x.grad.numpy(), g["fft.gx"], rtol=1e-4, atol=1e-5)
+    _check_grads(blk, "fft.", g)
+
+
+def test_g4_variance_predictor(no_dropout):
+    g = load_golden("g4_ops.npz")
+    _, mc, _, _ = PKG.config.load_configs("JVS-VCTK")
+    vp = _seed(fs2_cpu.VariancePredictor(mc), "vp.")
+    x = torch.from_numpy(g["vp.x"]).requires_grad_()
+    pad = torch.arange(x.shape[1])[None] >= torch.from_numpy(g["vp.lens"])[:, None]
+    y = vp(x, pad)
+    np.testing.assert_allclose(y.detach().numpy(), g["vp.y"], rtol=1e-5, atol=1e-5)
+    y.backward(torch.from_numpy(g["vp.gy"]))
+    np.testing.assert_allclose(x.grad.numpy(), g["vp.gx"], rtol=1e-4, atol=1e-5)
+    _check_grads(vp, "vp.", g)
+
+
+def test_g4_postnet(no_dropout):
+    g = load_golden("g4_ops.npz")
+    pn = _seed(fs2_cpu.PostNet(), "pn.")
+    pn.train()
+    x = torch.from_numpy(g["pn.x"]).requires_grad_()
+    y = pn(x)
+    np.testing.assert_allclose(y.detach().numpy(), g["pn.y"], rtol=1e-4, atol=1e-4)
+    y.backward(torch.from_numpy(g["pn.gy"]))
+    np.testing.assert_allclose(x.grad.numpy(), g["pn.gx"], rtol=1e-4, atol=1e-4)
+    _check_grads(pn, "pn.", g, rtol=2e-4)
+    for i in range(5):
+        np.testing.assert_allclose(pn.convolutions[i][1].running_mean.numpy(), g[f"pn.running_mean{i}"],
+                                   rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(pn.convolutions[i][1].running_var.numpy(), g[f"pn.running_var{i}"],
+                                   rtol=1e-5, atol=1e-6)
+
+
+def test_g4_gmm():
+    g = load_golden("g4_ops.npz")
+    enc = _seed(fs2_cpu.SpeakerMetaEncoder(4, 3, 256), "senc.")
+    gmm = enc(torch.from_numpy(g["gmm.meta"]))
+    e = torch.from_numpy(g["gmm.e"])
+    np.testing.assert_allclose(gmm.pi.detach().numpy(), g["gmm.pi"], rtol=1e-6)
+    np.testing.assert_allclose(gmm.log_prob(e).detach().numpy(), g["gmm.logp"], rtol=1e-6)
+    el = fs2_cpu.speaker_enc_loss(e, gmm)
+    np.testing.assert_allclose(float(el), float(g["gmm.eloss"]), rtol=1e-6)
+    (-el).backward()
+    for name, p in enc.named_parameters():
+        np.testing.assert_allclose(p.grad.numpy(), g[f"gmm.{name}.grad"], rtol=1e-5, atol=1e-7)
+
+
+@pytest.mark.parametrize("B,Ts", [(3, 16), (8, 32)])
+def test_g5_train_trajectory(no_dropout, B, Ts):
+    g = load_golden(f"g5_step_b{B}_t{Ts}.npz")
+    torch.manual_seed(0)
+    m, _ = fs2_cpu.build("JVS-VCTK")
+    m.train()
+    np.testing.assert_array_equal(m.encoder.position_enc.detach()[0, ::97, ::31].numpy(),
+                                  g["pos_enc_probe"])
+    opt = fs2_cpu.make_opt(m)
+    batch = PKG.data.to_device(PKG.data.syn_batch(B, Ts, seed=int(g["seed"])), "cpu")
+    for s in range(3):
+        losses, eloss, gn, out = fs2_cpu.train_step(m, opt, batch)
+        np.testing.assert_allclose(losses, g[f"s{s}.losses"], rtol=1e-5)
+        np.testing.assert_allclose(eloss, g[f"s{s}.eloss"], rtol=1e-5)
+        np.testing.assert_allclose(gn, g[f"s{s}.gnorm"], rtol=1e-4)
+        assert abs(fs2_cpu.lr_at(s + 1) - float(g[f"s{s}.lr"])) < 1e-15
+        np.testing.assert_array_equal(out[9].numpy(), g[f"s{s}.mel_lens"])
+        o, po = out[0].detach().double(), out[1].detach().double()
+        np.testing.assert_allclose([o.sum(), o.abs().sum(), po.sum(), po.abs().sum()],
+                                   g[f"s{s}.out_sum"], rtol=1e-4)

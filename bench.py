@@ -1,0 +1,179 @@
+"""Throughput of the FastSpeech2 + TacoSpawn training step on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (N > 1)
+
+A step is one full optimiser step of train.py:138-206 (forward, FastSpeech2Loss + GMM
+backward, clip_grad_norm_, Adam + LR schedule, zero_grad) on a synthetic SYN-48 batch per
+rank (B = 48, 128 phonemes x 512 frames padded) with inputs resident in HBM.
+value = valid mel frames of all ranks per second (max-over-ranks time, weak scaling).
+
+The JSON line also carries
+  roofline     the FFN Conv1d(k=9) implicit GEMM (the dominant kernel: 75% of the FFT-block
+               FLOPs), achieved FLOP/s from HIP events around its launches inside the timed
+               region, against the dense MFMA peak of the compute dtype;
+  cpu_baseline the CPU oracle (oracle/fs2_cpu.py, a restatement of the reference step) timed
+               on this host's cores on a bounded sample (rank 0, N = 1 only).
+"""
+import argparse
+import importlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+PKG = importlib.import_module("mid-attribute-speaker-generation_amd")
+M = importlib.import_module("mid-attribute-speaker-generation_amd.model")
+K = importlib.import_module("mid-attribute-speaker-generation_amd.kernels")
+TR = importlib.import_module("mid-attribute-speaker-generation_amd.train")
+
+PEAK = {"f32": (157.3, "TFLOP/s"), "bf16": (2500.0, "TFLOP/s")}
+
+
+class ConvTimer:
+    """HIP events around every k=9 conv GEMM launch (forward and data-gradient)."""
+
+    def __init__(self):
+        self.on = False
+        self.events, self.flops = [], []
+        self._orig = K.conv_gemm
+
+    def install(self):
+        orig = self._orig
+
+        def timed(x, wk, rows, seq_len, c_in, c_out, taps, pad, **kw):
+            if not (self.on and taps == 9):
+                return orig(x, wk, rows, seq_len, c_in, c_out, taps, pad, **kw)
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            y = orig(x, wk, rows, seq_len, c_in, c_out, taps, pad, **kw)
+            e.record()
+            self.events.append((s, e))
+            self.flops.append(2.0 * rows * c_out * c_in * taps)
+            return y
+
+        K.conv_gemm = timed
+
+    def result(self):
+        if not self.events:
+            return None, None, 0
+        torch.cuda.synchronize()
+        ms = [s.elapsed_time(e) for s, e in self.events]
+        return float(np.sum(self.flops)), float(np.sum(ms)) / 1e3, len(ms)
+
+
+def cpu_baseline(batch_np, steps=2):
+    from oracle import fs2_cpu
+    n_thr = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
+    torch.set_num_threads(n_thr)
+    ref, _ = fs2_cpu.build("JVS-VCTK")
+    ref.train()
+    opt = fs2_cpu.make_opt(ref)
+    b = PKG.data.to_device(batch_np, "cpu")
+    fs2_cpu.train_step(ref, opt, b)  # warm-up
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fs2_cpu.train_step(ref, opt, b)
+    dt = time.perf_counter() - t0
+    frames = int(np.sum(batch_np[7]))
+    return {"value": round(frames * steps / dt, 1), "unit": "mel-frames/s",
+            "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"oracle/fs2_cpu.py train step (dropout on), SYN-{len(batch_np[4])} "
+                      f"seed 0, {steps} timed steps after 1 warm-up, {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=48)
+    ap.add_argument("--src-len", type=int, default=128)
+    ap.add_argument("--dtype", default="f32", choices=["f32"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-roofline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    pp, mc, tc, path = PKG.config.load_configs("JVS-VCTK")
+    model = M.FastSpeech2(pp, mc, path, device=dev)
+    model.train()
+    model.seed(1234 + rank)
+    trainer = TR.Trainer(model, pp, mc, tc)
+    batch_np = PKG.data.syn_batch(args.batch, args.src_len, seed=rank)
+    batch = PKG.data.to_device(batch_np, dev)
+    frames_local = int(np.sum(batch_np[7]))
+    padded_local = int(args.batch * batch_np[8])
+
+    timer = ConvTimer()
+    if not args.no_roofline:
+        timer.install()
+    for _ in range(args.warmup):
+        trainer.step(batch)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    timer.on = True
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        losses, eloss, gnorm, _ = trainer.step(batch)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    timer.on = False
+    t = torch.tensor([dt], device=dev, dtype=torch.float64)
+    fr = torch.tensor([frames_local], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(fr)
+    dt, frames = float(t.item()), float(fr.item())
+    loss_now = float(losses[0])
+
+    if rank == 0:
+        flops, secs, n = timer.result()
+        roof = None
+        if flops:
+            peak, unit = PEAK[args.dtype]
+            ach = flops / secs / 1e12
+            roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": unit,
+                    "frac": round(ach / peak, 4), "traffic": None,
+                    "kernel": "conv_gemm_nt (FFN Conv1d k=9, fwd + dX)",
+                    "per_launch_flop": round(flops / n), "avg_launch_ms": round(secs / n * 1e3, 4)}
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(batch_np)
+        out = {"metric": "mel-frames/sec (node) FastSpeech2 train step, JVS-VCTK bs=48, 1/2/4/8 MI355X",
+               "value": round(frames * args.steps / dt, 1), "unit": "mel-frames/s",
+               "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+               "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
+               "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+               "data": "synthetic SYN-B (seeded, rank r uses seed r), random-init weights",
+               "config": {"workload": f"SYN-{args.batch}: FastSpeech2+TacoSpawn train step, "
+                                      f"B={args.batch}/GPU, {args.src_len} phonemes x "
+                                      f"{int(batch_np[8])} frames padded",
+                          "global_batch": args.batch * world, "seq_len": int(batch_np[8]),
+                          "valid_frames_per_rank_step": frames_local,
+                          "padded_frames_per_rank_step": padded_local,
+                          "parallelism": f"dp{world}"},
+               "roofline": roof, "cpu_baseline": cpu, "final_loss": round(loss_now, 5)}
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

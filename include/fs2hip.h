@@ -1,0 +1,247 @@
+/* fs2hip.h — C-ABI of libfs2hip.so, the gfx950 (MI355X) kernels of the FastSpeech2 +
+ * TacoSpawn-GMM training step.
+ *
+ * The reference (sarulab-speech/Mid-Attribute-Speaker-Generation) is pure PyTorch: it has no
+ * FFI.  Each entry point below replaces a *sequence of ATen ops* of the reference's
+ * `nn.Module`s; the citation on each names the reference lines it replaces
+ * (paths relative to the reference root).  The Python host in
+ * mid-attribute-speaker-generation_amd/ mirrors the reference module API on top of these.
+ *
+ * Conventions (all entry points):
+ *   - plain device pointers, int64 sizes, a dtype enum where storage type varies,
+ *     `stream` = hipStream_t (as void*), return 0 on success, <0 on error;
+ *     `fs2_last_error()` describes the last failure of the calling thread.
+ *   - no allocation, no host synchronisation: callers pass workspaces (size queries are
+ *     provided), so every call can be captured into a hipGraph.
+ *   - activations are (rows, channels) row-major = the reference's (B, T, C) layout;
+ *     row r of a batch of sequences of length seq_len is frame r % seq_len of utterance
+ *     r / seq_len.  Padding masks are given as per-utterance lengths (int64), a row being
+ *     padding when (r % seq_len) >= lens[r / seq_len] (utils/tools.py:155-163).
+ *   - dropout is counter-based (Philox4x32-10 keyed by seed, site, element index): the
+ *     backward entry points regenerate the forward mask from the same (seed, site).
+ */
+#ifndef FS2HIP_H
+#define FS2HIP_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { FS2_OK = 0, FS2_ERR_ARG = -1, FS2_ERR_LAUNCH = -2, FS2_ERR_DTYPE = -3 };
+enum { FS2_F32 = 0, FS2_BF16 = 1 };
+/* GEMM epilogue flags */
+enum {
+  FS2_EPI_BIAS = 1,          /* y += bias[n]                                   */
+  FS2_EPI_RELU = 2,          /* y = max(y, 0)                                  */
+  FS2_EPI_ADD_AUX = 4,       /* y += aux[m, n]   (residual-gradient fusion)    */
+  FS2_EPI_RELU_MASK_AUX = 8  /* y *= (aux[m, n] > 0)   (ReLU backward fusion)  */
+};
+
+const char* fs2_last_error(void);
+int fs2_abi_version(void);
+
+/* ---------------------------------------------------------------- convolution / linear
+ * Conv1d over time as an implicit GEMM on (rows, c_in) activations:
+ *   y[r, o] = sum_{j, c} wk[o, j*c_in + c] * x[r + j - pad, c]      (zero outside the utterance)
+ * A Linear layer is taps=1, pad=0.  Forward uses wk = fs2_conv_weight_prep's w_fwd; the
+ * data gradient is the same call on dy with w_bwd (flipped taps, transposed channels).
+ * Replaces nn.Conv1d / nn.Linear forward and their input-gradient:
+ *   transformer/SubLayers.py:39-41,53,85-89 ; model/modules.py:289-296 ;
+ *   transformer/Layers.py:59-64 ; model/fastspeech2.py:25-28,109.                       */
+int fs2_conv_gemm(int dtype, const void* x, int64_t ldx, const void* wk, void* y, int64_t ldy,
+                  int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out, int taps, int pad,
+                  const float* bias, int flags, const void* aux, int64_t ld_aux, void* stream);
+
+/* Weight re-layout (and cast for bf16) of a (c_out, c_in, taps) fp32 master weight:
+ *   w_fwd[o, j*c_in + c]        = w[o, c, j]
+ *   w_bwd[c, j*c_out + o]       = w[o, c, taps-1-j]      (either output may be NULL)     */
+int fs2_conv_weight_prep(int dtype, const float* w, int64_t c_out, int64_t c_in, int taps,
+                         void* w_fwd, void* w_bwd, void* stream);
+
+/* Weight gradient, accumulated into the fp32 (c_out, c_in, taps) master-gradient layout:
+ *   dw[o, c, j] += sum_r dy[r, o] * x[r + j - pad, c]
+ * Split-K over rows with per-split fp32 slabs in `ws` and an in-order reduction
+ * (bitwise reproducible).  `ws_bytes` >= fs2_conv_wgrad_ws_bytes(...).
+ * Replaces the weight half of ConvolutionBackward / AddmmBackward.                     */
+int64_t fs2_conv_wgrad_ws_bytes(int64_t rows, int64_t c_in, int64_t c_out, int taps);
+int fs2_conv_wgrad(int dtype, const void* dy, int64_t ldy, const void* x, int64_t ldx, float* dw,
+                   int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out, int taps, int pad,
+                   float* ws, int64_t ws_bytes, void* stream);
+
+/* Column sums (bias / LayerNorm-affine / BatchNorm gradients):
+ *   out[c] (+)= sum_r x[r, c]   in a fixed order (partials in ws, then in-order sum).   */
+int64_t fs2_colsum_ws_bytes(int64_t rows, int64_t cols);
+int fs2_colsum(int dtype, const void* x, int64_t ldx, int64_t rows, int64_t cols, float* out,
+               int accumulate, float* ws, int64_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------- attention
+ * Fused key-padding-masked softmax attention over the packed projection buffer
+ * qkv (rows, 3*heads*d_head) = [Q | K | V], head h at column block h (SubLayers.py:39-52,
+ * Modules.py:14-25: scores / temperature -> masked_fill(-inf) -> softmax -> @V).
+ * o (rows, heads*d_head) in the reference's (B, T, h*d_v) order; lse (batch*heads, seq_len)
+ * is saved for the backward.  scale = 1/temperature.  Only d_head = 128 is supported.   */
+int fs2_attn_fwd(int dtype, const void* qkv, void* o, float* lse, const int64_t* lens,
+                 int64_t batch, int64_t seq_len, int heads, int d_head, float scale, void* stream);
+/* d_qkv (rows, 3*heads*d_head) = gradient of the packed projections.
+ * ws_bytes >= fs2_attn_bwd_ws_bytes(batch, seq_len, heads).                            */
+int64_t fs2_attn_bwd_ws_bytes(int64_t batch, int64_t seq_len, int heads);
+int fs2_attn_bwd(int dtype, const void* qkv, const void* o, const void* d_o, const float* lse,
+                 void* d_qkv, const int64_t* lens, int64_t batch, int64_t seq_len, int heads,
+                 int d_head, float scale, float* ws, int64_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------- LayerNorm family
+ * Row LayerNorm (d = 256) with the fusions of the reference's call sites:
+ *   z   = dropout(y; p_in, site_in) + res          (res may be NULL)
+ *   u   = LN(z) * gamma + beta                      (eps 1e-5)
+ *   out = padded(row) ? 0 : dropout(u; p_out, site_out)
+ * and optionally a per-row dot with a Linear(256 -> 1): dot_out[r] = padded ? 0 : out.w + b.
+ *   SubLayers.py:54-55,91-93 + Layers.py:25,28   (p_in = dropout, res = residual, masked)
+ *   model/modules.py:209-250                      (p_out = dropout, dot = linear_layer)
+ * xhat/rstd are saved for the backward.  out_t: optional extra copy in `dtype`.       */
+int fs2_ln_fwd(int dtype, const float* y, const float* res, const float* gamma, const float* beta,
+               float* out, void* out_t, float* xhat, float* rstd, const int64_t* lens,
+               int64_t seq_len, int64_t rows, int d, float p_in, float p_out, uint64_t seed,
+               uint64_t site_in, uint64_t site_out, const float* dot_w, const float* dot_b,
+               float* dot_out, void* stream);
+/* Backward of fs2_ln_fwd.  Upstream gradient is dout (per element) or, in dot mode,
+ * ddot (per row).  Produces dy (gradient w.r.t. y before dropout, times (relu_y > 0) when
+ * relu_y != NULL), optionally adds dz into dres (+=), and accumulates dgamma, dbeta and
+ * (dot mode) dw_dot/db_dot into fp32 gradients.  ws >= fs2_ln_bwd_ws_bytes(rows, d). */
+int64_t fs2_ln_bwd_ws_bytes(int64_t rows, int d);
+int fs2_ln_bwd(int dtype, const float* dout, const float* ddot, const float* dot_w,
+               const float* xhat, const float* rstd, const float* gamma, const float* beta,
+               const int64_t* lens, int64_t seq_len, int64_t rows, int d, float p_in, float p_out,
+               uint64_t seed, uint64_t site_in, uint64_t site_out, const float* relu_y, float* dy,
+               void* dy_t, float* dres, float* dgamma, float* dbeta, float* dw_dot, float* db_dot,
+               float* ws, int64_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------- BatchNorm (PostNet)
+ * Training-mode BatchNorm1d over all rows (padded frames included) + optional tanh +
+ * dropout (transformer/Layers.py:129-137).  Stats are exact two-pass (mean, then centred
+ * sum of squares); running stats updated with momentum, unbiased variance.           */
+int64_t fs2_bn_ws_bytes(int64_t rows, int64_t c);
+int fs2_bn_fwd(int dtype, const float* z, int64_t rows, int64_t c, const float* gamma,
+               const float* beta, float eps, float momentum, float* running_mean,
+               float* running_var, float* mean, float* rstd, int act_tanh, float p,
+               uint64_t seed, uint64_t site, const float* res, float* out, void* out_t, float* ws,
+               int64_t ws_bytes, void* stream);
+int fs2_bn_bwd(int dtype, const float* dout, const float* z, const float* mean, const float* rstd,
+               const float* gamma, const float* beta, int64_t rows, int64_t c, int act_tanh,
+               float p, uint64_t seed, uint64_t site, float* dz, void* dz_t, float* dgamma,
+               float* dbeta, float* ws, int64_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------- embeddings, adaptor
+ * Encoder input: word_emb[text] + accent_emb[accent] + posenc[t] (transformer/Models.py:101-103). */
+int fs2_encoder_embed_fwd(const int64_t* texts, const int64_t* accents, const float* word_emb,
+                          const float* accent_emb, const float* posenc, int64_t batch,
+                          int64_t seq_len, int d, float* out, void* out_t, void* stream);
+/* out[i] = table[ids[i]]  (nn.Embedding lookup, e.g. speaker_emb, fastspeech2.py:81).  */
+int fs2_embedding_fwd(const int64_t* ids, const float* table, int64_t n, int d, float* out,
+                      void* stream);
+/* mask[b, t] = t >= lens[b]  (get_mask_from_lengths, utils/tools.py:155-163), 1 byte.   */
+int fs2_length_mask(const int64_t* lens, int64_t batch, int64_t max_len, uint8_t* mask,
+                    void* stream);
+/* dtable[ids[i]] += dout[i]  for ids[i] != padding_idx (padding_idx < 0: none).       */
+int fs2_embedding_bwd(const float* dout, const int64_t* ids, int64_t n, int d, int padding_idx,
+                      float* dtable, void* stream);
+/* out[b, t] = x[b, t] + table[ids[b]] over all t (model/fastspeech2.py:81-84).        */
+int fs2_rowvec_add_fwd(const float* x, const int64_t* ids, const float* table, int64_t batch,
+                       int64_t seq_len, int d, float* out, void* out_t, void* stream);
+int fs2_rowvec_add_bwd(const float* dout, const int64_t* ids, int64_t batch, int64_t seq_len,
+                       int d, float* dtable, void* stream);
+/* out = x + table[bucketize(values, bins)] (model/modules.py:80-100, torch.bucketize
+ * right=False: #bins < v).  values_dtype: FS2_F32 or 2 = f64.  idx (int32) saved.     */
+int fs2_bucket_embed_fwd(const float* x, const void* values, int values_dtype, const float* bins,
+                         int n_bins, const float* table, int64_t rows, int d, float* out,
+                         void* out_t, int32_t* idx, void* stream);
+int fs2_bucket_embed_bwd(const float* dout, const int32_t* idx, int64_t rows, int d,
+                         float* dtable, void* stream);
+int fs2_bucketize(const void* values, int values_dtype, const float* bins, int n_bins,
+                  int64_t n, int32_t* idx, void* stream);
+
+/* LengthRegulator (model/modules.py:161-194, utils/tools.py:363-381).
+ * fs2_lr_index: cum[b, i] = inclusive scan of max(trunc(d), 0); mel_len[b] = cum[b, Ts-1]
+ * (uncropped).  dur_dtype: 0 = int64, 1 = f32.                                       */
+int fs2_lr_index(const void* durations, int dur_dtype, int64_t batch, int64_t src_len,
+                 int32_t* cum, int64_t* mel_len, void* stream);
+/* src[b, t] = i with cum[i-1] <= t < cum[i], or -1 past mel_len (bit-exact index map). */
+int fs2_lr_source(const int32_t* cum, int64_t batch, int64_t src_len, int64_t out_len,
+                  int32_t* src, void* stream);
+/* out[b, t] = x[b, src[b, t]] (+ posenc[t] for every t < out_len when posenc != NULL) */
+int fs2_lr_expand_fwd(const float* x, const int32_t* cum, int64_t batch, int64_t src_len,
+                      int64_t out_len, int d, const float* posenc, float* out, void* out_t,
+                      void* stream);
+/* dx[b, i] = sum of dout[b, t] over the frames phoneme i was copied to (segmented, in order). */
+int fs2_lr_expand_bwd(const float* dout, const int32_t* cum, int64_t batch, int64_t src_len,
+                      int64_t out_len, int d, float* dx, void* stream);
+
+/* ---------------------------------------------------------------- losses, GMM
+ * FastSpeech2Loss (model/loss.py:19-92): masked L1 (mel, postnet), masked MSE (pitch,
+ * energy, log-duration vs log(d+1)) with device-side valid counts (no masked_select
+ * sync).  Masks are the reference's bool tensors (1 byte, true = padding): src_pad
+ * (batch, src_len), mel_pad (batch, mel_len); mel_tgt is cropped to mel_len frames.
+ * losses[6] = total, mel, postnet, pitch, energy, duration.  denoms (nullable, device):
+ * [mel elements, phonemes] overriding the local counts (data-parallel normalisation).
+ * The backward reads the denominators the forward left in ws; g_losses[6] (device) are the
+ * upstream gradients of the six outputs.                                               */
+int64_t fs2_fs2loss_ws_bytes(int64_t batch, int64_t mel_len);
+int fs2_fs2loss_fwd(const float* mel_out, const float* post_out, const float* mel_tgt,
+                    int64_t tgt_len, const float* p_pred, const float* e_pred,
+                    const float* logd_pred, const float* p_tgt, const float* e_tgt,
+                    const int64_t* d_tgt, const uint8_t* src_pad, const uint8_t* mel_pad,
+                    int64_t batch, int64_t src_len, int64_t mel_len, int n_mel,
+                    const float* denoms, float* losses, float* ws, int64_t ws_bytes, void* stream);
+int fs2_fs2loss_bwd(const float* mel_out, const float* post_out, const float* mel_tgt,
+                    int64_t tgt_len, const float* p_pred, const float* e_pred,
+                    const float* logd_pred, const float* p_tgt, const float* e_tgt,
+                    const int64_t* d_tgt, const uint8_t* src_pad, const uint8_t* mel_pad,
+                    int64_t batch, int64_t src_len, int64_t mel_len, int n_mel, const float* ws,
+                    const float* g_losses, float* d_mel_out, float* d_post_out, float* d_p,
+                    float* d_e, float* d_logd, void* stream);
+
+/* SpeakerMetaEncoder (model/fastspeech2.py:306-341): pi = softmax(W m + b),
+ * sigma = softplus(W m + b), mu = W m + b.  sigma_pre saved for the backward.          */
+int fs2_gmm_head_fwd(const float* meta, int64_t batch, int in_dim, int k, int d,
+                     const float* w_pi, const float* b_pi, const float* w_sigma,
+                     const float* b_sigma, const float* w_mu, const float* b_mu, float* pi,
+                     float* sigma, float* mu, float* sigma_pre, void* stream);
+/* log p(e_b) of MixtureSameFamily(Categorical(pi), Independent(Normal(mu, sigma), 1))
+ * (torch.distributions semantics incl. the probs clamp); resp (batch, k) saved;
+ * mean_out (nullable) = sum_b logp_b / batch  = SpeakerMetaEncLoss (model/loss.py:102-104). */
+int fs2_gmm_logprob(const float* e, const float* pi, const float* mu, const float* sigma,
+                    int64_t batch, int k, int d, float* logp, float* resp, float* mean_out,
+                    void* stream);
+/* Backward of  L = sum_b g_b * logp_b  through the GMM head into fp32 weight grads (+=). */
+int fs2_gmm_head_bwd(const float* meta, const float* e, const float* pi, const float* mu,
+                     const float* sigma, const float* sigma_pre, const float* resp,
+                     const float* g_logp, int64_t batch, int in_dim, int k, int d,
+                     float* dw_pi, float* db_pi, float* dw_sigma, float* db_sigma, float* dw_mu,
+                     float* db_mu, void* stream);
+/* Draw one embedding per row: component ~ Categorical(pi), e = mu + sigma * N(0,1)
+ * (model/fastspeech2.py:176-180 speaker_gen; Philox + Box-Muller).                    */
+int fs2_gmm_sample(const float* pi, const float* mu, const float* sigma, int64_t batch, int k,
+                   int d, uint64_t seed, uint64_t offset, float* out, int32_t* comp, void* stream);
+
+/* ---------------------------------------------------------------- optimiser
+ * clip_grad_norm_ + Adam over one flat fp32 parameter buffer (train.py:202,
+ * model/optimizer.py:10-51).  fs2_grad_norm writes norm_coef[0] = ||g||_2 and
+ * norm_coef[1] = min(1, max_norm / (norm + 1e-6)); fs2_adam_step multiplies g by
+ * norm_coef[1] on the fly (no extra pass over the gradients).                         */
+int64_t fs2_grad_norm_ws_bytes(int64_t n);
+int fs2_grad_norm(const float* g, int64_t n, float max_norm, float* norm_coef, float* ws,
+                  int64_t ws_bytes, void* stream);
+int fs2_adam_step(float* p, const float* g, float* m, float* v, int64_t n, const float* norm_coef,
+                  float lr, float beta1, float beta2, float eps, float bias_corr1,
+                  float bias_corr2_sqrt, void* stream);
+int fs2_fill(float* x, int64_t n, float value, void* stream);
+int fs2_add_i64(int64_t* x, int64_t n, int64_t value, void* stream); /* BN num_batches_tracked */
+int fs2_scale(float* x, int64_t n, float value, void* stream);
+/* x[i] = src[0] * scale  (device scalar broadcast, no host sync)                     */
+int fs2_fill_from(float* x, int64_t n, const float* src, float scale, void* stream);
+int fs2_add(float* out, const float* a, const float* b, int64_t n, void* stream); /* out = a + b */
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FS2HIP_H */

@@ -1,0 +1,92 @@
+// Error reporting and small utility entry points of the C-ABI.
+#include <stdarg.h>
+#include <stdio.h>
+
+#include "common.hpp"
+
+namespace fs2 {
+
+static thread_local char g_err[512] = "";
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+int launch_status(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error("%s: launch failed: %s", what, hipGetErrorString(e));
+    return FS2_ERR_LAUNCH;
+  }
+  return FS2_OK;
+}
+
+__global__ void fill_kernel(float* x, int64_t n, float v) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    x[i] = v;
+}
+__global__ void scale_kernel(float* x, int64_t n, float v) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    x[i] *= v;
+}
+
+__global__ void add_kernel(float* out, const float* a, const float* b, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = a[i] + b[i];
+}
+
+__global__ void fill_from_kernel(float* x, int64_t n, const float* src, float scale) {
+  const float v = src[0] * scale;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    x[i] = v;
+}
+
+static unsigned grid_for(int64_t n) {
+  int64_t b = (n + 255) / 256;
+  if (b > 8192) b = 8192;
+  if (b < 1) b = 1;
+  return (unsigned)b;
+}
+
+}  // namespace fs2
+
+using namespace fs2;
+
+extern "C" {
+
+const char* fs2_last_error(void) { return g_err; }
+
+int fs2_abi_version(void) { return 1; }
+
+int fs2_fill(float* x, int64_t n, float value, void* stream) {
+  if (n <= 0) return FS2_OK;
+  fill_kernel<<<grid_for(n), 256, 0, as_stream(stream)>>>(x, n, value);
+  return launch_status("fs2_fill");
+}
+
+int fs2_fill_from(float* x, int64_t n, const float* src, float scale, void* stream) {
+  if (n <= 0) return FS2_OK;
+  fill_from_kernel<<<grid_for(n), 256, 0, as_stream(stream)>>>(x, n, src, scale);
+  return launch_status("fs2_fill_from");
+}
+
+int fs2_add(float* out, const float* a, const float* b, int64_t n, void* stream) {
+  if (n <= 0) return FS2_OK;
+  add_kernel<<<grid_for(n), 256, 0, as_stream(stream)>>>(out, a, b, n);
+  return launch_status("fs2_add");
+}
+
+int fs2_scale(float* x, int64_t n, float value, void* stream) {
+  if (n <= 0) return FS2_OK;
+  scale_kernel<<<grid_for(n), 256, 0, as_stream(stream)>>>(x, n, value);
+  return launch_status("fs2_scale");
+}
+
+}  // extern "C"

@@ -1,0 +1,109 @@
+// Shared device helpers for the gfx950 kernels of libfs2hip.so.
+//
+// Wave64 everywhere: lane = threadIdx.x & 63; cross-lane reductions use __shfl_xor over
+// 64 lanes.  Dropout masks come from a counter-based Philox4x32-10 stream keyed by
+// (seed, site offset, element index), so backward recomputes the forward mask instead of
+// storing it.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/fs2hip.h"
+
+#define FS2_DEV __device__ __forceinline__
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+namespace fs2 {
+
+// ------------------------------------------------------------------ error reporting
+void set_error(const char* fmt, ...);
+int launch_status(const char* what);
+
+#define FS2_CHECK_ARG(cond, ...)                     \
+  do {                                               \
+    if (!(cond)) {                                   \
+      fs2::set_error(__VA_ARGS__);                   \
+      return FS2_ERR_ARG;                            \
+    }                                                \
+  } while (0)
+
+// in-order column reduction of partial rows (defined in gemm.hip):
+//   out[c] (+)= sum_p part[p * cols + c]
+int colsum_final_launch(const float* part, int64_t nparts, int64_t cols, float* out, int acc,
+                        hipStream_t st);
+int colsum_launch(const float* x, int64_t ldx, int64_t rows, int64_t cols, float* out, int acc,
+                  float* ws, hipStream_t st);
+
+// ------------------------------------------------------------------ wave reductions
+FS2_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+FS2_DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+// reduce across the 4 lane-groups of 16 (lanes l, l^16, l^32, l^48)
+FS2_DEV float group4_sum(float v) {
+  v += __shfl_xor(v, 16, 64);
+  v += __shfl_xor(v, 32, 64);
+  return v;
+}
+FS2_DEV float group4_max(float v) {
+  v = fmaxf(v, __shfl_xor(v, 16, 64));
+  v = fmaxf(v, __shfl_xor(v, 32, 64));
+  return v;
+}
+
+// ------------------------------------------------------------------ Philox4x32-10
+struct u32x4 {
+  uint32_t x, y, z, w;
+};
+FS2_DEV u32x4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint64_t seed) {
+  uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    uint32_t lo0 = c0 * 0xD2511F53u, hi0 = __umulhi(c0, 0xD2511F53u);
+    uint32_t lo1 = c2 * 0xCD9E8D57u, hi1 = __umulhi(c2, 0xCD9E8D57u);
+    uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+    c0 = n0;
+    c1 = lo1;
+    c2 = n2;
+    c3 = lo0;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return {c0, c1, c2, c3};
+}
+FS2_DEV float u01(uint32_t x) { return (float)(x >> 8) * (1.0f / 16777216.0f); }
+
+// Keep-scale for 4 consecutive elements e0..e0+3 (e0 % 4 == 0) of dropout site `site`.
+// Returns 0 (dropped) or 1/(1-p) (kept) per element.
+FS2_DEV f32x4 dropout4(uint64_t seed, uint64_t site, uint64_t e0, float p) {
+  if (p <= 0.f) return f32x4{1.f, 1.f, 1.f, 1.f};
+  uint64_t c = e0 >> 2;
+  u32x4 r = philox((uint32_t)c, (uint32_t)(c >> 32), (uint32_t)site, (uint32_t)(site >> 32), seed);
+  float s = 1.f / (1.f - p);
+  return f32x4{u01(r.x) >= p ? s : 0.f, u01(r.y) >= p ? s : 0.f, u01(r.z) >= p ? s : 0.f,
+               u01(r.w) >= p ? s : 0.f};
+}
+FS2_DEV float dropout1(uint64_t seed, uint64_t site, uint64_t e, float p) {
+  if (p <= 0.f) return 1.f;
+  f32x4 k = dropout4(seed, site, e & ~3ull, p);
+  int j = (int)(e & 3);
+  return j == 0 ? k.x : j == 1 ? k.y : j == 2 ? k.z : k.w;
+}
+
+// ------------------------------------------------------------------ vector memory
+FS2_DEV f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+FS2_DEV void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
+
+FS2_DEV int div_up(int a, int b) { return (a + b - 1) / b; }
+
+}  // namespace fs2
+
+static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }

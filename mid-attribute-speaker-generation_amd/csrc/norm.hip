@@ -1,0 +1,415 @@
+// LayerNorm (FFT blocks, variance predictors) and training-mode BatchNorm (PostNet).
+//
+// LayerNorm: one wave per 256-wide row, 4 consecutive channels per lane (one 16-B load,
+// one Philox call for the 4 dropout draws), wave-shuffle mean/variance.  The call-site
+// epilogues of the reference are fused in: dropout + residual before the norm
+// (SubLayers.py:54-55,91-93), padded-row zeroing after it (Layers.py:25,28), dropout
+// after it and the Linear(256 -> 1) head of the variance predictor (modules.py:209-250).
+// Backward recomputes nothing but the dropout masks: xhat and rstd are saved.
+// Affine/linear-head gradients are reduced per 64-row block in registers + LDS and then
+// summed over blocks in a fixed order (bitwise reproducible).
+//
+// BatchNorm: two-pass column statistics over every (utterance, frame) row, padded frames
+// included (the reference's BatchNorm1d sees them, Layers.py:129-137).
+#include <math.h>
+
+#include "common.hpp"
+
+namespace fs2 {
+
+constexpr int LN_D = 256;
+constexpr int LN_ROWS = 64;  // rows per block in the backward (16 per wave)
+
+struct LnFwd {
+  const float* y;
+  const float* res;
+  const float* gamma;
+  const float* beta;
+  float* out;
+  float* xhat;
+  float* rstd;
+  const int64_t* lens;
+  int64_t T, rows;
+  float p_in, p_out;
+  uint64_t seed, site_in, site_out;
+  const float* dot_w;
+  const float* dot_b;
+  float* dot_out;
+};
+
+FS2_DEV bool row_padded(const int64_t* lens, int64_t T, int64_t r) {
+  if (!lens) return false;
+  const int64_t b = r / T;
+  return (r - b * T) >= lens[b];
+}
+
+__global__ __launch_bounds__(256) void ln_fwd_f32(LnFwd a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= a.rows) return;
+  const int64_t e0 = r * LN_D + 4 * lane;
+  f32x4 z = ld4(a.y + e0);
+  if (a.p_in > 0.f) z *= dropout4(a.seed, a.site_in, (uint64_t)e0, a.p_in);
+  if (a.res) z += ld4(a.res + e0);
+  const float mean = wave_sum(z.x + z.y + z.z + z.w) * (1.f / LN_D);
+  const f32x4 c = z - mean;
+  const float var = wave_sum(c.x * c.x + c.y * c.y + c.z * c.z + c.w * c.w) * (1.f / LN_D);
+  const float rs = 1.f / sqrtf(var + 1e-5f);
+  const f32x4 xh = c * rs;
+  f32x4 u = xh * ld4(a.gamma + 4 * lane) + ld4(a.beta + 4 * lane);
+  if (a.p_out > 0.f) u *= dropout4(a.seed, a.site_out, (uint64_t)e0, a.p_out);
+  const bool pad = row_padded(a.lens, a.T, r);
+  if (pad && !a.dot_out) u = f32x4{0.f, 0.f, 0.f, 0.f};  // dot mode masks only the head output
+  st4(a.out + e0, u);
+  st4(a.xhat + e0, xh);
+  if (lane == 0) a.rstd[r] = rs;
+  if (a.dot_out) {
+    const f32x4 w = ld4(a.dot_w + 4 * lane);
+    const float d = wave_sum(u.x * w.x + u.y * w.y + u.z * w.z + u.w * w.w);
+    if (lane == 0) a.dot_out[r] = pad ? 0.f : d + a.dot_b[0];
+  }
+}
+
+struct LnBwd {
+  const float* dout;
+  const float* ddot;
+  const float* dot_w;
+  const float* xhat;
+  const float* rstd;
+  const float* gamma;
+  const float* beta;
+  const int64_t* lens;
+  int64_t T, rows;
+  float p_in, p_out;
+  uint64_t seed, site_in, site_out;
+  const float* relu_y;
+  float* dy;
+  float* dres;
+  float* part;  // [4][nblk][256]: dgamma, dbeta, dw_dot, (db_dot in slot 0 of row 3*?)
+  int64_t nblk;
+};
+
+__global__ __launch_bounds__(256) void ln_bwd_f32(LnBwd a) {
+  __shared__ f32x4 red[3][4][64];
+  __shared__ float redb[4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const f32x4 gam = ld4(a.gamma + 4 * lane);
+  const f32x4 bet = ld4(a.beta + 4 * lane);
+  f32x4 w = {0.f, 0.f, 0.f, 0.f};
+  if (a.ddot) w = ld4(a.dot_w + 4 * lane);
+  f32x4 pg = {0.f, 0.f, 0.f, 0.f}, pb = pg, pw = pg;
+  float pdb = 0.f;
+  const int64_t rbeg = (int64_t)blockIdx.x * LN_ROWS;
+  for (int i = wave; i < LN_ROWS; i += 4) {
+    const int64_t r = rbeg + i;
+    if (r >= a.rows) break;
+    const int64_t e0 = r * LN_D + 4 * lane;
+    const bool pad = row_padded(a.lens, a.T, r);
+    const f32x4 xh = ld4(a.xhat + e0);
+    const f32x4 mo = a.p_out > 0.f ? dropout4(a.seed, a.site_out, (uint64_t)e0, a.p_out)
+                                   : f32x4{1.f, 1.f, 1.f, 1.f};
+    f32x4 du;
+    if (a.ddot) {
+      const float gr = pad ? 0.f : a.ddot[r];
+      du = gr * w;
+      const f32x4 u = (xh * gam + bet) * mo;
+      pw += gr * u;
+      pdb += gr;
+    } else {
+      du = pad ? f32x4{0.f, 0.f, 0.f, 0.f} : ld4(a.dout + e0);
+    }
+    du *= mo;
+    pg += du * xh;
+    pb += du;
+    const f32x4 dxh = du * gam;
+    const float m1 = wave_sum(dxh.x + dxh.y + dxh.z + dxh.w) * (1.f / LN_D);
+    const float m2 =
+        wave_sum(dxh.x * xh.x + dxh.y * xh.y + dxh.z * xh.z + dxh.w * xh.w) * (1.f / LN_D);
+    const f32x4 dz = a.rstd[r] * (dxh - m1 - xh * m2);
+    if (a.dres) st4(a.dres + e0, ld4(a.dres + e0) + dz);
+    f32x4 dy = dz;
+    if (a.p_in > 0.f) dy *= dropout4(a.seed, a.site_in, (uint64_t)e0, a.p_in);
+    if (a.relu_y) {
+      const f32x4 yv = ld4(a.relu_y + e0);
+      dy.x = yv.x > 0.f ? dy.x : 0.f;
+      dy.y = yv.y > 0.f ? dy.y : 0.f;
+      dy.z = yv.z > 0.f ? dy.z : 0.f;
+      dy.w = yv.w > 0.f ? dy.w : 0.f;
+    }
+    st4(a.dy + e0, dy);
+  }
+  red[0][wave][lane] = pg;
+  red[1][wave][lane] = pb;
+  red[2][wave][lane] = pw;
+  if (lane == 0) redb[wave] = pdb;
+  __syncthreads();
+  if (wave < 3) {
+    f32x4 s = red[wave][0][lane] + red[wave][1][lane] + red[wave][2][lane] + red[wave][3][lane];
+    st4(a.part + ((int64_t)wave * a.nblk + blockIdx.x) * LN_D + 4 * lane, s);
+  } else if (lane == 0) {
+    a.part[3 * a.nblk * LN_D + blockIdx.x] = redb[0] + redb[1] + redb[2] + redb[3];
+  }
+}
+
+// ------------------------------------------------------------------ BatchNorm
+constexpr int BN_ROWS = 256;
+
+// MODE 0: sum z ; MODE 1: sum (z - mean)^2
+template <int MODE>
+__global__ void bn_partial(const float* z, const float* mean, int64_t rows, int64_t c, float* part) {
+  const int64_t col = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
+  const int ry = threadIdx.x >> 6;
+  const int64_t r0 = (int64_t)blockIdx.y * BN_ROWS;
+  __shared__ float red[4][64];
+  float s = 0.f;
+  if (col < c) {
+    const float mu = MODE == 1 ? mean[col] : 0.f;
+    const int64_t r1 = r0 + BN_ROWS < rows ? r0 + BN_ROWS : rows;
+    for (int64_t r = r0 + ry; r < r1; r += 4) {
+      const float v = z[r * c + col];
+      s += MODE == 0 ? v : (v - mu) * (v - mu);
+    }
+  }
+  red[ry][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (ry == 0 && col < c)
+    part[(int64_t)blockIdx.y * c + col] =
+        red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+}
+
+__global__ void bn_mean_final(const float* part, int64_t nparts, int64_t rows, int64_t c, float* mean) {
+  const int64_t col = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (col >= c) return;
+  float s = 0.f;
+  for (int64_t p = 0; p < nparts; ++p) s += part[p * c + col];
+  mean[col] = s / (float)rows;
+}
+
+__global__ void bn_var_final(const float* part, int64_t nparts, int64_t rows, int64_t c, float eps,
+                             float mom, const float* mean, float* rm, float* rv, float* rstd) {
+  const int64_t col = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (col >= c) return;
+  float s = 0.f;
+  for (int64_t p = 0; p < nparts; ++p) s += part[p * c + col];
+  const float var = s / (float)rows;
+  rstd[col] = 1.f / sqrtf(var + eps);
+  if (rm) rm[col] = (1.f - mom) * rm[col] + mom * mean[col];
+  if (rv) rv[col] = (1.f - mom) * rv[col] + mom * (rows > 1 ? s / (float)(rows - 1) : var);
+}
+
+__global__ void bn_apply(const float* z, const float* mean, const float* rstd, const float* gamma,
+                         const float* beta, int64_t rows, int64_t c, int act_tanh, float p,
+                         uint64_t seed, uint64_t site, const float* res, float* out) {
+  const int64_t n = rows * c;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t col = e % c;
+    float v = (z[e] - mean[col]) * rstd[col] * gamma[col] + beta[col];
+    if (act_tanh) v = tanhf(v);
+    if (p > 0.f) v *= dropout1(seed, site, (uint64_t)e, p);
+    if (res) v += res[e];
+    out[e] = v;
+  }
+}
+
+// g = dout * mask * act'(a);  partial sums of g and g * xhat
+FS2_DEV float bn_g(const float* dout, const float* z, float mu, float rs, float ga, float be,
+                   int act_tanh, float p, uint64_t seed, uint64_t site, int64_t e, float* xh_out) {
+  const float xh = (z[e] - mu) * rs;
+  *xh_out = xh;
+  float g = dout[e];
+  if (p > 0.f) g *= dropout1(seed, site, (uint64_t)e, p);
+  if (act_tanh) {
+    const float t = tanhf(xh * ga + be);
+    g *= 1.f - t * t;
+  }
+  return g;
+}
+
+__global__ void bn_bwd_partial(const float* dout, const float* z, const float* mean,
+                               const float* rstd, const float* gamma, const float* beta,
+                               int64_t rows, int64_t c, int act_tanh, float p, uint64_t seed,
+                               uint64_t site, float* part_g, float* part_gx) {
+  const int64_t col = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
+  const int ry = threadIdx.x >> 6;
+  const int64_t r0 = (int64_t)blockIdx.y * BN_ROWS;
+  __shared__ float red[2][4][64];
+  float sg = 0.f, sgx = 0.f;
+  if (col < c) {
+    const float mu = mean[col], rs = rstd[col], ga = gamma[col], be = beta[col];
+    const int64_t r1 = r0 + BN_ROWS < rows ? r0 + BN_ROWS : rows;
+    for (int64_t r = r0 + ry; r < r1; r += 4) {
+      float xh;
+      const float g = bn_g(dout, z, mu, rs, ga, be, act_tanh, p, seed, site, r * c + col, &xh);
+      sg += g;
+      sgx += g * xh;
+    }
+  }
+  red[0][ry][threadIdx.x & 63] = sg;
+  red[1][ry][threadIdx.x & 63] = sgx;
+  __syncthreads();
+  if (ry == 0 && col < c) {
+    const int t = threadIdx.x;
+    part_g[(int64_t)blockIdx.y * c + col] = red[0][0][t] + red[0][1][t] + red[0][2][t] + red[0][3][t];
+    part_gx[(int64_t)blockIdx.y * c + col] = red[1][0][t] + red[1][1][t] + red[1][2][t] + red[1][3][t];
+  }
+}
+
+__global__ void bn_bwd_final(const float* part_g, const float* part_gx, int64_t nparts, int64_t c,
+                             float* sums, float* dgamma, float* dbeta) {
+  const int64_t col = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (col >= c) return;
+  float sg = 0.f, sgx = 0.f;
+  for (int64_t p = 0; p < nparts; ++p) {
+    sg += part_g[p * c + col];
+    sgx += part_gx[p * c + col];
+  }
+  sums[col] = sg;
+  sums[c + col] = sgx;
+  if (dbeta) dbeta[col] += sg;
+  if (dgamma) dgamma[col] += sgx;
+}
+
+__global__ void bn_bwd_apply(const float* dout, const float* z, const float* mean, const float* rstd,
+                             const float* gamma, const float* beta, const float* sums, int64_t rows,
+                             int64_t c, int act_tanh, float p, uint64_t seed, uint64_t site,
+                             float* dz) {
+  const int64_t n = rows * c;
+  const float inv_m = 1.f / (float)rows;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t col = e % c;
+    float xh;
+    const float g = bn_g(dout, z, mean[col], rstd[col], gamma[col], beta[col], act_tanh, p, seed,
+                         site, e, &xh);
+    dz[e] = gamma[col] * rstd[col] * (g - sums[col] * inv_m - xh * sums[c + col] * inv_m);
+  }
+}
+
+static unsigned ew_grid(int64_t n) {
+  int64_t b = (n + 255) / 256;
+  if (b > 8192) b = 8192;
+  return (unsigned)(b < 1 ? 1 : b);
+}
+
+}  // namespace fs2
+
+using namespace fs2;
+
+extern "C" {
+
+int fs2_ln_fwd(int dtype, const float* y, const float* res, const float* gamma, const float* beta,
+               float* out, void* out_t, float* xhat, float* rstd, const int64_t* lens,
+               int64_t seq_len, int64_t rows, int d, float p_in, float p_out, uint64_t seed,
+               uint64_t site_in, uint64_t site_out, const float* dot_w, const float* dot_b,
+               float* dot_out, void* stream) {
+  if (dtype != FS2_F32) {
+    set_error("fs2_ln_fwd: dtype %d not built", dtype);
+    return FS2_ERR_DTYPE;
+  }
+  FS2_CHECK_ARG(d == LN_D, "fs2_ln_fwd: only d = 256 is supported (got %d)", d);
+  FS2_CHECK_ARG(!lens || seq_len > 0, "fs2_ln_fwd: lens given without seq_len");
+  FS2_CHECK_ARG(!dot_out || (dot_w && dot_b), "fs2_ln_fwd: dot_out needs dot_w/dot_b");
+  (void)out_t;
+  if (rows == 0) return FS2_OK;
+  LnFwd a{y, res, gamma, beta, out, xhat, rstd, lens, seq_len, rows, p_in, p_out, seed,
+          site_in, site_out, dot_w, dot_b, dot_out};
+  ln_fwd_f32<<<(unsigned)((rows + 3) / 4), 256, 0, as_stream(stream)>>>(a);
+  return launch_status("fs2_ln_fwd");
+}
+
+int64_t fs2_ln_bwd_ws_bytes(int64_t rows, int d) {
+  const int64_t nblk = (rows + LN_ROWS - 1) / LN_ROWS;
+  return (3 * nblk * (int64_t)d + nblk) * 4;
+}
+
+int fs2_ln_bwd(int dtype, const float* dout, const float* ddot, const float* dot_w,
+               const float* xhat, const float* rstd, const float* gamma, const float* beta,
+               const int64_t* lens, int64_t seq_len, int64_t rows, int d, float p_in, float p_out,
+               uint64_t seed, uint64_t site_in, uint64_t site_out, const float* relu_y, float* dy,
+               void* dy_t, float* dres, float* dgamma, float* dbeta, float* dw_dot, float* db_dot,
+               float* ws, int64_t ws_bytes, void* stream) {
+  if (dtype != FS2_F32) {
+    set_error("fs2_ln_bwd: dtype %d not built", dtype);
+    return FS2_ERR_DTYPE;
+  }
+  FS2_CHECK_ARG(d == LN_D, "fs2_ln_bwd: only d = 256 is supported (got %d)", d);
+  FS2_CHECK_ARG((dout != nullptr) != (ddot != nullptr), "fs2_ln_bwd: give exactly one of dout/ddot");
+  FS2_CHECK_ARG(!ddot || dot_w, "fs2_ln_bwd: ddot needs dot_w");
+  FS2_CHECK_ARG(ws_bytes >= fs2_ln_bwd_ws_bytes(rows, d), "fs2_ln_bwd: workspace too small");
+  (void)dy_t;
+  if (rows == 0) return FS2_OK;
+  hipStream_t st = as_stream(stream);
+  const int64_t nblk = (rows + LN_ROWS - 1) / LN_ROWS;
+  LnBwd a{dout, ddot, dot_w, xhat, rstd, gamma, beta, lens, seq_len, rows, p_in, p_out, seed,
+          site_in, site_out, relu_y, dy, dres, ws, nblk};
+  ln_bwd_f32<<<(unsigned)nblk, 256, 0, st>>>(a);
+  int rc = launch_status("fs2_ln_bwd");
+  if (rc) return rc;
+  if (dgamma && (rc = colsum_final_launch(ws, nblk, LN_D, dgamma, 1, st))) return rc;
+  if (dbeta && (rc = colsum_final_launch(ws + nblk * LN_D, nblk, LN_D, dbeta, 1, st))) return rc;
+  if (ddot && dw_dot && (rc = colsum_final_launch(ws + 2 * nblk * LN_D, nblk, LN_D, dw_dot, 1, st)))
+    return rc;
+  if (ddot && db_dot && (rc = colsum_final_launch(ws + 3 * nblk * LN_D, nblk, 1, db_dot, 1, st)))
+    return rc;
+  return FS2_OK;
+}
+
+int64_t fs2_bn_ws_bytes(int64_t rows, int64_t c) {
+  const int64_t nparts = (rows + BN_ROWS - 1) / BN_ROWS;
+  return (2 * nparts * c + 2 * c) * 4;
+}
+
+int fs2_bn_fwd(int dtype, const float* z, int64_t rows, int64_t c, const float* gamma,
+               const float* beta, float eps, float momentum, float* running_mean,
+               float* running_var, float* mean, float* rstd, int act_tanh, float p,
+               uint64_t seed, uint64_t site, const float* res, float* out, void* out_t, float* ws,
+               int64_t ws_bytes, void* stream) {
+  if (dtype != FS2_F32) {
+    set_error("fs2_bn_fwd: dtype %d not built", dtype);
+    return FS2_ERR_DTYPE;
+  }
+  FS2_CHECK_ARG(rows > 0 && c > 0, "fs2_bn_fwd: empty input");
+  FS2_CHECK_ARG(ws_bytes >= fs2_bn_ws_bytes(rows, c), "fs2_bn_fwd: workspace too small");
+  (void)out_t;
+  hipStream_t st = as_stream(stream);
+  const int64_t nparts = (rows + BN_ROWS - 1) / BN_ROWS;
+  dim3 grid((unsigned)((c + 63) / 64), (unsigned)nparts);
+  const unsigned cg = (unsigned)((c + 255) / 256);
+  bn_partial<0><<<grid, 256, 0, st>>>(z, nullptr, rows, c, ws);
+  bn_mean_final<<<cg, 256, 0, st>>>(ws, nparts, rows, c, mean);
+  bn_partial<1><<<grid, 256, 0, st>>>(z, mean, rows, c, ws);
+  bn_var_final<<<cg, 256, 0, st>>>(ws, nparts, rows, c, eps, momentum, mean, running_mean,
+                                   running_var, rstd);
+  bn_apply<<<ew_grid(rows * c), 256, 0, st>>>(z, mean, rstd, gamma, beta, rows, c, act_tanh, p,
+                                              seed, site, res, out);
+  return launch_status("fs2_bn_fwd");
+}
+
+int fs2_bn_bwd(int dtype, const float* dout, const float* z, const float* mean, const float* rstd,
+               const float* gamma, const float* beta, int64_t rows, int64_t c, int act_tanh,
+               float p, uint64_t seed, uint64_t site, float* dz, void* dz_t, float* dgamma,
+               float* dbeta, float* ws, int64_t ws_bytes, void* stream) {
+  if (dtype != FS2_F32) {
+    set_error("fs2_bn_bwd: dtype %d not built", dtype);
+    return FS2_ERR_DTYPE;
+  }
+  FS2_CHECK_ARG(rows > 0 && c > 0, "fs2_bn_bwd: empty input");
+  FS2_CHECK_ARG(ws_bytes >= fs2_bn_ws_bytes(rows, c), "fs2_bn_bwd: workspace too small");
+  (void)dz_t;
+  hipStream_t st = as_stream(stream);
+  const int64_t nparts = (rows + BN_ROWS - 1) / BN_ROWS;
+  float* part_g = ws;
+  float* part_gx = ws + nparts * c;
+  float* sums = ws + 2 * nparts * c;
+  dim3 grid((unsigned)((c + 63) / 64), (unsigned)nparts);
+  bn_bwd_partial<<<grid, 256, 0, st>>>(dout, z, mean, rstd, gamma, beta, rows, c, act_tanh, p,
+                                       seed, site, part_g, part_gx);
+  bn_bwd_final<<<(unsigned)((c + 255) / 256), 256, 0, st>>>(part_g, part_gx, nparts, c, sums,
+                                                             dgamma, dbeta);
+  bn_bwd_apply<<<ew_grid(rows * c), 256, 0, st>>>(dout, z, mean, rstd, gamma, beta, sums, rows, c,
+                                                  act_tanh, p, seed, site, dz);
+  return launch_status("fs2_bn_bwd");
+}
+
+}  // extern "C"

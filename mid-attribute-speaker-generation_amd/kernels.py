@@ -1,0 +1,366 @@
+"""Tensor-level wrappers over the C-ABI (``include/fs2hip.h``).
+
+Each wrapper checks device/dtype/contiguity on the host, allocates outputs and workspaces
+from PyTorch's caching allocator, and launches on the current HIP stream.  They never fall
+back to PyTorch math: a wrong input raises, a missing library raises.
+"""
+import torch
+
+from ._lib import lib
+
+F32 = 0
+BF16 = 1
+F64 = 2
+EPI_BIAS, EPI_RELU, EPI_ADD_AUX, EPI_RELU_MASK_AUX = 1, 2, 4, 8
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def _dev(*ts):
+    for t in ts:
+        if t is not None:
+            if not t.is_cuda:
+                raise RuntimeError("fs2 kernels need tensors on the GPU (no CPU path exists)")
+            if not t.is_contiguous():
+                raise RuntimeError("fs2 kernels need contiguous tensors")
+
+
+def f32(t):
+    if t.dtype != torch.float32:
+        raise RuntimeError(f"expected float32, got {t.dtype}")
+    return t
+
+
+def ws(nbytes, device):
+    return torch.empty(max(int(nbytes) // 4, 1), dtype=torch.float32, device=device)
+
+
+# ------------------------------------------------------------------ GEMM / conv
+def conv_gemm(x, wk, rows, seq_len, c_in, c_out, taps, pad, bias=None, flags=0, aux=None,
+              out=None, ldx=None):
+    _dev(x, wk, bias, aux)
+    if out is None:
+        out = torch.empty(rows, c_out, dtype=torch.float32, device=x.device)
+    if bias is not None:
+        flags |= EPI_BIAS
+    lib.fs2_conv_gemm(F32, ptr(x), ldx or c_in, ptr(wk), ptr(out), c_out, rows, seq_len, c_in,
+                      c_out, taps, pad, ptr(bias), flags, ptr(aux), c_out, stream())
+    return out
+
+
+def weight_prep(w, c_out, c_in, taps, w_fwd=None, w_bwd=None):
+    _dev(w)
+    lib.fs2_conv_weight_prep(F32, ptr(w), c_out, c_in, taps, ptr(w_fwd), ptr(w_bwd), stream())
+
+
+def conv_wgrad(dy, x, dw, rows, seq_len, c_in, c_out, taps, pad):
+    _dev(dy, x, dw)
+    n = lib.fs2_conv_wgrad_ws_bytes(rows, c_in, c_out, taps)
+    w = ws(n, dy.device)
+    lib.fs2_conv_wgrad(F32, ptr(dy), c_out, ptr(x), c_in, ptr(dw), rows, seq_len, c_in, c_out,
+                       taps, pad, ptr(w), n, stream())
+
+
+def colsum(x, rows, cols, out, accumulate=True):
+    _dev(x, out)
+    n = lib.fs2_colsum_ws_bytes(rows, cols)
+    w = ws(n, x.device)
+    lib.fs2_colsum(F32, ptr(x), cols, rows, cols, ptr(out), int(accumulate), ptr(w), n, stream())
+
+
+# ------------------------------------------------------------------ attention
+def attn_fwd(qkv, lens, batch, seq_len, heads, d_head, scale):
+    _dev(qkv, lens)
+    o = torch.empty(batch * seq_len, heads * d_head, dtype=torch.float32, device=qkv.device)
+    lse = torch.empty(batch * heads, seq_len, dtype=torch.float32, device=qkv.device)
+    lib.fs2_attn_fwd(F32, ptr(qkv), ptr(o), ptr(lse), ptr(lens), batch, seq_len, heads, d_head,
+                     scale, stream())
+    return o, lse
+
+
+def attn_bwd(qkv, o, d_o, lse, lens, batch, seq_len, heads, d_head, scale):
+    _dev(qkv, o, d_o, lse, lens)
+    dqkv = torch.empty_like(qkv)
+    n = lib.fs2_attn_bwd_ws_bytes(batch, seq_len, heads)
+    w = ws(n, qkv.device)
+    lib.fs2_attn_bwd(F32, ptr(qkv), ptr(o), ptr(d_o), ptr(lse), ptr(dqkv), ptr(lens), batch,
+                     seq_len, heads, d_head, scale, ptr(w), n, stream())
+    return dqkv
+
+
+# ------------------------------------------------------------------ LayerNorm
+def ln_fwd(y, gamma, beta, res=None, lens=None, seq_len=1, p_in=0.0, p_out=0.0, seed=0,
+           site_in=0, site_out=0, dot_w=None, dot_b=None):
+    _dev(y, gamma, beta, res, lens, dot_w, dot_b)
+    rows, d = y.shape
+    out = torch.empty_like(y)
+    xhat = torch.empty_like(y)
+    rstd = torch.empty(rows, dtype=torch.float32, device=y.device)
+    dot = torch.empty(rows, dtype=torch.float32, device=y.device) if dot_w is not None else None
+    lib.fs2_ln_fwd(F32, ptr(y), ptr(res), ptr(gamma), ptr(beta), ptr(out), None, ptr(xhat),
+                   ptr(rstd), ptr(lens), seq_len, rows, d, p_in, p_out, seed, site_in, site_out,
+                   ptr(dot_w), ptr(dot_b), ptr(dot), stream())
+    return out, xhat, rstd, dot
+
+
+def ln_bwd(xhat, rstd, gamma, beta, dgamma, dbeta, dout=None, ddot=None, dot_w=None,
+           dw_dot=None, db_dot=None, lens=None, seq_len=1, p_in=0.0, p_out=0.0, seed=0,
+           site_in=0, site_out=0, relu_y=None, dres=None):
+    _dev(xhat, rstd, gamma, beta, dout, ddot, dot_w, relu_y, dres, lens)
+    rows, d = xhat.shape
+    dy = torch.empty_like(xhat)
+    n = lib.fs2_ln_bwd_ws_bytes(rows, d)
+    w = ws(n, xhat.device)
+    lib.fs2_ln_bwd(F32, ptr(dout), ptr(ddot), ptr(dot_w), ptr(xhat), ptr(rstd), ptr(gamma),
+                   ptr(beta), ptr(lens), seq_len, rows, d, p_in, p_out, seed, site_in, site_out,
+                   ptr(relu_y), ptr(dy), None, ptr(dres), ptr(dgamma), ptr(dbeta), ptr(dw_dot),
+                   ptr(db_dot), ptr(w), n, stream())
+    return dy
+
+
+# ------------------------------------------------------------------ BatchNorm
+def bn_fwd(z, gamma, beta, running_mean, running_var, act_tanh, p, seed, site, res=None,
+           eps=1e-5, momentum=0.1):
+    _dev(z, gamma, beta, running_mean, running_var, res)
+    rows, c = z.shape
+    out = torch.empty_like(z)
+    mean = torch.empty(c, dtype=torch.float32, device=z.device)
+    rstd = torch.empty(c, dtype=torch.float32, device=z.device)
+    n = lib.fs2_bn_ws_bytes(rows, c)
+    w = ws(n, z.device)
+    lib.fs2_bn_fwd(F32, ptr(z), rows, c, ptr(gamma), ptr(beta), eps, momentum, ptr(running_mean),
+                   ptr(running_var), ptr(mean), ptr(rstd), int(act_tanh), p, seed, site, ptr(res),
+                   ptr(out), None, ptr(w), n, stream())
+    return out, mean, rstd
+
+
+def bn_bwd(dout, z, mean, rstd, gamma, beta, dgamma, dbeta, act_tanh, p, seed, site):
+    _dev(dout, z, mean, rstd, gamma, beta, dgamma, dbeta)
+    rows, c = z.shape
+    dz = torch.empty_like(z)
+    n = lib.fs2_bn_ws_bytes(rows, c)
+    w = ws(n, z.device)
+    lib.fs2_bn_bwd(F32, ptr(dout), ptr(z), ptr(mean), ptr(rstd), ptr(gamma), ptr(beta), rows, c,
+                   int(act_tanh), p, seed, site, ptr(dz), None, ptr(dgamma), ptr(dbeta), ptr(w), n,
+                   stream())
+    return dz
+
+
+# ------------------------------------------------------------------ embeddings / adaptor
+def encoder_embed(texts, accents, word_emb, accent_emb, posenc, batch, seq_len, d):
+    _dev(texts, accents, word_emb, accent_emb, posenc)
+    out = torch.empty(batch * seq_len, d, dtype=torch.float32, device=word_emb.device)
+    lib.fs2_encoder_embed_fwd(ptr(texts), ptr(accents), ptr(word_emb), ptr(accent_emb), ptr(posenc),
+                              batch, seq_len, d, ptr(out), None, stream())
+    return out
+
+
+def embedding_fwd(ids, table):
+    _dev(ids, table)
+    n, d = ids.numel(), table.shape[1]
+    out = torch.empty(n, d, dtype=torch.float32, device=table.device)
+    lib.fs2_embedding_fwd(ptr(ids), ptr(table), n, d, ptr(out), stream())
+    return out
+
+
+def embedding_bwd(dout, ids, dtable, padding_idx=-1):
+    _dev(dout, ids, dtable)
+    lib.fs2_embedding_bwd(ptr(dout), ptr(ids), ids.numel(), dtable.shape[1], padding_idx,
+                          ptr(dtable), stream())
+
+
+def length_mask(lens, max_len):
+    _dev(lens)
+    m = torch.empty(lens.numel(), max_len, dtype=torch.bool, device=lens.device)
+    lib.fs2_length_mask(ptr(lens), lens.numel(), max_len, ptr(m), stream())
+    return m
+
+
+def rowvec_add(x, ids, table, batch, seq_len):
+    _dev(x, ids, table)
+    out = torch.empty_like(x)
+    lib.fs2_rowvec_add_fwd(ptr(x), ptr(ids), ptr(table), batch, seq_len, x.shape[1], ptr(out),
+                           None, stream())
+    return out
+
+
+def rowvec_add_bwd(dout, ids, dtable, batch, seq_len):
+    _dev(dout, ids, dtable)
+    lib.fs2_rowvec_add_bwd(ptr(dout), ptr(ids), batch, seq_len, dout.shape[1], ptr(dtable), stream())
+
+
+def _vals_dtype(v):
+    if v.dtype == torch.float32:
+        return F32
+    if v.dtype == torch.float64:
+        return F64
+    raise RuntimeError(f"bucketize values must be float32/float64, got {v.dtype}")
+
+
+def bucket_embed(x, values, bins, table):
+    _dev(x, values, bins, table)
+    rows, d = x.shape
+    out = torch.empty_like(x)
+    idx = torch.empty(rows, dtype=torch.int32, device=x.device)
+    lib.fs2_bucket_embed_fwd(ptr(x), ptr(values), _vals_dtype(values), ptr(bins), bins.numel(),
+                             ptr(table), rows, d, ptr(out), None, ptr(idx), stream())
+    return out, idx
+
+
+def bucket_embed_bwd(dout, idx, dtable):
+    _dev(dout, idx, dtable)
+    lib.fs2_bucket_embed_bwd(ptr(dout), ptr(idx), idx.numel(), dout.shape[1], ptr(dtable), stream())
+
+
+def bucketize(values, bins):
+    _dev(values, bins)
+    idx = torch.empty(values.shape, dtype=torch.int32, device=values.device)
+    lib.fs2_bucketize(ptr(values), _vals_dtype(values), ptr(bins), bins.numel(), values.numel(),
+                      ptr(idx), stream())
+    return idx
+
+
+def lr_index(durations):
+    _dev(durations)
+    B, Ts = durations.shape
+    if durations.dtype == torch.int64:
+        dt = 0
+    elif durations.dtype == torch.float32:
+        dt = 1
+    else:
+        raise RuntimeError(f"durations must be int64 or float32, got {durations.dtype}")
+    cum = torch.empty(B, Ts, dtype=torch.int32, device=durations.device)
+    mel_len = torch.empty(B, dtype=torch.int64, device=durations.device)
+    lib.fs2_lr_index(ptr(durations), dt, B, Ts, ptr(cum), ptr(mel_len), stream())
+    return cum, mel_len
+
+
+def lr_source(cum, out_len):
+    _dev(cum)
+    B, Ts = cum.shape
+    src = torch.empty(B, out_len, dtype=torch.int32, device=cum.device)
+    lib.fs2_lr_source(ptr(cum), B, Ts, out_len, ptr(src), stream())
+    return src
+
+
+def lr_expand(x, cum, out_len, posenc=None):
+    _dev(x, cum, posenc)
+    B, Ts = cum.shape
+    d = x.shape[-1]
+    out = torch.empty(B * out_len, d, dtype=torch.float32, device=x.device)
+    lib.fs2_lr_expand_fwd(ptr(x), ptr(cum), B, Ts, out_len, d, ptr(posenc), ptr(out), None, stream())
+    return out
+
+
+def lr_expand_bwd(dout, cum, out_len, d):
+    _dev(dout, cum)
+    B, Ts = cum.shape
+    dx = torch.empty(B * Ts, d, dtype=torch.float32, device=dout.device)
+    lib.fs2_lr_expand_bwd(ptr(dout), ptr(cum), B, Ts, out_len, d, ptr(dx), stream())
+    return dx
+
+
+# ------------------------------------------------------------------ losses / GMM
+def fs2loss_fwd(mel_out, post_out, mel_tgt, p, e, logd, p_t, e_t, d_t, src_pad, mel_pad,
+                denoms=None):
+    _dev(mel_out, post_out, mel_tgt, p, e, logd, p_t, e_t, d_t, src_pad, mel_pad, denoms)
+    B, Tm, n_mel = mel_out.shape
+    Ts = p.shape[1]
+    losses = torch.empty(6, dtype=torch.float32, device=mel_out.device)
+    n = lib.fs2_fs2loss_ws_bytes(B, Tm)
+    w = ws(n, mel_out.device)
+    lib.fs2_fs2loss_fwd(ptr(mel_out), ptr(post_out), ptr(mel_tgt), mel_tgt.shape[1], ptr(p), ptr(e),
+                        ptr(logd), ptr(p_t), ptr(e_t), ptr(d_t), ptr(src_pad), ptr(mel_pad), B, Ts,
+                        Tm, n_mel, ptr(denoms), ptr(losses), ptr(w), n, stream())
+    return losses, w
+
+
+def fs2loss_bwd(mel_out, post_out, mel_tgt, p, e, logd, p_t, e_t, d_t, src_pad, mel_pad, w, g6):
+    B, Tm, n_mel = mel_out.shape
+    Ts = p.shape[1]
+    outs = [torch.empty_like(t) for t in (mel_out, post_out, p, e, logd)]
+    lib.fs2_fs2loss_bwd(ptr(mel_out), ptr(post_out), ptr(mel_tgt), mel_tgt.shape[1], ptr(p), ptr(e),
+                        ptr(logd), ptr(p_t), ptr(e_t), ptr(d_t), ptr(src_pad), ptr(mel_pad), B, Ts,
+                        Tm, n_mel, ptr(w), ptr(g6), *[ptr(o) for o in outs], stream())
+    return outs
+
+
+def gmm_head_fwd(meta, w_pi, b_pi, w_s, b_s, w_mu, b_mu, K, D):
+    _dev(meta, w_pi, b_pi, w_s, b_s, w_mu, b_mu)
+    B, in_dim = meta.shape
+    dev = meta.device
+    pi = torch.empty(B, K, dtype=torch.float32, device=dev)
+    sigma = torch.empty(B, K, D, dtype=torch.float32, device=dev)
+    mu = torch.empty(B, K, D, dtype=torch.float32, device=dev)
+    sigma_pre = torch.empty(B, K, D, dtype=torch.float32, device=dev)
+    lib.fs2_gmm_head_fwd(ptr(meta), B, in_dim, K, D, ptr(w_pi), ptr(b_pi), ptr(w_s), ptr(b_s),
+                         ptr(w_mu), ptr(b_mu), ptr(pi), ptr(sigma), ptr(mu), ptr(sigma_pre), stream())
+    return pi, mu, sigma, sigma_pre
+
+
+def gmm_logprob(e, pi, mu, sigma, want_mean=False):
+    _dev(e, pi, mu, sigma)
+    B, K, D = mu.shape
+    logp = torch.empty(B, dtype=torch.float32, device=e.device)
+    resp = torch.empty(B, K, dtype=torch.float32, device=e.device)
+    mean = torch.empty((), dtype=torch.float32, device=e.device) if want_mean else None
+    lib.fs2_gmm_logprob(ptr(e), ptr(pi), ptr(mu), ptr(sigma), B, K, D, ptr(logp), ptr(resp),
+                        ptr(mean), stream())
+    return logp, resp, mean
+
+
+def gmm_head_bwd(meta, e, pi, mu, sigma, sigma_pre, resp, g_logp, grads):
+    B, K, D = mu.shape
+    lib.fs2_gmm_head_bwd(ptr(meta), ptr(e), ptr(pi), ptr(mu), ptr(sigma), ptr(sigma_pre), ptr(resp),
+                         ptr(g_logp), B, meta.shape[1], K, D, *[ptr(g) for g in grads], stream())
+
+
+def gmm_sample(pi, mu, sigma, seed, offset=0):
+    _dev(pi, mu, sigma)
+    B, K, D = mu.shape
+    out = torch.empty(B, D, dtype=torch.float32, device=mu.device)
+    comp = torch.empty(B, dtype=torch.int32, device=mu.device)
+    lib.fs2_gmm_sample(ptr(pi), ptr(mu), ptr(sigma), B, K, D, seed, offset, ptr(out), ptr(comp),
+                       stream())
+    return out, comp
+
+
+# ------------------------------------------------------------------ optimiser
+def grad_norm(g, max_norm, norm_coef):
+    n = lib.fs2_grad_norm_ws_bytes(g.numel())
+    w = ws(n, g.device)
+    lib.fs2_grad_norm(ptr(g), g.numel(), float(max_norm), ptr(norm_coef), ptr(w), n, stream())
+
+
+def adam_step(p, g, m, v, norm_coef, lr, beta1, beta2, eps, bc1, bc2_sqrt):
+    lib.fs2_adam_step(ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), ptr(norm_coef), float(lr),
+                      float(beta1), float(beta2), float(eps), float(bc1), float(bc2_sqrt), stream())
+
+
+def fill_(t, value):
+    _dev(t)
+    lib.fs2_fill(ptr(t), t.numel(), float(value), stream())
+    return t
+
+
+def zeros(shape, device):
+    return fill_(torch.empty(shape, dtype=torch.float32, device=device), 0.0)
+
+
+def add(a, b, out=None):
+    _dev(a, b)
+    out = torch.empty_like(a) if out is None else out
+    lib.fs2_add(ptr(out), ptr(a), ptr(b), a.numel(), stream())
+    return out
+
+
+def add_i64_(t, value):
+    _dev(t)
+    lib.fs2_add_i64(ptr(t), t.numel(), int(value), stream())
+    return t

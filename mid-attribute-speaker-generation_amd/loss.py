@@ -1,0 +1,116 @@
+"""Losses of the training step and the TacoSpawn GMM prior object.
+
+Drop-ins for ``model/loss.py``: ``FastSpeech2Loss(preprocess_config, model_config)`` returns
+the same 6-tuple (total, mel, postnet, pitch, energy, duration) and ``SpeakerMetaEncLoss``
+the same mean log-likelihood; both are single HIP launches (plus a finaliser) with
+device-side valid counts, so no ``masked_select`` host sync remains.
+"""
+import torch
+import torch.nn as nn
+
+from . import kernels as K
+
+
+class FS2LossFn(torch.autograd.Function):
+    @staticmethod
+    def forward(fctx, mel_out, post_out, p, e, log_d, mels, p_t, e_t, d_t, src_pad, mel_pad, denoms):
+        T = mel_out.shape[1]
+        args = (mel_out.contiguous(), post_out.contiguous(), mels.contiguous(), p.contiguous(),
+                e.contiguous(), log_d.contiguous(), p_t.contiguous().float(),
+                e_t.contiguous().float(), d_t.contiguous(), src_pad.contiguous(),
+                mel_pad[:, :T].contiguous())
+        losses, ws = K.fs2loss_fwd(*args, denoms=denoms)
+        fctx.args, fctx.ws = args, ws
+        return tuple(losses[i] for i in range(6))
+
+    @staticmethod
+    def backward(fctx, *g):
+        dev = fctx.ws.device
+        g6 = torch.stack([x.reshape(()) if x is not None else torch.zeros((), device=dev) for x in g])
+        a = fctx.args
+        d_mel, d_post, d_p, d_e, d_d = K.fs2loss_bwd(a[0], a[1], a[2], a[3], a[4], a[5], a[6], a[7],
+                                                     a[8], a[9], a[10], fctx.ws, g6.float().contiguous())
+        fctx.args = None
+        return (d_mel, d_post, d_p, d_e, d_d) + (None,) * 7
+
+
+class FastSpeech2Loss(nn.Module):
+    """``model/loss.py:5-92`` (phoneme-level pitch/energy)."""
+
+    def __init__(self, preprocess_config, model_config):
+        super().__init__()
+        for key in ("pitch", "energy"):
+            assert preprocess_config[key]["feature"] == "phoneme_level", \
+                "frame-level variance losses are not built"
+        self.denoms = None  # data-parallel: device [mel elements, phonemes] of the global batch
+
+    def forward(self, inputs, predictions):
+        mels, _, _, p_t, e_t, d_t = inputs[6:12]
+        (mel_out, post_out, p, e, log_d, _, src_masks, mel_masks, _, _) = predictions[:10]
+        return FS2LossFn.apply(mel_out, post_out, p, e, log_d, mels, p_t, e_t, d_t, src_masks,
+                               mel_masks, self.denoms)
+
+
+class GMMMeanLogProbFn(torch.autograd.Function):
+    """scale * mean_b log p(e_b); backward into the head's weight gradients
+    (fastspeech2.py:322-341, loss.py:102-104)."""
+
+    @staticmethod
+    def forward(fctx, token, e, gmm, scale):
+        e = e.detach().contiguous().float()
+        _, resp, mean = K.gmm_logprob(e, gmm.pi, gmm.mu, gmm.sigma, want_mean=True)
+        if scale != 1.0:
+            K.lib.fs2_scale(K.ptr(mean), 1, float(scale), K.stream())
+        fctx.saved = (e, resp, gmm, scale)
+        return mean
+
+    @staticmethod
+    def backward(fctx, g):
+        e, resp, gmm, scale = fctx.saved
+        B = e.shape[0]
+        gl = torch.empty(B, dtype=torch.float32, device=e.device)
+        K.lib.fs2_fill_from(K.ptr(gl), B, K.ptr(g.contiguous()), float(scale) / B, K.stream())
+        K.gmm_head_bwd(gmm.meta, e, gmm.pi, gmm.mu, gmm.sigma, gmm.sigma_pre, resp, gl,
+                       gmm.head.grads())
+        fctx.saved = None
+        return None, None, None, None
+
+
+class GMMPrior:
+    """The reference's ``MixtureSameFamily(Categorical(pi), Independent(Normal(mu, sigma), 1))``
+    (``model/fastspeech2.py:336-341``) as device tensors, with HIP log_prob / sample."""
+
+    def __init__(self, pi, mu, sigma, sigma_pre=None, meta=None, head=None):
+        self.pi, self.mu, self.sigma = pi, mu, sigma
+        self.sigma_pre, self.meta, self.head = sigma_pre, meta, head
+
+    def log_prob(self, e):
+        logp, _, _ = K.gmm_logprob(e.detach().contiguous().float(), self.pi, self.mu, self.sigma)
+        return logp
+
+    def mean_log_prob(self, e, scale=1.0):
+        token = getattr(self.head, "_tok", None)
+        if token is None:
+            logp, _, mean = K.gmm_logprob(e.detach().contiguous().float(), self.pi, self.mu,
+                                          self.sigma, want_mean=True)
+            return mean
+        return GMMMeanLogProbFn.apply(token, e, self, float(scale))
+
+    def sample(self, seed=None, offset=0):
+        import numpy as np
+        if seed is None:
+            seed = int(np.random.default_rng().integers(0, 2 ** 62))
+        out, _ = K.gmm_sample(self.pi, self.mu, self.sigma, int(seed), int(offset))
+        return out
+
+
+class SpeakerMetaEncLoss(nn.Module):
+    """``model/loss.py:94-105``: sum_b log p(e_b) / B (the caller backprops its negative)."""
+
+    def __init__(self, preprocess_config, model_config):
+        super().__init__()
+        self.K = model_config["speaker_generation"]["GMM_mixtures"]
+        self.scale = 1.0  # data-parallel: B_local / B_global
+
+    def forward(self, input, prediction):
+        return prediction.mean_log_prob(input, self.scale)

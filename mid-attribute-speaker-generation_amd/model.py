@@ -1,0 +1,800 @@
+"""FastSpeech2 + TacoSpawn GMM, host side: the reference's module API on HIP kernels.
+
+Drop-in for ``model.fastspeech2.FastSpeech2`` (``model/fastspeech2.py:15-341``): same
+constructor ``(preprocess_config, model_config, config_path)``, same ``forward`` signature
+and 12-tuple, same 242 state-dict keys and shapes, same ``model.parameters()`` order (so a
+reference checkpoint and its Adam state load unchanged).  Every tensor op of the training
+path runs in ``csrc/libfs2hip.so``; the submodules here are parameter containers plus a
+hand-written forward/backward per block, wired to autograd at block granularity:
+
+  EncoderFn        embed + 4 FFT blocks               (transformer/Models.py:77-112)
+  VarianceAdaptorFn speaker add, 3 predictors, bucketized pitch/energy embeddings,
+                   LengthRegulator + decoder position encoding
+                                                      (fastspeech2.py:80-85, modules.py:102-194,
+                                                       Models.py:165-174)
+  DecoderFn        6 FFT blocks                       (transformer/Models.py:151-183)
+  MelHeadFn        mel_linear + PostNet + residual    (fastspeech2.py:109-111, Layers.py:67-137)
+  (loss.py)        FastSpeech2Loss, GMM log-likelihood
+
+Parameters live in one flat fp32 buffer (``ParamArena``), laid out in reverse backward
+order so gradient buckets complete front-to-back; kernels accumulate weight gradients
+straight into the flat gradient buffer (``param.grad`` are views of it).
+"""
+import math
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import config as cfg
+from . import kernels as K
+
+D_HEAD = 128
+
+# ----------------------------------------------------------------------------- containers
+
+
+class Linear(nn.Module):
+    def __init__(self, d_in, d_out, bias=True):
+        super().__init__()
+        self.in_features, self.out_features = d_in, d_out
+        self.weight = nn.Parameter(torch.empty(d_out, d_in))
+        self.bias = nn.Parameter(torch.empty(d_out)) if bias else None
+        bound = 1.0 / math.sqrt(d_in)  # nn.Linear default init
+        with torch.no_grad():
+            nn.init.kaiming_uniform_(self.weight, a=math.sqrt(5))
+            if self.bias is not None:
+                self.bias.uniform_(-bound, bound)
+
+
+class Conv1d(nn.Module):
+    def __init__(self, c_in, c_out, k, padding):
+        super().__init__()
+        self.c_in, self.c_out, self.k, self.padding = c_in, c_out, k, padding
+        self.weight = nn.Parameter(torch.empty(c_out, c_in, k))
+        self.bias = nn.Parameter(torch.empty(c_out))
+        bound = 1.0 / math.sqrt(c_in * k)
+        with torch.no_grad():
+            nn.init.kaiming_uniform_(self.weight, a=math.sqrt(5))
+            self.bias.uniform_(-bound, bound)
+
+
+class LayerNorm(nn.Module):
+    def __init__(self, d):
+        super().__init__()
+        self.weight = nn.Parameter(torch.ones(d))
+        self.bias = nn.Parameter(torch.zeros(d))
+
+
+class Embedding(nn.Module):
+    def __init__(self, n, d, padding_idx=None):
+        super().__init__()
+        self.padding_idx = -1 if padding_idx is None else padding_idx
+        self.weight = nn.Parameter(torch.randn(n, d))
+        if padding_idx is not None:
+            with torch.no_grad():
+                self.weight[padding_idx].zero_()
+
+
+class BatchNorm1d(nn.Module):
+    def __init__(self, c):
+        super().__init__()
+        self.weight = nn.Parameter(torch.ones(c))
+        self.bias = nn.Parameter(torch.zeros(c))
+        self.register_buffer("running_mean", torch.zeros(c))
+        self.register_buffer("running_var", torch.ones(c))
+        self.register_buffer("num_batches_tracked", torch.tensor(0, dtype=torch.long))
+
+
+class _ConvWrap(nn.Module):
+    """``.conv`` holder: the reference's ``Conv`` (modules.py:253) / ``ConvNorm`` (Layers.py:33)."""
+
+    def __init__(self, c_in, c_out, k, padding):
+        super().__init__()
+        self.conv = Conv1d(c_in, c_out, k, padding)
+
+
+def sinusoid_table(n_position, d_hid):
+    """``transformer/Models.py:10-30`` (float64 angles, stored float32)."""
+    pos = np.arange(n_position, dtype=np.float64)[:, None]
+    denom = np.array([np.power(10000, 2 * (j // 2) / d_hid) for j in range(d_hid)])
+    ang = pos / denom[None, :]
+    tab = np.empty_like(ang)
+    tab[:, 0::2] = np.sin(ang[:, 0::2])
+    tab[:, 1::2] = np.cos(ang[:, 1::2])
+    return torch.from_numpy(tab.astype(np.float32))
+
+
+# ----------------------------------------------------------------------------- runtime state
+
+
+class StepCtx:
+    """Per-forward dropout state: one Philox seed per step, one site id per dropout call."""
+
+    def __init__(self, seed, training, dropout):
+        self.seed = int(seed)
+        self.drop = bool(training and dropout)
+
+    def p(self, p):
+        return float(p) if self.drop else 0.0
+
+
+def _g(p):
+    """Flat-buffer gradient view of parameter ``p`` (set up by ParamArena)."""
+    return p._fs2_grad
+
+
+def _linear_prep(lin, c_out=None, c_in=None, w=None):
+    """fp32: forward uses the (out, in) weight as is; backward needs its transpose."""
+    w = lin.weight if w is None else w
+    c_out = lin.out_features if c_out is None else c_out
+    c_in = lin.in_features if c_in is None else c_in
+    if getattr(lin, "_w_bwd", None) is None or lin._w_bwd.numel() != c_out * c_in:
+        lin._w_bwd = torch.empty(c_in, c_out, dtype=torch.float32, device=w.device)
+    K.weight_prep(w, c_out, c_in, 1, None, lin._w_bwd)
+
+
+def _conv_prep(conv):
+    if getattr(conv, "_w_fwd", None) is None:
+        n = conv.c_out * conv.c_in * conv.k
+        conv._w_fwd = torch.empty(n, dtype=torch.float32, device=conv.weight.device)
+        conv._w_bwd = torch.empty(n, dtype=torch.float32, device=conv.weight.device)
+    K.weight_prep(conv.weight, conv.c_out, conv.c_in, conv.k, conv._w_fwd, conv._w_bwd)
+
+
+# ----------------------------------------------------------------------------- FFT block
+
+
+class MultiHeadAttention(nn.Module):
+    """Parameters of ``transformer/SubLayers.py:8-57``."""
+
+    def __init__(self, n_head, d_model, d_k, dropout):
+        super().__init__()
+        self.n_head, self.d_k, self.p = n_head, d_k, dropout
+        self.w_qs = Linear(d_model, n_head * d_k)
+        self.w_ks = Linear(d_model, n_head * d_k)
+        self.w_vs = Linear(d_model, n_head * d_k)
+        self.layer_norm = LayerNorm(d_model)
+        self.fc = Linear(n_head * d_k, d_model)
+
+
+class PositionwiseFeedForward(nn.Module):
+    """Parameters of ``transformer/SubLayers.py:60-93``."""
+
+    def __init__(self, d_in, d_hid, kernel_size, dropout):
+        super().__init__()
+        self.p = dropout
+        self.w_1 = Conv1d(d_in, d_hid, kernel_size[0], (kernel_size[0] - 1) // 2)
+        self.w_2 = Conv1d(d_hid, d_in, kernel_size[1], (kernel_size[1] - 1) // 2)
+        self.layer_norm = LayerNorm(d_in)
+
+
+class FFTBlock(nn.Module):
+    """``transformer/Layers.py:11-30``: post-LN MHA + Conv1d FFN, padded rows zeroed."""
+
+    def __init__(self, d_model, n_head, d_inner, kernel_size, dropout):
+        super().__init__()
+        self.d = d_model
+        self.slf_attn = MultiHeadAttention(n_head, d_model, d_model // n_head, dropout)
+        self.pos_ffn = PositionwiseFeedForward(d_model, d_inner, kernel_size, dropout)
+        self.site = 0  # assigned by FastSpeech2
+
+    # fused views over the arena: [Wq; Wk; Wv] (3hd, d) and [bq; bk; bv]
+    def _qkv(self):
+        a = self.slf_attn
+        return self._qkv_w, self._qkv_b, self._qkv_gw, self._qkv_gb
+
+    def prep(self):
+        a, f = self.slf_attn, self.pos_ffn
+        n3 = 3 * a.n_head * a.d_k
+        wq, bq = a.w_qs.weight, a.w_qs.bias
+        self._qkv_w = _flat_view(wq, n3 * self.d).view(n3, self.d)
+        self._qkv_b = _flat_view(bq, n3)
+        self._qkv_gw = _flat_view(_g(wq), n3 * self.d).view(n3, self.d)
+        self._qkv_gb = _flat_view(_g(bq), n3)
+        if getattr(self, "_qkv_wb", None) is None:
+            self._qkv_wb = torch.empty(self.d, n3, dtype=torch.float32, device=wq.device)
+        K.weight_prep(self._qkv_w, n3, self.d, 1, None, self._qkv_wb)
+        _linear_prep(a.fc)
+        _conv_prep(f.w_1)
+        _conv_prep(f.w_2)
+
+    def fwd(self, x, lens, B, T, ctx):
+        a, f = self.slf_attn, self.pos_ffn
+        M, d = x.shape
+        n3 = 3 * a.n_head * a.d_k
+        p = ctx.p(a.p)
+        qkv = K.conv_gemm(x, self._qkv_w, M, T, d, n3, 1, 0, bias=self._qkv_b)
+        o, lse = K.attn_fwd(qkv, lens, B, T, a.n_head, a.d_k, 1.0 / math.sqrt(a.d_k))
+        y1 = K.conv_gemm(o, a.fc.weight, M, T, a.n_head * a.d_k, d, 1, 0, bias=a.fc.bias)
+        x1, xh1, rs1, _ = K.ln_fwd(y1, a.layer_norm.weight, a.layer_norm.bias, res=x, lens=lens,
+                                   seq_len=T, p_in=p, seed=ctx.seed, site_in=self.site)
+        w1, w2 = f.w_1, f.w_2
+        h = K.conv_gemm(x1, w1._w_fwd, M, T, d, w1.c_out, w1.k, w1.padding, bias=w1.bias,
+                        flags=K.EPI_RELU)
+        y2 = K.conv_gemm(h, w2._w_fwd, M, T, w2.c_in, d, w2.k, w2.padding, bias=w2.bias)
+        x2, xh2, rs2, _ = K.ln_fwd(y2, f.layer_norm.weight, f.layer_norm.bias, res=x1, lens=lens,
+                                   seq_len=T, p_in=p, seed=ctx.seed, site_in=self.site + 1)
+        saved = (x, qkv, o, lse, x1, h, xh1, rs1, xh2, rs2, p, ctx.seed, lens, B, T)
+        return x2, saved
+
+    def bwd(self, dx2, saved):
+        a, f = self.slf_attn, self.pos_ffn
+        x, qkv, o, lse, x1, h, xh1, rs1, xh2, rs2, p, seed, lens, B, T = saved
+        M, d = x.shape
+        n3 = 3 * a.n_head * a.d_k
+        w1, w2 = f.w_1, f.w_2
+        ln2, ln1 = f.layer_norm, a.layer_norm
+        # LN2 (masked, dropout before the residual add): dx1 starts as dz2
+        dx1 = K.zeros((M, d), x.device)
+        dy2 = K.ln_bwd(xh2, rs2, ln2.weight, ln2.bias, _g(ln2.weight), _g(ln2.bias), dout=dx2,
+                       lens=lens, seq_len=T, p_in=p, seed=seed, site_in=self.site + 1, dres=dx1)
+        K.colsum(dy2, M, d, _g(w2.bias))
+        K.conv_wgrad(dy2, h, _g(w2.weight), M, T, w2.c_in, d, w2.k, w2.padding)
+        dh = K.conv_gemm(dy2, w2._w_bwd, M, T, d, w2.c_in, w2.k, w2.padding,
+                         flags=K.EPI_RELU_MASK_AUX, aux=h)
+        K.colsum(dh, M, w1.c_out, _g(w1.bias))
+        K.conv_wgrad(dh, x1, _g(w1.weight), M, T, d, w1.c_out, w1.k, w1.padding)
+        K.conv_gemm(dh, w1._w_bwd, M, T, w1.c_out, d, w1.k, w1.padding, flags=K.EPI_ADD_AUX,
+                    aux=dx1, out=dx1)
+        # LN1 -> fc -> attention -> QKV
+        dx = K.zeros((M, d), x.device)
+        dy1 = K.ln_bwd(xh1, rs1, ln1.weight, ln1.bias, _g(ln1.weight), _g(ln1.bias), dout=dx1,
+                       lens=lens, seq_len=T, p_in=p, seed=seed, site_in=self.site, dres=dx)
+        hd = a.n_head * a.d_k
+        K.colsum(dy1, M, d, _g(a.fc.bias))
+        K.conv_wgrad(dy1, o, _g(a.fc.weight), M, T, hd, d, 1, 0)
+        do = K.conv_gemm(dy1, a.fc._w_bwd, M, T, d, hd, 1, 0)
+        dqkv = K.attn_bwd(qkv, o, do, lse, lens, B, T, a.n_head, a.d_k, 1.0 / math.sqrt(a.d_k))
+        K.colsum(dqkv, M, n3, self._qkv_gb)
+        K.conv_wgrad(dqkv, x, self._qkv_gw, M, T, d, n3, 1, 0)
+        K.conv_gemm(dqkv, self._qkv_wb, M, T, n3, d, 1, 0, flags=K.EPI_ADD_AUX, aux=dx, out=dx)
+        return dx
+
+
+def _flat_view(t, n):
+    """A 1-D view of ``n`` elements starting at ``t``'s first element (same storage)."""
+    return t.detach().as_strided((n,), (1,), t.storage_offset())
+
+
+def _ffn_stack(config, side):
+    t = config["transformer"]
+    d = t[f"{side}_hidden"]
+    return [FFTBlock(d, t[f"{side}_head"], t["conv_filter_size"], t["conv_kernel_size"],
+                     t[f"{side}_dropout"]) for _ in range(t[f"{side}_layer"])]
+
+
+class Encoder(nn.Module):
+    """``transformer/Models.py:33-112``."""
+
+    def __init__(self, config):
+        super().__init__()
+        d = config["transformer"]["encoder_hidden"]
+        self.d = d
+        self.max_seq_len = config["max_seq_len"]
+        self.src_word_emb = Embedding(429, d, padding_idx=0)
+        self.src_accent_emb = Embedding(5, d, padding_idx=0)
+        self.position_enc = nn.Parameter(sinusoid_table(config["max_seq_len"] + 1, d)[None],
+                                         requires_grad=False)
+        self.layer_stack = nn.ModuleList(_ffn_stack(config, "encoder"))
+
+
+class Decoder(nn.Module):
+    """``transformer/Models.py:115-183``."""
+
+    def __init__(self, config):
+        super().__init__()
+        d = config["transformer"]["decoder_hidden"]
+        self.d = d
+        self.max_seq_len = config["max_seq_len"]
+        self.position_enc = nn.Parameter(sinusoid_table(config["max_seq_len"] + 1, d)[None],
+                                         requires_grad=False)
+        self.layer_stack = nn.ModuleList(_ffn_stack(config, "decoder"))
+
+
+# ----------------------------------------------------------------------------- adaptor
+
+
+class VariancePredictor(nn.Module):
+    """``model/modules.py:197-250``: 2 x (Conv1d k=3 -> ReLU -> LN -> Dropout) -> Linear."""
+
+    def __init__(self, config):
+        super().__init__()
+        d = config["transformer"]["encoder_hidden"]
+        fs = config["variance_predictor"]["filter_size"]
+        k = config["variance_predictor"]["kernel_size"]
+        self.p = config["variance_predictor"]["dropout"]
+        self.conv_layer = nn.Module()
+        self.conv_layer.conv1d_1 = _ConvWrap(d, fs, k, (k - 1) // 2)
+        self.conv_layer.layer_norm_1 = LayerNorm(fs)
+        self.conv_layer.conv1d_2 = _ConvWrap(fs, fs, k, 1)  # padding hard-coded (modules.py:230)
+        self.conv_layer.layer_norm_2 = LayerNorm(fs)
+        self.linear_layer = Linear(fs, 1)
+        self.site = 0
+
+    def prep(self):
+        _conv_prep(self.conv_layer.conv1d_1.conv)
+        _conv_prep(self.conv_layer.conv1d_2.conv)
+
+    def fwd(self, x, lens, B, T, ctx):
+        c = self.conv_layer
+        c1, c2 = c.conv1d_1.conv, c.conv1d_2.conv
+        M = x.shape[0]
+        p = ctx.p(self.p)
+        h1 = K.conv_gemm(x, c1._w_fwd, M, T, c1.c_in, c1.c_out, c1.k, c1.padding, bias=c1.bias,
+                         flags=K.EPI_RELU)
+        u1, xh1, rs1, _ = K.ln_fwd(h1, c.layer_norm_1.weight, c.layer_norm_1.bias, p_out=p,
+                                   seed=ctx.seed, site_out=self.site)
+        h2 = K.conv_gemm(u1, c2._w_fwd, M, T, c2.c_in, c2.c_out, c2.k, c2.padding, bias=c2.bias,
+                         flags=K.EPI_RELU)
+        _, xh2, rs2, pred = K.ln_fwd(h2, c.layer_norm_2.weight, c.layer_norm_2.bias, lens=lens,
+                                     seq_len=T, p_out=p, seed=ctx.seed, site_out=self.site + 1,
+                                     dot_w=self.linear_layer.weight, dot_b=self.linear_layer.bias)
+        saved = (x, h1, u1, h2, xh1, rs1, xh2, rs2, p, ctx.seed, lens, T)
+        return pred.view(B, T), saved
+
+    def bwd(self, dpred, saved, dx_acc):
+        """Backward; the input gradient is *added* into ``dx_acc`` (in place)."""
+        x, h1, u1, h2, xh1, rs1, xh2, rs2, p, seed, lens, T = saved
+        c = self.conv_layer
+        c1, c2 = c.conv1d_1.conv, c.conv1d_2.conv
+        ln1, ln2, lin = c.layer_norm_1, c.layer_norm_2, self.linear_layer
+        M = x.shape[0]
+        dh2 = K.ln_bwd(xh2, rs2, ln2.weight, ln2.bias, _g(ln2.weight), _g(ln2.bias),
+                       ddot=dpred.contiguous().view(-1), dot_w=lin.weight, dw_dot=_g(lin.weight),
+                       db_dot=_g(lin.bias), lens=lens, seq_len=T, p_out=p, seed=seed,
+                       site_out=self.site + 1, relu_y=h2)
+        K.colsum(dh2, M, c2.c_out, _g(c2.bias))
+        K.conv_wgrad(dh2, u1, _g(c2.weight), M, T, c2.c_in, c2.c_out, c2.k, c2.padding)
+        du1 = K.conv_gemm(dh2, c2._w_bwd, M, T, c2.c_out, c2.c_in, c2.k, c2.padding)
+        dh1 = K.ln_bwd(xh1, rs1, ln1.weight, ln1.bias, _g(ln1.weight), _g(ln1.bias), dout=du1,
+                       p_out=p, seed=seed, site_out=self.site, relu_y=h1)
+        K.colsum(dh1, M, c1.c_out, _g(c1.bias))
+        K.conv_wgrad(dh1, x, _g(c1.weight), M, T, c1.c_in, c1.c_out, c1.k, c1.padding)
+        K.conv_gemm(dh1, c1._w_bwd, M, T, c1.c_out, c1.c_in, c1.k, c1.padding,
+                    flags=K.EPI_ADD_AUX, aux=dx_acc, out=dx_acc)
+
+
+class VarianceAdaptor(nn.Module):
+    """``model/modules.py:17-158`` (phoneme-level pitch and energy, linear bins)."""
+
+    def __init__(self, preprocess_config, model_config, config_path):
+        super().__init__()
+        d = model_config["transformer"]["encoder_hidden"]
+        n_bins = model_config["variance_embedding"]["n_bins"]
+        for key in ("pitch", "energy"):
+            assert preprocess_config[key]["feature"] == "phoneme_level", \
+                "frame-level variance features are not built (SURVEY.md §8a row 10)"
+            assert model_config["variance_embedding"][f"{key}_quantization"] == "linear", \
+                "log quantisation is not built"
+        p_min, p_max, e_min, e_max = cfg.pitch_energy_range(config_path)
+        self.duration_predictor = VariancePredictor(model_config)
+        self.pitch_predictor = VariancePredictor(model_config)
+        self.energy_predictor = VariancePredictor(model_config)
+        self.pitch_bins = nn.Parameter(torch.linspace(p_min, p_max, n_bins - 1), requires_grad=False)
+        self.energy_bins = nn.Parameter(torch.linspace(e_min, e_max, n_bins - 1), requires_grad=False)
+        self.pitch_embedding = Embedding(n_bins, d)
+        self.energy_embedding = Embedding(n_bins, d)
+
+
+# ----------------------------------------------------------------------------- PostNet
+
+
+class PostNet(nn.Module):
+    """``transformer/Layers.py:67-137``: 5 x (Conv1d k=5 + BatchNorm1d), tanh on 0-3,
+    dropout 0.5 on all (hard-coded, active in training)."""
+
+    def __init__(self, n_mel=80, dim=512, k=5, n=5):
+        super().__init__()
+        chans = [n_mel] + [dim] * (n - 1) + [n_mel]
+        self.convolutions = nn.ModuleList(
+            nn.Sequential(_ConvWrap(chans[i], chans[i + 1], k, (k - 1) // 2),
+                          BatchNorm1d(chans[i + 1])) for i in range(n))
+        self.site = 0
+
+    def prep(self):
+        for layer in self.convolutions:
+            _conv_prep(layer[0].conv)
+
+    def fwd(self, x, B, T, ctx):
+        """x: (M, n_mel) mel_linear output; returns postnet(x) + x."""
+        M = x.shape[0]
+        a = x
+        saved = []
+        n = len(self.convolutions)
+        p = ctx.p(0.5)
+        for i, layer in enumerate(self.convolutions):
+            conv, bn = layer[0].conv, layer[1]
+            z = K.conv_gemm(a, conv._w_fwd, M, T, conv.c_in, conv.c_out, conv.k, conv.padding,
+                            bias=conv.bias)
+            rm, rv = (bn.running_mean, bn.running_var) if self.training else (None, None)
+            out, mean, rstd = K.bn_fwd(z, bn.weight, bn.bias, rm, rv, i < n - 1, p, ctx.seed,
+                                       self.site + i, res=x if i == n - 1 else None)
+            if self.training:
+                K.add_i64_(bn.num_batches_tracked, 1)
+            saved.append((a, z, mean, rstd))
+            a = out
+        return a, (saved, p, ctx.seed, T)
+
+    def bwd(self, dout, saved, dx_acc):
+        """dout: grad of postnet(x) + x; adds the postnet input grad into ``dx_acc``."""
+        layers, p, seed, T = saved
+        n = len(self.convolutions)
+        d = dout
+        for i in range(n - 1, -1, -1):
+            conv, bn = self.convolutions[i][0].conv, self.convolutions[i][1]
+            a, z, mean, rstd = layers[i]
+            M = z.shape[0]
+            dz = K.bn_bwd(d, z, mean, rstd, bn.weight, bn.bias, _g(bn.weight), _g(bn.bias),
+                          i < n - 1, p, seed, self.site + i)
+            K.colsum(dz, M, conv.c_out, _g(conv.bias))
+            K.conv_wgrad(dz, a, _g(conv.weight), M, T, conv.c_in, conv.c_out, conv.k, conv.padding)
+            if i > 0:
+                d = K.conv_gemm(dz, conv._w_bwd, M, T, conv.c_out, conv.c_in, conv.k, conv.padding)
+            else:
+                K.conv_gemm(dz, conv._w_bwd, M, T, conv.c_out, conv.c_in, conv.k, conv.padding,
+                            flags=K.EPI_ADD_AUX, aux=dx_acc, out=dx_acc)
+
+
+# ----------------------------------------------------------------------------- GMM head
+
+
+class SpeakerMetaEncoder(nn.Module):
+    """TacoSpawn head, ``model/fastspeech2.py:306-341``."""
+
+    def __init__(self, preprocess_config, model_config):
+        super().__init__()
+        self.input_dim = cfg.meta_dim(preprocess_config)
+        self.K = model_config["speaker_generation"]["GMM_mixtures"]
+        self.D = model_config["transformer"]["encoder_hidden"]
+        self.pi_linear = nn.Sequential(Linear(self.input_dim, self.K), nn.Softmax(dim=1))
+        self.sigma_linear = nn.Sequential(Linear(self.input_dim, self.K * self.D), nn.Softplus())
+        self.mu_linear = Linear(self.input_dim, self.K * self.D)
+
+    def forward(self, meta):
+        from .loss import GMMPrior
+        meta = meta.contiguous().float()
+        pi, mu, sigma, sigma_pre = K.gmm_head_fwd(
+            meta, self.pi_linear[0].weight, self.pi_linear[0].bias, self.sigma_linear[0].weight,
+            self.sigma_linear[0].bias, self.mu_linear.weight, self.mu_linear.bias, self.K, self.D)
+        return GMMPrior(pi, mu, sigma, sigma_pre=sigma_pre, meta=meta, head=self)
+
+    def grads(self):
+        return [_g(self.pi_linear[0].weight), _g(self.pi_linear[0].bias),
+                _g(self.sigma_linear[0].weight), _g(self.sigma_linear[0].bias),
+                _g(self.mu_linear.weight), _g(self.mu_linear.bias)]
+
+
+# ----------------------------------------------------------------------------- arena
+
+
+class ParamArena:
+    """One flat fp32 buffer for all trainable parameters and one for their gradients.
+
+    ``order`` is the flat layout (reverse backward order); each parameter's ``.data`` and
+    ``.grad`` become views, so the module API (state_dict, parameters(), .grad) is unchanged
+    while kernels, the optimiser and the gradient all-reduce see contiguous buffers."""
+
+    def __init__(self, params, device):
+        self.params = list(params)
+        offs, n = [], 0
+        for p in self.params:
+            offs.append(n)
+            n += (p.numel() + 3) // 4 * 4  # 16-B aligned sections
+        self.numel = n
+        self.flat = torch.zeros(n, dtype=torch.float32, device=device)
+        self.grad = torch.zeros(n, dtype=torch.float32, device=device)
+        self.offsets = offs
+        with torch.no_grad():
+            for p, o in zip(self.params, offs):
+                v = self.flat[o:o + p.numel()]
+                v.copy_(p.data.reshape(-1).to(device))
+                p.data = v.view(p.shape)
+                p._fs2_grad = self.grad[o:o + p.numel()].view(p.shape)
+                p.grad = p._fs2_grad
+        self.version = 0
+
+    def zero_grad(self):
+        K.fill_(self.grad, 0.0)
+        for p in self.params:
+            p.grad = p._fs2_grad
+
+
+def fft_param_order(b):
+    """Flat layout of one FFT block: q/k/v weights (then biases) adjacent for the fused GEMM."""
+    f, a = b.pos_ffn, b.slf_attn
+    return [f.layer_norm.weight, f.layer_norm.bias, f.w_2.weight, f.w_2.bias, f.w_1.weight,
+            f.w_1.bias, a.layer_norm.weight, a.layer_norm.bias, a.fc.weight, a.fc.bias,
+            a.w_qs.weight, a.w_ks.weight, a.w_vs.weight, a.w_qs.bias, a.w_ks.bias, a.w_vs.bias]
+
+
+def vp_param_order(v):
+    c = v.conv_layer
+    return [v.linear_layer.weight, v.linear_layer.bias, c.layer_norm_2.weight, c.layer_norm_2.bias,
+            c.conv1d_2.conv.weight, c.conv1d_2.conv.bias, c.layer_norm_1.weight,
+            c.layer_norm_1.bias, c.conv1d_1.conv.weight, c.conv1d_1.conv.bias]
+
+
+def postnet_param_order(pn):
+    out = []
+    for layer in reversed(pn.convolutions):
+        out += [layer[1].weight, layer[1].bias, layer[0].conv.weight, layer[0].conv.bias]
+    return out
+
+
+def _flat_order(m):
+    """Reverse-backward layout of the whole model (see ParamArena)."""
+    out = []
+
+    def add(*ps):
+        out.extend(ps)
+
+    def fft(b):
+        add(*fft_param_order(b))
+
+    def vp(v):
+        add(*vp_param_order(v))
+
+    add(*postnet_param_order(m.postnet))
+    add(m.mel_linear.weight, m.mel_linear.bias)
+    for b in reversed(m.decoder.layer_stack):
+        fft(b)
+    va = m.variance_adaptor
+    add(va.energy_embedding.weight)
+    vp(va.energy_predictor)
+    add(va.pitch_embedding.weight)
+    vp(va.pitch_predictor)
+    vp(va.duration_predictor)
+    add(m.speaker_emb.weight)
+    for b in reversed(m.encoder.layer_stack):
+        fft(b)
+    add(m.encoder.src_accent_emb.weight, m.encoder.src_word_emb.weight)
+    e = m.speaker_enc
+    add(e.pi_linear[0].weight, e.pi_linear[0].bias, e.sigma_linear[0].weight,
+        e.sigma_linear[0].bias, e.mu_linear.weight, e.mu_linear.bias)
+    train = [p for p in m.parameters() if p.requires_grad]
+    assert len(out) == len(train) and {id(p) for p in out} == {id(p) for p in train}, \
+        "flat layout must cover every trainable parameter exactly once"
+    return out
+
+
+# ----------------------------------------------------------------------------- autograd
+
+
+class EncoderFn(torch.autograd.Function):
+    @staticmethod
+    def forward(fctx, token, enc, texts, accents, lens, B, T, ctx):
+        x = K.encoder_embed(texts, accents, enc.src_word_emb.weight, enc.src_accent_emb.weight,
+                            enc.position_enc, B, T, enc.d)
+        saved = []
+        for layer in enc.layer_stack:
+            x, s = layer.fwd(x, lens, B, T, ctx)
+            saved.append(s)
+        fctx.enc, fctx.saved, fctx.ids = enc, saved, (texts, accents)
+        return x
+
+    @staticmethod
+    def backward(fctx, dx):
+        enc = fctx.enc
+        dx = dx.contiguous()
+        for layer, s in zip(reversed(enc.layer_stack), reversed(fctx.saved)):
+            dx = layer.bwd(dx, s)
+        texts, accents = fctx.ids
+        K.embedding_bwd(dx, texts, _g(enc.src_word_emb.weight), 0)
+        K.embedding_bwd(dx, accents, _g(enc.src_accent_emb.weight), 0)
+        fctx.saved = None
+        return (None,) * 8
+
+
+class VarianceAdaptorFn(torch.autograd.Function):
+    """Speaker add + variance adaptor (training branch) + decoder position encoding."""
+
+    @staticmethod
+    def forward(fctx, token, enc_out, m, speakers, src_lens, p_t, e_t, d_t, B, Ts, T_dec, ctx):
+        va = m.variance_adaptor
+        x0 = K.rowvec_add(enc_out, speakers, m.speaker_emb.weight, B, Ts)
+        log_d, s_d = va.duration_predictor.fwd(x0, src_lens, B, Ts, ctx)
+        p, s_p = va.pitch_predictor.fwd(x0, src_lens, B, Ts, ctx)
+        x1, idx_p = K.bucket_embed(x0, p_t.contiguous().view(-1), va.pitch_bins, va.pitch_embedding.weight)
+        e, s_e = va.energy_predictor.fwd(x1, src_lens, B, Ts, ctx)
+        x2, idx_e = K.bucket_embed(x1, e_t.contiguous().view(-1), va.energy_bins,
+                                   va.energy_embedding.weight)
+        cum, mel_len = K.lr_index(d_t.contiguous())
+        x_lr = K.lr_expand(x2, cum, T_dec, posenc=m.decoder.position_enc)
+        fctx.m, fctx.saved = m, (s_d, s_p, s_e, idx_p, idx_e, cum, speakers, B, Ts, T_dec)
+        fctx.mark_non_differentiable(mel_len)
+        return x_lr, log_d, p, e, mel_len
+
+    @staticmethod
+    def backward(fctx, d_xlr, d_logd, d_p, d_e, _):
+        m = fctx.m
+        va = m.variance_adaptor
+        s_d, s_p, s_e, idx_p, idx_e, cum, speakers, B, Ts, T_dec = fctx.saved
+        d = m.encoder.d
+        if d_xlr is None:
+            dx = K.zeros((B * Ts, d), m._token.device)
+        else:
+            dx = K.lr_expand_bwd(d_xlr.contiguous(), cum, T_dec, d)
+        K.bucket_embed_bwd(dx, idx_e, _g(va.energy_embedding.weight))
+        if d_e is not None:
+            va.energy_predictor.bwd(d_e, s_e, dx)
+        K.bucket_embed_bwd(dx, idx_p, _g(va.pitch_embedding.weight))
+        if d_p is not None:
+            va.pitch_predictor.bwd(d_p, s_p, dx)
+        if d_logd is not None:
+            va.duration_predictor.bwd(d_logd, s_d, dx)
+        K.rowvec_add_bwd(dx, speakers, _g(m.speaker_emb.weight), B, Ts)
+        fctx.saved = None
+        return (None, dx) + (None,) * 10
+
+
+class DecoderFn(torch.autograd.Function):
+    @staticmethod
+    def forward(fctx, token, x, dec, lens, B, T, ctx):
+        saved = []
+        for layer in dec.layer_stack:
+            x, s = layer.fwd(x, lens, B, T, ctx)
+            saved.append(s)
+        fctx.dec, fctx.saved = dec, saved
+        return x
+
+    @staticmethod
+    def backward(fctx, dx):
+        dx = dx.contiguous()
+        for layer, s in zip(reversed(fctx.dec.layer_stack), reversed(fctx.saved)):
+            dx = layer.bwd(dx, s)
+        fctx.saved = None
+        return None, dx, None, None, None, None, None
+
+
+class MelHeadFn(torch.autograd.Function):
+    """mel_linear + (postnet(out) + out)."""
+
+    @staticmethod
+    def forward(fctx, token, x, m, B, T, ctx):
+        lin = m.mel_linear
+        M = x.shape[0]
+        out = K.conv_gemm(x, lin.weight, M, T, lin.in_features, lin.out_features, 1, 0,
+                          bias=lin.bias)
+        post, s = m.postnet.fwd(out, B, T, ctx)
+        fctx.m, fctx.saved = m, (x, s, B, T)
+        return out.view(B, T, -1), post.view(B, T, -1)
+
+    @staticmethod
+    def backward(fctx, d_out, d_post):
+        m = fctx.m
+        x, s, B, T = fctx.saved
+        lin = m.mel_linear
+        M = x.shape[0]
+        n_mel = lin.out_features
+        d_out = d_out.contiguous().view(M, n_mel) if d_out is not None else None
+        if d_post is not None:
+            d_post = d_post.contiguous().view(M, n_mel)
+            dm = K.add(d_out, d_post) if d_out is not None else d_post.clone()
+            m.postnet.bwd(d_post, s, dm)
+        else:
+            dm = d_out
+        K.colsum(dm, M, n_mel, _g(lin.bias))
+        K.conv_wgrad(dm, x, _g(lin.weight), M, T, lin.in_features, n_mel, 1, 0)
+        dx = K.conv_gemm(dm, lin._w_bwd, M, T, n_mel, lin.in_features, 1, 0)
+        fctx.saved = None
+        return None, dx, None, None, None, None
+
+
+# ----------------------------------------------------------------------------- top level
+
+
+class FastSpeech2(nn.Module):
+    """``model/fastspeech2.py:15-303`` on the HIP kernels (multi_speaker, no JDIT)."""
+
+    def __init__(self, preprocess_config, model_config, config_path, device="cuda"):
+        super().__init__()
+        self.model_config = model_config
+        assert not model_config["jdit"]["use_jdit"], "JDIT aligner is out of scope (SURVEY.md §2.1)"
+        assert model_config["multi_speaker"], "single-speaker FastSpeech2 is not built"
+        self.encoder = Encoder(model_config)
+        self.variance_adaptor = VarianceAdaptor(preprocess_config, model_config, config_path)
+        self.decoder = Decoder(model_config)
+        self.mel_linear = Linear(model_config["transformer"]["decoder_hidden"],
+                                 preprocess_config["mel"]["n_mel_channels"])
+        self.postnet = PostNet()
+        self.speaker_emb = Embedding(cfg.n_speakers(config_path),
+                                     model_config["transformer"]["encoder_hidden"])
+        self.speaker_enc = SpeakerMetaEncoder(preprocess_config, model_config)
+        # dropout site ids (2 per FFT block / variance predictor, 5 for the PostNet)
+        site = 16
+        for b in list(self.encoder.layer_stack) + list(self.decoder.layer_stack):
+            b.site, site = site, site + 2
+        va = self.variance_adaptor
+        for v in (va.duration_predictor, va.pitch_predictor, va.energy_predictor):
+            v.site, site = site, site + 2
+        self.postnet.site = site
+        self.dropout = True
+        self._seed_rng = np.random.default_rng(0)
+        self._arena = None
+        self.to(device)
+
+    # -- plumbing ---------------------------------------------------------------------
+    def _apply(self, fn, *args, **kwargs):
+        r = super()._apply(fn, *args, **kwargs)
+        self._arena = None  # parameters were re-materialised: rebuild the flat views lazily
+        return r
+
+    def arena(self):
+        if self._arena is None:
+            dev = self.encoder.position_enc.device
+            if dev.type != "cuda":
+                raise RuntimeError("FastSpeech2 (fs2-mi355x) runs on the GPU only; move it with .cuda()")
+            self._arena = ParamArena(_flat_order(self), dev)
+            self._token = torch.zeros((), device=dev, requires_grad=True)
+            self.speaker_enc._tok = self._token
+        return self._arena
+
+    def seed(self, s):
+        """Seed the per-step dropout stream (Philox keys are drawn from it)."""
+        self._seed_rng = np.random.default_rng(s)
+
+    def prep_weights(self):
+        for b in list(self.encoder.layer_stack) + list(self.decoder.layer_stack):
+            b.prep()
+        va = self.variance_adaptor
+        for v in (va.duration_predictor, va.pitch_predictor, va.energy_predictor):
+            v.prep()
+        self.postnet.prep()
+        _linear_prep(self.mel_linear)
+
+    # -- forward ----------------------------------------------------------------------
+    def forward(self, speakers, texts, src_lens, max_src_len, mels=None, mel_lens=None,
+                max_mel_len=None, p_targets=None, e_targets=None, d_targets=None,
+                p_control=1.0, e_control=1.0, d_control=1.0, accents=None, speaker_meta=None):
+        if p_targets is None or e_targets is None or d_targets is None or mel_lens is None:
+            raise NotImplementedError("inference branch (no targets) is SURVEY.md §8f row f1")
+        if accents is None:
+            raise ValueError("accents are required in training (transformer/Models.py:101)")
+        self.arena()
+        self.prep_weights()
+        ctx = StepCtx(self._seed_rng.integers(0, 2 ** 62), self.training, self.dropout)
+        B, Ts = texts.shape
+        max_src_len = int(max_src_len)
+        max_mel_len = int(max_mel_len)
+        assert Ts == max_src_len, "texts must be padded to max_src_len"
+        src_lens = src_lens.contiguous().long()
+        mel_lens = mel_lens.contiguous().long()
+        src_masks = K.length_mask(src_lens, max_src_len)
+        T_dec = min(max_mel_len, self.decoder.max_seq_len)  # Models.py:166-174
+        mel_masks = K.length_mask(mel_lens, T_dec)
+
+        tok = self._token
+        enc = EncoderFn.apply(tok, self.encoder, texts.contiguous(), accents.contiguous(), src_lens,
+                              B, Ts, ctx)
+        speaker_emb_s = K.embedding_fwd(speakers.contiguous(), self.speaker_emb.weight)
+        gmm = self.speaker_enc(speaker_meta)
+        x_lr, log_d, p, e, mel_len = VarianceAdaptorFn.apply(
+            tok, enc, self, speakers.contiguous(), src_lens, p_targets, e_targets, d_targets, B, Ts,
+            T_dec, ctx)
+        x = DecoderFn.apply(tok, x_lr, self.decoder, mel_lens, B, T_dec, ctx)
+        output, postnet_output = MelHeadFn.apply(tok, x, self, B, T_dec, ctx)
+        return (output, postnet_output, p, e, log_d, d_targets, src_masks, mel_masks, src_lens,
+                mel_len, gmm, speaker_emb_s)
+
+    def speaker_gen(self, speaker_meta, seed=None):
+        """``model/fastspeech2.py:176-180``: one embedding drawn from the attribute prior."""
+        with torch.no_grad():
+            gmm = self.speaker_enc(speaker_meta)
+            return gmm.sample(seed=seed)
+
+    def speaker_distribution(self, speaker_meta):
+        with torch.no_grad():
+            return self.speaker_enc(speaker_meta)
+
+    def load_state_dict(self, state_dict, strict=True, assign=False):
+        r = super().load_state_dict(state_dict, strict=strict, assign=False)
+        if self._arena is not None:
+            self._arena.version += 1
+        return r
+
+
+def build(config_name="JVS-VCTK", device="cuda"):
+    """Model + configs from a bundled config (``configs/<name>``)."""
+    pp, mc, tc, path = cfg.load_configs(config_name)
+    return FastSpeech2(pp, mc, path, device=device), (pp, mc, tc)

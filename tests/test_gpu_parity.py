@@ -40,10 +40,26 @@ def seeded(module, prefix):
     return module
 
 
+# Gradients that are zero in exact arithmetic (fp32 noise only): the key-projection bias
+# (softmax is invariant to a per-query constant shift) and conv biases followed by
+# training-mode BatchNorm (the batch mean removes them).  They are checked against the
+# scale of their layer's weight gradient instead of their own (noise) scale.
+def _structural_zero(name):
+    return name.endswith("slf_attn.w_ks.bias") or ("postnet" in name or name.startswith("pn.")
+                                                     or "convolutions" in name) and name.endswith(".0.conv.bias")
+
+
 def check_grads(params, prefix, g, rtol=2e-4):
+    params = list(params)
+    by_name = dict(params)
     for name, p in params:
         key = f"{prefix}{name}"
         if f"{key}.gsum" not in g:
+            continue
+        if _structural_zero(name):
+            w = by_name[name.rsplit(".", 1)[0] + ".weight"]
+            ref = np.abs(M._g(w).detach().double().cpu().numpy()).max()
+            assert np.abs(M._g(p).detach().double().cpu().numpy()).max() <= 1e-3 * ref, key
             continue
         gg = M._g(p).detach().reshape(-1).double().cpu().numpy()
         s = g[f"{key}.gsum"]
@@ -137,11 +153,12 @@ def test_gmm_sampler_moments():
     c = torch.bincount(comp.long(), minlength=3).float() / 20000
     close(c, [0.2, 0.5, 0.3], 0.05, "component frequencies")
     x = out[:, 0].double()
-    close(x.mean(), 0.2 * -2 + 0.3 * 3, 0.05, "mixture mean")
+    n = x.numel()
+    assert abs(x.mean().item() - 0.5) < 4 * x.std().item() / n ** 0.5, "mixture mean"
     for k, (m, s) in enumerate([(-2, 0.5), (0, 1.0), (3, 0.25)]):
-        xs = out[comp == k].double()
-        close(xs.mean(), m, 0.02 + 0.05 * abs(m) / max(abs(m), 1), f"comp {k} mean")
-        close(xs.std(), s, 0.05, f"comp {k} std")
+        xs = out[comp == k].double().reshape(-1)
+        assert abs(xs.mean().item() - m) < 4 * s / xs.numel() ** 0.5, f"comp {k} mean"
+        assert abs(xs.std().item() - s) < 0.02 * s, f"comp {k} std"
 
 
 def _hip_trainer(B, Ts, seed=0):
@@ -196,5 +213,9 @@ def test_step_vs_oracle_full_tensors():
     ours = dict(model.named_parameters())
     for name, p in ref.named_parameters():
         if p.grad is None:
+            continue
+        if _structural_zero(name):
+            w = dict(ref.named_parameters())[name.rsplit(".", 1)[0] + ".weight"]
+            assert M._g(ours[name]).abs().max().item() <= 1e-3 * w.grad.abs().max().item(), name
             continue
         close(M._g(ours[name]), p.grad, 2e-4, name)

@@ -95,7 +95,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=48)
     ap.add_argument("--src-len", type=int, default=128)
-    ap.add_argument("--dtype", default="f32", choices=["f32"])
+    ap.add_argument("--dtype", default="bf16", choices=["f32", "bf16"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     args = ap.parse_args()
@@ -109,7 +109,8 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     pp, mc, tc, path = PKG.config.load_configs("JVS-VCTK")
-    model = M.FastSpeech2(pp, mc, path, device=dev)
+    cdt = {"f32": torch.float32, "bf16": torch.bfloat16}[args.dtype]
+    model = M.FastSpeech2(pp, mc, path, device=dev, compute_dtype=cdt)
     model.train()
     model.seed(1234 + rank)
     trainer = TR.Trainer(model, pp, mc, tc)

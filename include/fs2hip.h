@@ -35,7 +35,9 @@ enum {
   FS2_EPI_BIAS = 1,          /* y += bias[n]                                   */
   FS2_EPI_RELU = 2,          /* y = max(y, 0)                                  */
   FS2_EPI_ADD_AUX = 4,       /* y += aux[m, n]   (residual-gradient fusion)    */
-  FS2_EPI_RELU_MASK_AUX = 8  /* y *= (aux[m, n] > 0)   (ReLU backward fusion)  */
+  FS2_EPI_RELU_MASK_AUX = 8, /* y *= (aux[m, n] > 0)   (ReLU backward fusion)  */
+  FS2_EPI_OUT_BF16 = 16,     /* bf16 path: store y as bf16 (default fp32)       */
+  FS2_EPI_AUX_BF16 = 32      /* bf16 path: aux is bf16 (default fp32)           */
 };
 
 const char* fs2_last_error(void);
@@ -44,6 +46,8 @@ int fs2_abi_version(void);
 /* ---------------------------------------------------------------- convolution / linear
  * Conv1d over time as an implicit GEMM on (rows, c_in) activations:
  *   y[r, o] = sum_{j, c} wk[o, j*c_in + c] * x[r + j - pad, c]      (zero outside the utterance)
+ * dtype FS2_F32: x, wk fp32 (exact f32 MFMA); FS2_BF16: x, wk bf16 (bf16 MFMA, fp32
+ * accumulate), y fp32 or bf16 (FS2_EPI_OUT_BF16).
  * A Linear layer is taps=1, pad=0.  Forward uses wk = fs2_conv_weight_prep's w_fwd; the
  * data gradient is the same call on dy with w_bwd (flipped taps, transposed channels).
  * Replaces nn.Conv1d / nn.Linear forward and their input-gradient:
@@ -235,6 +239,8 @@ int fs2_adam_step(float* p, const float* g, float* m, float* v, int64_t n, const
                   float lr, float beta1, float beta2, float eps, float bias_corr1,
                   float bias_corr2_sqrt, void* stream);
 int fs2_fill(float* x, int64_t n, float value, void* stream);
+/* y = bf16(x), round to nearest even (compute copies for the bf16 path)              */
+int fs2_cast_bf16(const float* x, void* y, int64_t n, void* stream);
 int fs2_add_i64(int64_t* x, int64_t n, int64_t value, void* stream); /* BN num_batches_tracked */
 int fs2_scale(float* x, int64_t n, float value, void* stream);
 /* x[i] = src[0] * scale  (device scalar broadcast, no host sync)                     */

@@ -321,13 +321,15 @@ extern "C" {
 
 int fs2_attn_fwd(int dtype, const void* qkv, void* o, float* lse, const int64_t* lens,
                  int64_t batch, int64_t seq_len, int heads, int d_head, float scale, void* stream) {
+  FS2_CHECK_ARG(d_head == DH, "fs2_attn_fwd: only d_head = 128 is supported (got %d)", d_head);
+  FS2_CHECK_ARG(batch >= 0 && seq_len > 0 && heads > 0, "fs2_attn_fwd: bad shape");
+  if (batch == 0) return FS2_OK;
+  if (dtype == FS2_BF16)
+    return attn_fwd_bf16_launch(qkv, o, lse, lens, batch, seq_len, heads, scale, as_stream(stream));
   if (dtype != FS2_F32) {
     set_error("fs2_attn_fwd: dtype %d not built", dtype);
     return FS2_ERR_DTYPE;
   }
-  FS2_CHECK_ARG(d_head == DH, "fs2_attn_fwd: only d_head = 128 is supported (got %d)", d_head);
-  FS2_CHECK_ARG(batch >= 0 && seq_len > 0 && heads > 0, "fs2_attn_fwd: bad shape");
-  if (batch == 0) return FS2_OK;
   dim3 grid((unsigned)((seq_len + QB - 1) / QB), (unsigned)(batch * heads));
   attn_fwd_f32<<<grid, 256, 0, as_stream(stream)>>>((const float*)qkv, (float*)o, lse, lens,
                                                      (int)seq_len, heads, scale);
@@ -341,14 +343,17 @@ int64_t fs2_attn_bwd_ws_bytes(int64_t batch, int64_t seq_len, int heads) {
 int fs2_attn_bwd(int dtype, const void* qkv, const void* o, const void* d_o, const float* lse,
                  void* d_qkv, const int64_t* lens, int64_t batch, int64_t seq_len, int heads,
                  int d_head, float scale, float* ws, int64_t ws_bytes, void* stream) {
-  if (dtype != FS2_F32) {
-    set_error("fs2_attn_bwd: dtype %d not built", dtype);
-    return FS2_ERR_DTYPE;
-  }
   FS2_CHECK_ARG(d_head == DH, "fs2_attn_bwd: only d_head = 128 is supported (got %d)", d_head);
   FS2_CHECK_ARG(ws_bytes >= fs2_attn_bwd_ws_bytes(batch, seq_len, heads),
                 "fs2_attn_bwd: workspace too small");
   if (batch == 0) return FS2_OK;
+  if (dtype == FS2_BF16)
+    return attn_bwd_bf16_launch(qkv, o, d_o, lse, d_qkv, lens, batch, seq_len, heads, scale, ws,
+                                as_stream(stream));
+  if (dtype != FS2_F32) {
+    set_error("fs2_attn_bwd: dtype %d not built", dtype);
+    return FS2_ERR_DTYPE;
+  }
   hipStream_t st = as_stream(stream);
   const int64_t rows = batch * seq_len;
   const int64_t waves = rows * heads;

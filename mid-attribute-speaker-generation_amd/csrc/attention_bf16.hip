@@ -1,0 +1,361 @@
+// bf16 fused attention (d_head = 128) on v_mfma_f32_16x16x32_bf16, fp32 softmax/accumulate.
+//
+// Same decomposition as attention.hip (transposed scores: each lane owns one query column
+// in the forward / dQ kernels, one key column in the dK/dV kernel).  The second product of
+// each kernel contracts over keys (or queries), which sit in the *rows* of the LDS tiles:
+// its A operand is read with ds_read_b64_tr_b16 (4 consecutive rows of one column per lane),
+// and its B operand is the fp32 score accumulator packed to bf16 in place — the MFMA
+// C-layout gives lane (g, col) the rows {16s + 4g + r}, so the 8 k-slots of a 32-deep step
+// are taken as rows {32c + 4g + r} u {32c + 16 + 4g + r} on both operands.
+#include <math.h>
+
+#include "common.hpp"
+
+namespace fs2 {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef unsigned short u16;
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+namespace {
+constexpr int DH = 128;
+constexpr int QB = 64;
+constexpr int LDR = DH + 8;   // 272-B rows: conflict-free ds_read_b128 row fragments
+constexpr int LDT = DH + 16;  // 288-B rows: conflict-free ds_read_b64_tr_b16
+
+#define MFMA_BF16(a, b, c) __builtin_amdgcn_mfma_f32_16x16x32_bf16((a), (b), (c), 0, 0, 0)
+
+FS2_DEV float bf2f(u16 v) { return __uint_as_float(((uint32_t)v) << 16); }
+FS2_DEV u16 f2bf(float f) {
+  __bf16 b = (__bf16)f;
+  return *reinterpret_cast<u16*>(&b);
+}
+
+// 64 x 128 bf16 tile, rows r0.., row stride ld (elements) in global, LDS stride LDS_LD
+template <int LDS_LD>
+FS2_DEV void load_tile(u16* dst, const u16* base, int64_t ld, int r0, int nrows, int tid) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = tid + i * 256, row = c >> 4, col = (c & 15) * 8;
+    const int r = r0 + row;
+    uint4 v = r < nrows ? *reinterpret_cast<const uint4*>(base + (int64_t)r * ld + col)
+                        : make_uint4(0u, 0u, 0u, 0u);
+    *reinterpret_cast<uint4*>(&dst[row * LDS_LD + col]) = v;
+  }
+}
+
+// per-lane row fragment: d = 32c + 8g .. +7 for c < 4
+FS2_DEV void load_frag(bf16x8 (&f)[4], const u16* rowp, int g) {
+#pragma unroll
+  for (int c = 0; c < 4; ++c) f[c] = *reinterpret_cast<const bf16x8*>(rowp + 32 * c + 8 * g);
+}
+
+// S-type product over d = 128: rows (row0 + r16) of an LDS tile (stride LD) x lane fragment
+template <int LD>
+FS2_DEV f32x4 dot_tile(const u16* S, int row0, const bf16x8 (&f)[4], int g, int r16) {
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  const u16* p = S + (row0 + r16) * LD + 8 * g;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) acc = MFMA_BF16(*reinterpret_cast<const bf16x8*>(p + 32 * c), f[c], acc);
+  return acc;
+}
+
+// transposed fragment of 16 columns (col0..) over rows {rb + 4g + q} and {rb + 16 + 4g + q}
+template <int LD>
+FS2_DEV bf16x8 tr_frag(const u16* img, int rb, int col0, int g, int q, int p) {
+  const u16* p0 = img + (rb + 4 * g + q) * LD + col0 + 4 * p;
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0 + 16 * LD));
+  return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+FS2_DEV bf16x8 pack8(const f32x4& a, const f32x4& b) {
+  bf16x8 r;
+  r[0] = (__bf16)a.x; r[1] = (__bf16)a.y; r[2] = (__bf16)a.z; r[3] = (__bf16)a.w;
+  r[4] = (__bf16)b.x; r[5] = (__bf16)b.y; r[6] = (__bf16)b.z; r[7] = (__bf16)b.w;
+  return r;
+}
+
+// acc[ds] += sum over 32 rows (rb..rb+31) of T^T[d][row] * w[row]   (8 d-subtiles)
+template <int LD>
+FS2_DEV void accum_t(f32x4 (&acc)[8], const u16* S, int rb, const bf16x8& w, int g, int q, int p) {
+#pragma unroll
+  for (int ds = 0; ds < 8; ++ds) acc[ds] = MFMA_BF16(tr_frag<LD>(S, rb, 16 * ds, g, q, p), w, acc[ds]);
+}
+
+FS2_DEV void store4_bf16(u16* p, const f32x4& v) {
+  uint2 w;
+  w.x = (uint32_t)f2bf(v.x) | ((uint32_t)f2bf(v.y) << 16);
+  w.y = (uint32_t)f2bf(v.z) | ((uint32_t)f2bf(v.w) << 16);
+  *reinterpret_cast<uint2*>(p) = w;
+}
+}  // namespace
+
+__global__ __launch_bounds__(256) void attn_fwd_bf16(const u16* __restrict__ qkv, u16* __restrict__ o,
+                                                     float* __restrict__ lse,
+                                                     const int64_t* __restrict__ lens, int T, int H,
+                                                     float scale) {
+  __shared__ __attribute__((aligned(16))) u16 Ks[QB * LDR];
+  __shared__ __attribute__((aligned(16))) u16 Vs[QB * LDT];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, r16 = lane & 15;
+  const int q4 = r16 >> 2, p4 = r16 & 3;
+  const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
+  const int L = (int)min(lens[b], (int64_t)T);
+  const int64_t ld = 3LL * H * DH, ldo = (int64_t)H * DH;
+  const int q0 = blockIdx.x * QB;
+  const u16* base = qkv + (int64_t)b * T * ld;
+  u16* obase = o + (int64_t)b * T * ldo + h * DH;
+
+  if (q0 >= L) {
+    for (int e = tid; e < QB * DH / 8; e += 256) {
+      const int row = e / (DH / 8), col = (e % (DH / 8)) * 8, q = q0 + row;
+      if (q < T) *reinterpret_cast<uint4*>(obase + (int64_t)q * ldo + col) = make_uint4(0u, 0u, 0u, 0u);
+    }
+    if (tid < QB && q0 + tid < T) lse[(int64_t)bh * T + q0 + tid] = 0.f;
+    return;
+  }
+  const int q = q0 + wave * 16 + r16;
+  bf16x8 qf[4];
+  load_frag(qf, base + (int64_t)min(q, T - 1) * ld + h * DH, g);
+
+  float m_run = -INFINITY, l_run = 0.f;
+  f32x4 oacc[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) oacc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nkt = (L + QB - 1) / QB;
+  for (int kt = 0; kt < nkt; ++kt) {
+    __syncthreads();
+    load_tile<LDR>(Ks, base + (int64_t)H * DH + h * DH, ld, kt * QB, T, tid);
+    load_tile<LDT>(Vs, base + 2LL * H * DH + h * DH, ld, kt * QB, T, tid);
+    __syncthreads();
+    f32x4 s[4];
+    float mt = -INFINITY;
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+      s[st] = dot_tile<LDR>(Ks, 16 * st, qf, g, r16);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = kt * QB + 16 * st + 4 * g + r;
+        const float x = key < L ? s[st][r] * scale : -INFINITY;
+        s[st][r] = x;
+        mt = fmaxf(mt, x);
+      }
+    }
+    mt = group4_max(mt);
+    const float m_new = fmaxf(m_run, mt);
+    const float alpha = __expf(m_run - m_new);
+    float ps = 0.f;
+#pragma unroll
+    for (int st = 0; st < 4; ++st)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float pv = __expf(s[st][r] - m_new);
+        s[st][r] = pv;
+        ps += pv;
+      }
+    ps = group4_sum(ps);
+    l_run = l_run * alpha + ps;
+    m_run = m_new;
+#pragma unroll
+    for (int ds = 0; ds < 8; ++ds) oacc[ds] *= alpha;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) accum_t<LDT>(oacc, Vs, 32 * c, pack8(s[2 * c], s[2 * c + 1]), g, q4, p4);
+  }
+  if (q < T) {
+    const float inv = 1.f / l_run;
+#pragma unroll
+    for (int ds = 0; ds < 8; ++ds) store4_bf16(obase + (int64_t)q * ldo + 16 * ds + 4 * g, oacc[ds] * inv);
+    if (g == 0) lse[(int64_t)bh * T + q] = m_run + __logf(l_run);
+  }
+}
+
+__global__ void attn_bwd_delta_bf16(const u16* __restrict__ o, const u16* __restrict__ d_o,
+                                    float* __restrict__ delta, int64_t rows, int T, int H) {
+  const int64_t w = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (w >= rows * H) return;
+  const int64_t r = w / H;
+  const int h = (int)(w - r * H);
+  const u16* po = o + r * H * DH + h * DH + 2 * lane;
+  const u16* pd = d_o + r * H * DH + h * DH + 2 * lane;
+  float s = wave_sum(bf2f(po[0]) * bf2f(pd[0]) + bf2f(po[1]) * bf2f(pd[1]));
+  if (lane == 0) {
+    const int64_t b = r / T, q = r - b * T;
+    delta[(b * H + h) * T + q] = s;
+  }
+}
+
+__global__ __launch_bounds__(256) void attn_bwd_dq_bf16(const u16* __restrict__ qkv,
+                                                        const u16* __restrict__ d_o,
+                                                        const float* __restrict__ lse,
+                                                        const float* __restrict__ delta,
+                                                        u16* __restrict__ d_qkv,
+                                                        const int64_t* __restrict__ lens, int T,
+                                                        int H, float scale) {
+  __shared__ __attribute__((aligned(16))) u16 Ks[QB * LDR];
+  __shared__ __attribute__((aligned(16))) u16 Vs[QB * LDR];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, r16 = lane & 15;
+  const int q4 = r16 >> 2, p4 = r16 & 3;
+  const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
+  const int L = (int)min(lens[b], (int64_t)T);
+  const int64_t ld = 3LL * H * DH, ldo = (int64_t)H * DH;
+  const int q0 = blockIdx.x * QB;
+  const u16* base = qkv + (int64_t)b * T * ld;
+  u16* dbase = d_qkv + (int64_t)b * T * ld + h * DH;
+
+  if (q0 >= L) {
+    for (int e = tid; e < QB * DH / 8; e += 256) {
+      const int row = e / (DH / 8), col = (e % (DH / 8)) * 8, qq = q0 + row;
+      if (qq < T) *reinterpret_cast<uint4*>(dbase + (int64_t)qq * ld + col) = make_uint4(0u, 0u, 0u, 0u);
+    }
+    return;
+  }
+  const int q = q0 + wave * 16 + r16;
+  const int qc = min(q, T - 1);
+  bf16x8 qf[4], df[4];
+  load_frag(qf, base + (int64_t)qc * ld + h * DH, g);
+  load_frag(df, d_o + ((int64_t)b * T + qc) * ldo + h * DH, g);
+  const float my_lse = lse[(int64_t)bh * T + qc];
+  const float my_delta = delta[(int64_t)bh * T + qc];
+  const bool qvalid = q < L;
+
+  f32x4 dq[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) dq[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nkt = (L + QB - 1) / QB;
+  for (int kt = 0; kt < nkt; ++kt) {
+    __syncthreads();
+    load_tile<LDR>(Ks, base + (int64_t)H * DH + h * DH, ld, kt * QB, T, tid);
+    load_tile<LDR>(Vs, base + 2LL * H * DH + h * DH, ld, kt * QB, T, tid);
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      f32x4 dsv[2];
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        const int st = 2 * c + half;
+        const f32x4 s = dot_tile<LDR>(Ks, 16 * st, qf, g, r16);   // S^T[key][q]
+        const f32x4 dp = dot_tile<LDR>(Vs, 16 * st, df, g, r16);  // dP^T[key][q]
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = kt * QB + 16 * st + 4 * g + r;
+          const float pv = (key < L && qvalid) ? __expf(s[r] * scale - my_lse) : 0.f;
+          dsv[half][r] = pv * (dp[r] - my_delta);
+        }
+      }
+      accum_t<LDR>(dq, Ks, 32 * c, pack8(dsv[0], dsv[1]), g, q4, p4);  // dQ^T += K^T dS^T
+    }
+  }
+  if (q < T) {
+#pragma unroll
+    for (int ds = 0; ds < 8; ++ds) store4_bf16(dbase + (int64_t)q * ld + 16 * ds + 4 * g, dq[ds] * scale);
+  }
+}
+
+__global__ __launch_bounds__(256) void attn_bwd_dkdv_bf16(const u16* __restrict__ qkv,
+                                                          const u16* __restrict__ d_o,
+                                                          const float* __restrict__ lse,
+                                                          const float* __restrict__ delta,
+                                                          u16* __restrict__ d_qkv,
+                                                          const int64_t* __restrict__ lens, int T,
+                                                          int H, float scale) {
+  __shared__ __attribute__((aligned(16))) u16 Qs[QB * LDR];
+  __shared__ __attribute__((aligned(16))) u16 Ds[QB * LDR];
+  __shared__ float lse_s[QB], del_s[QB];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, r16 = lane & 15;
+  const int q4 = r16 >> 2, p4 = r16 & 3;
+  const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
+  const int L = (int)min(lens[b], (int64_t)T);
+  const int64_t ld = 3LL * H * DH, ldo = (int64_t)H * DH;
+  const int k0 = blockIdx.x * QB;
+  const u16* base = qkv + (int64_t)b * T * ld;
+  u16* dk_base = d_qkv + (int64_t)b * T * ld + (int64_t)H * DH + h * DH;
+  u16* dv_base = d_qkv + (int64_t)b * T * ld + 2LL * H * DH + h * DH;
+
+  if (k0 >= L) {
+    for (int e = tid; e < QB * DH / 8; e += 256) {
+      const int row = e / (DH / 8), col = (e % (DH / 8)) * 8, k = k0 + row;
+      if (k < T) {
+        *reinterpret_cast<uint4*>(dk_base + (int64_t)k * ld + col) = make_uint4(0u, 0u, 0u, 0u);
+        *reinterpret_cast<uint4*>(dv_base + (int64_t)k * ld + col) = make_uint4(0u, 0u, 0u, 0u);
+      }
+    }
+    return;
+  }
+  const int key = k0 + wave * 16 + r16;
+  const int kc = min(key, T - 1);
+  bf16x8 kf[4], vf[4];
+  load_frag(kf, base + (int64_t)kc * ld + (int64_t)H * DH + h * DH, g);
+  load_frag(vf, base + (int64_t)kc * ld + 2LL * H * DH + h * DH, g);
+  const bool kvalid = key < L;
+
+  f32x4 dk[8], dv[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) dk[i] = dv[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nqt = (L + QB - 1) / QB;
+  for (int qt = 0; qt < nqt; ++qt) {
+    __syncthreads();
+    load_tile<LDR>(Qs, base + h * DH, ld, qt * QB, T, tid);
+    load_tile<LDR>(Ds, d_o + (int64_t)b * T * ldo + h * DH, ldo, qt * QB, T, tid);
+    if (tid < QB) {
+      const int qq = qt * QB + tid;
+      lse_s[tid] = qq < T ? lse[(int64_t)bh * T + qq] : 0.f;
+      del_s[tid] = qq < T ? delta[(int64_t)bh * T + qq] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      f32x4 pp[2], dsv[2];
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        const int qs = 2 * c + half;
+        const f32x4 s = dot_tile<LDR>(Qs, 16 * qs, kf, g, r16);   // S[q][key]
+        const f32x4 dp = dot_tile<LDR>(Ds, 16 * qs, vf, g, r16);  // dP[q][key]
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int ql = 16 * qs + 4 * g + r, qq = qt * QB + ql;
+          const float pv = (qq < L && kvalid) ? __expf(s[r] * scale - lse_s[ql]) : 0.f;
+          pp[half][r] = pv;
+          dsv[half][r] = pv * (dp[r] - del_s[ql]);
+        }
+      }
+      accum_t<LDR>(dv, Ds, 32 * c, pack8(pp[0], pp[1]), g, q4, p4);    // dV^T += dO^T P
+      accum_t<LDR>(dk, Qs, 32 * c, pack8(dsv[0], dsv[1]), g, q4, p4);  // dK^T += Q^T dS
+    }
+  }
+  if (key < T) {
+#pragma unroll
+    for (int ds = 0; ds < 8; ++ds) {
+      store4_bf16(dk_base + (int64_t)key * ld + 16 * ds + 4 * g, dk[ds] * scale);
+      store4_bf16(dv_base + (int64_t)key * ld + 16 * ds + 4 * g, dv[ds]);
+    }
+  }
+}
+
+int attn_fwd_bf16_launch(const void* qkv, void* o, float* lse, const int64_t* lens, int64_t batch,
+                         int64_t seq_len, int heads, float scale, hipStream_t st) {
+  dim3 grid((unsigned)((seq_len + QB - 1) / QB), (unsigned)(batch * heads));
+  attn_fwd_bf16<<<grid, 256, 0, st>>>((const u16*)qkv, (u16*)o, lse, lens, (int)seq_len, heads, scale);
+  return launch_status("fs2_attn_fwd(bf16)");
+}
+
+int attn_bwd_bf16_launch(const void* qkv, const void* o, const void* d_o, const float* lse,
+                         void* d_qkv, const int64_t* lens, int64_t batch, int64_t seq_len,
+                         int heads, float scale, float* ws, hipStream_t st) {
+  const int64_t rows = batch * seq_len;
+  const int64_t waves = rows * heads;
+  attn_bwd_delta_bf16<<<(unsigned)((waves * 64 + 255) / 256), 256, 0, st>>>(
+      (const u16*)o, (const u16*)d_o, ws, rows, (int)seq_len, heads);
+  dim3 grid((unsigned)((seq_len + QB - 1) / QB), (unsigned)(batch * heads));
+  attn_bwd_dq_bf16<<<grid, 256, 0, st>>>((const u16*)qkv, (const u16*)d_o, lse, ws, (u16*)d_qkv,
+                                         lens, (int)seq_len, heads, scale);
+  attn_bwd_dkdv_bf16<<<grid, 256, 0, st>>>((const u16*)qkv, (const u16*)d_o, lse, ws, (u16*)d_qkv,
+                                           lens, (int)seq_len, heads, scale);
+  return launch_status("fs2_attn_bwd(bf16)");
+}
+
+}  // namespace fs2

@@ -36,6 +36,24 @@ int colsum_final_launch(const float* part, int64_t nparts, int64_t cols, float* 
 int colsum_launch(const float* x, int64_t ldx, int64_t rows, int64_t cols, float* out, int acc,
                   float* ws, hipStream_t st);
 
+// bf16 launchers (gemm_bf16.hip)
+int conv_gemm_bf16_launch(const void* x, int64_t ldx, const void* wk, void* y, int64_t ldy,
+                          int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out, int taps,
+                          int pad, const float* bias, int flags, const void* aux, int64_t ld_aux,
+                          hipStream_t st);
+int conv_wgrad_bf16_launch(const void* dy, int64_t ldy, const void* x, int64_t ldx, float* slab,
+                           int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out, int taps,
+                           int pad, int splits, hipStream_t st);
+int weight_prep_bf16_launch(const float* w, int64_t c_out, int64_t c_in, int taps, void* wf,
+                            void* wb, hipStream_t st);
+int attn_fwd_bf16_launch(const void* qkv, void* o, float* lse, const int64_t* lens, int64_t batch,
+                         int64_t seq_len, int heads, float scale, hipStream_t st);
+int attn_bwd_bf16_launch(const void* qkv, const void* o, const void* d_o, const float* lse,
+                         void* d_qkv, const int64_t* lens, int64_t batch, int64_t seq_len,
+                         int heads, float scale, float* ws, hipStream_t st);
+int colsum_bf16_launch(const void* x, int64_t ldx, int64_t rows, int64_t cols, float* out, int acc,
+                       float* ws, hipStream_t st);
+
 // ------------------------------------------------------------------ wave reductions
 FS2_DEV float wave_sum(float v) {
 #pragma unroll
@@ -103,6 +121,18 @@ FS2_DEV f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 FS2_DEV void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
 
 FS2_DEV int div_up(int a, int b) { return (a + b - 1) / b; }
+
+// bf16 compute copies (round to nearest even; gfx950 v_cvt_pk_bf16_f32)
+FS2_DEV unsigned short to_bf16(float f) {
+  __bf16 b = (__bf16)f;
+  return *reinterpret_cast<unsigned short*>(&b);
+}
+FS2_DEV void st4_bf16(void* p, f32x4 v) {
+  uint2 w;
+  w.x = (uint32_t)to_bf16(v.x) | ((uint32_t)to_bf16(v.y) << 16);
+  w.y = (uint32_t)to_bf16(v.z) | ((uint32_t)to_bf16(v.w) << 16);
+  *reinterpret_cast<uint2*>(p) = w;
+}
 
 }  // namespace fs2
 

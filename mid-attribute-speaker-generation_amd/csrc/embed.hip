@@ -14,7 +14,7 @@ namespace fs2 {
 
 __global__ void encoder_embed(const int64_t* texts, const int64_t* accents, const float* wtab,
                               const float* atab, const float* pos, int64_t rows, int64_t T, int d,
-                              float* out) {
+                              float* out, unsigned short* out_t) {
   const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   if (r >= rows) return;
@@ -23,6 +23,7 @@ __global__ void encoder_embed(const int64_t* texts, const int64_t* accents, cons
   for (int c = 4 * lane; c < d; c += 256) {
     f32x4 v = ld4(wtab + ti * d + c) + ld4(atab + ai * d + c) + ld4(pos + t * d + c);
     st4(out + r * d + c, v);
+    if (out_t) st4_bf16(out_t + r * d + c, v);
   }
 }
 
@@ -37,12 +38,16 @@ __global__ void embedding_bwd(const float* dout, const int64_t* ids, int64_t n, 
 }
 
 __global__ void rowvec_add(const float* x, const int64_t* ids, const float* tab, int64_t rows,
-                           int64_t T, int d, float* out) {
+                           int64_t T, int d, float* out, unsigned short* out_t) {
   const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   if (r >= rows) return;
   const int64_t id = ids[r / T];
-  for (int c = 4 * lane; c < d; c += 256) st4(out + r * d + c, ld4(x + r * d + c) + ld4(tab + id * d + c));
+  for (int c = 4 * lane; c < d; c += 256) {
+    const f32x4 v = ld4(x + r * d + c) + ld4(tab + id * d + c);
+    st4(out + r * d + c, v);
+    if (out_t) st4_bf16(out_t + r * d + c, v);
+  }
 }
 
 // dtab[ids[b]] += sum_t dout[b, t]   (one block per utterance, thread per channel)
@@ -69,13 +74,18 @@ FS2_DEV int lower_bound(const float* bins, int n, V v) {
 
 template <typename V>
 __global__ void bucket_embed(const float* x, const V* vals, const float* bins, int nb,
-                             const float* tab, int64_t rows, int d, float* out, int32_t* idx) {
+                             const float* tab, int64_t rows, int d, float* out, int32_t* idx,
+                             unsigned short* out_t) {
   const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   if (r >= rows) return;
   const int k = lower_bound<V>(bins, nb, vals[r]);
   if (lane == 0 && idx) idx[r] = k;
-  for (int c = 4 * lane; c < d; c += 256) st4(out + r * d + c, ld4(x + r * d + c) + ld4(tab + (int64_t)k * d + c));
+  for (int c = 4 * lane; c < d; c += 256) {
+    const f32x4 v = ld4(x + r * d + c) + ld4(tab + (int64_t)k * d + c);
+    st4(out + r * d + c, v);
+    if (out_t) st4_bf16(out_t + r * d + c, v);
+  }
 }
 
 template <typename V>
@@ -148,7 +158,7 @@ __global__ void lr_source(const int32_t* cum, int64_t B, int64_t Ts, int64_t Tou
 }
 
 __global__ void lr_expand(const float* x, const int32_t* cum, int64_t B, int64_t Ts, int64_t Tout,
-                          int d, const float* pos, float* out) {
+                          int d, const float* pos, float* out, unsigned short* out_t) {
   const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   if (r >= B * Tout) return;
@@ -158,6 +168,7 @@ __global__ void lr_expand(const float* x, const int32_t* cum, int64_t B, int64_t
     f32x4 v = i < Ts ? ld4(x + (b * Ts + i) * d + c) : f32x4{0.f, 0.f, 0.f, 0.f};
     if (pos) v += ld4(pos + t * d + c);
     st4(out + r * d + c, v);
+    if (out_t) st4_bf16(out_t + r * d + c, v);
   }
 }
 
@@ -204,12 +215,11 @@ int fs2_encoder_embed_fwd(const int64_t* texts, const int64_t* accents, const fl
                           const float* accent_emb, const float* posenc, int64_t batch,
                           int64_t seq_len, int d, float* out, void* out_t, void* stream) {
   FS2_CHECK_ARG(d % 4 == 0, "fs2_encoder_embed_fwd: d must be a multiple of 4");
-  (void)out_t;
   const int64_t rows = batch * seq_len;
   if (rows == 0) return FS2_OK;
   encoder_embed<<<rows_grid(rows), 256, 0, as_stream(stream)>>>(texts, accents, word_emb,
                                                                 accent_emb, posenc, rows, seq_len,
-                                                                d, out);
+                                                                d, out, (unsigned short*)out_t);
   return launch_status("fs2_encoder_embed_fwd");
 }
 
@@ -238,10 +248,10 @@ int fs2_embedding_bwd(const float* dout, const int64_t* ids, int64_t n, int d, i
 int fs2_rowvec_add_fwd(const float* x, const int64_t* ids, const float* table, int64_t batch,
                        int64_t seq_len, int d, float* out, void* out_t, void* stream) {
   FS2_CHECK_ARG(d % 4 == 0, "fs2_rowvec_add_fwd: d must be a multiple of 4");
-  (void)out_t;
   const int64_t rows = batch * seq_len;
   if (rows == 0) return FS2_OK;
-  rowvec_add<<<rows_grid(rows), 256, 0, as_stream(stream)>>>(x, ids, table, rows, seq_len, d, out);
+  rowvec_add<<<rows_grid(rows), 256, 0, as_stream(stream)>>>(x, ids, table, rows, seq_len, d, out,
+                                                             (unsigned short*)out_t);
   return launch_status("fs2_rowvec_add_fwd");
 }
 
@@ -256,15 +266,14 @@ int fs2_bucket_embed_fwd(const float* x, const void* values, int values_dtype, c
                          int n_bins, const float* table, int64_t rows, int d, float* out,
                          void* out_t, int32_t* idx, void* stream) {
   FS2_CHECK_ARG(d % 4 == 0, "fs2_bucket_embed_fwd: d must be a multiple of 4");
-  (void)out_t;
   if (rows == 0) return FS2_OK;
   hipStream_t st = as_stream(stream);
   if (values_dtype == FS2_F32)
     bucket_embed<float><<<rows_grid(rows), 256, 0, st>>>(x, (const float*)values, bins, n_bins,
-                                                         table, rows, d, out, idx);
+                                                         table, rows, d, out, idx, (unsigned short*)out_t);
   else if (values_dtype == 2)
     bucket_embed<double><<<rows_grid(rows), 256, 0, st>>>(x, (const double*)values, bins, n_bins,
-                                                          table, rows, d, out, idx);
+                                                          table, rows, d, out, idx, (unsigned short*)out_t);
   else {
     set_error("fs2_bucket_embed_fwd: values dtype %d", values_dtype);
     return FS2_ERR_DTYPE;
@@ -324,11 +333,10 @@ int fs2_lr_expand_fwd(const float* x, const int32_t* cum, int64_t batch, int64_t
                       int64_t out_len, int d, const float* posenc, float* out, void* out_t,
                       void* stream) {
   FS2_CHECK_ARG(d % 4 == 0, "fs2_lr_expand_fwd: d must be a multiple of 4");
-  (void)out_t;
   const int64_t rows = batch * out_len;
   if (rows == 0) return FS2_OK;
   lr_expand<<<rows_grid(rows), 256, 0, as_stream(stream)>>>(x, cum, batch, src_len, out_len, d,
-                                                            posenc, out);
+                                                            posenc, out, (unsigned short*)out_t);
   return launch_status("fs2_lr_expand_fwd");
 }
 

@@ -349,17 +349,21 @@ extern "C" {
 int fs2_conv_gemm(int dtype, const void* x, int64_t ldx, const void* wk, void* y, int64_t ldy,
                   int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out, int taps, int pad,
                   const float* bias, int flags, const void* aux, int64_t ld_aux, void* stream) {
-  if (dtype != FS2_F32) {
-    set_error("fs2_conv_gemm: dtype %d not built", dtype);
-    return FS2_ERR_DTYPE;
-  }
-  FS2_CHECK_ARG(c_in % 4 == 0 && ldx % 4 == 0, "fs2_conv_gemm: c_in/ldx must be multiples of 4");
   FS2_CHECK_ARG(rows >= 0 && seq_len > 0 && taps >= 1 && pad >= 0 && pad < taps,
                 "fs2_conv_gemm: bad geometry");
   FS2_CHECK_ARG(!(flags & FS2_EPI_BIAS) || bias, "fs2_conv_gemm: bias flag without bias");
   FS2_CHECK_ARG(!(flags & (FS2_EPI_ADD_AUX | FS2_EPI_RELU_MASK_AUX)) || aux,
                 "fs2_conv_gemm: aux flag without aux");
   if (rows == 0) return FS2_OK;
+  if (dtype == FS2_BF16)
+    return conv_gemm_bf16_launch(x, ldx, wk, y, ldy, rows, seq_len, c_in, c_out, taps, pad, bias,
+                                 flags, aux, ld_aux, as_stream(stream));
+  if (dtype != FS2_F32) {
+    set_error("fs2_conv_gemm: dtype %d not built", dtype);
+    return FS2_ERR_DTYPE;
+  }
+  FS2_CHECK_ARG(!(flags & (FS2_EPI_OUT_BF16 | FS2_EPI_AUX_BF16)), "fs2_conv_gemm: bf16 flags on the fp32 path");
+  FS2_CHECK_ARG(c_in % 4 == 0 && ldx % 4 == 0, "fs2_conv_gemm: c_in/ldx must be multiples of 4");
   ConvArgs a{(const float*)x, ldx, (const float*)wk, (float*)y, ldy, rows, seq_len, (int)c_in,
              (int)c_out, taps, pad, (int)(taps * c_in), bias, flags, (const float*)aux, ld_aux};
   hipStream_t st = as_stream(stream);
@@ -376,12 +380,13 @@ int fs2_conv_gemm(int dtype, const void* x, int64_t ldx, const void* wk, void* y
 
 int fs2_conv_weight_prep(int dtype, const float* w, int64_t c_out, int64_t c_in, int taps,
                          void* w_fwd, void* w_bwd, void* stream) {
+  const int64_t total = c_out * c_in * taps;
+  if (total == 0) return FS2_OK;
+  if (dtype == FS2_BF16) return weight_prep_bf16_launch(w, c_out, c_in, taps, w_fwd, w_bwd, as_stream(stream));
   if (dtype != FS2_F32) {
     set_error("fs2_conv_weight_prep: dtype %d not built", dtype);
     return FS2_ERR_DTYPE;
   }
-  const int64_t total = c_out * c_in * taps;
-  if (total == 0) return FS2_OK;
   unsigned blocks = (unsigned)((total + 255) / 256);
   if (blocks > 4096) blocks = 4096;
   weight_prep_f32<<<blocks, 256, 0, as_stream(stream)>>>(w, (int)c_out, (int)c_in, taps,
@@ -396,6 +401,20 @@ int64_t fs2_conv_wgrad_ws_bytes(int64_t rows, int64_t c_in, int64_t c_out, int t
 int fs2_conv_wgrad(int dtype, const void* dy, int64_t ldy, const void* x, int64_t ldx, float* dw,
                    int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out, int taps, int pad,
                    float* ws, int64_t ws_bytes, void* stream) {
+  if (dtype == FS2_BF16) {
+    FS2_CHECK_ARG(ws_bytes >= fs2_conv_wgrad_ws_bytes(rows, c_in, c_out, taps),
+                  "fs2_conv_wgrad: workspace too small");
+    if (rows == 0) return FS2_OK;
+    const int S = wgrad_splits(rows, c_in, c_out, taps);
+    int rc = conv_wgrad_bf16_launch(dy, ldy, x, ldx, ws, rows, seq_len, c_in, c_out, taps, pad, S,
+                                    as_stream(stream));
+    if (rc) return rc;
+    const int64_t total = c_out * c_in * taps;
+    unsigned blocks = (unsigned)((total + 255) / 256);
+    if (blocks > 4096) blocks = 4096;
+    wgrad_reduce<<<blocks, 256, 0, as_stream(stream)>>>(ws, S, (int)c_out, (int)c_in, taps, dw);
+    return launch_status("fs2_conv_wgrad");
+  }
   if (dtype != FS2_F32) {
     set_error("fs2_conv_wgrad: dtype %d not built", dtype);
     return FS2_ERR_DTYPE;
@@ -426,14 +445,16 @@ int64_t fs2_colsum_ws_bytes(int64_t rows, int64_t cols) {
 
 int fs2_colsum(int dtype, const void* x, int64_t ldx, int64_t rows, int64_t cols, float* out,
                int accumulate, float* ws, int64_t ws_bytes, void* stream) {
-  if (dtype != FS2_F32) {
-    set_error("fs2_colsum: dtype %d not built", dtype);
-    return FS2_ERR_DTYPE;
-  }
   FS2_CHECK_ARG(ws_bytes >= fs2_colsum_ws_bytes(rows, cols), "fs2_colsum: workspace too small");
   if (rows == 0) {
     if (!accumulate) (void)hipMemsetAsync(out, 0, cols * 4, as_stream(stream));
     return FS2_OK;
+  }
+  if (dtype == FS2_BF16)
+    return colsum_bf16_launch(x, ldx, rows, cols, out, accumulate, ws, as_stream(stream));
+  if (dtype != FS2_F32) {
+    set_error("fs2_colsum: dtype %d not built", dtype);
+    return FS2_ERR_DTYPE;
   }
   return colsum_launch((const float*)x, ldx, rows, cols, out, accumulate, ws, as_stream(stream));
 }

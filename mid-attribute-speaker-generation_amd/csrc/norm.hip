@@ -35,6 +35,7 @@ struct LnFwd {
   const float* dot_w;
   const float* dot_b;
   float* dot_out;
+  unsigned short* out_t;  // optional bf16 copy of out
 };
 
 FS2_DEV bool row_padded(const int64_t* lens, int64_t T, int64_t r) {
@@ -61,6 +62,7 @@ __global__ __launch_bounds__(256) void ln_fwd_f32(LnFwd a) {
   const bool pad = row_padded(a.lens, a.T, r);
   if (pad && !a.dot_out) u = f32x4{0.f, 0.f, 0.f, 0.f};  // dot mode masks only the head output
   st4(a.out + e0, u);
+  if (a.out_t) st4_bf16(a.out_t + e0, u);
   st4(a.xhat + e0, xh);
   if (lane == 0) a.rstd[r] = rs;
   if (a.dot_out) {
@@ -85,8 +87,9 @@ struct LnBwd {
   const float* relu_y;
   float* dy;
   float* dres;
-  float* part;  // [4][nblk][256]: dgamma, dbeta, dw_dot, (db_dot in slot 0 of row 3*?)
+  float* part;  // [3][nblk][256] dgamma, dbeta, dw_dot partials, then [nblk] db_dot partials
   int64_t nblk;
+  unsigned short* dy_t;  // optional bf16 copy of dy
 };
 
 __global__ __launch_bounds__(256) void ln_bwd_f32(LnBwd a) {
@@ -137,6 +140,7 @@ __global__ __launch_bounds__(256) void ln_bwd_f32(LnBwd a) {
       dy.w = yv.w > 0.f ? dy.w : 0.f;
     }
     st4(a.dy + e0, dy);
+    if (a.dy_t) st4_bf16(a.dy_t + e0, dy);
   }
   red[0][wave][lane] = pg;
   red[1][wave][lane] = pb;
@@ -199,7 +203,8 @@ __global__ void bn_var_final(const float* part, int64_t nparts, int64_t rows, in
 
 __global__ void bn_apply(const float* z, const float* mean, const float* rstd, const float* gamma,
                          const float* beta, int64_t rows, int64_t c, int act_tanh, float p,
-                         uint64_t seed, uint64_t site, const float* res, float* out) {
+                         uint64_t seed, uint64_t site, const float* res, float* out,
+                         unsigned short* out_t) {
   const int64_t n = rows * c;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n;
        e += (int64_t)gridDim.x * blockDim.x) {
@@ -209,6 +214,7 @@ __global__ void bn_apply(const float* z, const float* mean, const float* rstd, c
     if (p > 0.f) v *= dropout1(seed, site, (uint64_t)e, p);
     if (res) v += res[e];
     out[e] = v;
+    if (out_t) out_t[e] = to_bf16(v);
   }
 }
 
@@ -273,7 +279,7 @@ __global__ void bn_bwd_final(const float* part_g, const float* part_gx, int64_t 
 __global__ void bn_bwd_apply(const float* dout, const float* z, const float* mean, const float* rstd,
                              const float* gamma, const float* beta, const float* sums, int64_t rows,
                              int64_t c, int act_tanh, float p, uint64_t seed, uint64_t site,
-                             float* dz) {
+                             float* dz, unsigned short* dz_t) {
   const int64_t n = rows * c;
   const float inv_m = 1.f / (float)rows;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n;
@@ -282,7 +288,9 @@ __global__ void bn_bwd_apply(const float* dout, const float* z, const float* mea
     float xh;
     const float g = bn_g(dout, z, mean[col], rstd[col], gamma[col], beta[col], act_tanh, p, seed,
                          site, e, &xh);
-    dz[e] = gamma[col] * rstd[col] * (g - sums[col] * inv_m - xh * sums[c + col] * inv_m);
+    const float v = gamma[col] * rstd[col] * (g - sums[col] * inv_m - xh * sums[c + col] * inv_m);
+    dz[e] = v;
+    if (dz_t) dz_t[e] = to_bf16(v);
   }
 }
 
@@ -298,22 +306,27 @@ using namespace fs2;
 
 extern "C" {
 
+// dtype selects the storage of the optional compute copies (out_t / dy_t / dz_t):
+// FS2_F32 = none (the fp32 tensors are the GEMM operands), FS2_BF16 = bf16 copies.
+static int copy_dtype_ok(int dtype, const char* what) {
+  if (dtype == FS2_F32 || dtype == FS2_BF16) return FS2_OK;
+  set_error("%s: dtype %d not built", what, dtype);
+  return FS2_ERR_DTYPE;
+}
+
 int fs2_ln_fwd(int dtype, const float* y, const float* res, const float* gamma, const float* beta,
                float* out, void* out_t, float* xhat, float* rstd, const int64_t* lens,
                int64_t seq_len, int64_t rows, int d, float p_in, float p_out, uint64_t seed,
                uint64_t site_in, uint64_t site_out, const float* dot_w, const float* dot_b,
                float* dot_out, void* stream) {
-  if (dtype != FS2_F32) {
-    set_error("fs2_ln_fwd: dtype %d not built", dtype);
-    return FS2_ERR_DTYPE;
-  }
+  if (int rc = copy_dtype_ok(dtype, "fs2_ln_fwd")) return rc;
   FS2_CHECK_ARG(d == LN_D, "fs2_ln_fwd: only d = 256 is supported (got %d)", d);
   FS2_CHECK_ARG(!lens || seq_len > 0, "fs2_ln_fwd: lens given without seq_len");
   FS2_CHECK_ARG(!dot_out || (dot_w && dot_b), "fs2_ln_fwd: dot_out needs dot_w/dot_b");
-  (void)out_t;
   if (rows == 0) return FS2_OK;
   LnFwd a{y, res, gamma, beta, out, xhat, rstd, lens, seq_len, rows, p_in, p_out, seed,
-          site_in, site_out, dot_w, dot_b, dot_out};
+          site_in, site_out, dot_w, dot_b, dot_out,
+          dtype == FS2_BF16 ? (unsigned short*)out_t : nullptr};
   ln_fwd_f32<<<(unsigned)((rows + 3) / 4), 256, 0, as_stream(stream)>>>(a);
   return launch_status("fs2_ln_fwd");
 }
@@ -329,20 +342,17 @@ int fs2_ln_bwd(int dtype, const float* dout, const float* ddot, const float* dot
                uint64_t seed, uint64_t site_in, uint64_t site_out, const float* relu_y, float* dy,
                void* dy_t, float* dres, float* dgamma, float* dbeta, float* dw_dot, float* db_dot,
                float* ws, int64_t ws_bytes, void* stream) {
-  if (dtype != FS2_F32) {
-    set_error("fs2_ln_bwd: dtype %d not built", dtype);
-    return FS2_ERR_DTYPE;
-  }
+  if (int rc = copy_dtype_ok(dtype, "fs2_ln_bwd")) return rc;
   FS2_CHECK_ARG(d == LN_D, "fs2_ln_bwd: only d = 256 is supported (got %d)", d);
   FS2_CHECK_ARG((dout != nullptr) != (ddot != nullptr), "fs2_ln_bwd: give exactly one of dout/ddot");
   FS2_CHECK_ARG(!ddot || dot_w, "fs2_ln_bwd: ddot needs dot_w");
   FS2_CHECK_ARG(ws_bytes >= fs2_ln_bwd_ws_bytes(rows, d), "fs2_ln_bwd: workspace too small");
-  (void)dy_t;
   if (rows == 0) return FS2_OK;
   hipStream_t st = as_stream(stream);
   const int64_t nblk = (rows + LN_ROWS - 1) / LN_ROWS;
   LnBwd a{dout, ddot, dot_w, xhat, rstd, gamma, beta, lens, seq_len, rows, p_in, p_out, seed,
-          site_in, site_out, relu_y, dy, dres, ws, nblk};
+          site_in, site_out, relu_y, dy, dres, ws, nblk,
+          dtype == FS2_BF16 ? (unsigned short*)dy_t : nullptr};
   ln_bwd_f32<<<(unsigned)nblk, 256, 0, st>>>(a);
   int rc = launch_status("fs2_ln_bwd");
   if (rc) return rc;
@@ -365,13 +375,9 @@ int fs2_bn_fwd(int dtype, const float* z, int64_t rows, int64_t c, const float* 
                float* running_var, float* mean, float* rstd, int act_tanh, float p,
                uint64_t seed, uint64_t site, const float* res, float* out, void* out_t, float* ws,
                int64_t ws_bytes, void* stream) {
-  if (dtype != FS2_F32) {
-    set_error("fs2_bn_fwd: dtype %d not built", dtype);
-    return FS2_ERR_DTYPE;
-  }
+  if (int rc = copy_dtype_ok(dtype, "fs2_bn_fwd")) return rc;
   FS2_CHECK_ARG(rows > 0 && c > 0, "fs2_bn_fwd: empty input");
   FS2_CHECK_ARG(ws_bytes >= fs2_bn_ws_bytes(rows, c), "fs2_bn_fwd: workspace too small");
-  (void)out_t;
   hipStream_t st = as_stream(stream);
   const int64_t nparts = (rows + BN_ROWS - 1) / BN_ROWS;
   dim3 grid((unsigned)((c + 63) / 64), (unsigned)nparts);
@@ -382,7 +388,8 @@ int fs2_bn_fwd(int dtype, const float* z, int64_t rows, int64_t c, const float* 
   bn_var_final<<<cg, 256, 0, st>>>(ws, nparts, rows, c, eps, momentum, mean, running_mean,
                                    running_var, rstd);
   bn_apply<<<ew_grid(rows * c), 256, 0, st>>>(z, mean, rstd, gamma, beta, rows, c, act_tanh, p,
-                                              seed, site, res, out);
+                                              seed, site, res, out,
+                                              dtype == FS2_BF16 ? (unsigned short*)out_t : nullptr);
   return launch_status("fs2_bn_fwd");
 }
 
@@ -390,13 +397,9 @@ int fs2_bn_bwd(int dtype, const float* dout, const float* z, const float* mean, 
                const float* gamma, const float* beta, int64_t rows, int64_t c, int act_tanh,
                float p, uint64_t seed, uint64_t site, float* dz, void* dz_t, float* dgamma,
                float* dbeta, float* ws, int64_t ws_bytes, void* stream) {
-  if (dtype != FS2_F32) {
-    set_error("fs2_bn_bwd: dtype %d not built", dtype);
-    return FS2_ERR_DTYPE;
-  }
+  if (int rc = copy_dtype_ok(dtype, "fs2_bn_bwd")) return rc;
   FS2_CHECK_ARG(rows > 0 && c > 0, "fs2_bn_bwd: empty input");
   FS2_CHECK_ARG(ws_bytes >= fs2_bn_ws_bytes(rows, c), "fs2_bn_bwd: workspace too small");
-  (void)dz_t;
   hipStream_t st = as_stream(stream);
   const int64_t nparts = (rows + BN_ROWS - 1) / BN_ROWS;
   float* part_g = ws;
@@ -408,7 +411,8 @@ int fs2_bn_bwd(int dtype, const float* dout, const float* z, const float* mean, 
   bn_bwd_final<<<(unsigned)((c + 255) / 256), 256, 0, st>>>(part_g, part_gx, nparts, c, sums,
                                                              dgamma, dbeta);
   bn_bwd_apply<<<ew_grid(rows * c), 256, 0, st>>>(dout, z, mean, rstd, gamma, beta, sums, rows, c,
-                                                  act_tanh, p, seed, site, dz);
+                                                  act_tanh, p, seed, site, dz,
+                                                  dtype == FS2_BF16 ? (unsigned short*)dz_t : nullptr);
   return launch_status("fs2_bn_bwd");
 }
 

@@ -1,8 +1,12 @@
 """Tensor-level wrappers over the C-ABI (``include/fs2hip.h``).
 
 Each wrapper checks device/dtype/contiguity on the host, allocates outputs and workspaces
-from PyTorch's caching allocator, and launches on the current HIP stream.  They never fall
-back to PyTorch math: a wrong input raises, a missing library raises.
+from PyTorch's caching allocator, and launches on the current HIP stream.  The storage type
+of a GEMM/attention operand is taken from the tensor (float32 -> exact f32 MFMA path,
+bfloat16 -> bf16 MFMA path, fp32 accumulation either way).  Norm/embedding kernels always
+compute in fp32 and can emit a bf16 *compute copy* of their output (``copy=torch.bfloat16``)
+for the next GEMM.  There is no PyTorch-math fallback: a wrong input raises, a missing
+library raises.
 """
 import torch
 
@@ -11,7 +15,8 @@ from ._lib import lib
 F32 = 0
 BF16 = 1
 F64 = 2
-EPI_BIAS, EPI_RELU, EPI_ADD_AUX, EPI_RELU_MASK_AUX = 1, 2, 4, 8
+EPI_BIAS, EPI_RELU, EPI_ADD_AUX, EPI_RELU_MASK_AUX, EPI_OUT_BF16, EPI_AUX_BF16 = 1, 2, 4, 8, 16, 32
+_CODE = {torch.float32: F32, torch.bfloat16: BF16}
 
 
 def stream():
@@ -31,134 +36,167 @@ def _dev(*ts):
                 raise RuntimeError("fs2 kernels need contiguous tensors")
 
 
-def f32(t):
-    if t.dtype != torch.float32:
-        raise RuntimeError(f"expected float32, got {t.dtype}")
-    return t
+def code(dtype):
+    try:
+        return _CODE[dtype]
+    except KeyError:
+        raise RuntimeError(f"unsupported compute dtype {dtype}") from None
 
 
 def ws(nbytes, device):
     return torch.empty(max(int(nbytes) // 4, 1), dtype=torch.float32, device=device)
 
 
+def _copy(shape, copy, device):
+    return None if copy is None else torch.empty(shape, dtype=copy, device=device)
+
+
 # ------------------------------------------------------------------ GEMM / conv
 def conv_gemm(x, wk, rows, seq_len, c_in, c_out, taps, pad, bias=None, flags=0, aux=None,
-              out=None, ldx=None):
+              out=None, ldx=None, out_dtype=torch.float32):
+    """y = conv(x) (+bias, epilogue flags); x/wk fp32 or bf16 (same), y fp32 or bf16."""
     _dev(x, wk, bias, aux)
+    if x.dtype != wk.dtype:
+        raise RuntimeError(f"conv_gemm operand dtypes differ: {x.dtype} vs {wk.dtype}")
     if out is None:
-        out = torch.empty(rows, c_out, dtype=torch.float32, device=x.device)
+        out = torch.empty(rows, c_out, dtype=out_dtype, device=x.device)
     if bias is not None:
         flags |= EPI_BIAS
-    lib.fs2_conv_gemm(F32, ptr(x), ldx or c_in, ptr(wk), ptr(out), c_out, rows, seq_len, c_in,
-                      c_out, taps, pad, ptr(bias), flags, ptr(aux), c_out, stream())
+    if out.dtype == torch.bfloat16:
+        flags |= EPI_OUT_BF16
+    if aux is not None and aux.dtype == torch.bfloat16:
+        flags |= EPI_AUX_BF16
+    lib.fs2_conv_gemm(code(x.dtype), ptr(x), ldx or c_in, ptr(wk), ptr(out), c_out, rows, seq_len,
+                      c_in, c_out, taps, pad, ptr(bias), flags, ptr(aux), c_out, stream())
     return out
 
 
 def weight_prep(w, c_out, c_in, taps, w_fwd=None, w_bwd=None):
     _dev(w)
-    lib.fs2_conv_weight_prep(F32, ptr(w), c_out, c_in, taps, ptr(w_fwd), ptr(w_bwd), stream())
+    dt = (w_fwd if w_fwd is not None else w_bwd).dtype
+    lib.fs2_conv_weight_prep(code(dt), ptr(w), c_out, c_in, taps, ptr(w_fwd), ptr(w_bwd), stream())
 
 
 def conv_wgrad(dy, x, dw, rows, seq_len, c_in, c_out, taps, pad):
     _dev(dy, x, dw)
+    if dy.dtype != x.dtype:
+        raise RuntimeError(f"conv_wgrad operand dtypes differ: {dy.dtype} vs {x.dtype}")
     n = lib.fs2_conv_wgrad_ws_bytes(rows, c_in, c_out, taps)
     w = ws(n, dy.device)
-    lib.fs2_conv_wgrad(F32, ptr(dy), c_out, ptr(x), c_in, ptr(dw), rows, seq_len, c_in, c_out,
-                       taps, pad, ptr(w), n, stream())
+    lib.fs2_conv_wgrad(code(dy.dtype), ptr(dy), c_out, ptr(x), c_in, ptr(dw), rows, seq_len, c_in,
+                       c_out, taps, pad, ptr(w), n, stream())
 
 
 def colsum(x, rows, cols, out, accumulate=True):
     _dev(x, out)
     n = lib.fs2_colsum_ws_bytes(rows, cols)
     w = ws(n, x.device)
-    lib.fs2_colsum(F32, ptr(x), cols, rows, cols, ptr(out), int(accumulate), ptr(w), n, stream())
+    lib.fs2_colsum(code(x.dtype), ptr(x), cols, rows, cols, ptr(out), int(accumulate), ptr(w), n,
+                   stream())
+
+
+def cast_bf16(x):
+    _dev(x)
+    y = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
+    lib.fs2_cast_bf16(ptr(x), ptr(y), x.numel(), stream())
+    return y
 
 
 # ------------------------------------------------------------------ attention
 def attn_fwd(qkv, lens, batch, seq_len, heads, d_head, scale):
     _dev(qkv, lens)
-    o = torch.empty(batch * seq_len, heads * d_head, dtype=torch.float32, device=qkv.device)
+    o = torch.empty(batch * seq_len, heads * d_head, dtype=qkv.dtype, device=qkv.device)
     lse = torch.empty(batch * heads, seq_len, dtype=torch.float32, device=qkv.device)
-    lib.fs2_attn_fwd(F32, ptr(qkv), ptr(o), ptr(lse), ptr(lens), batch, seq_len, heads, d_head,
-                     scale, stream())
+    lib.fs2_attn_fwd(code(qkv.dtype), ptr(qkv), ptr(o), ptr(lse), ptr(lens), batch, seq_len, heads,
+                     d_head, scale, stream())
     return o, lse
 
 
 def attn_bwd(qkv, o, d_o, lse, lens, batch, seq_len, heads, d_head, scale):
     _dev(qkv, o, d_o, lse, lens)
+    if not (qkv.dtype == o.dtype == d_o.dtype):
+        raise RuntimeError("attn_bwd operands must share a dtype")
     dqkv = torch.empty_like(qkv)
     n = lib.fs2_attn_bwd_ws_bytes(batch, seq_len, heads)
     w = ws(n, qkv.device)
-    lib.fs2_attn_bwd(F32, ptr(qkv), ptr(o), ptr(d_o), ptr(lse), ptr(dqkv), ptr(lens), batch,
-                     seq_len, heads, d_head, scale, ptr(w), n, stream())
+    lib.fs2_attn_bwd(code(qkv.dtype), ptr(qkv), ptr(o), ptr(d_o), ptr(lse), ptr(dqkv), ptr(lens),
+                     batch, seq_len, heads, d_head, scale, ptr(w), n, stream())
     return dqkv
 
 
 # ------------------------------------------------------------------ LayerNorm
 def ln_fwd(y, gamma, beta, res=None, lens=None, seq_len=1, p_in=0.0, p_out=0.0, seed=0,
-           site_in=0, site_out=0, dot_w=None, dot_b=None):
+           site_in=0, site_out=0, dot_w=None, dot_b=None, copy=None):
+    """Returns (out fp32, out compute copy or None, xhat, rstd, dot)."""
     _dev(y, gamma, beta, res, lens, dot_w, dot_b)
     rows, d = y.shape
     out = torch.empty_like(y)
+    out_t = _copy(y.shape, copy, y.device)
     xhat = torch.empty_like(y)
     rstd = torch.empty(rows, dtype=torch.float32, device=y.device)
     dot = torch.empty(rows, dtype=torch.float32, device=y.device) if dot_w is not None else None
-    lib.fs2_ln_fwd(F32, ptr(y), ptr(res), ptr(gamma), ptr(beta), ptr(out), None, ptr(xhat),
-                   ptr(rstd), ptr(lens), seq_len, rows, d, p_in, p_out, seed, site_in, site_out,
-                   ptr(dot_w), ptr(dot_b), ptr(dot), stream())
-    return out, xhat, rstd, dot
+    lib.fs2_ln_fwd(BF16 if copy is not None else F32, ptr(y), ptr(res), ptr(gamma), ptr(beta),
+                   ptr(out), ptr(out_t), ptr(xhat), ptr(rstd), ptr(lens), seq_len, rows, d, p_in,
+                   p_out, seed, site_in, site_out, ptr(dot_w), ptr(dot_b), ptr(dot), stream())
+    return out, out_t, xhat, rstd, dot
 
 
 def ln_bwd(xhat, rstd, gamma, beta, dgamma, dbeta, dout=None, ddot=None, dot_w=None,
            dw_dot=None, db_dot=None, lens=None, seq_len=1, p_in=0.0, p_out=0.0, seed=0,
-           site_in=0, site_out=0, relu_y=None, dres=None):
+           site_in=0, site_out=0, relu_y=None, dres=None, copy=None):
+    """Returns (dy fp32, dy compute copy or None)."""
     _dev(xhat, rstd, gamma, beta, dout, ddot, dot_w, relu_y, dres, lens)
     rows, d = xhat.shape
     dy = torch.empty_like(xhat)
+    dy_t = _copy(xhat.shape, copy, xhat.device)
     n = lib.fs2_ln_bwd_ws_bytes(rows, d)
     w = ws(n, xhat.device)
-    lib.fs2_ln_bwd(F32, ptr(dout), ptr(ddot), ptr(dot_w), ptr(xhat), ptr(rstd), ptr(gamma),
-                   ptr(beta), ptr(lens), seq_len, rows, d, p_in, p_out, seed, site_in, site_out,
-                   ptr(relu_y), ptr(dy), None, ptr(dres), ptr(dgamma), ptr(dbeta), ptr(dw_dot),
-                   ptr(db_dot), ptr(w), n, stream())
-    return dy
+    lib.fs2_ln_bwd(BF16 if copy is not None else F32, ptr(dout), ptr(ddot), ptr(dot_w), ptr(xhat),
+                   ptr(rstd), ptr(gamma), ptr(beta), ptr(lens), seq_len, rows, d, p_in, p_out,
+                   seed, site_in, site_out, ptr(relu_y), ptr(dy), ptr(dy_t), ptr(dres),
+                   ptr(dgamma), ptr(dbeta), ptr(dw_dot), ptr(db_dot), ptr(w), n, stream())
+    return dy, dy_t
 
 
 # ------------------------------------------------------------------ BatchNorm
 def bn_fwd(z, gamma, beta, running_mean, running_var, act_tanh, p, seed, site, res=None,
-           eps=1e-5, momentum=0.1):
+           eps=1e-5, momentum=0.1, copy=None):
     _dev(z, gamma, beta, running_mean, running_var, res)
     rows, c = z.shape
     out = torch.empty_like(z)
+    out_t = _copy(z.shape, copy, z.device)
     mean = torch.empty(c, dtype=torch.float32, device=z.device)
     rstd = torch.empty(c, dtype=torch.float32, device=z.device)
     n = lib.fs2_bn_ws_bytes(rows, c)
     w = ws(n, z.device)
-    lib.fs2_bn_fwd(F32, ptr(z), rows, c, ptr(gamma), ptr(beta), eps, momentum, ptr(running_mean),
-                   ptr(running_var), ptr(mean), ptr(rstd), int(act_tanh), p, seed, site, ptr(res),
-                   ptr(out), None, ptr(w), n, stream())
-    return out, mean, rstd
+    lib.fs2_bn_fwd(BF16 if copy is not None else F32, ptr(z), rows, c, ptr(gamma), ptr(beta), eps,
+                   momentum, ptr(running_mean), ptr(running_var), ptr(mean), ptr(rstd),
+                   int(act_tanh), p, seed, site, ptr(res), ptr(out), ptr(out_t), ptr(w), n,
+                   stream())
+    return out, out_t, mean, rstd
 
 
-def bn_bwd(dout, z, mean, rstd, gamma, beta, dgamma, dbeta, act_tanh, p, seed, site):
+def bn_bwd(dout, z, mean, rstd, gamma, beta, dgamma, dbeta, act_tanh, p, seed, site, copy=None):
     _dev(dout, z, mean, rstd, gamma, beta, dgamma, dbeta)
     rows, c = z.shape
     dz = torch.empty_like(z)
+    dz_t = _copy(z.shape, copy, z.device)
     n = lib.fs2_bn_ws_bytes(rows, c)
     w = ws(n, z.device)
-    lib.fs2_bn_bwd(F32, ptr(dout), ptr(z), ptr(mean), ptr(rstd), ptr(gamma), ptr(beta), rows, c,
-                   int(act_tanh), p, seed, site, ptr(dz), None, ptr(dgamma), ptr(dbeta), ptr(w), n,
-                   stream())
-    return dz
+    lib.fs2_bn_bwd(BF16 if copy is not None else F32, ptr(dout), ptr(z), ptr(mean), ptr(rstd),
+                   ptr(gamma), ptr(beta), rows, c, int(act_tanh), p, seed, site, ptr(dz), ptr(dz_t),
+                   ptr(dgamma), ptr(dbeta), ptr(w), n, stream())
+    return dz, dz_t
 
 
 # ------------------------------------------------------------------ embeddings / adaptor
-def encoder_embed(texts, accents, word_emb, accent_emb, posenc, batch, seq_len, d):
+def encoder_embed(texts, accents, word_emb, accent_emb, posenc, batch, seq_len, d, copy=None):
     _dev(texts, accents, word_emb, accent_emb, posenc)
     out = torch.empty(batch * seq_len, d, dtype=torch.float32, device=word_emb.device)
+    out_t = _copy(out.shape, copy, out.device)
     lib.fs2_encoder_embed_fwd(ptr(texts), ptr(accents), ptr(word_emb), ptr(accent_emb), ptr(posenc),
-                              batch, seq_len, d, ptr(out), None, stream())
-    return out
+                              batch, seq_len, d, ptr(out), ptr(out_t), stream())
+    return out, out_t
 
 
 def embedding_fwd(ids, table):
@@ -182,12 +220,13 @@ def length_mask(lens, max_len):
     return m
 
 
-def rowvec_add(x, ids, table, batch, seq_len):
+def rowvec_add(x, ids, table, batch, seq_len, copy=None):
     _dev(x, ids, table)
     out = torch.empty_like(x)
+    out_t = _copy(x.shape, copy, x.device)
     lib.fs2_rowvec_add_fwd(ptr(x), ptr(ids), ptr(table), batch, seq_len, x.shape[1], ptr(out),
-                           None, stream())
-    return out
+                           ptr(out_t), stream())
+    return out, out_t
 
 
 def rowvec_add_bwd(dout, ids, dtable, batch, seq_len):
@@ -203,14 +242,15 @@ def _vals_dtype(v):
     raise RuntimeError(f"bucketize values must be float32/float64, got {v.dtype}")
 
 
-def bucket_embed(x, values, bins, table):
+def bucket_embed(x, values, bins, table, copy=None):
     _dev(x, values, bins, table)
     rows, d = x.shape
     out = torch.empty_like(x)
+    out_t = _copy(x.shape, copy, x.device)
     idx = torch.empty(rows, dtype=torch.int32, device=x.device)
     lib.fs2_bucket_embed_fwd(ptr(x), ptr(values), _vals_dtype(values), ptr(bins), bins.numel(),
-                             ptr(table), rows, d, ptr(out), None, ptr(idx), stream())
-    return out, idx
+                             ptr(table), rows, d, ptr(out), ptr(out_t), ptr(idx), stream())
+    return out, out_t, idx
 
 
 def bucket_embed_bwd(dout, idx, dtable):
@@ -249,13 +289,15 @@ def lr_source(cum, out_len):
     return src
 
 
-def lr_expand(x, cum, out_len, posenc=None):
+def lr_expand(x, cum, out_len, posenc=None, copy=None):
     _dev(x, cum, posenc)
     B, Ts = cum.shape
     d = x.shape[-1]
     out = torch.empty(B * out_len, d, dtype=torch.float32, device=x.device)
-    lib.fs2_lr_expand_fwd(ptr(x), ptr(cum), B, Ts, out_len, d, ptr(posenc), ptr(out), None, stream())
-    return out
+    out_t = _copy(out.shape, copy, x.device)
+    lib.fs2_lr_expand_fwd(ptr(x), ptr(cum), B, Ts, out_len, d, ptr(posenc), ptr(out), ptr(out_t),
+                          stream())
+    return out, out_t
 
 
 def lr_expand_bwd(dout, cum, out_len, d):
@@ -331,7 +373,7 @@ def gmm_sample(pi, mu, sigma, seed, offset=0):
     return out, comp
 
 
-# ------------------------------------------------------------------ optimiser
+# ------------------------------------------------------------------ optimiser / misc
 def grad_norm(g, max_norm, norm_coef):
     n = lib.fs2_grad_norm_ws_bytes(g.numel())
     w = ws(n, g.device)

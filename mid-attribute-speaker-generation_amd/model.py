@@ -105,18 +105,28 @@ def sinusoid_table(n_position, d_hid):
     return torch.from_numpy(tab.astype(np.float32))
 
 
+
+
 # ----------------------------------------------------------------------------- runtime state
 
 
 class StepCtx:
-    """Per-forward dropout state: one Philox seed per step, one site id per dropout call."""
+    """Per-forward state: compute dtype of the GEMM operands, one Philox seed per step (one
+    site id per dropout call, assigned at construction)."""
 
-    def __init__(self, seed, training, dropout):
+    def __init__(self, seed, training, dropout, cdt=torch.float32):
         self.seed = int(seed)
         self.drop = bool(training and dropout)
+        self.cdt = cdt
+        self.copy = None if cdt == torch.float32 else cdt  # bf16 compute copies wanted?
 
     def p(self, p):
         return float(p) if self.drop else 0.0
+
+
+def _t(f, t):
+    """Compute-dtype view of an activation: the bf16 copy if one was made, else the fp32."""
+    return f if t is None else t
 
 
 def _g(p):
@@ -124,22 +134,43 @@ def _g(p):
     return p._fs2_grad
 
 
-def _linear_prep(lin, c_out=None, c_in=None, w=None):
-    """fp32: forward uses the (out, in) weight as is; backward needs its transpose."""
-    w = lin.weight if w is None else w
+def _buf(holder, name, n, dtype, device):
+    t = getattr(holder, name, None)
+    if t is None or t.numel() != n or t.dtype != dtype:
+        t = torch.empty(n, dtype=dtype, device=device)
+        setattr(holder, name, t)
+    return t
+
+
+class _WeightHolder:
+    """Compute-layout weights of a fused projection that has no module of its own (QKV)."""
+
+    def __init__(self, d_in, d_out):
+        self.in_features, self.out_features = d_in, d_out
+
+
+def _linear_prep(lin, cdt, w=None, c_out=None, c_in=None):
+    """Compute-layout weights of a Linear: w_fwd (out, in) and its transpose w_bwd (in, out).
+    fp32 forward uses the master weight itself."""
+    w = lin.weight.detach() if w is None else w
     c_out = lin.out_features if c_out is None else c_out
     c_in = lin.in_features if c_in is None else c_in
-    if getattr(lin, "_w_bwd", None) is None or lin._w_bwd.numel() != c_out * c_in:
-        lin._w_bwd = torch.empty(c_in, c_out, dtype=torch.float32, device=w.device)
-    K.weight_prep(w, c_out, c_in, 1, None, lin._w_bwd)
+    wb = _buf(lin, "_w_bwd", c_in * c_out, cdt, w.device).view(c_in, c_out)
+    if cdt == torch.float32:
+        lin._w_fwd = w.reshape(c_out, c_in)
+        K.weight_prep(w, c_out, c_in, 1, None, wb)
+    else:
+        wf = _buf(lin, "_w_fwd_b", c_out * c_in, cdt, w.device).view(c_out, c_in)
+        lin._w_fwd = wf
+        K.weight_prep(w, c_out, c_in, 1, wf, wb)
+    lin._w_bwd = wb
 
 
-def _conv_prep(conv):
-    if getattr(conv, "_w_fwd", None) is None:
-        n = conv.c_out * conv.c_in * conv.k
-        conv._w_fwd = torch.empty(n, dtype=torch.float32, device=conv.weight.device)
-        conv._w_bwd = torch.empty(n, dtype=torch.float32, device=conv.weight.device)
-    K.weight_prep(conv.weight, conv.c_out, conv.c_in, conv.k, conv._w_fwd, conv._w_bwd)
+def _conv_prep(conv, cdt):
+    n = conv.c_out * conv.c_in * conv.k
+    wf = _buf(conv, "_w_fwd", n, cdt, conv.weight.device)
+    wb = _buf(conv, "_w_bwd", n, cdt, conv.weight.device)
+    K.weight_prep(conv.weight.detach(), conv.c_out, conv.c_in, conv.k, wf, wb)
 
 
 # ----------------------------------------------------------------------------- FFT block
@@ -169,8 +200,16 @@ class PositionwiseFeedForward(nn.Module):
         self.layer_norm = LayerNorm(d_in)
 
 
+def _flat_view(t, n):
+    """A 1-D view of ``n`` elements starting at ``t``'s first element (same storage)."""
+    return t.detach().as_strided((n,), (1,), t.storage_offset())
+
+
 class FFTBlock(nn.Module):
-    """``transformer/Layers.py:11-30``: post-LN MHA + Conv1d FFN, padded rows zeroed."""
+    """``transformer/Layers.py:11-30``: post-LN MHA + Conv1d FFN, padded rows zeroed.
+
+    fwd/bwd take and return activations as (fp32, compute copy) pairs; the fp32 tensor is
+    the residual stream, the copy (bf16 on the bf16 path) feeds the next GEMM."""
 
     def __init__(self, d_model, n_head, d_inner, kernel_size, dropout):
         super().__init__()
@@ -179,82 +218,84 @@ class FFTBlock(nn.Module):
         self.pos_ffn = PositionwiseFeedForward(d_model, d_inner, kernel_size, dropout)
         self.site = 0  # assigned by FastSpeech2
 
-    # fused views over the arena: [Wq; Wk; Wv] (3hd, d) and [bq; bk; bv]
-    def _qkv(self):
-        a = self.slf_attn
-        return self._qkv_w, self._qkv_b, self._qkv_gw, self._qkv_gb
-
-    def prep(self):
+    def prep(self, cdt):
         a, f = self.slf_attn, self.pos_ffn
         n3 = 3 * a.n_head * a.d_k
         wq, bq = a.w_qs.weight, a.w_qs.bias
-        self._qkv_w = _flat_view(wq, n3 * self.d).view(n3, self.d)
+        # fused [Wq; Wk; Wv] (3hd, d) and [bq; bk; bv]: adjacent in the arena (fft_param_order)
+        q = self.__dict__.get("_qkv_holder")
+        if q is None:
+            q = self._qkv_holder = _WeightHolder(self.d, n3)
         self._qkv_b = _flat_view(bq, n3)
         self._qkv_gw = _flat_view(_g(wq), n3 * self.d).view(n3, self.d)
         self._qkv_gb = _flat_view(_g(bq), n3)
-        if getattr(self, "_qkv_wb", None) is None:
-            self._qkv_wb = torch.empty(self.d, n3, dtype=torch.float32, device=wq.device)
-        K.weight_prep(self._qkv_w, n3, self.d, 1, None, self._qkv_wb)
-        _linear_prep(a.fc)
-        _conv_prep(f.w_1)
-        _conv_prep(f.w_2)
+        _linear_prep(q, cdt, w=_flat_view(wq, n3 * self.d).view(n3, self.d))
+        _linear_prep(a.fc, cdt)
+        _conv_prep(f.w_1, cdt)
+        _conv_prep(f.w_2, cdt)
 
-    def fwd(self, x, lens, B, T, ctx):
+    def fwd(self, x, x_t, lens, B, T, ctx):
         a, f = self.slf_attn, self.pos_ffn
         M, d = x.shape
-        n3 = 3 * a.n_head * a.d_k
+        q = self._qkv_holder
+        n3 = q.out_features
         p = ctx.p(a.p)
-        qkv = K.conv_gemm(x, self._qkv_w, M, T, d, n3, 1, 0, bias=self._qkv_b)
+        x_c = _t(x, x_t)
+        qkv = K.conv_gemm(x_c, q._w_fwd, M, T, d, n3, 1, 0, bias=self._qkv_b, out_dtype=ctx.cdt)
         o, lse = K.attn_fwd(qkv, lens, B, T, a.n_head, a.d_k, 1.0 / math.sqrt(a.d_k))
-        y1 = K.conv_gemm(o, a.fc.weight, M, T, a.n_head * a.d_k, d, 1, 0, bias=a.fc.bias)
-        x1, xh1, rs1, _ = K.ln_fwd(y1, a.layer_norm.weight, a.layer_norm.bias, res=x, lens=lens,
-                                   seq_len=T, p_in=p, seed=ctx.seed, site_in=self.site)
+        y1 = K.conv_gemm(o, a.fc._w_fwd, M, T, a.n_head * a.d_k, d, 1, 0, bias=a.fc.bias)
+        x1, x1_t, xh1, rs1, _ = K.ln_fwd(y1, a.layer_norm.weight, a.layer_norm.bias, res=x,
+                                         lens=lens, seq_len=T, p_in=p, seed=ctx.seed,
+                                         site_in=self.site, copy=ctx.copy)
         w1, w2 = f.w_1, f.w_2
-        h = K.conv_gemm(x1, w1._w_fwd, M, T, d, w1.c_out, w1.k, w1.padding, bias=w1.bias,
-                        flags=K.EPI_RELU)
+        x1_c = _t(x1, x1_t)
+        h = K.conv_gemm(x1_c, w1._w_fwd, M, T, d, w1.c_out, w1.k, w1.padding, bias=w1.bias,
+                        flags=K.EPI_RELU, out_dtype=ctx.cdt)
         y2 = K.conv_gemm(h, w2._w_fwd, M, T, w2.c_in, d, w2.k, w2.padding, bias=w2.bias)
-        x2, xh2, rs2, _ = K.ln_fwd(y2, f.layer_norm.weight, f.layer_norm.bias, res=x1, lens=lens,
-                                   seq_len=T, p_in=p, seed=ctx.seed, site_in=self.site + 1)
-        saved = (x, qkv, o, lse, x1, h, xh1, rs1, xh2, rs2, p, ctx.seed, lens, B, T)
-        return x2, saved
+        x2, x2_t, xh2, rs2, _ = K.ln_fwd(y2, f.layer_norm.weight, f.layer_norm.bias, res=x1,
+                                         lens=lens, seq_len=T, p_in=p, seed=ctx.seed,
+                                         site_in=self.site + 1, copy=ctx.copy)
+        saved = (x_c, qkv, o, lse, x1_c, h, xh1, rs1, xh2, rs2, p, ctx, lens, B, T)
+        return x2, x2_t, saved
 
     def bwd(self, dx2, saved):
         a, f = self.slf_attn, self.pos_ffn
-        x, qkv, o, lse, x1, h, xh1, rs1, xh2, rs2, p, seed, lens, B, T = saved
-        M, d = x.shape
-        n3 = 3 * a.n_head * a.d_k
+        x_c, qkv, o, lse, x1_c, h, xh1, rs1, xh2, rs2, p, ctx, lens, B, T = saved
+        M, d = x_c.shape
+        q = self._qkv_holder
+        n3 = q.out_features
+        seed, cdt = ctx.seed, ctx.cdt
         w1, w2 = f.w_1, f.w_2
         ln2, ln1 = f.layer_norm, a.layer_norm
-        # LN2 (masked, dropout before the residual add): dx1 starts as dz2
-        dx1 = K.zeros((M, d), x.device)
-        dy2 = K.ln_bwd(xh2, rs2, ln2.weight, ln2.bias, _g(ln2.weight), _g(ln2.bias), dout=dx2,
-                       lens=lens, seq_len=T, p_in=p, seed=seed, site_in=self.site + 1, dres=dx1)
+        # LN2 (masked; dropout before the residual add): dx1 starts as dz2
+        dx1 = K.zeros((M, d), x_c.device)
+        dy2, dy2_t = K.ln_bwd(xh2, rs2, ln2.weight, ln2.bias, _g(ln2.weight), _g(ln2.bias),
+                              dout=dx2, lens=lens, seq_len=T, p_in=p, seed=seed,
+                              site_in=self.site + 1, dres=dx1, copy=ctx.copy)
+        dy2_c = _t(dy2, dy2_t)
         K.colsum(dy2, M, d, _g(w2.bias))
-        K.conv_wgrad(dy2, h, _g(w2.weight), M, T, w2.c_in, d, w2.k, w2.padding)
-        dh = K.conv_gemm(dy2, w2._w_bwd, M, T, d, w2.c_in, w2.k, w2.padding,
-                         flags=K.EPI_RELU_MASK_AUX, aux=h)
+        K.conv_wgrad(dy2_c, h, _g(w2.weight), M, T, w2.c_in, d, w2.k, w2.padding)
+        dh = K.conv_gemm(dy2_c, w2._w_bwd, M, T, d, w2.c_in, w2.k, w2.padding,
+                         flags=K.EPI_RELU_MASK_AUX, aux=h, out_dtype=cdt)
         K.colsum(dh, M, w1.c_out, _g(w1.bias))
-        K.conv_wgrad(dh, x1, _g(w1.weight), M, T, d, w1.c_out, w1.k, w1.padding)
+        K.conv_wgrad(dh, x1_c, _g(w1.weight), M, T, d, w1.c_out, w1.k, w1.padding)
         K.conv_gemm(dh, w1._w_bwd, M, T, w1.c_out, d, w1.k, w1.padding, flags=K.EPI_ADD_AUX,
                     aux=dx1, out=dx1)
         # LN1 -> fc -> attention -> QKV
-        dx = K.zeros((M, d), x.device)
-        dy1 = K.ln_bwd(xh1, rs1, ln1.weight, ln1.bias, _g(ln1.weight), _g(ln1.bias), dout=dx1,
-                       lens=lens, seq_len=T, p_in=p, seed=seed, site_in=self.site, dres=dx)
+        dx = K.zeros((M, d), x_c.device)
+        dy1, dy1_t = K.ln_bwd(xh1, rs1, ln1.weight, ln1.bias, _g(ln1.weight), _g(ln1.bias),
+                              dout=dx1, lens=lens, seq_len=T, p_in=p, seed=seed,
+                              site_in=self.site, dres=dx, copy=ctx.copy)
+        dy1_c = _t(dy1, dy1_t)
         hd = a.n_head * a.d_k
         K.colsum(dy1, M, d, _g(a.fc.bias))
-        K.conv_wgrad(dy1, o, _g(a.fc.weight), M, T, hd, d, 1, 0)
-        do = K.conv_gemm(dy1, a.fc._w_bwd, M, T, d, hd, 1, 0)
+        K.conv_wgrad(dy1_c, o, _g(a.fc.weight), M, T, hd, d, 1, 0)
+        do = K.conv_gemm(dy1_c, a.fc._w_bwd, M, T, d, hd, 1, 0, out_dtype=cdt)
         dqkv = K.attn_bwd(qkv, o, do, lse, lens, B, T, a.n_head, a.d_k, 1.0 / math.sqrt(a.d_k))
         K.colsum(dqkv, M, n3, self._qkv_gb)
-        K.conv_wgrad(dqkv, x, self._qkv_gw, M, T, d, n3, 1, 0)
-        K.conv_gemm(dqkv, self._qkv_wb, M, T, n3, d, 1, 0, flags=K.EPI_ADD_AUX, aux=dx, out=dx)
+        K.conv_wgrad(dqkv, x_c, self._qkv_gw, M, T, d, n3, 1, 0)
+        K.conv_gemm(dqkv, q._w_bwd, M, T, n3, d, 1, 0, flags=K.EPI_ADD_AUX, aux=dx, out=dx)
         return dx
-
-
-def _flat_view(t, n):
-    """A 1-D view of ``n`` elements starting at ``t``'s first element (same storage)."""
-    return t.detach().as_strided((n,), (1,), t.storage_offset())
 
 
 def _ffn_stack(config, side):
@@ -312,46 +353,54 @@ class VariancePredictor(nn.Module):
         self.linear_layer = Linear(fs, 1)
         self.site = 0
 
-    def prep(self):
-        _conv_prep(self.conv_layer.conv1d_1.conv)
-        _conv_prep(self.conv_layer.conv1d_2.conv)
+    def prep(self, cdt):
+        _conv_prep(self.conv_layer.conv1d_1.conv, cdt)
+        _conv_prep(self.conv_layer.conv1d_2.conv, cdt)
 
-    def fwd(self, x, lens, B, T, ctx):
+    def fwd(self, x, x_t, lens, B, T, ctx):
         c = self.conv_layer
         c1, c2 = c.conv1d_1.conv, c.conv1d_2.conv
         M = x.shape[0]
         p = ctx.p(self.p)
-        h1 = K.conv_gemm(x, c1._w_fwd, M, T, c1.c_in, c1.c_out, c1.k, c1.padding, bias=c1.bias,
+        x_c = _t(x, x_t)
+        h1 = K.conv_gemm(x_c, c1._w_fwd, M, T, c1.c_in, c1.c_out, c1.k, c1.padding, bias=c1.bias,
                          flags=K.EPI_RELU)
-        u1, xh1, rs1, _ = K.ln_fwd(h1, c.layer_norm_1.weight, c.layer_norm_1.bias, p_out=p,
-                                   seed=ctx.seed, site_out=self.site)
-        h2 = K.conv_gemm(u1, c2._w_fwd, M, T, c2.c_in, c2.c_out, c2.k, c2.padding, bias=c2.bias,
+        u1, u1_t, xh1, rs1, _ = K.ln_fwd(h1, c.layer_norm_1.weight, c.layer_norm_1.bias, p_out=p,
+                                         seed=ctx.seed, site_out=self.site, copy=ctx.copy)
+        u1_c = _t(u1, u1_t)
+        h2 = K.conv_gemm(u1_c, c2._w_fwd, M, T, c2.c_in, c2.c_out, c2.k, c2.padding, bias=c2.bias,
                          flags=K.EPI_RELU)
-        _, xh2, rs2, pred = K.ln_fwd(h2, c.layer_norm_2.weight, c.layer_norm_2.bias, lens=lens,
-                                     seq_len=T, p_out=p, seed=ctx.seed, site_out=self.site + 1,
-                                     dot_w=self.linear_layer.weight, dot_b=self.linear_layer.bias)
-        saved = (x, h1, u1, h2, xh1, rs1, xh2, rs2, p, ctx.seed, lens, T)
+        _, _, xh2, rs2, pred = K.ln_fwd(h2, c.layer_norm_2.weight, c.layer_norm_2.bias, lens=lens,
+                                        seq_len=T, p_out=p, seed=ctx.seed, site_out=self.site + 1,
+                                        dot_w=self.linear_layer.weight,
+                                        dot_b=self.linear_layer.bias)
+        saved = (x_c, h1, u1_c, h2, xh1, rs1, xh2, rs2, p, ctx, lens, T)
         return pred.view(B, T), saved
 
     def bwd(self, dpred, saved, dx_acc):
-        """Backward; the input gradient is *added* into ``dx_acc`` (in place)."""
-        x, h1, u1, h2, xh1, rs1, xh2, rs2, p, seed, lens, T = saved
+        """Backward; the input gradient is *added* into ``dx_acc`` (fp32, in place)."""
+        x_c, h1, u1_c, h2, xh1, rs1, xh2, rs2, p, ctx, lens, T = saved
         c = self.conv_layer
         c1, c2 = c.conv1d_1.conv, c.conv1d_2.conv
         ln1, ln2, lin = c.layer_norm_1, c.layer_norm_2, self.linear_layer
-        M = x.shape[0]
-        dh2 = K.ln_bwd(xh2, rs2, ln2.weight, ln2.bias, _g(ln2.weight), _g(ln2.bias),
-                       ddot=dpred.contiguous().view(-1), dot_w=lin.weight, dw_dot=_g(lin.weight),
-                       db_dot=_g(lin.bias), lens=lens, seq_len=T, p_out=p, seed=seed,
-                       site_out=self.site + 1, relu_y=h2)
+        M = x_c.shape[0]
+        seed = ctx.seed
+        dh2, dh2_t = K.ln_bwd(xh2, rs2, ln2.weight, ln2.bias, _g(ln2.weight), _g(ln2.bias),
+                              ddot=dpred.contiguous().view(-1), dot_w=lin.weight,
+                              dw_dot=_g(lin.weight), db_dot=_g(lin.bias), lens=lens, seq_len=T,
+                              p_out=p, seed=seed, site_out=self.site + 1, relu_y=h2,
+                              copy=ctx.copy)
+        dh2_c = _t(dh2, dh2_t)
         K.colsum(dh2, M, c2.c_out, _g(c2.bias))
-        K.conv_wgrad(dh2, u1, _g(c2.weight), M, T, c2.c_in, c2.c_out, c2.k, c2.padding)
-        du1 = K.conv_gemm(dh2, c2._w_bwd, M, T, c2.c_out, c2.c_in, c2.k, c2.padding)
-        dh1 = K.ln_bwd(xh1, rs1, ln1.weight, ln1.bias, _g(ln1.weight), _g(ln1.bias), dout=du1,
-                       p_out=p, seed=seed, site_out=self.site, relu_y=h1)
+        K.conv_wgrad(dh2_c, u1_c, _g(c2.weight), M, T, c2.c_in, c2.c_out, c2.k, c2.padding)
+        du1 = K.conv_gemm(dh2_c, c2._w_bwd, M, T, c2.c_out, c2.c_in, c2.k, c2.padding)
+        dh1, dh1_t = K.ln_bwd(xh1, rs1, ln1.weight, ln1.bias, _g(ln1.weight), _g(ln1.bias),
+                              dout=du1, p_out=p, seed=seed, site_out=self.site, relu_y=h1,
+                              copy=ctx.copy)
+        dh1_c = _t(dh1, dh1_t)
         K.colsum(dh1, M, c1.c_out, _g(c1.bias))
-        K.conv_wgrad(dh1, x, _g(c1.weight), M, T, c1.c_in, c1.c_out, c1.k, c1.padding)
-        K.conv_gemm(dh1, c1._w_bwd, M, T, c1.c_out, c1.c_in, c1.k, c1.padding,
+        K.conv_wgrad(dh1_c, x_c, _g(c1.weight), M, T, c1.c_in, c1.c_out, c1.k, c1.padding)
+        K.conv_gemm(dh1_c, c1._w_bwd, M, T, c1.c_out, c1.c_in, c1.k, c1.padding,
                     flags=K.EPI_ADD_AUX, aux=dx_acc, out=dx_acc)
 
 
@@ -392,47 +441,55 @@ class PostNet(nn.Module):
                           BatchNorm1d(chans[i + 1])) for i in range(n))
         self.site = 0
 
-    def prep(self):
+    def prep(self, cdt):
         for layer in self.convolutions:
-            _conv_prep(layer[0].conv)
+            _conv_prep(layer[0].conv, cdt)
 
-    def fwd(self, x, B, T, ctx):
+    def fwd(self, x, x_t, B, T, ctx):
         """x: (M, n_mel) mel_linear output; returns postnet(x) + x."""
+        if not self.training:
+            raise NotImplementedError("eval-mode PostNet (running-stat BatchNorm) is part of the "
+                                      "inference path, SURVEY.md §8f row f1")
         M = x.shape[0]
-        a = x
+        a_c = _t(x, x_t)
         saved = []
         n = len(self.convolutions)
         p = ctx.p(0.5)
+        out = None
         for i, layer in enumerate(self.convolutions):
             conv, bn = layer[0].conv, layer[1]
-            z = K.conv_gemm(a, conv._w_fwd, M, T, conv.c_in, conv.c_out, conv.k, conv.padding,
+            z = K.conv_gemm(a_c, conv._w_fwd, M, T, conv.c_in, conv.c_out, conv.k, conv.padding,
                             bias=conv.bias)
             rm, rv = (bn.running_mean, bn.running_var) if self.training else (None, None)
-            out, mean, rstd = K.bn_fwd(z, bn.weight, bn.bias, rm, rv, i < n - 1, p, ctx.seed,
-                                       self.site + i, res=x if i == n - 1 else None)
+            last = i == n - 1
+            out, out_t, mean, rstd = K.bn_fwd(z, bn.weight, bn.bias, rm, rv, not last, p, ctx.seed,
+                                              self.site + i, res=x if last else None,
+                                              copy=None if last else ctx.copy)
             if self.training:
                 K.add_i64_(bn.num_batches_tracked, 1)
-            saved.append((a, z, mean, rstd))
-            a = out
-        return a, (saved, p, ctx.seed, T)
+            saved.append((a_c, z, mean, rstd))
+            a_c = _t(out, out_t)
+        return out, (saved, p, ctx, T)
 
     def bwd(self, dout, saved, dx_acc):
         """dout: grad of postnet(x) + x; adds the postnet input grad into ``dx_acc``."""
-        layers, p, seed, T = saved
+        layers, p, ctx, T = saved
         n = len(self.convolutions)
         d = dout
         for i in range(n - 1, -1, -1):
             conv, bn = self.convolutions[i][0].conv, self.convolutions[i][1]
-            a, z, mean, rstd = layers[i]
+            a_c, z, mean, rstd = layers[i]
             M = z.shape[0]
-            dz = K.bn_bwd(d, z, mean, rstd, bn.weight, bn.bias, _g(bn.weight), _g(bn.bias),
-                          i < n - 1, p, seed, self.site + i)
+            dz, dz_t = K.bn_bwd(d, z, mean, rstd, bn.weight, bn.bias, _g(bn.weight), _g(bn.bias),
+                                i < n - 1, p, ctx.seed, self.site + i, copy=ctx.copy)
+            dz_c = _t(dz, dz_t)
             K.colsum(dz, M, conv.c_out, _g(conv.bias))
-            K.conv_wgrad(dz, a, _g(conv.weight), M, T, conv.c_in, conv.c_out, conv.k, conv.padding)
+            K.conv_wgrad(dz_c, a_c, _g(conv.weight), M, T, conv.c_in, conv.c_out, conv.k,
+                         conv.padding)
             if i > 0:
-                d = K.conv_gemm(dz, conv._w_bwd, M, T, conv.c_out, conv.c_in, conv.k, conv.padding)
+                d = K.conv_gemm(dz_c, conv._w_bwd, M, T, conv.c_out, conv.c_in, conv.k, conv.padding)
             else:
-                K.conv_gemm(dz, conv._w_bwd, M, T, conv.c_out, conv.c_in, conv.k, conv.padding,
+                K.conv_gemm(dz_c, conv._w_bwd, M, T, conv.c_out, conv.c_in, conv.k, conv.padding,
                             flags=K.EPI_ADD_AUX, aux=dx_acc, out=dx_acc)
 
 
@@ -558,17 +615,21 @@ def _flat_order(m):
     return out
 
 
+
+
 # ----------------------------------------------------------------------------- autograd
+# Block-granular autograd nodes.  Differentiable tensors crossing them are the fp32
+# activations; the compute copies (bf16 path) travel as non-differentiable side outputs.
 
 
 class EncoderFn(torch.autograd.Function):
     @staticmethod
     def forward(fctx, token, enc, texts, accents, lens, B, T, ctx):
-        x = K.encoder_embed(texts, accents, enc.src_word_emb.weight, enc.src_accent_emb.weight,
-                            enc.position_enc, B, T, enc.d)
+        x, x_t = K.encoder_embed(texts, accents, enc.src_word_emb.weight, enc.src_accent_emb.weight,
+                                 enc.position_enc, B, T, enc.d, copy=ctx.copy)
         saved = []
         for layer in enc.layer_stack:
-            x, s = layer.fwd(x, lens, B, T, ctx)
+            x, x_t, s = layer.fwd(x, x_t, lens, B, T, ctx)
             saved.append(s)
         fctx.enc, fctx.saved, fctx.ids = enc, saved, (texts, accents)
         return x
@@ -592,21 +653,23 @@ class VarianceAdaptorFn(torch.autograd.Function):
     @staticmethod
     def forward(fctx, token, enc_out, m, speakers, src_lens, p_t, e_t, d_t, B, Ts, T_dec, ctx):
         va = m.variance_adaptor
-        x0 = K.rowvec_add(enc_out, speakers, m.speaker_emb.weight, B, Ts)
-        log_d, s_d = va.duration_predictor.fwd(x0, src_lens, B, Ts, ctx)
-        p, s_p = va.pitch_predictor.fwd(x0, src_lens, B, Ts, ctx)
-        x1, idx_p = K.bucket_embed(x0, p_t.contiguous().view(-1), va.pitch_bins, va.pitch_embedding.weight)
-        e, s_e = va.energy_predictor.fwd(x1, src_lens, B, Ts, ctx)
-        x2, idx_e = K.bucket_embed(x1, e_t.contiguous().view(-1), va.energy_bins,
-                                   va.energy_embedding.weight)
+        x0, x0_t = K.rowvec_add(enc_out, speakers, m.speaker_emb.weight, B, Ts, copy=ctx.copy)
+        log_d, s_d = va.duration_predictor.fwd(x0, x0_t, src_lens, B, Ts, ctx)
+        p, s_p = va.pitch_predictor.fwd(x0, x0_t, src_lens, B, Ts, ctx)
+        x1, x1_t, idx_p = K.bucket_embed(x0, p_t.contiguous().view(-1), va.pitch_bins,
+                                         va.pitch_embedding.weight, copy=ctx.copy)
+        e, s_e = va.energy_predictor.fwd(x1, x1_t, src_lens, B, Ts, ctx)
+        x2, _, idx_e = K.bucket_embed(x1, e_t.contiguous().view(-1), va.energy_bins,
+                                      va.energy_embedding.weight)
         cum, mel_len = K.lr_index(d_t.contiguous())
-        x_lr = K.lr_expand(x2, cum, T_dec, posenc=m.decoder.position_enc)
+        x_lr, x_lr_t = K.lr_expand(x2, cum, T_dec, posenc=m.decoder.position_enc, copy=ctx.copy)
         fctx.m, fctx.saved = m, (s_d, s_p, s_e, idx_p, idx_e, cum, speakers, B, Ts, T_dec)
-        fctx.mark_non_differentiable(mel_len)
-        return x_lr, log_d, p, e, mel_len
+        side = x_lr_t if x_lr_t is not None else torch.empty(0, device=x_lr.device)
+        fctx.mark_non_differentiable(mel_len, side)
+        return x_lr, log_d, p, e, mel_len, side
 
     @staticmethod
-    def backward(fctx, d_xlr, d_logd, d_p, d_e, _):
+    def backward(fctx, d_xlr, d_logd, d_p, d_e, _a, _b):
         m = fctx.m
         va = m.variance_adaptor
         s_d, s_p, s_e, idx_p, idx_e, cum, speakers, B, Ts, T_dec = fctx.saved
@@ -630,42 +693,47 @@ class VarianceAdaptorFn(torch.autograd.Function):
 
 class DecoderFn(torch.autograd.Function):
     @staticmethod
-    def forward(fctx, token, x, dec, lens, B, T, ctx):
+    def forward(fctx, token, x, x_t, dec, lens, B, T, ctx):
+        x_t = x_t if x_t.numel() else None
         saved = []
         for layer in dec.layer_stack:
-            x, s = layer.fwd(x, lens, B, T, ctx)
+            x, x_t, s = layer.fwd(x, x_t, lens, B, T, ctx)
             saved.append(s)
         fctx.dec, fctx.saved = dec, saved
-        return x
+        side = x_t if x_t is not None else torch.empty(0, device=x.device)
+        fctx.mark_non_differentiable(side)
+        return x, side
 
     @staticmethod
-    def backward(fctx, dx):
+    def backward(fctx, dx, _):
         dx = dx.contiguous()
         for layer, s in zip(reversed(fctx.dec.layer_stack), reversed(fctx.saved)):
             dx = layer.bwd(dx, s)
         fctx.saved = None
-        return None, dx, None, None, None, None, None
+        return None, dx, None, None, None, None, None, None
 
 
 class MelHeadFn(torch.autograd.Function):
     """mel_linear + (postnet(out) + out)."""
 
     @staticmethod
-    def forward(fctx, token, x, m, B, T, ctx):
+    def forward(fctx, token, x, x_t, m, B, T, ctx):
         lin = m.mel_linear
         M = x.shape[0]
-        out = K.conv_gemm(x, lin.weight, M, T, lin.in_features, lin.out_features, 1, 0,
+        x_c = x_t if x_t.numel() else x
+        out = K.conv_gemm(x_c, lin._w_fwd, M, T, lin.in_features, lin.out_features, 1, 0,
                           bias=lin.bias)
-        post, s = m.postnet.fwd(out, B, T, ctx)
-        fctx.m, fctx.saved = m, (x, s, B, T)
+        out_t = K.cast_bf16(out) if ctx.copy is not None else None
+        post, s = m.postnet.fwd(out, out_t, B, T, ctx)
+        fctx.m, fctx.saved = m, (x_c, s, B, T, ctx)
         return out.view(B, T, -1), post.view(B, T, -1)
 
     @staticmethod
     def backward(fctx, d_out, d_post):
         m = fctx.m
-        x, s, B, T = fctx.saved
+        x_c, s, B, T, ctx = fctx.saved
         lin = m.mel_linear
-        M = x.shape[0]
+        M = x_c.shape[0]
         n_mel = lin.out_features
         d_out = d_out.contiguous().view(M, n_mel) if d_out is not None else None
         if d_post is not None:
@@ -674,20 +742,26 @@ class MelHeadFn(torch.autograd.Function):
             m.postnet.bwd(d_post, s, dm)
         else:
             dm = d_out
+        dm_c = K.cast_bf16(dm) if ctx.copy is not None else dm
         K.colsum(dm, M, n_mel, _g(lin.bias))
-        K.conv_wgrad(dm, x, _g(lin.weight), M, T, lin.in_features, n_mel, 1, 0)
-        dx = K.conv_gemm(dm, lin._w_bwd, M, T, n_mel, lin.in_features, 1, 0)
+        K.conv_wgrad(dm_c, x_c, _g(lin.weight), M, T, lin.in_features, n_mel, 1, 0)
+        dx = K.conv_gemm(dm_c, lin._w_bwd, M, T, n_mel, lin.in_features, 1, 0)
         fctx.saved = None
-        return None, dx, None, None, None, None
+        return None, dx, None, None, None, None, None
 
 
 # ----------------------------------------------------------------------------- top level
 
 
 class FastSpeech2(nn.Module):
-    """``model/fastspeech2.py:15-303`` on the HIP kernels (multi_speaker, no JDIT)."""
+    """``model/fastspeech2.py:15-303`` on the HIP kernels (multi_speaker, no JDIT).
 
-    def __init__(self, preprocess_config, model_config, config_path, device="cuda"):
+    ``compute_dtype``: ``torch.float32`` (exact f32 MFMA; the parity path) or
+    ``torch.bfloat16`` (bf16 MFMA operands with fp32 accumulation, fp32 master weights,
+    fp32 residual stream, norms, softmax statistics, losses and optimiser)."""
+
+    def __init__(self, preprocess_config, model_config, config_path, device="cuda",
+                 compute_dtype=torch.float32):
         super().__init__()
         self.model_config = model_config
         assert not model_config["jdit"]["use_jdit"], "JDIT aligner is out of scope (SURVEY.md §2.1)"
@@ -710,6 +784,7 @@ class FastSpeech2(nn.Module):
             v.site, site = site, site + 2
         self.postnet.site = site
         self.dropout = True
+        self.compute_dtype = compute_dtype
         self._seed_rng = np.random.default_rng(0)
         self._arena = None
         self.to(device)
@@ -735,13 +810,14 @@ class FastSpeech2(nn.Module):
         self._seed_rng = np.random.default_rng(s)
 
     def prep_weights(self):
+        cdt = self.compute_dtype
         for b in list(self.encoder.layer_stack) + list(self.decoder.layer_stack):
-            b.prep()
+            b.prep(cdt)
         va = self.variance_adaptor
         for v in (va.duration_predictor, va.pitch_predictor, va.energy_predictor):
-            v.prep()
-        self.postnet.prep()
-        _linear_prep(self.mel_linear)
+            v.prep(cdt)
+        self.postnet.prep(cdt)
+        _linear_prep(self.mel_linear, cdt)
 
     # -- forward ----------------------------------------------------------------------
     def forward(self, speakers, texts, src_lens, max_src_len, mels=None, mel_lens=None,
@@ -753,7 +829,8 @@ class FastSpeech2(nn.Module):
             raise ValueError("accents are required in training (transformer/Models.py:101)")
         self.arena()
         self.prep_weights()
-        ctx = StepCtx(self._seed_rng.integers(0, 2 ** 62), self.training, self.dropout)
+        ctx = StepCtx(self._seed_rng.integers(0, 2 ** 62), self.training, self.dropout,
+                      self.compute_dtype)
         B, Ts = texts.shape
         max_src_len = int(max_src_len)
         max_mel_len = int(max_mel_len)
@@ -769,11 +846,11 @@ class FastSpeech2(nn.Module):
                               B, Ts, ctx)
         speaker_emb_s = K.embedding_fwd(speakers.contiguous(), self.speaker_emb.weight)
         gmm = self.speaker_enc(speaker_meta)
-        x_lr, log_d, p, e, mel_len = VarianceAdaptorFn.apply(
+        x_lr, log_d, p, e, mel_len, x_lr_t = VarianceAdaptorFn.apply(
             tok, enc, self, speakers.contiguous(), src_lens, p_targets, e_targets, d_targets, B, Ts,
             T_dec, ctx)
-        x = DecoderFn.apply(tok, x_lr, self.decoder, mel_lens, B, T_dec, ctx)
-        output, postnet_output = MelHeadFn.apply(tok, x, self, B, T_dec, ctx)
+        x, x_t = DecoderFn.apply(tok, x_lr, x_lr_t, self.decoder, mel_lens, B, T_dec, ctx)
+        output, postnet_output = MelHeadFn.apply(tok, x, x_t, self, B, T_dec, ctx)
         return (output, postnet_output, p, e, log_d, d_targets, src_masks, mel_masks, src_lens,
                 mel_len, gmm, speaker_emb_s)
 
@@ -794,7 +871,7 @@ class FastSpeech2(nn.Module):
         return r
 
 
-def build(config_name="JVS-VCTK", device="cuda"):
+def build(config_name="JVS-VCTK", device="cuda", compute_dtype=torch.float32):
     """Model + configs from a bundled config (``configs/<name>``)."""
     pp, mc, tc, path = cfg.load_configs(config_name)
-    return FastSpeech2(pp, mc, path, device=device), (pp, mc, tc)
+    return FastSpeech2(pp, mc, path, device=device, compute_dtype=compute_dtype), (pp, mc, tc)

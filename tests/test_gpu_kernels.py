@@ -121,16 +121,16 @@ def test_layernorm(mode):
     p = 0.0 if mode in ("res_mask", "dot") else 0.3
     kw = dict(seed=123, site_in=7, site_out=9)
     if mode == "res_mask":
-        out, xh, rs, _ = K.ln_fwd(y, g, bta, res=res, lens=lens, seq_len=T, **kw)
+        out, _, xh, rs, _ = K.ln_fwd(y, g, bta, res=res, lens=lens, seq_len=T, **kw)
         ref = F.layer_norm(y + res, (d,), g, bta, 1e-5).masked_fill(pad[:, None], 0)
         close(out, ref, 2e-5)
     elif mode == "dot":
-        out, xh, rs, dot = K.ln_fwd(y, g, bta, lens=lens, seq_len=T, dot_w=w, dot_b=wb, **kw)
+        out, _, xh, rs, dot = K.ln_fwd(y, g, bta, lens=lens, seq_len=T, dot_w=w, dot_b=wb, **kw)
         ref_u = F.layer_norm(y, (d,), g, bta, 1e-5)
         close(out, ref_u, 2e-5)
         close(dot, (ref_u @ w + wb).masked_fill(pad, 0), 2e-5)
     else:
-        out, xh, rs, _ = K.ln_fwd(y, g, bta, p_out=p, **kw)
+        out, _, xh, rs, _ = K.ln_fwd(y, g, bta, p_out=p, **kw)
         ref_u = F.layer_norm(y, (d,), g, bta, 1e-5)
         keep = out != 0
         frac = keep.float().mean().item()
@@ -146,7 +146,7 @@ def test_layernorm(mode):
         dout = rnd(M, d, seed=11)
         ref.backward(dout)
         dres = torch.zeros(M, d, device=DEV)
-        dy = K.ln_bwd(xh, rs, g, bta, dg, db, dout=dout, lens=lens, seq_len=T, dres=dres, **kw)
+        dy, _ = K.ln_bwd(xh, rs, g, bta, dg, db, dout=dout, lens=lens, seq_len=T, dres=dres, **kw)
         close(dy, yr.grad)
         close(dres, rr.grad)
     elif mode == "dot":
@@ -155,7 +155,7 @@ def test_layernorm(mode):
         ddot = rnd(M, seed=12)
         ref.backward(ddot)
         dw, dwb = torch.zeros(d, device=DEV), torch.zeros(1, device=DEV)
-        dy = K.ln_bwd(xh, rs, g, bta, dg, db, ddot=ddot, dot_w=w, dw_dot=dw, db_dot=dwb,
+        dy, _ = K.ln_bwd(xh, rs, g, bta, dg, db, ddot=ddot, dot_w=w, dw_dot=dw, db_dot=dwb,
                       lens=lens, seq_len=T, **kw)
         close(dy, yr.grad)
         close(dw, wr.grad)
@@ -165,7 +165,7 @@ def test_layernorm(mode):
         dout = rnd(M, d, seed=13)
         ref.backward(dout)
         relu_y = y if mode == "relu_drop" else None
-        dy = K.ln_bwd(xh, rs, g, bta, dg, db, dout=dout, p_out=p, relu_y=relu_y, **kw)
+        dy, _ = K.ln_bwd(xh, rs, g, bta, dg, db, dout=dout, p_out=p, relu_y=relu_y, **kw)
         want = yr.grad * (y > 0) if relu_y is not None else yr.grad
         close(dy, want)
     close(dg, gr.grad)
@@ -179,7 +179,7 @@ def test_batchnorm(act, res):
     g, b = 1 + 0.1 * rnd(c, seed=2), 0.1 * rnd(c, seed=3)
     rm, rv = torch.zeros(c, device=DEV), torch.ones(c, device=DEV)
     r = rnd(M, c, seed=4) if res else None
-    out, mean, rstd = K.bn_fwd(z, g, b, rm, rv, act, 0.0, 1, 2, res=r)
+    out, _, mean, rstd = K.bn_fwd(z, g, b, rm, rv, act, 0.0, 1, 2, res=r)
     zr, gr, br = z.clone().requires_grad_(), g.clone().requires_grad_(), b.clone().requires_grad_()
     rm2, rv2 = torch.zeros(c, device=DEV), torch.ones(c, device=DEV)
     ref = F.batch_norm(zr, rm2, rv2, gr, br, training=True, momentum=0.1, eps=1e-5)
@@ -193,7 +193,7 @@ def test_batchnorm(act, res):
     dout = rnd(M, c, seed=5)
     ref.backward(dout)
     dg, db = torch.zeros(c, device=DEV), torch.zeros(c, device=DEV)
-    dz = K.bn_bwd(dout, z, mean, rstd, g, b, dg, db, act, 0.0, 1, 2)
+    dz, _ = K.bn_bwd(dout, z, mean, rstd, g, b, dg, db, act, 0.0, 1, 2)
     close(dz, zr.grad)
     close(dg, gr.grad)
     close(db, br.grad)
@@ -220,7 +220,7 @@ def test_length_regulator_golden_and_random():
     pos = rnd(300, d, seed=4)
     cum, mel_len = K.lr_index(dur)
     for T in (int(mel_len.max()), 100):
-        out = K.lr_expand(x, cum, T, posenc=pos)
+        out, _ = K.lr_expand(x, cum, T, posenc=pos)
         src, ml = index_math.lr_source_map(dur.cpu().numpy(), T)
         np.testing.assert_array_equal(K.lr_source(cum, T).cpu().numpy(), src)
         np.testing.assert_array_equal(mel_len.cpu().numpy(), ml)
@@ -259,7 +259,7 @@ def test_embeddings():
     texts[0, -3:] = 0
     acc = torch.randint(0, 5, (B, T), device=DEV)
     wt, at, pos = rnd(429, d, seed=1), rnd(5, d, seed=2), rnd(20, d, seed=3)
-    out = K.encoder_embed(texts, acc, wt, at, pos, B, T, d)
+    out, _ = K.encoder_embed(texts, acc, wt, at, pos, B, T, d)
     close(out, (wt[texts] + at[acc] + pos[:T]).reshape(B * T, d), 1e-6)
     dout = rnd(B * T, d, seed=4)
     dwt = torch.zeros_like(wt)
@@ -270,7 +270,7 @@ def test_embeddings():
     spk = torch.tensor([3, 3, 7], device=DEV)
     st = rnd(9, d, seed=5)
     x = rnd(B * T, d, seed=6)
-    close(K.rowvec_add(x, spk, st, B, T), (x.view(B, T, d) + st[spk][:, None]).reshape(-1, d), 1e-6)
+    close(K.rowvec_add(x, spk, st, B, T)[0], (x.view(B, T, d) + st[spk][:, None]).reshape(-1, d), 1e-6)
     dst = torch.zeros_like(st)
     K.rowvec_add_bwd(dout, spk, dst, B, T)
     close(dst, torch.zeros_like(st).index_add_(0, spk, dout.view(B, T, d).sum(1)), 1e-5)
@@ -295,3 +295,81 @@ def test_grad_norm_adam():
         opt.step()
         K.adam_step(p, g, m, v, nc, 1e-3, 0.9, 0.98, 1e-9, 1 - 0.9 ** t, math.sqrt(1 - 0.98 ** t))
     close(p, pr.detach(), 1e-5)
+
+
+# ------------------------------------------------------------------ bf16 path
+def bf(t):
+    return t.to(torch.bfloat16)
+
+
+@pytest.mark.parametrize("B,T,cin,cout,k", [(2, 37, 256, 1024, 9), (3, 50, 1024, 256, 1),
+                                            (2, 64, 80, 512, 5), (1, 33, 512, 80, 5),
+                                            (4, 16, 256, 768, 1), (5, 130, 256, 256, 3),
+                                            (48, 128, 256, 1024, 9)])
+def test_conv_gemm_bf16(B, T, cin, cout, k):
+    """bf16 operands, fp32 accumulation: compare with fp32 math on the same bf16-rounded data."""
+    pad = (k - 1) // 2
+    x = bf(rnd(B * T, cin, seed=1))
+    w = bf(rnd(cout, cin, k, scale=1 / math.sqrt(cin * k), seed=2)).float()
+    b = rnd(cout, seed=3)
+    wf = torch.empty(cout * cin * k, device=DEV, dtype=torch.bfloat16)
+    wb = torch.empty(cout * cin * k, device=DEV, dtype=torch.bfloat16)
+    K.weight_prep(w, cout, cin, k, wf, wb)
+    ref = ref_conv(x.float(), w, b, B, T, pad)
+    y = K.conv_gemm(x, wf, B * T, T, cin, cout, k, pad, bias=b)
+    close(y, ref, 1e-5)
+    yb = K.conv_gemm(x, wf, B * T, T, cin, cout, k, pad, bias=b, flags=K.EPI_RELU,
+                     out_dtype=torch.bfloat16)
+    close(yb.float(), F.relu(ref), 8e-3)
+    dy = bf(rnd(B * T, cout, seed=4))
+    xr = x.float().clone().requires_grad_()
+    wr = w.clone().requires_grad_()
+    ref_conv(xr, wr, b, B, T, pad).backward(dy.float())
+    aux = rnd(B * T, cin, seed=5)
+    dx = K.conv_gemm(dy, wb, B * T, T, cout, cin, k, pad, flags=K.EPI_ADD_AUX, aux=aux)
+    close(dx, xr.grad + aux, 1e-5)
+    auxb = bf(rnd(B * T, cin, seed=6))
+    dm = K.conv_gemm(dy, wb, B * T, T, cout, cin, k, pad, flags=K.EPI_RELU_MASK_AUX, aux=auxb,
+                     out_dtype=torch.bfloat16)
+    close(dm.float(), xr.grad * (auxb.float() > 0), 8e-3)
+    dw = torch.zeros_like(w)
+    K.conv_wgrad(dy, x, dw, B * T, T, cin, cout, k, pad)
+    close(dw, wr.grad, 1e-5)
+    db = torch.zeros(cout, device=DEV)
+    K.colsum(dy, B * T, cout, db)
+    close(db, dy.float().sum(0), 1e-5)
+
+
+@pytest.mark.parametrize("B,T,lens", [(2, 64, [64, 40]), (3, 130, [130, 77, 1]),
+                                      (2, 512, [512, 300])])
+def test_attention_bf16(B, T, lens):
+    H, dh = 2, 128
+    lens_t = torch.tensor(lens, device=DEV)
+    qkv = bf(rnd(B * T, 3 * H * dh, seed=7))
+    o, lse = K.attn_fwd(qkv, lens_t, B, T, H, dh, 1 / math.sqrt(dh))
+    assert o.dtype == torch.bfloat16
+    qr = qkv.float().clone().requires_grad_()
+    ro = ref_attn(qr, lens_t, B, T, H, dh)
+    valid = (torch.arange(T, device=DEV)[None, :] < lens_t[:, None]).reshape(-1)
+    close(o.float()[valid], ro[valid], 1.5e-2)
+    do = bf(rnd(B * T, H * dh, seed=8) * valid[:, None])
+    ro.backward(do.float())
+    dqkv = K.attn_bwd(qkv, o, do, lse, lens_t, B, T, H, dh, 1 / math.sqrt(dh))
+    close(dqkv.float(), qr.grad, 3e-2)
+
+
+def test_norm_copies_bf16():
+    M, d = 300, 256
+    y, r = rnd(M, d, seed=1), rnd(M, d, seed=2)
+    g, b = 1 + 0.1 * rnd(d, seed=3), 0.1 * rnd(d, seed=4)
+    out, out_t, xh, rs, _ = K.ln_fwd(y, g, b, res=r, copy=torch.bfloat16)
+    assert out_t.dtype == torch.bfloat16 and torch.equal(out_t, out.to(torch.bfloat16))
+    dg, db = torch.zeros(d, device=DEV), torch.zeros(d, device=DEV)
+    dy, dy_t = K.ln_bwd(xh, rs, g, b, dg, db, dout=rnd(M, d, seed=5), copy=torch.bfloat16)
+    assert torch.equal(dy_t, dy.to(torch.bfloat16))
+    z = rnd(M, 512, seed=6)
+    o2, o2_t, mean, rstd = K.bn_fwd(z, torch.ones(512, device=DEV), torch.zeros(512, device=DEV),
+                                    None, None, True, 0.0, 0, 0, copy=torch.bfloat16)
+    assert torch.equal(o2_t, o2.to(torch.bfloat16))
+    x = rnd(M, d, seed=7)
+    assert torch.equal(K.cast_bf16(x), x.to(torch.bfloat16))

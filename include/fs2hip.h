@@ -62,6 +62,11 @@ int fs2_conv_gemm(int dtype, const void* x, int64_t ldx, const void* wk, void* y
  *   w_bwd[c, j*c_out + o]       = w[o, c, taps-1-j]      (either output may be NULL)     */
 int fs2_conv_weight_prep(int dtype, const float* w, int64_t c_out, int64_t c_in, int taps,
                          void* w_fwd, void* w_bwd, void* stream);
+/* The same for every layer of the model in one launch: jobs (device, int64) holds
+ * n_jobs rows {w, c_out, c_in, taps, w_fwd, w_bwd, first, end} where [first, end) numbers
+ * the job's elements consecutively and total = end of the last job.                  */
+int fs2_weight_prep_batch(int dtype, const int64_t* jobs, int n_jobs, int64_t total,
+                          void* stream);
 
 /* Weight gradient, accumulated into the fp32 (c_out, c_in, taps) master-gradient layout:
  *   dw[o, c, j] += sum_r dy[r, o] * x[r + j - pad, c]
@@ -111,14 +116,16 @@ int fs2_ln_fwd(int dtype, const float* y, const float* res, const float* gamma, 
 /* Backward of fs2_ln_fwd.  Upstream gradient is dout (per element) or, in dot mode,
  * ddot (per row).  Produces dy (gradient w.r.t. y before dropout, times (relu_y > 0) when
  * relu_y != NULL), optionally adds dz into dres (+=), and accumulates dgamma, dbeta and
- * (dot mode) dw_dot/db_dot into fp32 gradients.  ws >= fs2_ln_bwd_ws_bytes(rows, d). */
+ * (dot mode) dw_dot/db_dot into fp32 gradients; dbias_in (nullable) += sum over rows of
+ * dy — the bias gradient of the layer that produced y, fused here instead of a separate
+ * column sum.  ws >= fs2_ln_bwd_ws_bytes(rows, d).                                   */
 int64_t fs2_ln_bwd_ws_bytes(int64_t rows, int d);
 int fs2_ln_bwd(int dtype, const float* dout, const float* ddot, const float* dot_w,
                const float* xhat, const float* rstd, const float* gamma, const float* beta,
                const int64_t* lens, int64_t seq_len, int64_t rows, int d, float p_in, float p_out,
                uint64_t seed, uint64_t site_in, uint64_t site_out, const float* relu_y, float* dy,
                void* dy_t, float* dres, float* dgamma, float* dbeta, float* dw_dot, float* db_dot,
-               float* ws, int64_t ws_bytes, void* stream);
+               float* dbias_in, float* ws, int64_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------- BatchNorm (PostNet)
  * Training-mode BatchNorm1d over all rows (padded frames included) + optional tanh +
@@ -212,10 +219,15 @@ int fs2_gmm_head_fwd(const float* meta, int64_t batch, int in_dim, int k, int d,
                      float* sigma, float* mu, float* sigma_pre, void* stream);
 /* log p(e_b) of MixtureSameFamily(Categorical(pi), Independent(Normal(mu, sigma), 1))
  * (torch.distributions semantics incl. the probs clamp); resp (batch, k) saved;
- * mean_out (nullable) = sum_b logp_b / batch  = SpeakerMetaEncLoss (model/loss.py:102-104). */
+ * mean_out (nullable) = sum_b logp_b / batch  = SpeakerMetaEncLoss (model/loss.py:102-104);
+ * denom (nullable, device) replaces batch by the global batch (data parallel).       */
 int fs2_gmm_logprob(const float* e, const float* pi, const float* mu, const float* sigma,
                     int64_t batch, int k, int d, float* logp, float* resp, float* mean_out,
-                    void* stream);
+                    const float* denom, void* stream);
+/* out[3] = [sum_b min(mel_lens, mel_len) * n_mel, sum_b min(src_lens, src_len), batch]:
+ * this rank's loss denominators, all-reduced into the global ones (data parallel).  */
+int fs2_dp_counts(const int64_t* src_lens, const int64_t* mel_lens, int64_t batch,
+                  int64_t src_len, int64_t mel_len, int n_mel, float* out, void* stream);
 /* Backward of  L = sum_b g_b * logp_b  through the GMM head into fp32 weight grads (+=). */
 int fs2_gmm_head_bwd(const float* meta, const float* e, const float* pi, const float* mu,
                      const float* sigma, const float* sigma_pre, const float* resp,
@@ -243,8 +255,9 @@ int fs2_fill(float* x, int64_t n, float value, void* stream);
 int fs2_cast_bf16(const float* x, void* y, int64_t n, void* stream);
 int fs2_add_i64(int64_t* x, int64_t n, int64_t value, void* stream); /* BN num_batches_tracked */
 int fs2_scale(float* x, int64_t n, float value, void* stream);
-/* x[i] = src[0] * scale  (device scalar broadcast, no host sync)                     */
-int fs2_fill_from(float* x, int64_t n, const float* src, float scale, void* stream);
+/* x[i] = src[0] * scale / (den ? den[0] : 1)  (device scalar broadcast, no host sync) */
+int fs2_fill_from(float* x, int64_t n, const float* src, float scale, const float* den,
+                  void* stream);
 int fs2_add(float* out, const float* a, const float* b, int64_t n, void* stream); /* out = a + b */
 
 #ifdef __cplusplus

@@ -41,8 +41,9 @@ __global__ void add_kernel(float* out, const float* a, const float* b, int64_t n
     out[i] = a[i] + b[i];
 }
 
-__global__ void fill_from_kernel(float* x, int64_t n, const float* src, float scale) {
-  const float v = src[0] * scale;
+__global__ void fill_from_kernel(float* x, int64_t n, const float* src, float scale,
+                                 const float* den) {
+  const float v = src[0] * scale / (den ? den[0] : 1.f);
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x)
     x[i] = v;
@@ -71,9 +72,10 @@ int fs2_fill(float* x, int64_t n, float value, void* stream) {
   return launch_status("fs2_fill");
 }
 
-int fs2_fill_from(float* x, int64_t n, const float* src, float scale, void* stream) {
+int fs2_fill_from(float* x, int64_t n, const float* src, float scale, const float* den,
+                  void* stream) {
   if (n <= 0) return FS2_OK;
-  fill_from_kernel<<<grid_for(n), 256, 0, as_stream(stream)>>>(x, n, src, scale);
+  fill_from_kernel<<<grid_for(n), 256, 0, as_stream(stream)>>>(x, n, src, scale, den);
   return launch_status("fs2_fill_from");
 }
 

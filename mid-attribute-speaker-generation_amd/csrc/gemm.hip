@@ -304,12 +304,26 @@ __global__ void colsum_partial(const float* x, int64_t ldx, int64_t rows, int64_
     part[(int64_t)blockIdx.y * cols + c] = red[0][threadIdx.x] + red[1][threadIdx.x] +
                                           red[2][threadIdx.x] + red[3][threadIdx.x];
 }
-__global__ void colsum_final(const float* part, int64_t nparts, int64_t cols, float* out, int acc) {
-  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= cols) return;
+// 64 columns x 16 partial-lanes per block: lane y sums partials y, y+16, ... (independent
+// loads in flight), then the 16 lane sums are added in lane order (deterministic).
+__global__ __launch_bounds__(1024) void colsum_final(const float* part, int64_t nparts,
+                                                     int64_t cols, float* out, int acc) {
+  __shared__ float red[16][65];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int64_t c = (int64_t)blockIdx.x * 64 + tx;
   float s = 0.f;
-  for (int64_t p = 0; p < nparts; ++p) s += part[p * cols + c];
-  out[c] = acc ? out[c] + s : s;
+  if (c < cols) {
+#pragma unroll 4
+    for (int64_t p = ty; p < nparts; p += 16) s += part[p * cols + c];
+  }
+  red[ty][tx] = s;
+  __syncthreads();
+  if (ty == 0 && c < cols) {
+    float t = 0.f;
+#pragma unroll
+    for (int y = 0; y < 16; ++y) t += red[y][tx];
+    out[c] = acc ? out[c] + t : t;
+  }
 }
 
 int colsum_launch(const float* x, int64_t ldx, int64_t rows, int64_t cols, float* out, int acc,
@@ -318,14 +332,14 @@ int colsum_launch(const float* x, int64_t ldx, int64_t rows, int64_t cols, float
   if (nparts == 0) return FS2_OK;
   dim3 grid((unsigned)((cols + 63) / 64), (unsigned)nparts);
   colsum_partial<<<grid, 256, 0, st>>>(x, ldx, rows, cols, ws);
-  colsum_final<<<(unsigned)((cols + 255) / 256), 256, 0, st>>>(ws, nparts, cols, out, acc);
+  colsum_final<<<(unsigned)((cols + 63) / 64), 1024, 0, st>>>(ws, nparts, cols, out, acc);
   return launch_status("colsum");
 }
 
 int colsum_final_launch(const float* part, int64_t nparts, int64_t cols, float* out, int acc,
                         hipStream_t st) {
   if (cols <= 0) return FS2_OK;
-  colsum_final<<<(unsigned)((cols + 255) / 256), 256, 0, st>>>(part, nparts, cols, out, acc);
+  colsum_final<<<(unsigned)((cols + 63) / 64), 1024, 0, st>>>(part, nparts, cols, out, acc);
   return launch_status("colsum_final");
 }
 

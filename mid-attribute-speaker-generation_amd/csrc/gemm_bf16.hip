@@ -297,6 +297,36 @@ __global__ void weight_prep_bf16(const float* w, int Cout, int Cin, int taps, u1
   }
 }
 
+// All layers' re-layouts in one launch.  jobs[j] = {src, c_out, c_in, taps, w_fwd, w_bwd,
+// first element, end element} (int64), elements numbered consecutively over the jobs.
+template <typename OutT>
+__global__ void weight_prep_batch(const int64_t* __restrict__ jobs, int n_jobs, int64_t total) {
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    int lo = 0, hi = n_jobs - 1;
+    while (lo < hi) {  // last job whose first element <= e
+      const int mid = (lo + hi + 1) >> 1;
+      if (jobs[mid * 8 + 6] <= e) lo = mid;
+      else hi = mid - 1;
+    }
+    const int64_t* jb = jobs + lo * 8;
+    const float* w = (const float*)jb[0];
+    const int64_t Cout = jb[1], Cin = jb[2], taps = jb[3];
+    OutT* wf = (OutT*)jb[4];
+    OutT* wb = (OutT*)jb[5];
+    const int64_t i = e - jb[6];
+    const int64_t o = i / (Cin * taps);
+    const int64_t rem = i - o * Cin * taps;
+    const int64_t c = rem / taps, j = rem - c * taps;
+    const float v = w[i];
+    OutT ov;
+    if constexpr (sizeof(OutT) == 2) ov = f2bf(v);
+    else ov = v;
+    if (wf) wf[o * taps * Cin + j * Cin + c] = ov;
+    if (wb) wb[c * taps * Cout + (taps - 1 - j) * Cout + o] = ov;
+  }
+}
+
 __global__ void cast_bf16_kernel(const float* x, u16* y, int64_t n) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x)
@@ -371,6 +401,22 @@ int colsum_bf16_launch(const void* x, int64_t ldx, int64_t rows, int64_t cols, f
 }
 
 }  // namespace fs2
+
+extern "C" int fs2_weight_prep_batch(int dtype, const int64_t* jobs, int n_jobs, int64_t total,
+                                     void* stream) {
+  if (n_jobs <= 0 || total <= 0) return FS2_OK;
+  int64_t b = (total + 255) / 256;
+  if (b > 8192) b = 8192;
+  if (dtype == FS2_BF16)
+    fs2::weight_prep_batch<unsigned short><<<(unsigned)b, 256, 0, as_stream(stream)>>>(jobs, n_jobs, total);
+  else if (dtype == FS2_F32)
+    fs2::weight_prep_batch<float><<<(unsigned)b, 256, 0, as_stream(stream)>>>(jobs, n_jobs, total);
+  else {
+    fs2::set_error("fs2_weight_prep_batch: dtype %d not built", dtype);
+    return FS2_ERR_DTYPE;
+  }
+  return fs2::launch_status("fs2_weight_prep_batch");
+}
 
 extern "C" int fs2_cast_bf16(const float* x, void* y, int64_t n, void* stream) {
   if (n <= 0) return FS2_OK;

@@ -68,12 +68,21 @@ __global__ void fs2loss_partial(const float* mel_out, const float* post_out, con
 }
 
 // losses = [total, mel, post, pitch, energy, duration]; dens[0..1] = (mel elements, phonemes)
-__global__ void fs2loss_final(const float* part, int64_t np, int n_mel, const float* denoms,
-                              float* losses, float* dens) {
+// 8 sums x 32 lanes: lane j of sum k adds partials j, j+32, ... in double; lanes are then
+// added in lane order (deterministic)
+__global__ __launch_bounds__(256) void fs2loss_final(const float* part, int64_t np, int n_mel,
+                                                     const float* denoms, float* losses,
+                                                     float* dens) {
+  __shared__ double red[8][33];
+  const int k = threadIdx.x >> 5, j = threadIdx.x & 31;
+  double v = 0.0;
+  for (int64_t p = j; p < np; p += 32) v += part[p * 8 + k];
+  red[k][j] = v;
+  __syncthreads();
   if (threadIdx.x != 0) return;
   double s[7] = {0, 0, 0, 0, 0, 0, 0};
-  for (int64_t p = 0; p < np; ++p)
-    for (int k = 0; k < 7; ++k) s[k] += part[p * 8 + k];
+  for (int kk = 0; kk < 7; ++kk)
+    for (int jj = 0; jj < 32; ++jj) s[kk] += red[kk][jj];
   const double dm = denoms ? denoms[0] : s[5] * n_mel;
   const double dsr = denoms ? denoms[1] : s[6];
   dens[0] = (float)dm;
@@ -284,11 +293,25 @@ __global__ void gmm_head_bwd(const float* meta, const float* e, const float* pi,
   db[row] += acc_b;
 }
 
-__global__ void mean_k(const float* x, int64_t n, float* out) {
+__global__ void mean_k(const float* x, int64_t n, float* out, const float* den) {
   if (threadIdx.x != 0) return;
   float s = 0.f;  // python sum() over the batch, in order (model/loss.py:104)
   for (int64_t i = 0; i < n; ++i) s += x[i];
-  out[0] = s / (float)n;
+  out[0] = s / (den ? den[0] : (float)n);
+}
+
+// data-parallel denominators of this rank's batch: [valid mel elements, valid phonemes, B]
+__global__ void dp_counts(const int64_t* src_lens, const int64_t* mel_lens, int64_t B,
+                          int64_t src_len, int64_t mel_len, int n_mel, float* out) {
+  if (threadIdx.x != 0) return;
+  double m = 0, s = 0;
+  for (int64_t b = 0; b < B; ++b) {
+    m += (double)(mel_lens[b] < mel_len ? mel_lens[b] : mel_len);
+    s += (double)(src_lens[b] < src_len ? src_lens[b] : src_len);
+  }
+  out[0] = (float)(m * n_mel);
+  out[1] = (float)s;
+  out[2] = (float)B;
 }
 
 __global__ void gmm_sample(const float* pi, const float* mu, const float* sigma, int64_t B, int K,
@@ -341,7 +364,7 @@ int fs2_fs2loss_fwd(const float* mel_out, const float* post_out, const float* me
   fs2loss_partial<<<(unsigned)np, 256, 0, st>>>(mel_out, post_out, mel_tgt, tgt_len, p_pred, e_pred,
                                                 logd_pred, p_tgt, e_tgt, d_tgt, src_pad, mel_pad,
                                                 batch, src_len, mel_len, n_mel, np - 1, ws);
-  fs2loss_final<<<1, 64, 0, st>>>(ws, np, n_mel, denoms, losses, ws + np * 8);
+  fs2loss_final<<<1, 256, 0, st>>>(ws, np, n_mel, denoms, losses, ws + np * 8);
   return launch_status("fs2_fs2loss_fwd");
 }
 
@@ -383,11 +406,11 @@ int fs2_gmm_head_fwd(const float* meta, int64_t batch, int in_dim, int k, int d,
 
 int fs2_gmm_logprob(const float* e, const float* pi, const float* mu, const float* sigma,
                     int64_t batch, int k, int d, float* logp, float* resp, float* mean_out,
-                    void* stream) {
+                    const float* denom, void* stream) {
   FS2_CHECK_ARG(k >= 1 && k <= 16, "fs2_gmm_logprob: k <= 16");
   if (batch == 0) return FS2_OK;
   gmm_logprob<<<(unsigned)batch, 256, 0, as_stream(stream)>>>(e, pi, mu, sigma, k, d, logp, resp);
-  if (mean_out) mean_k<<<1, 64, 0, as_stream(stream)>>>(logp, batch, mean_out);
+  if (mean_out) mean_k<<<1, 64, 0, as_stream(stream)>>>(logp, batch, mean_out, denom);
   return launch_status("fs2_gmm_logprob");
 }
 
@@ -402,6 +425,12 @@ int fs2_gmm_head_bwd(const float* meta, const float* e, const float* pi, const f
       meta, e, pi, mu, sigma, sigma_pre, resp, g_logp, batch, in_dim, k, d, dw_pi, db_pi, dw_sigma,
       db_sigma, dw_mu, db_mu);
   return launch_status("fs2_gmm_head_bwd");
+}
+
+int fs2_dp_counts(const int64_t* src_lens, const int64_t* mel_lens, int64_t batch,
+                  int64_t src_len, int64_t mel_len, int n_mel, float* out, void* stream) {
+  dp_counts<<<1, 64, 0, as_stream(stream)>>>(src_lens, mel_lens, batch, src_len, mel_len, n_mel, out);
+  return launch_status("fs2_dp_counts");
 }
 
 int fs2_gmm_sample(const float* pi, const float* mu, const float* sigma, int64_t batch, int k,

@@ -93,14 +93,14 @@ struct LnBwd {
 };
 
 __global__ __launch_bounds__(256) void ln_bwd_f32(LnBwd a) {
-  __shared__ f32x4 red[3][4][64];
+  __shared__ f32x4 red[4][4][64];
   __shared__ float redb[4];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const f32x4 gam = ld4(a.gamma + 4 * lane);
   const f32x4 bet = ld4(a.beta + 4 * lane);
   f32x4 w = {0.f, 0.f, 0.f, 0.f};
   if (a.ddot) w = ld4(a.dot_w + 4 * lane);
-  f32x4 pg = {0.f, 0.f, 0.f, 0.f}, pb = pg, pw = pg;
+  f32x4 pg = {0.f, 0.f, 0.f, 0.f}, pb = pg, pw = pg, py = pg;
   float pdb = 0.f;
   const int64_t rbeg = (int64_t)blockIdx.x * LN_ROWS;
   for (int i = wave; i < LN_ROWS; i += 4) {
@@ -141,18 +141,18 @@ __global__ __launch_bounds__(256) void ln_bwd_f32(LnBwd a) {
     }
     st4(a.dy + e0, dy);
     if (a.dy_t) st4_bf16(a.dy_t + e0, dy);
+    py += dy;  // bias gradient of the layer that produced y (fused colsum)
   }
   red[0][wave][lane] = pg;
   red[1][wave][lane] = pb;
   red[2][wave][lane] = pw;
+  red[3][wave][lane] = py;
   if (lane == 0) redb[wave] = pdb;
   __syncthreads();
-  if (wave < 3) {
-    f32x4 s = red[wave][0][lane] + red[wave][1][lane] + red[wave][2][lane] + red[wave][3][lane];
-    st4(a.part + ((int64_t)wave * a.nblk + blockIdx.x) * LN_D + 4 * lane, s);
-  } else if (lane == 0) {
-    a.part[3 * a.nblk * LN_D + blockIdx.x] = redb[0] + redb[1] + redb[2] + redb[3];
-  }
+  const f32x4 s = red[wave][0][lane] + red[wave][1][lane] + red[wave][2][lane] + red[wave][3][lane];
+  st4(a.part + ((int64_t)wave * a.nblk + blockIdx.x) * LN_D + 4 * lane, s);
+  if (threadIdx.x == 0)
+    a.part[4 * a.nblk * LN_D + blockIdx.x] = redb[0] + redb[1] + redb[2] + redb[3];
 }
 
 // ------------------------------------------------------------------ BatchNorm
@@ -181,20 +181,43 @@ __global__ void bn_partial(const float* z, const float* mean, int64_t rows, int6
         red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
 }
 
-__global__ void bn_mean_final(const float* part, int64_t nparts, int64_t rows, int64_t c, float* mean) {
-  const int64_t col = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (col >= c) return;
+// in-order column sum of partial rows: 64 columns x 16 lanes per block (see colsum_final)
+FS2_DEV float col_reduce(const float* part, int64_t nparts, int64_t c, int64_t col, int tx, int ty,
+                         float (*red)[65]) {
   float s = 0.f;
-  for (int64_t p = 0; p < nparts; ++p) s += part[p * c + col];
-  mean[col] = s / (float)rows;
+  if (col < c) {
+#pragma unroll 4
+    for (int64_t p = ty; p < nparts; p += 16) s += part[p * c + col];
+  }
+  red[ty][tx] = s;
+  __syncthreads();
+  float t = 0.f;
+  if (ty == 0) {
+#pragma unroll
+    for (int y = 0; y < 16; ++y) t += red[y][tx];
+  }
+  __syncthreads();
+  return t;
 }
 
-__global__ void bn_var_final(const float* part, int64_t nparts, int64_t rows, int64_t c, float eps,
-                             float mom, const float* mean, float* rm, float* rv, float* rstd) {
-  const int64_t col = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (col >= c) return;
-  float s = 0.f;
-  for (int64_t p = 0; p < nparts; ++p) s += part[p * c + col];
+__global__ __launch_bounds__(1024) void bn_mean_final(const float* part, int64_t nparts, int64_t rows,
+                                                      int64_t c, float* mean) {
+  __shared__ float red[16][65];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int64_t col = (int64_t)blockIdx.x * 64 + tx;
+  const float s = col_reduce(part, nparts, c, col, tx, ty, red);
+  if (ty == 0 && col < c) mean[col] = s / (float)rows;
+}
+
+__global__ __launch_bounds__(1024) void bn_var_final(const float* part, int64_t nparts, int64_t rows,
+                                                     int64_t c, float eps, float mom,
+                                                     const float* mean, float* rm, float* rv,
+                                                     float* rstd) {
+  __shared__ float red[16][65];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int64_t col = (int64_t)blockIdx.x * 64 + tx;
+  const float s = col_reduce(part, nparts, c, col, tx, ty, red);
+  if (ty != 0 || col >= c) return;
   const float var = s / (float)rows;
   rstd[col] = 1.f / sqrtf(var + eps);
   if (rm) rm[col] = (1.f - mom) * rm[col] + mom * mean[col];
@@ -261,15 +284,15 @@ __global__ void bn_bwd_partial(const float* dout, const float* z, const float* m
   }
 }
 
-__global__ void bn_bwd_final(const float* part_g, const float* part_gx, int64_t nparts, int64_t c,
-                             float* sums, float* dgamma, float* dbeta) {
-  const int64_t col = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (col >= c) return;
-  float sg = 0.f, sgx = 0.f;
-  for (int64_t p = 0; p < nparts; ++p) {
-    sg += part_g[p * c + col];
-    sgx += part_gx[p * c + col];
-  }
+__global__ __launch_bounds__(1024) void bn_bwd_final(const float* part_g, const float* part_gx,
+                                                     int64_t nparts, int64_t c, float* sums,
+                                                     float* dgamma, float* dbeta) {
+  __shared__ float red[16][65];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int64_t col = (int64_t)blockIdx.x * 64 + tx;
+  const float sg = col_reduce(part_g, nparts, c, col, tx, ty, red);
+  const float sgx = col_reduce(part_gx, nparts, c, col, tx, ty, red);
+  if (ty != 0 || col >= c) return;
   sums[col] = sg;
   sums[c + col] = sgx;
   if (dbeta) dbeta[col] += sg;
@@ -333,7 +356,7 @@ int fs2_ln_fwd(int dtype, const float* y, const float* res, const float* gamma, 
 
 int64_t fs2_ln_bwd_ws_bytes(int64_t rows, int d) {
   const int64_t nblk = (rows + LN_ROWS - 1) / LN_ROWS;
-  return (3 * nblk * (int64_t)d + nblk) * 4;
+  return (4 * nblk * (int64_t)d + nblk) * 4;
 }
 
 int fs2_ln_bwd(int dtype, const float* dout, const float* ddot, const float* dot_w,
@@ -341,7 +364,7 @@ int fs2_ln_bwd(int dtype, const float* dout, const float* ddot, const float* dot
                const int64_t* lens, int64_t seq_len, int64_t rows, int d, float p_in, float p_out,
                uint64_t seed, uint64_t site_in, uint64_t site_out, const float* relu_y, float* dy,
                void* dy_t, float* dres, float* dgamma, float* dbeta, float* dw_dot, float* db_dot,
-               float* ws, int64_t ws_bytes, void* stream) {
+               float* dbias_in, float* ws, int64_t ws_bytes, void* stream) {
   if (int rc = copy_dtype_ok(dtype, "fs2_ln_bwd")) return rc;
   FS2_CHECK_ARG(d == LN_D, "fs2_ln_bwd: only d = 256 is supported (got %d)", d);
   FS2_CHECK_ARG((dout != nullptr) != (ddot != nullptr), "fs2_ln_bwd: give exactly one of dout/ddot");
@@ -360,7 +383,9 @@ int fs2_ln_bwd(int dtype, const float* dout, const float* ddot, const float* dot
   if (dbeta && (rc = colsum_final_launch(ws + nblk * LN_D, nblk, LN_D, dbeta, 1, st))) return rc;
   if (ddot && dw_dot && (rc = colsum_final_launch(ws + 2 * nblk * LN_D, nblk, LN_D, dw_dot, 1, st)))
     return rc;
-  if (ddot && db_dot && (rc = colsum_final_launch(ws + 3 * nblk * LN_D, nblk, 1, db_dot, 1, st)))
+  if (ddot && db_dot && (rc = colsum_final_launch(ws + 4 * nblk * LN_D, nblk, 1, db_dot, 1, st)))
+    return rc;
+  if (dbias_in && (rc = colsum_final_launch(ws + 3 * nblk * LN_D, nblk, LN_D, dbias_in, 1, st)))
     return rc;
   return FS2_OK;
 }
@@ -381,11 +406,11 @@ int fs2_bn_fwd(int dtype, const float* z, int64_t rows, int64_t c, const float* 
   hipStream_t st = as_stream(stream);
   const int64_t nparts = (rows + BN_ROWS - 1) / BN_ROWS;
   dim3 grid((unsigned)((c + 63) / 64), (unsigned)nparts);
-  const unsigned cg = (unsigned)((c + 255) / 256);
+  const unsigned cg = (unsigned)((c + 63) / 64);
   bn_partial<0><<<grid, 256, 0, st>>>(z, nullptr, rows, c, ws);
-  bn_mean_final<<<cg, 256, 0, st>>>(ws, nparts, rows, c, mean);
+  bn_mean_final<<<cg, 1024, 0, st>>>(ws, nparts, rows, c, mean);
   bn_partial<1><<<grid, 256, 0, st>>>(z, mean, rows, c, ws);
-  bn_var_final<<<cg, 256, 0, st>>>(ws, nparts, rows, c, eps, momentum, mean, running_mean,
+  bn_var_final<<<cg, 1024, 0, st>>>(ws, nparts, rows, c, eps, momentum, mean, running_mean,
                                    running_var, rstd);
   bn_apply<<<ew_grid(rows * c), 256, 0, st>>>(z, mean, rstd, gamma, beta, rows, c, act_tanh, p,
                                               seed, site, res, out,
@@ -408,7 +433,7 @@ int fs2_bn_bwd(int dtype, const float* dout, const float* z, const float* mean, 
   dim3 grid((unsigned)((c + 63) / 64), (unsigned)nparts);
   bn_bwd_partial<<<grid, 256, 0, st>>>(dout, z, mean, rstd, gamma, beta, rows, c, act_tanh, p,
                                        seed, site, part_g, part_gx);
-  bn_bwd_final<<<(unsigned)((c + 255) / 256), 256, 0, st>>>(part_g, part_gx, nparts, c, sums,
+  bn_bwd_final<<<(unsigned)((c + 63) / 64), 1024, 0, st>>>(part_g, part_gx, nparts, c, sums,
                                                              dgamma, dbeta);
   bn_bwd_apply<<<ew_grid(rows * c), 256, 0, st>>>(dout, z, mean, rstd, gamma, beta, sums, rows, c,
                                                   act_tanh, p, seed, site, dz,

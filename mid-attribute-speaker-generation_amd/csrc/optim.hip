@@ -31,10 +31,20 @@ __global__ void sumsq_partial(const float* g, int64_t n, float* part) {
   if (threadIdx.x == 0) part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
 }
 
-__global__ void norm_final(const float* part, int np, float max_norm, float* norm_coef) {
+// one block of GN_BLOCKS threads: fixed-shape tree over the partials in double
+__global__ __launch_bounds__(1024) void norm_final(const float* part, int np, float max_norm,
+                                                   float* norm_coef) {
+  __shared__ double red[1024];
+  double v = 0.0;
+  for (int i = threadIdx.x; i < np; i += blockDim.x) v += part[i];
+  red[threadIdx.x] = v;
+  __syncthreads();
+  for (int off = blockDim.x / 2; off > 0; off >>= 1) {
+    if ((int)threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+    __syncthreads();
+  }
   if (threadIdx.x != 0) return;
-  double s = 0.0;
-  for (int i = 0; i < np; ++i) s += part[i];
+  const double s = red[0];
   const float norm = (float)sqrt(s);
   norm_coef[0] = norm;
   const float coef = max_norm / (norm + 1e-6f);
@@ -94,7 +104,7 @@ int fs2_grad_norm(const float* g, int64_t n, float max_norm, float* norm_coef, f
   FS2_CHECK_ARG(((uintptr_t)g & 15) == 0, "fs2_grad_norm: gradient buffer must be 16-B aligned");
   hipStream_t st = as_stream(stream);
   sumsq_partial<<<GN_BLOCKS, 256, 0, st>>>(g, n, ws);
-  norm_final<<<1, 64, 0, st>>>(ws, GN_BLOCKS, max_norm, norm_coef);
+  norm_final<<<1, 1024, 0, st>>>(ws, GN_BLOCKS, max_norm, norm_coef);
   return launch_status("fs2_grad_norm");
 }
 

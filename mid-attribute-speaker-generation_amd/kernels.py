@@ -143,8 +143,8 @@ def ln_fwd(y, gamma, beta, res=None, lens=None, seq_len=1, p_in=0.0, p_out=0.0, 
 
 def ln_bwd(xhat, rstd, gamma, beta, dgamma, dbeta, dout=None, ddot=None, dot_w=None,
            dw_dot=None, db_dot=None, lens=None, seq_len=1, p_in=0.0, p_out=0.0, seed=0,
-           site_in=0, site_out=0, relu_y=None, dres=None, copy=None):
-    """Returns (dy fp32, dy compute copy or None)."""
+           site_in=0, site_out=0, relu_y=None, dres=None, copy=None, dbias_in=None):
+    """Returns (dy fp32, dy compute copy or None); dbias_in (+)= column sums of dy."""
     _dev(xhat, rstd, gamma, beta, dout, ddot, dot_w, relu_y, dres, lens)
     rows, d = xhat.shape
     dy = torch.empty_like(xhat)
@@ -154,7 +154,8 @@ def ln_bwd(xhat, rstd, gamma, beta, dgamma, dbeta, dout=None, ddot=None, dot_w=N
     lib.fs2_ln_bwd(BF16 if copy is not None else F32, ptr(dout), ptr(ddot), ptr(dot_w), ptr(xhat),
                    ptr(rstd), ptr(gamma), ptr(beta), ptr(lens), seq_len, rows, d, p_in, p_out,
                    seed, site_in, site_out, ptr(relu_y), ptr(dy), ptr(dy_t), ptr(dres),
-                   ptr(dgamma), ptr(dbeta), ptr(dw_dot), ptr(db_dot), ptr(w), n, stream())
+                   ptr(dgamma), ptr(dbeta), ptr(dw_dot), ptr(db_dot), ptr(dbias_in), ptr(w), n,
+                   stream())
     return dy, dy_t
 
 
@@ -346,15 +347,23 @@ def gmm_head_fwd(meta, w_pi, b_pi, w_s, b_s, w_mu, b_mu, K, D):
     return pi, mu, sigma, sigma_pre
 
 
-def gmm_logprob(e, pi, mu, sigma, want_mean=False):
-    _dev(e, pi, mu, sigma)
+def gmm_logprob(e, pi, mu, sigma, want_mean=False, denom=None):
+    _dev(e, pi, mu, sigma, denom)
     B, K, D = mu.shape
     logp = torch.empty(B, dtype=torch.float32, device=e.device)
     resp = torch.empty(B, K, dtype=torch.float32, device=e.device)
     mean = torch.empty((), dtype=torch.float32, device=e.device) if want_mean else None
     lib.fs2_gmm_logprob(ptr(e), ptr(pi), ptr(mu), ptr(sigma), B, K, D, ptr(logp), ptr(resp),
-                        ptr(mean), stream())
+                        ptr(mean), ptr(denom), stream())
     return logp, resp, mean
+
+
+def dp_counts(src_lens, mel_lens, src_len, mel_len, n_mel):
+    _dev(src_lens, mel_lens)
+    out = torch.empty(3, dtype=torch.float32, device=src_lens.device)
+    lib.fs2_dp_counts(ptr(src_lens), ptr(mel_lens), src_lens.numel(), src_len, mel_len, n_mel,
+                      ptr(out), stream())
+    return out
 
 
 def gmm_head_bwd(meta, e, pi, mu, sigma, sigma_pre, resp, g_logp, grads):

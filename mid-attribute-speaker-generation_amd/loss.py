@@ -56,22 +56,25 @@ class GMMMeanLogProbFn(torch.autograd.Function):
     (fastspeech2.py:322-341, loss.py:102-104)."""
 
     @staticmethod
-    def forward(fctx, token, e, gmm, scale):
+    def forward(fctx, token, e, gmm, denom):
         e = e.detach().contiguous().float()
-        _, resp, mean = K.gmm_logprob(e, gmm.pi, gmm.mu, gmm.sigma, want_mean=True)
-        if scale != 1.0:
-            K.lib.fs2_scale(K.ptr(mean), 1, float(scale), K.stream())
-        fctx.saved = (e, resp, gmm, scale)
+        _, resp, mean = K.gmm_logprob(e, gmm.pi, gmm.mu, gmm.sigma, want_mean=True, denom=denom)
+        fctx.saved = (e, resp, gmm, denom)
         return mean
 
     @staticmethod
     def backward(fctx, g):
-        e, resp, gmm, scale = fctx.saved
+        e, resp, gmm, denom = fctx.saved
         B = e.shape[0]
         gl = torch.empty(B, dtype=torch.float32, device=e.device)
-        K.lib.fs2_fill_from(K.ptr(gl), B, K.ptr(g.contiguous()), float(scale) / B, K.stream())
+        # d mean / d logp_b = 1 / (global) batch
+        K.lib.fs2_fill_from(K.ptr(gl), B, K.ptr(g.contiguous()), 1.0 if denom is not None else 1.0 / B,
+                            K.ptr(denom), K.stream())
         K.gmm_head_bwd(gmm.meta, e, gmm.pi, gmm.mu, gmm.sigma, gmm.sigma_pre, resp, gl,
                        gmm.head.grads())
+        hooks = getattr(gmm.head, "_model_hooks", None)
+        if hooks is not None and hooks["grad"] is not None:
+            hooks["grad"](gmm.head.params())
         fctx.saved = None
         return None, None, None, None
 
@@ -88,13 +91,14 @@ class GMMPrior:
         logp, _, _ = K.gmm_logprob(e.detach().contiguous().float(), self.pi, self.mu, self.sigma)
         return logp
 
-    def mean_log_prob(self, e, scale=1.0):
+    def mean_log_prob(self, e, denom=None):
+        """sum_b log p(e_b) / B, or / denom[0] (device; the global batch when data parallel)."""
         token = getattr(self.head, "_tok", None)
         if token is None:
             logp, _, mean = K.gmm_logprob(e.detach().contiguous().float(), self.pi, self.mu,
-                                          self.sigma, want_mean=True)
+                                          self.sigma, want_mean=True, denom=denom)
             return mean
-        return GMMMeanLogProbFn.apply(token, e, self, float(scale))
+        return GMMMeanLogProbFn.apply(token, e, self, denom)
 
     def sample(self, seed=None, offset=0):
         import numpy as np
@@ -110,7 +114,7 @@ class SpeakerMetaEncLoss(nn.Module):
     def __init__(self, preprocess_config, model_config):
         super().__init__()
         self.K = model_config["speaker_generation"]["GMM_mixtures"]
-        self.scale = 1.0  # data-parallel: B_local / B_global
+        self.denom = None  # data-parallel: device [global batch]
 
     def forward(self, input, prediction):
-        return prediction.mean_log_prob(input, self.scale)
+        return prediction.mean_log_prob(input, self.denom)

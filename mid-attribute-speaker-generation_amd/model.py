@@ -119,9 +119,15 @@ class StepCtx:
         self.drop = bool(training and dropout)
         self.cdt = cdt
         self.copy = None if cdt == torch.float32 else cdt  # bf16 compute copies wanted?
+        self.hook = None  # gradient-ready callback (data-parallel bucketed all-reduce)
 
     def p(self, p):
         return float(p) if self.drop else 0.0
+
+    def notify(self, params):
+        """Tell the gradient hook that these parameters' gradients are final."""
+        if self.hook is not None:
+            self.hook(params)
 
 
 def _t(f, t):
@@ -149,7 +155,16 @@ class _WeightHolder:
         self.in_features, self.out_features = d_in, d_out
 
 
-def _linear_prep(lin, cdt, w=None, c_out=None, c_in=None):
+def _prep(w, c_out, c_in, taps, wf, wb, jobs):
+    """Launch the re-layout now, or (jobs given) record it for the one-launch batch."""
+    if jobs is None:
+        K.weight_prep(w, c_out, c_in, taps, wf, wb)
+    else:
+        jobs.append((w.data_ptr(), c_out, c_in, taps, 0 if wf is None else wf.data_ptr(),
+                     0 if wb is None else wb.data_ptr()))
+
+
+def _linear_prep(lin, cdt, w=None, c_out=None, c_in=None, jobs=None):
     """Compute-layout weights of a Linear: w_fwd (out, in) and its transpose w_bwd (in, out).
     fp32 forward uses the master weight itself."""
     w = lin.weight.detach() if w is None else w
@@ -158,19 +173,19 @@ def _linear_prep(lin, cdt, w=None, c_out=None, c_in=None):
     wb = _buf(lin, "_w_bwd", c_in * c_out, cdt, w.device).view(c_in, c_out)
     if cdt == torch.float32:
         lin._w_fwd = w.reshape(c_out, c_in)
-        K.weight_prep(w, c_out, c_in, 1, None, wb)
+        _prep(w, c_out, c_in, 1, None, wb, jobs)
     else:
         wf = _buf(lin, "_w_fwd_b", c_out * c_in, cdt, w.device).view(c_out, c_in)
         lin._w_fwd = wf
-        K.weight_prep(w, c_out, c_in, 1, wf, wb)
+        _prep(w, c_out, c_in, 1, wf, wb, jobs)
     lin._w_bwd = wb
 
 
-def _conv_prep(conv, cdt):
+def _conv_prep(conv, cdt, jobs=None):
     n = conv.c_out * conv.c_in * conv.k
     wf = _buf(conv, "_w_fwd", n, cdt, conv.weight.device)
     wb = _buf(conv, "_w_bwd", n, cdt, conv.weight.device)
-    K.weight_prep(conv.weight.detach(), conv.c_out, conv.c_in, conv.k, wf, wb)
+    _prep(conv.weight.detach(), conv.c_out, conv.c_in, conv.k, wf, wb, jobs)
 
 
 # ----------------------------------------------------------------------------- FFT block
@@ -218,7 +233,7 @@ class FFTBlock(nn.Module):
         self.pos_ffn = PositionwiseFeedForward(d_model, d_inner, kernel_size, dropout)
         self.site = 0  # assigned by FastSpeech2
 
-    def prep(self, cdt):
+    def prep(self, cdt, jobs=None):
         a, f = self.slf_attn, self.pos_ffn
         n3 = 3 * a.n_head * a.d_k
         wq, bq = a.w_qs.weight, a.w_qs.bias
@@ -229,10 +244,10 @@ class FFTBlock(nn.Module):
         self._qkv_b = _flat_view(bq, n3)
         self._qkv_gw = _flat_view(_g(wq), n3 * self.d).view(n3, self.d)
         self._qkv_gb = _flat_view(_g(bq), n3)
-        _linear_prep(q, cdt, w=_flat_view(wq, n3 * self.d).view(n3, self.d))
-        _linear_prep(a.fc, cdt)
-        _conv_prep(f.w_1, cdt)
-        _conv_prep(f.w_2, cdt)
+        _linear_prep(q, cdt, w=_flat_view(wq, n3 * self.d).view(n3, self.d), jobs=jobs)
+        _linear_prep(a.fc, cdt, jobs=jobs)
+        _conv_prep(f.w_1, cdt, jobs)
+        _conv_prep(f.w_2, cdt, jobs)
 
     def fwd(self, x, x_t, lens, B, T, ctx):
         a, f = self.slf_attn, self.pos_ffn
@@ -271,9 +286,9 @@ class FFTBlock(nn.Module):
         dx1 = K.zeros((M, d), x_c.device)
         dy2, dy2_t = K.ln_bwd(xh2, rs2, ln2.weight, ln2.bias, _g(ln2.weight), _g(ln2.bias),
                               dout=dx2, lens=lens, seq_len=T, p_in=p, seed=seed,
-                              site_in=self.site + 1, dres=dx1, copy=ctx.copy)
+                              site_in=self.site + 1, dres=dx1, copy=ctx.copy,
+                              dbias_in=_g(w2.bias))
         dy2_c = _t(dy2, dy2_t)
-        K.colsum(dy2, M, d, _g(w2.bias))
         K.conv_wgrad(dy2_c, h, _g(w2.weight), M, T, w2.c_in, d, w2.k, w2.padding)
         dh = K.conv_gemm(dy2_c, w2._w_bwd, M, T, d, w2.c_in, w2.k, w2.padding,
                          flags=K.EPI_RELU_MASK_AUX, aux=h, out_dtype=cdt)
@@ -285,10 +300,9 @@ class FFTBlock(nn.Module):
         dx = K.zeros((M, d), x_c.device)
         dy1, dy1_t = K.ln_bwd(xh1, rs1, ln1.weight, ln1.bias, _g(ln1.weight), _g(ln1.bias),
                               dout=dx1, lens=lens, seq_len=T, p_in=p, seed=seed,
-                              site_in=self.site, dres=dx, copy=ctx.copy)
+                              site_in=self.site, dres=dx, copy=ctx.copy, dbias_in=_g(a.fc.bias))
         dy1_c = _t(dy1, dy1_t)
         hd = a.n_head * a.d_k
-        K.colsum(dy1, M, d, _g(a.fc.bias))
         K.conv_wgrad(dy1_c, o, _g(a.fc.weight), M, T, hd, d, 1, 0)
         do = K.conv_gemm(dy1_c, a.fc._w_bwd, M, T, d, hd, 1, 0, out_dtype=cdt)
         dqkv = K.attn_bwd(qkv, o, do, lse, lens, B, T, a.n_head, a.d_k, 1.0 / math.sqrt(a.d_k))
@@ -353,9 +367,9 @@ class VariancePredictor(nn.Module):
         self.linear_layer = Linear(fs, 1)
         self.site = 0
 
-    def prep(self, cdt):
-        _conv_prep(self.conv_layer.conv1d_1.conv, cdt)
-        _conv_prep(self.conv_layer.conv1d_2.conv, cdt)
+    def prep(self, cdt, jobs=None):
+        _conv_prep(self.conv_layer.conv1d_1.conv, cdt, jobs)
+        _conv_prep(self.conv_layer.conv1d_2.conv, cdt, jobs)
 
     def fwd(self, x, x_t, lens, B, T, ctx):
         c = self.conv_layer
@@ -389,16 +403,14 @@ class VariancePredictor(nn.Module):
                               ddot=dpred.contiguous().view(-1), dot_w=lin.weight,
                               dw_dot=_g(lin.weight), db_dot=_g(lin.bias), lens=lens, seq_len=T,
                               p_out=p, seed=seed, site_out=self.site + 1, relu_y=h2,
-                              copy=ctx.copy)
+                              copy=ctx.copy, dbias_in=_g(c2.bias))
         dh2_c = _t(dh2, dh2_t)
-        K.colsum(dh2, M, c2.c_out, _g(c2.bias))
         K.conv_wgrad(dh2_c, u1_c, _g(c2.weight), M, T, c2.c_in, c2.c_out, c2.k, c2.padding)
         du1 = K.conv_gemm(dh2_c, c2._w_bwd, M, T, c2.c_out, c2.c_in, c2.k, c2.padding)
         dh1, dh1_t = K.ln_bwd(xh1, rs1, ln1.weight, ln1.bias, _g(ln1.weight), _g(ln1.bias),
                               dout=du1, p_out=p, seed=seed, site_out=self.site, relu_y=h1,
-                              copy=ctx.copy)
+                              copy=ctx.copy, dbias_in=_g(c1.bias))
         dh1_c = _t(dh1, dh1_t)
-        K.colsum(dh1, M, c1.c_out, _g(c1.bias))
         K.conv_wgrad(dh1_c, x_c, _g(c1.weight), M, T, c1.c_in, c1.c_out, c1.k, c1.padding)
         K.conv_gemm(dh1_c, c1._w_bwd, M, T, c1.c_out, c1.c_in, c1.k, c1.padding,
                     flags=K.EPI_ADD_AUX, aux=dx_acc, out=dx_acc)
@@ -441,9 +453,9 @@ class PostNet(nn.Module):
                           BatchNorm1d(chans[i + 1])) for i in range(n))
         self.site = 0
 
-    def prep(self, cdt):
+    def prep(self, cdt, jobs=None):
         for layer in self.convolutions:
-            _conv_prep(layer[0].conv, cdt)
+            _conv_prep(layer[0].conv, cdt, jobs)
 
     def fwd(self, x, x_t, B, T, ctx):
         """x: (M, n_mel) mel_linear output; returns postnet(x) + x."""
@@ -516,10 +528,12 @@ class SpeakerMetaEncoder(nn.Module):
             self.sigma_linear[0].bias, self.mu_linear.weight, self.mu_linear.bias, self.K, self.D)
         return GMMPrior(pi, mu, sigma, sigma_pre=sigma_pre, meta=meta, head=self)
 
+    def params(self):
+        return [self.pi_linear[0].weight, self.pi_linear[0].bias, self.sigma_linear[0].weight,
+                self.sigma_linear[0].bias, self.mu_linear.weight, self.mu_linear.bias]
+
     def grads(self):
-        return [_g(self.pi_linear[0].weight), _g(self.pi_linear[0].bias),
-                _g(self.sigma_linear[0].weight), _g(self.sigma_linear[0].bias),
-                _g(self.mu_linear.weight), _g(self.mu_linear.bias)]
+        return [_g(p) for p in self.params()]
 
 
 # ----------------------------------------------------------------------------- arena
@@ -631,7 +645,7 @@ class EncoderFn(torch.autograd.Function):
         for layer in enc.layer_stack:
             x, x_t, s = layer.fwd(x, x_t, lens, B, T, ctx)
             saved.append(s)
-        fctx.enc, fctx.saved, fctx.ids = enc, saved, (texts, accents)
+        fctx.enc, fctx.saved, fctx.ids, fctx.ctx = enc, saved, (texts, accents), ctx
         return x
 
     @staticmethod
@@ -640,9 +654,11 @@ class EncoderFn(torch.autograd.Function):
         dx = dx.contiguous()
         for layer, s in zip(reversed(enc.layer_stack), reversed(fctx.saved)):
             dx = layer.bwd(dx, s)
+            fctx.ctx.notify(fft_param_order(layer))
         texts, accents = fctx.ids
         K.embedding_bwd(dx, texts, _g(enc.src_word_emb.weight), 0)
         K.embedding_bwd(dx, accents, _g(enc.src_accent_emb.weight), 0)
+        fctx.ctx.notify([enc.src_accent_emb.weight, enc.src_word_emb.weight])
         fctx.saved = None
         return (None,) * 8
 
@@ -663,7 +679,7 @@ class VarianceAdaptorFn(torch.autograd.Function):
                                       va.energy_embedding.weight)
         cum, mel_len = K.lr_index(d_t.contiguous())
         x_lr, x_lr_t = K.lr_expand(x2, cum, T_dec, posenc=m.decoder.position_enc, copy=ctx.copy)
-        fctx.m, fctx.saved = m, (s_d, s_p, s_e, idx_p, idx_e, cum, speakers, B, Ts, T_dec)
+        fctx.m, fctx.saved = m, (s_d, s_p, s_e, idx_p, idx_e, cum, speakers, B, Ts, T_dec, ctx)
         side = x_lr_t if x_lr_t is not None else torch.empty(0, device=x_lr.device)
         fctx.mark_non_differentiable(mel_len, side)
         return x_lr, log_d, p, e, mel_len, side
@@ -672,7 +688,7 @@ class VarianceAdaptorFn(torch.autograd.Function):
     def backward(fctx, d_xlr, d_logd, d_p, d_e, _a, _b):
         m = fctx.m
         va = m.variance_adaptor
-        s_d, s_p, s_e, idx_p, idx_e, cum, speakers, B, Ts, T_dec = fctx.saved
+        s_d, s_p, s_e, idx_p, idx_e, cum, speakers, B, Ts, T_dec, ctx = fctx.saved
         d = m.encoder.d
         if d_xlr is None:
             dx = K.zeros((B * Ts, d), m._token.device)
@@ -681,12 +697,16 @@ class VarianceAdaptorFn(torch.autograd.Function):
         K.bucket_embed_bwd(dx, idx_e, _g(va.energy_embedding.weight))
         if d_e is not None:
             va.energy_predictor.bwd(d_e, s_e, dx)
+        ctx.notify([va.energy_embedding.weight] + vp_param_order(va.energy_predictor))
         K.bucket_embed_bwd(dx, idx_p, _g(va.pitch_embedding.weight))
         if d_p is not None:
             va.pitch_predictor.bwd(d_p, s_p, dx)
+        ctx.notify([va.pitch_embedding.weight] + vp_param_order(va.pitch_predictor))
         if d_logd is not None:
             va.duration_predictor.bwd(d_logd, s_d, dx)
+        ctx.notify(vp_param_order(va.duration_predictor))
         K.rowvec_add_bwd(dx, speakers, _g(m.speaker_emb.weight), B, Ts)
+        ctx.notify([m.speaker_emb.weight])
         fctx.saved = None
         return (None, dx) + (None,) * 10
 
@@ -699,7 +719,7 @@ class DecoderFn(torch.autograd.Function):
         for layer in dec.layer_stack:
             x, x_t, s = layer.fwd(x, x_t, lens, B, T, ctx)
             saved.append(s)
-        fctx.dec, fctx.saved = dec, saved
+        fctx.dec, fctx.saved, fctx.ctx = dec, saved, ctx
         side = x_t if x_t is not None else torch.empty(0, device=x.device)
         fctx.mark_non_differentiable(side)
         return x, side
@@ -709,6 +729,7 @@ class DecoderFn(torch.autograd.Function):
         dx = dx.contiguous()
         for layer, s in zip(reversed(fctx.dec.layer_stack), reversed(fctx.saved)):
             dx = layer.bwd(dx, s)
+            fctx.ctx.notify(fft_param_order(layer))
         fctx.saved = None
         return None, dx, None, None, None, None, None, None
 
@@ -742,10 +763,12 @@ class MelHeadFn(torch.autograd.Function):
             m.postnet.bwd(d_post, s, dm)
         else:
             dm = d_out
+        ctx.notify(postnet_param_order(m.postnet))
         dm_c = K.cast_bf16(dm) if ctx.copy is not None else dm
         K.colsum(dm, M, n_mel, _g(lin.bias))
         K.conv_wgrad(dm_c, x_c, _g(lin.weight), M, T, lin.in_features, n_mel, 1, 0)
         dx = K.conv_gemm(dm_c, lin._w_bwd, M, T, n_mel, lin.in_features, 1, 0)
+        ctx.notify([lin.weight, lin.bias])
         fctx.saved = None
         return None, dx, None, None, None, None, None
 
@@ -787,12 +810,15 @@ class FastSpeech2(nn.Module):
         self.compute_dtype = compute_dtype
         self._seed_rng = np.random.default_rng(0)
         self._arena = None
+        self._prep = None
+        self._hooks = {"grad": None}  # gradient-ready callback, see StepCtx.notify
         self.to(device)
 
     # -- plumbing ---------------------------------------------------------------------
     def _apply(self, fn, *args, **kwargs):
         r = super()._apply(fn, *args, **kwargs)
         self._arena = None  # parameters were re-materialised: rebuild the flat views lazily
+        self._prep = None
         return r
 
     def arena(self):
@@ -803,6 +829,7 @@ class FastSpeech2(nn.Module):
             self._arena = ParamArena(_flat_order(self), dev)
             self._token = torch.zeros((), device=dev, requires_grad=True)
             self.speaker_enc._tok = self._token
+            self.speaker_enc._model_hooks = self._hooks
         return self._arena
 
     def seed(self, s):
@@ -810,14 +837,26 @@ class FastSpeech2(nn.Module):
         self._seed_rng = np.random.default_rng(s)
 
     def prep_weights(self):
+        """Re-lay out (and cast) every weight for the GEMMs: one batched launch per step; the
+        job table (pointers into the arena and the compute-weight buffers) is built once."""
         cdt = self.compute_dtype
-        for b in list(self.encoder.layer_stack) + list(self.decoder.layer_stack):
-            b.prep(cdt)
-        va = self.variance_adaptor
-        for v in (va.duration_predictor, va.pitch_predictor, va.energy_predictor):
-            v.prep(cdt)
-        self.postnet.prep(cdt)
-        _linear_prep(self.mel_linear, cdt)
+        if self._prep is None or self._prep[0] != cdt:
+            jobs = []
+            for b in list(self.encoder.layer_stack) + list(self.decoder.layer_stack):
+                b.prep(cdt, jobs)
+            va = self.variance_adaptor
+            for v in (va.duration_predictor, va.pitch_predictor, va.energy_predictor):
+                v.prep(cdt, jobs)
+            self.postnet.prep(cdt, jobs)
+            _linear_prep(self.mel_linear, cdt, jobs=jobs)
+            rows, first = [], 0
+            for (w, co, ci, k, wf, wb) in jobs:
+                rows.append([w, co, ci, k, wf, wb, first, first + co * ci * k])
+                first += co * ci * k
+            table = torch.tensor(rows, dtype=torch.int64).to(self._arena.flat.device)
+            self._prep = (cdt, table, len(rows), first)
+        cdt, table, n, total = self._prep
+        K.lib.fs2_weight_prep_batch(K.code(cdt), K.ptr(table), n, total, K.stream())
 
     # -- forward ----------------------------------------------------------------------
     def forward(self, speakers, texts, src_lens, max_src_len, mels=None, mel_lens=None,
@@ -831,6 +870,7 @@ class FastSpeech2(nn.Module):
         self.prep_weights()
         ctx = StepCtx(self._seed_rng.integers(0, 2 ** 62), self.training, self.dropout,
                       self.compute_dtype)
+        ctx.hook = self._hooks["grad"]
         B, Ts = texts.shape
         max_src_len = int(max_src_len)
         max_mel_len = int(max_mel_len)

@@ -5,11 +5,15 @@ Single process: ``train_step`` is line-for-line the reference's step semantics
 (forward, FastSpeech2Loss backward, negated speaker-prior log-likelihood backward,
 clip_grad_norm_, ScheduledOptim.step_and_update_lr, zero_grad).
 
-Data parallel: one process per GPU, batch sharded by utterance.  Each rank
-normalises its masked means by the *global* valid counts and the GMM term by the global
-batch, so the all-reduced (summed) gradient equals the 1-process gradient of the global
-batch; the sum runs over RCCL on the flat gradient buffer.  BatchNorm statistics stay
-per rank (DataParallel's per-replica semantics).
+Data parallel: one process per GPU, batch sharded by utterance.
+* Each rank normalises its masked means by the *global* valid counts and the GMM term by
+  the global batch (one 3-float all-reduce of device-side counts before the forward, no host
+  sync), so the summed gradient equals the 1-process gradient of the global batch.
+* Gradients are all-reduced (sum) over RCCL in ~32 MB buckets of the flat fp32 gradient
+  buffer.  The buffer is laid out in reverse backward order, every block's backward reports
+  its parameters as final (``StepCtx.notify``), and a bucket's all-reduce is launched as soon
+  as all of its parameters are final, so communication overlaps the rest of the backward.
+* BatchNorm statistics stay per rank (DataParallel's per-replica semantics).
 """
 import torch
 import torch.distributed as dist
@@ -33,42 +37,89 @@ def train_step(model, optimizer, Loss, eLoss, batch, grad_clip_thresh=1.0, grad_
     return losses, eloss, gnorm, output
 
 
+class GradBuckets:
+    """Bucketed, backward-overlapped all-reduce of the arena's flat gradient buffer."""
+
+    def __init__(self, arena, group=None, bucket_bytes=32 << 20):
+        self.arena, self.group = arena, group
+        index = {id(p): i for i, p in enumerate(arena.params)}
+        buckets, cur, size = [], [], 0
+        for i, p in enumerate(arena.params):
+            cur.append(i)
+            size += p.numel() * 4
+            if size >= bucket_bytes:
+                buckets.append(cur)
+                cur, size = [], 0
+        if cur:
+            buckets.append(cur)
+        self.bucket_of = {pid: b for b, idxs in enumerate(buckets) for pid in
+                          (id(arena.params[i]) for i in idxs)}
+        self.ranges = []
+        for idxs in buckets:
+            last = idxs[-1]
+            self.ranges.append((arena.offsets[idxs[0]],
+                                arena.offsets[last] + arena.params[last].numel()))
+        self.sizes = [len(idxs) for idxs in buckets]
+        del index
+        self.reset()
+
+    def reset(self):
+        self.left = list(self.sizes)
+        self.next = 0  # buckets launch strictly in index order (same order on every rank)
+        self.works = []
+
+    def _launch(self, b):
+        s, e = self.ranges[b]
+        self.works.append(dist.all_reduce(self.arena.grad[s:e], group=self.group, async_op=True))
+
+    def ready(self, params):
+        for p in params:
+            self.left[self.bucket_of[id(p)]] -= 1
+        while self.next < len(self.sizes) and self.left[self.next] == 0:
+            self._launch(self.next)
+            self.next += 1
+
+    def finish(self):
+        while self.next < len(self.sizes):  # includes parameters without a gradient this step
+            self._launch(self.next)
+            self.next += 1
+        for w in self.works:
+            w.wait()  # stream-ordered: the clip/Adam kernels queue behind the collectives
+        self.reset()
+
+
 class Trainer:
     """Model + loss + optimiser for one rank (``world_size`` 1 = plain single-GPU)."""
 
     def __init__(self, model, preprocess_config, model_config, train_config, current_step=0,
-                 process_group=None):
+                 process_group=None, bucket_bytes=32 << 20):
         self.model = model
         self.Loss = FastSpeech2Loss(preprocess_config, model_config)
         self.eLoss = SpeakerMetaEncLoss(preprocess_config, model_config)
         self.opt = ScheduledOptim(model, train_config, model_config, current_step)
         self.clip = train_config["optimizer"]["grad_clip_thresh"]
         self.pg = process_group
-        self.world = dist.get_world_size(process_group) if (dist.is_initialized()) else 1
+        self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
+        self.buckets = None
         if self.world > 1:
+            arena = model.arena()
             with torch.no_grad():  # identical initial weights on every rank
-                dist.broadcast(model.arena().flat, src=0, group=process_group)
+                dist.broadcast(arena.flat, src=0, group=process_group)
+            self.buckets = GradBuckets(arena, process_group, bucket_bytes)
+            model._hooks["grad"] = self.buckets.ready
 
-    def _global_norm(self, batch):
-        """Global denominators [mel elements, phonemes] and batch size via one tiny all-reduce."""
-        mel_lens, src_lens = batch[7], batch[4]
+    def _global_denominators(self, batch):
         T_dec = min(int(batch[8]), self.model.decoder.max_seq_len)
-        n_mel = self.model.mel_linear.out_features
-        loc = torch.stack([mel_lens.clamp(max=T_dec).sum().float() * n_mel,
-                           src_lens.sum().float(), torch.tensor(float(src_lens.numel()),
-                                                                device=src_lens.device)])
-        glob = loc.clone()
-        dist.all_reduce(glob, group=self.pg)
-        return glob
+        counts = K.dp_counts(batch[4].contiguous().long(), batch[7].contiguous().long(),
+                             int(batch[5]), T_dec, self.model.mel_linear.out_features)
+        dist.all_reduce(counts, group=self.pg)
+        return counts
 
     def step(self, batch):
         if self.world > 1:
-            glob = self._global_norm(batch)
-            self.Loss.denoms = glob[:2].contiguous()
-            self.eLoss.scale = float(batch[4].numel()) / float(glob[2].item())
+            glob = self._global_denominators(batch)
+            self.Loss.denoms = glob[0:2]
+            self.eLoss.denom = glob[2:3]
             return train_step(self.model, self.opt, self.Loss, self.eLoss, batch, self.clip,
-                              grad_sync=self._all_reduce)
+                              grad_sync=self.buckets.finish)
         return train_step(self.model, self.opt, self.Loss, self.eLoss, batch, self.clip)
-
-    def _all_reduce(self):
-        dist.all_reduce(self.model.arena().grad, group=self.pg)

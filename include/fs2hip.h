@@ -63,20 +63,21 @@ int fs2_conv_gemm(int dtype, const void* x, int64_t ldx, const void* wk, void* y
 int fs2_conv_weight_prep(int dtype, const float* w, int64_t c_out, int64_t c_in, int taps,
                          void* w_fwd, void* w_bwd, void* stream);
 /* The same for every layer of the model in one launch: jobs (device, int64) holds
- * n_jobs rows {w, c_out, c_in, taps, w_fwd, w_bwd, first, end} where [first, end) numbers
- * the job's elements consecutively and total = end of the last job.                  */
-int fs2_weight_prep_batch(int dtype, const int64_t* jobs, int n_jobs, int64_t total,
-                          void* stream);
+ * n_jobs rows {w, c_out, c_in, taps, w_fwd, w_bwd, 0, 0}; max_c_out / max_c_in bound the
+ * rows' c_out / c_in; taps <= 9.                                                       */
+int fs2_weight_prep_batch(int dtype, const int64_t* jobs, int n_jobs, int64_t max_c_out,
+                          int64_t max_c_in, void* stream);
 
-/* Weight gradient, accumulated into the fp32 (c_out, c_in, taps) master-gradient layout:
+/* Weight (and optionally bias) gradient, accumulated into the fp32 master-gradient layout:
  *   dw[o, c, j] += sum_r dy[r, o] * x[r + j - pad, c]
+ *   db[o]       += sum_r dy[r, o]                          (db may be NULL)
  * Split-K over rows with per-split fp32 slabs in `ws` and an in-order reduction
  * (bitwise reproducible).  `ws_bytes` >= fs2_conv_wgrad_ws_bytes(...).
- * Replaces the weight half of ConvolutionBackward / AddmmBackward.                     */
+ * Replaces the weight/bias half of ConvolutionBackward / AddmmBackward.                */
 int64_t fs2_conv_wgrad_ws_bytes(int64_t rows, int64_t c_in, int64_t c_out, int taps);
 int fs2_conv_wgrad(int dtype, const void* dy, int64_t ldy, const void* x, int64_t ldx, float* dw,
-                   int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out, int taps, int pad,
-                   float* ws, int64_t ws_bytes, void* stream);
+                   float* db, int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out, int taps,
+                   int pad, float* ws, int64_t ws_bytes, void* stream);
 
 /* Column sums (bias / LayerNorm-affine / BatchNorm gradients):
  *   out[c] (+)= sum_r x[r, c]   in a fixed order (partials in ws, then in-order sum).   */

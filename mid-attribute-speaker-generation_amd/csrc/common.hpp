@@ -33,6 +33,19 @@ int launch_status(const char* what);
 //   out[c] (+)= sum_p part[p * cols + c]
 int colsum_final_launch(const float* part, int64_t nparts, int64_t cols, float* out, int acc,
                         hipStream_t st);
+struct ColsumJob {
+  const float* part;
+  int64_t nparts, cols;
+  float* out;
+};
+struct ColsumJobs {
+  ColsumJob job[6];
+  int n, acc;
+  void add(const float* part, int64_t nparts, int64_t cols, float* out) {
+    job[n++] = ColsumJob{part, nparts, cols, out};
+  }
+};
+int colsum_final_multi_launch(const ColsumJobs& jobs, hipStream_t st);
 int colsum_launch(const float* x, int64_t ldx, int64_t rows, int64_t cols, float* out, int acc,
                   float* ws, hipStream_t st);
 
@@ -41,6 +54,13 @@ int conv_gemm_bf16_launch(const void* x, int64_t ldx, const void* wk, void* y, i
                           int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out, int taps,
                           int pad, const float* bias, int flags, const void* aux, int64_t ld_aux,
                           hipStream_t st);
+int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, int64_t ldy,
+                          int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out, int taps,
+                          int pad, const float* bias, int flags, const void* aux, int64_t ld_aux,
+                          hipStream_t st);
+int conv_wgrad_glds_launch(const void* dy, int64_t ldy, const void* x, int64_t ldx, float* dw,
+                           float* db, int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out,
+                           int taps, int pad, int splits, float* ws, hipStream_t st);
 int conv_wgrad_bf16_launch(const void* dy, int64_t ldy, const void* x, int64_t ldx, float* slab,
                            int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out, int taps,
                            int pad, int splits, hipStream_t st);

@@ -326,6 +326,37 @@ __global__ __launch_bounds__(1024) void colsum_final(const float* part, int64_t 
   }
 }
 
+// Several independent finals in one launch (blockIdx.y = job), each as colsum_final.
+__global__ __launch_bounds__(1024) void colsum_final_multi(ColsumJobs jobs) {
+  __shared__ float red[16][65];
+  const ColsumJob& jb = jobs.job[blockIdx.y];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int64_t c = (int64_t)blockIdx.x * 64 + tx;
+  if ((int64_t)blockIdx.x * 64 >= jb.cols) return;  // block-uniform
+  float s = 0.f;
+  if (c < jb.cols) {
+#pragma unroll 4
+    for (int64_t p = ty; p < jb.nparts; p += 16) s += jb.part[p * jb.cols + c];
+  }
+  red[ty][tx] = s;
+  __syncthreads();
+  if (ty == 0 && c < jb.cols) {
+    float t = 0.f;
+#pragma unroll
+    for (int y = 0; y < 16; ++y) t += red[y][tx];
+    jb.out[c] = jobs.acc ? jb.out[c] + t : t;
+  }
+}
+
+int colsum_final_multi_launch(const ColsumJobs& jobs, hipStream_t st) {
+  if (jobs.n == 0) return FS2_OK;
+  int64_t maxc = 0;
+  for (int i = 0; i < jobs.n; ++i) maxc = jobs.job[i].cols > maxc ? jobs.job[i].cols : maxc;
+  dim3 grid((unsigned)((maxc + 63) / 64), (unsigned)jobs.n);
+  colsum_final_multi<<<grid, 1024, 0, st>>>(jobs);
+  return launch_status("colsum_final_multi");
+}
+
 int colsum_launch(const float* x, int64_t ldx, int64_t rows, int64_t cols, float* out, int acc,
                   float* ws, hipStream_t st) {
   const int64_t nparts = (rows + CS_ROWS - 1) / CS_ROWS;
@@ -346,10 +377,15 @@ int colsum_final_launch(const float* part, int64_t nparts, int64_t cols, float* 
 static int wgrad_splits(int64_t rows, int64_t c_in, int64_t c_out, int taps) {
   const int64_t Kp = (int64_t)taps * c_in;
   const int64_t tiles = ((c_out + 127) / 128) * ((Kp + 127) / 128);
-  int64_t s = (512 + tiles - 1) / tiles;
-  int64_t max_s = rows / 512;  // keep >= 16 k-tiles per split
+  // ~640 blocks (2-3 per CU), >= 4 k-tiles of 64 rows per split, and the fp32 slabs
+  // (written once, read once by the reduction) kept to ~24 MB unless that leaves < 4 splits.
+  int64_t s = (640 + tiles - 1) / tiles;
+  const int64_t slab = c_out * Kp * 4;
+  int64_t max_s = rows / 256;
+  const int64_t mem_s = (24 << 20) / slab > 4 ? (24 << 20) / slab : 4;
+  if (max_s > mem_s) max_s = mem_s;
   if (s > max_s) s = max_s;
-  if (s > 16) s = 16;
+  if (s > 64) s = 64;
   if (s < 1) s = 1;
   return (int)s;
 }
@@ -409,17 +445,29 @@ int fs2_conv_weight_prep(int dtype, const float* w, int64_t c_out, int64_t c_in,
 }
 
 int64_t fs2_conv_wgrad_ws_bytes(int64_t rows, int64_t c_in, int64_t c_out, int taps) {
-  return (int64_t)wgrad_splits(rows, c_in, c_out, taps) * c_out * taps * c_in * 4;
+  const int64_t S = wgrad_splits(rows, c_in, c_out, taps);
+  const int64_t bias_part = S * c_out > ((rows + CS_ROWS - 1) / CS_ROWS) * c_out
+                                ? S * c_out : ((rows + CS_ROWS - 1) / CS_ROWS) * c_out;
+  return (S * c_out * taps * c_in + bias_part) * 4;
 }
 
 int fs2_conv_wgrad(int dtype, const void* dy, int64_t ldy, const void* x, int64_t ldx, float* dw,
-                   int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out, int taps, int pad,
-                   float* ws, int64_t ws_bytes, void* stream) {
+                   float* db, int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out, int taps,
+                   int pad, float* ws, int64_t ws_bytes, void* stream) {
+  const int64_t slab_floats = (int64_t)wgrad_splits(rows, c_in, c_out, taps) * c_out * taps * c_in;
   if (dtype == FS2_BF16) {
     FS2_CHECK_ARG(ws_bytes >= fs2_conv_wgrad_ws_bytes(rows, c_in, c_out, taps),
                   "fs2_conv_wgrad: workspace too small");
     if (rows == 0) return FS2_OK;
     const int S = wgrad_splits(rows, c_in, c_out, taps);
+    static int old = -1;
+    if (old < 0) {
+      const char* e = getenv("FS2_GEMM_OLD");
+      old = e && e[0] == '1';
+    }
+    if (!old)
+      return conv_wgrad_glds_launch(dy, ldy, x, ldx, dw, db, rows, seq_len, c_in, c_out, taps, pad,
+                                    S, ws, as_stream(stream));
     int rc = conv_wgrad_bf16_launch(dy, ldy, x, ldx, ws, rows, seq_len, c_in, c_out, taps, pad, S,
                                     as_stream(stream));
     if (rc) return rc;
@@ -427,6 +475,7 @@ int fs2_conv_wgrad(int dtype, const void* dy, int64_t ldy, const void* x, int64_
     unsigned blocks = (unsigned)((total + 255) / 256);
     if (blocks > 4096) blocks = 4096;
     wgrad_reduce<<<blocks, 256, 0, as_stream(stream)>>>(ws, S, (int)c_out, (int)c_in, taps, dw);
+    if (db) return colsum_bf16_launch(dy, ldy, rows, c_out, db, 1, ws + slab_floats, as_stream(stream));
     return launch_status("fs2_conv_wgrad");
   }
   if (dtype != FS2_F32) {
@@ -450,6 +499,7 @@ int fs2_conv_wgrad(int dtype, const void* dy, int64_t ldy, const void* x, int64_
   unsigned blocks = (unsigned)((total + 255) / 256);
   if (blocks > 4096) blocks = 4096;
   wgrad_reduce<<<blocks, 256, 0, st>>>(ws, S, (int)c_out, (int)c_in, taps, dw);
+  if (db) return colsum_launch((const float*)dy, ldy, rows, c_out, db, 1, ws + slab_floats, st);
   return launch_status("fs2_conv_wgrad");
 }
 

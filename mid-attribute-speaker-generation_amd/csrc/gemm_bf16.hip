@@ -297,33 +297,48 @@ __global__ void weight_prep_bf16(const float* w, int Cout, int Cin, int taps, u1
   }
 }
 
-// All layers' re-layouts in one launch.  jobs[j] = {src, c_out, c_in, taps, w_fwd, w_bwd,
-// first element, end element} (int64), elements numbered consecutively over the jobs.
+// All layers' re-layouts in one launch.  jobs[j] = {src, c_out, c_in, taps, w_fwd, w_bwd, -, -}
+// (int64).  Block (x, j) re-lays out one tile of job j: 64 output channels x CT input channels
+// x all taps.  The source rows are read as contiguous CT*taps runs into LDS (already cast),
+// then w_fwd is written as CT-long runs per (o, tap) and w_bwd as 64-long runs per (c, tap).
 template <typename OutT>
-__global__ void weight_prep_batch(const int64_t* __restrict__ jobs, int n_jobs, int64_t total) {
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
-       e += (int64_t)gridDim.x * blockDim.x) {
-    int lo = 0, hi = n_jobs - 1;
-    while (lo < hi) {  // last job whose first element <= e
-      const int mid = (lo + hi + 1) >> 1;
-      if (jobs[mid * 8 + 6] <= e) lo = mid;
-      else hi = mid - 1;
+__global__ __launch_bounds__(256) void weight_prep_tiles(const int64_t* __restrict__ jobs,
+                                                         int tiles_c_max) {
+  constexpr int CT = sizeof(OutT) == 2 ? 32 : 16;
+  constexpr int MAXT = 9;
+  constexpr int LD = CT * MAXT + 1;  // odd row stride (in OutT units of 2 or 4 B)
+  __shared__ OutT tile[64 * LD];
+  const int64_t* jb = jobs + (int64_t)blockIdx.y * 8;
+  const float* w = (const float*)jb[0];
+  const int Cout = (int)jb[1], Cin = (int)jb[2], taps = (int)jb[3];
+  OutT* wf = (OutT*)jb[4];
+  OutT* wb = (OutT*)jb[5];
+  const int tc = blockIdx.x % tiles_c_max, to = blockIdx.x / tiles_c_max;
+  const int o0 = to * 64, c0 = tc * CT;
+  if (o0 >= Cout || c0 >= Cin) return;
+  const int no = Cout - o0 < 64 ? Cout - o0 : 64;
+  const int nc = Cin - c0 < CT ? Cin - c0 : CT;
+  const int run = nc * taps;  // contiguous source elements per row
+  const int64_t Q = (int64_t)Cin * taps;
+  for (int e = threadIdx.x; e < no * run; e += 256) {
+    const int r = e / run, q = e - r * run;
+    const float v = w[(int64_t)(o0 + r) * Q + (int64_t)c0 * taps + q];
+    if constexpr (sizeof(OutT) == 2) tile[r * LD + q] = f2bf(v);
+    else tile[r * LD + q] = v;
+  }
+  __syncthreads();
+  if (wf) {  // wf[o, j*Cin + c]
+    for (int e = threadIdx.x; e < no * taps * CT; e += 256) {
+      const int c = e % CT, rj = e / CT, j = rj % taps, r = rj / taps;
+      if (c < nc) wf[(int64_t)(o0 + r) * Q + (int64_t)j * Cin + c0 + c] = tile[r * LD + c * taps + j];
     }
-    const int64_t* jb = jobs + lo * 8;
-    const float* w = (const float*)jb[0];
-    const int64_t Cout = jb[1], Cin = jb[2], taps = jb[3];
-    OutT* wf = (OutT*)jb[4];
-    OutT* wb = (OutT*)jb[5];
-    const int64_t i = e - jb[6];
-    const int64_t o = i / (Cin * taps);
-    const int64_t rem = i - o * Cin * taps;
-    const int64_t c = rem / taps, j = rem - c * taps;
-    const float v = w[i];
-    OutT ov;
-    if constexpr (sizeof(OutT) == 2) ov = f2bf(v);
-    else ov = v;
-    if (wf) wf[o * taps * Cin + j * Cin + c] = ov;
-    if (wb) wb[c * taps * Cout + (taps - 1 - j) * Cout + o] = ov;
+  }
+  if (wb) {  // wb[c*taps + taps-1-j, o]
+    for (int e = threadIdx.x; e < nc * taps * 64; e += 256) {
+      const int r = e & 63, cj = e >> 6, j = cj % taps, c = cj / taps;
+      if (r < no)
+        wb[((int64_t)(c0 + c) * taps + (taps - 1 - j)) * Cout + o0 + r] = tile[r * LD + c * taps + j];
+    }
   }
 }
 
@@ -355,6 +370,14 @@ int conv_gemm_bf16_launch(const void* x, int64_t ldx, const void* wk, void* y, i
                           int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out, int taps,
                           int pad, const float* bias, int flags, const void* aux, int64_t ld_aux,
                           hipStream_t st) {
+  static int old = -1;
+  if (old < 0) {
+    const char* e = getenv("FS2_GEMM_OLD");
+    old = e && e[0] == '1';
+  }
+  if (!old)
+    return conv_gemm_glds_launch(x, ldx, wk, y, ldy, rows, seq_len, c_in, c_out, taps, pad, bias,
+                                 flags, aux, ld_aux, st);
   FS2_CHECK_ARG(c_in % 8 == 0 && ldx % 8 == 0, "fs2_conv_gemm(bf16): c_in/ldx must be multiples of 8");
   ConvArgsB a{(const u16*)x, ldx, (const u16*)wk, y, ldy, rows, seq_len, (int)c_in, (int)c_out,
               taps, pad, (int)(taps * c_in), bias, flags, aux, ld_aux};
@@ -402,15 +425,16 @@ int colsum_bf16_launch(const void* x, int64_t ldx, int64_t rows, int64_t cols, f
 
 }  // namespace fs2
 
-extern "C" int fs2_weight_prep_batch(int dtype, const int64_t* jobs, int n_jobs, int64_t total,
-                                     void* stream) {
-  if (n_jobs <= 0 || total <= 0) return FS2_OK;
-  int64_t b = (total + 255) / 256;
-  if (b > 8192) b = 8192;
+extern "C" int fs2_weight_prep_batch(int dtype, const int64_t* jobs, int n_jobs, int64_t max_c_out,
+                                     int64_t max_c_in, void* stream) {
+  if (n_jobs <= 0 || max_c_out <= 0 || max_c_in <= 0) return FS2_OK;
+  const int ct = dtype == FS2_BF16 ? 32 : 16;
+  const int tiles_c = (int)((max_c_in + ct - 1) / ct);
+  dim3 grid((unsigned)(tiles_c * ((max_c_out + 63) / 64)), (unsigned)n_jobs);
   if (dtype == FS2_BF16)
-    fs2::weight_prep_batch<unsigned short><<<(unsigned)b, 256, 0, as_stream(stream)>>>(jobs, n_jobs, total);
+    fs2::weight_prep_tiles<unsigned short><<<grid, 256, 0, as_stream(stream)>>>(jobs, tiles_c);
   else if (dtype == FS2_F32)
-    fs2::weight_prep_batch<float><<<(unsigned)b, 256, 0, as_stream(stream)>>>(jobs, n_jobs, total);
+    fs2::weight_prep_tiles<float><<<grid, 256, 0, as_stream(stream)>>>(jobs, tiles_c);
   else {
     fs2::set_error("fs2_weight_prep_batch: dtype %d not built", dtype);
     return FS2_ERR_DTYPE;

@@ -1,0 +1,663 @@
+// bf16 implicit-GEMM Conv1d / Linear, forward and dX ("NT"), staged by LDS-DMA.
+//
+//   y[r, o] = epilogue( sum_{j,c} wk[o, j*Cin + c] * x[r + j - pad, c] )
+//
+// Tile BM x BN x 64, 4 waves (2 x 2), v_mfma_f32_16x16x32_bf16.  Both operand tiles are
+// filled with global_load_lds_dwordx4: one wave-instruction writes 1 KiB = 8 rows x 128 B of
+// a lane-linear [rows][64] bf16 image.  The image is XOR-swizzled on the SOURCE address
+// (16-B chunk c of row R lands at chunk c ^ ((R >> 1) & 7)), so the ds_read_b128 fragment
+// reads of 16 consecutive rows hit 16 distinct 16-B bank slots.  The conv tap shift lives in
+// the per-lane source address: rows outside their utterance (and rows/channels past the
+// matrix edge) read a 16-B zero line instead, so padding costs no branches in the loop.
+// Row-dependent address parts (utterance start, frame index) are computed once per block;
+// per k-tile only the tap index and channel offset change (scalar when Cin % 64 == 0).
+//
+// STAGES = 1: load; vmcnt(0); barrier; MFMA; barrier (occupancy 3-4 blocks/CU hides the
+//             load phase of one block under the MFMA phase of the others).
+// STAGES = 2: the next tile's DMA is issued before the current tile's MFMAs and stays in
+//             flight across the barrier (counted vmcnt, raw s_barrier).
+//
+// Blocks are renumbered XCD-aware (bijective remap): each XCD runs a contiguous range of
+// (m, n) tiles, n fastest, so an A row band is fetched from HBM once per XCD L2.
+//
+// Epilogue: accumulators go through LDS (fp32, 132-float rows, conflict-free writes) and
+// leave as 8-element row vectors: bias, residual/aux add, ReLU, ReLU-mask and the bf16 cast
+// are applied on 16-B (bf16) / 32-B (fp32) coalesced stores.
+#include "common.hpp"
+
+namespace fs2 {
+
+typedef __bf16 bf16x8g __attribute__((ext_vector_type(8)));
+typedef unsigned short u16;
+
+__device__ __attribute__((aligned(128))) uint4 g_zero_line[8];  // zero source for OOB chunks
+
+struct GldsArgs {
+  const u16* x;
+  int64_t ldx;
+  const u16* w;
+  void* y;
+  int64_t ldy;
+  int64_t M, T;
+  int Cin, N, taps, pad, K;
+  const float* bias;
+  int flags;
+  const void* aux;
+  int64_t ld_aux;
+  int tiles_m, tiles_n;
+  int vec;  // 8-wide epilogue legal (N, ldy, ld_aux multiples of 8; aligned pointers)
+};
+
+FS2_DEV void glds16(const void* src, u16* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds(
+      (const __attribute__((address_space(1))) void*)src,
+      (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+
+FS2_DEV float bfv(u16 v) { return __uint_as_float(((uint32_t)v) << 16); }
+FS2_DEV u16 fbv(float f) {
+  __bf16 b = (__bf16)f;
+  return *reinterpret_cast<u16*>(&b);
+}
+
+template <int BM, int BN, int STAGES, bool TAPALIGNED>
+__global__ __launch_bounds__(256) void conv_gemm_nt_glds(GldsArgs a) {
+  constexpr int BK = 64;
+  constexpr int AW = BM / 32, BW = BN / 32;  // glds per wave per tile (8 rows each)
+  constexpr int MI = BM / 32, NI = BN / 32;  // 16x16 fragments per wave (2x2 waves)
+  constexpr int STAGE_E = (BM + BN) * BK;    // elements per stage
+  constexpr int EPI_LD = BN + 4;             // fp32 epilogue row stride
+  constexpr int EPI_E = (BM / 2) * EPI_LD * 2;
+  constexpr int SMEM_E = STAGES * STAGE_E > EPI_E ? STAGES * STAGE_E : EPI_E;
+  __shared__ __attribute__((aligned(1024))) u16 smem[SMEM_E];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int g = lane >> 4, r16 = lane & 15;
+
+  // XCD-aware bijective renumbering of the 1-D grid
+  const int nwg = a.tiles_m * a.tiles_n;
+  const int orig = blockIdx.x, xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int tn = wg % a.tiles_n, tm = wg / a.tiles_n;
+  const int64_t m0 = (int64_t)tm * BM;
+  const int n0 = tn * BN;
+
+  // ---- per-lane source descriptors (fixed over the k loop)
+  const int lrow = lane >> 3;  // row within the 8-row piece
+  const u16* zero = reinterpret_cast<const u16*>(g_zero_line);
+  int64_t a_base[AW];  // element offset of the row's utterance start (or -1: row invalid)
+  int a_t[AW];         // frame index within the utterance
+  int a_lc[AW];        // logical 16-B chunk this lane fetches
+#pragma unroll
+  for (int i = 0; i < AW; ++i) {
+    const int R = (wave * AW + i) * 8 + lrow;
+    const int64_t m = m0 + R;
+    a_lc[i] = (lane & 7) ^ ((R >> 1) & 7);
+    if (m < a.M) {
+      const int64_t s = m / a.T;
+      a_t[i] = (int)(m - s * a.T);
+      a_base[i] = s * a.T;
+    } else {
+      a_t[i] = 0;
+      a_base[i] = -1;
+    }
+  }
+  const u16* b_src[BW];
+  int b_lc[BW];
+#pragma unroll
+  for (int i = 0; i < BW; ++i) {
+    const int R = (wave * BW + i) * 8 + lrow;
+    const int n = n0 + R;
+    b_lc[i] = (lane & 7) ^ ((R >> 1) & 7);
+    b_src[i] = n < a.N ? a.w + (int64_t)n * a.K + b_lc[i] * 8 : nullptr;
+  }
+
+  const int nk = (a.K + BK - 1) / BK;
+  auto issue = [&](int kt, int stage) {
+    u16* As = smem + stage * STAGE_E;
+    u16* Bs = As + BM * BK;
+    const int k0 = kt * BK;
+    int j0 = 0, c0 = 0;
+    if constexpr (TAPALIGNED) {
+      j0 = k0 / a.Cin;
+      c0 = k0 - j0 * a.Cin;
+    }
+#pragma unroll
+    for (int i = 0; i < AW; ++i) {
+      const u16* src = zero;
+      int j = j0, c = c0 + a_lc[i] * 8;
+      bool kok = true;
+      if constexpr (!TAPALIGNED) {
+        const int k = k0 + a_lc[i] * 8;
+        kok = k < a.K;
+        j = k / a.Cin;
+        c = k - j * a.Cin;
+      }
+      const int tt = a_t[i] + j - a.pad;
+      if (kok && a_base[i] >= 0 && tt >= 0 && tt < a.T)
+        src = a.x + (a_base[i] + tt) * a.ldx + c;
+      glds16(src, As + (wave * AW + i) * 8 * BK);
+    }
+#pragma unroll
+    for (int i = 0; i < BW; ++i) {
+      const u16* src = zero;
+      bool kok = true;
+      if constexpr (!TAPALIGNED) kok = k0 + b_lc[i] * 8 < a.K;
+      if (b_src[i] && kok) src = b_src[i] + k0;
+      glds16(src, Bs + (wave * BW + i) * 8 * BK);
+    }
+  };
+
+  f32x4 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // fragment element offsets (swizzle depends only on r16 because row bases are 16-aligned)
+  const int sw = (r16 >> 1) & 7;
+  const int fo0 = r16 * BK + ((0 * 4 + g) ^ sw) * 8;
+  const int fo1 = r16 * BK + ((1 * 4 + g) ^ sw) * 8;
+  auto compute = [&](int stage) {
+    const u16* As = smem + stage * STAGE_E + wm * (BM / 2) * BK;
+    const u16* Bs = smem + stage * STAGE_E + BM * BK + wn * (BN / 2) * BK;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int fo = ks ? fo1 : fo0;
+      bf16x8g fa[MI], fb[NI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) fa[i] = *reinterpret_cast<const bf16x8g*>(As + i * 16 * BK + fo);
+#pragma unroll
+      for (int j = 0; j < NI; ++j) fb[j] = *reinterpret_cast<const bf16x8g*>(Bs + j * 16 * BK + fo);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  if constexpr (STAGES == 1) {
+    for (int kt = 0; kt < nk; ++kt) {
+      issue(kt, 0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      compute(0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+  } else {
+    issue(0, 0);
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt + 1 < nk) {
+        issue(kt + 1, (kt + 1) & 1);
+        if constexpr (AW + BW == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else if constexpr (AW + BW == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        else if constexpr (AW + BW == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();
+      compute(kt & 1);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+  }
+
+  // ---- epilogue through LDS, one half (wm) at a time
+  float* Cs = reinterpret_cast<float*>(smem);
+  const bool out_bf16 = a.flags & FS2_EPI_OUT_BF16, aux_bf16 = a.flags & FS2_EPI_AUX_BF16;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (wm == h) {
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            Cs[(i * 16 + 4 * g + r) * EPI_LD + wn * (BN / 2) + j * 16 + r16] = acc[i][j][r];
+    }
+    __syncthreads();
+    constexpr int TPR = BN / 8;           // threads per row
+    constexpr int RPP = 256 / TPR;        // rows per pass
+    const int cc = (tid % TPR) * 8;
+    const int n = n0 + cc;
+#pragma unroll
+    for (int p = 0; p < (BM / 2) / RPP; ++p) {
+      const int rr = p * RPP + tid / TPR;
+      const int64_t m = m0 + h * (BM / 2) + rr;
+      if (m >= a.M || n >= a.N) continue;
+      float v[8];
+      const f32x4 lo = *reinterpret_cast<const f32x4*>(Cs + rr * EPI_LD + cc);
+      const f32x4 hi = *reinterpret_cast<const f32x4*>(Cs + rr * EPI_LD + cc + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = lo[e];
+        v[e + 4] = hi[e];
+      }
+      if (a.vec) {
+        if (a.flags & FS2_EPI_BIAS) {
+          const f32x4 b0 = *reinterpret_cast<const f32x4*>(a.bias + n);
+          const f32x4 b1 = *reinterpret_cast<const f32x4*>(a.bias + n + 4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[e] += b0[e];
+            v[e + 4] += b1[e];
+          }
+        }
+        float av[8];
+        if (a.flags & (FS2_EPI_ADD_AUX | FS2_EPI_RELU_MASK_AUX)) {
+          if (aux_bf16) {
+            const uint4 raw = *reinterpret_cast<const uint4*>((const u16*)a.aux + m * a.ld_aux + n);
+            const uint32_t wv[4] = {raw.x, raw.y, raw.z, raw.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              av[2 * e] = __uint_as_float(wv[e] << 16);
+              av[2 * e + 1] = __uint_as_float(wv[e] & 0xffff0000u);
+            }
+          } else {
+            const float* ap = (const float*)a.aux + m * a.ld_aux + n;
+            const f32x4 a0 = *reinterpret_cast<const f32x4*>(ap);
+            const f32x4 a1 = *reinterpret_cast<const f32x4*>(ap + 4);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              av[e] = a0[e];
+              av[e + 4] = a1[e];
+            }
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          if (a.flags & FS2_EPI_ADD_AUX) v[e] += av[e];
+          if (a.flags & FS2_EPI_RELU) v[e] = fmaxf(v[e], 0.f);
+          if (a.flags & FS2_EPI_RELU_MASK_AUX) v[e] = av[e] > 0.f ? v[e] : 0.f;
+        }
+        if (out_bf16) {
+          uint4 o;
+          o.x = (uint32_t)fbv(v[0]) | ((uint32_t)fbv(v[1]) << 16);
+          o.y = (uint32_t)fbv(v[2]) | ((uint32_t)fbv(v[3]) << 16);
+          o.z = (uint32_t)fbv(v[4]) | ((uint32_t)fbv(v[5]) << 16);
+          o.w = (uint32_t)fbv(v[6]) | ((uint32_t)fbv(v[7]) << 16);
+          *reinterpret_cast<uint4*>((u16*)a.y + m * a.ldy + n) = o;
+        } else {
+          float* yp = (float*)a.y + m * a.ldy + n;
+          *reinterpret_cast<f32x4*>(yp) = f32x4{v[0], v[1], v[2], v[3]};
+          *reinterpret_cast<f32x4*>(yp + 4) = f32x4{v[4], v[5], v[6], v[7]};
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          if (n + e >= a.N) break;
+          float x = v[e];
+          if (a.flags & FS2_EPI_BIAS) x += a.bias[n + e];
+          float av = 0.f;
+          if (a.flags & (FS2_EPI_ADD_AUX | FS2_EPI_RELU_MASK_AUX))
+            av = aux_bf16 ? bfv(((const u16*)a.aux)[m * a.ld_aux + n + e])
+                          : ((const float*)a.aux)[m * a.ld_aux + n + e];
+          if (a.flags & FS2_EPI_ADD_AUX) x += av;
+          if (a.flags & FS2_EPI_RELU) x = fmaxf(x, 0.f);
+          if (a.flags & FS2_EPI_RELU_MASK_AUX) x = av > 0.f ? x : 0.f;
+          if (out_bf16) ((u16*)a.y)[m * a.ldy + n + e] = fbv(x);
+          else ((float*)a.y)[m * a.ldy + n + e] = x;
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+static int g_wvariant = -1;  // FS2_WGRAD_STAGES: 1 or 2 (default 1)
+
+// ------------------------------------------------------------------------ weight gradient
+//   slab[z][o][kk] = sum_{m in split z} dy[m, o] * x~[m, kk],  x~[m, j*Cin + c] = x[m + j - pad, c]
+//   bslab[z][o]    = sum_{m in split z} dy[m, o]            (bias gradient, optional)
+//
+// Both operands are k-major ([reduction rows][channels]).  Tiles 128 (o) x 128 (kk) x 64
+// rows; each operand's LDS image is [64 rows][128] bf16 (256-B rows), filled lane-linearly by
+// glds (4 rows per wave-instruction) with the 16-B chunk swizzle c ^ ((R & 7) << 1) on the
+// source, and read with ds_read_b64_tr_b16: a fragment's 8 k come from rows {4g+q} and
+// {16+4g+q} of the 32-row k-step, so each 32-lane half reads 8 distinct rows x 2 chunks =
+// 16 distinct bank slots.  The frame index of each staged row is carried incrementally
+// across k-tiles (no division in the loop).  The bias gradient rides on the same A
+// fragments: the waves of the first kk column tile multiply them by a ones fragment.
+struct WgradGlds {
+  const u16* dy;
+  int64_t ldy;
+  const u16* x;
+  int64_t ldx;
+  float* slab;
+  float* bslab;
+  int64_t M, T;
+  int Cin, Cout, taps, pad, Kp;
+  int64_t rows_per_split;
+  int tiles_o, tiles_k, splits;
+};
+
+typedef short s16x4g __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4g lds_s16x4g;
+
+template <int STAGES>
+__global__ __launch_bounds__(256) void conv_wgrad_tn_glds(WgradGlds a) {
+  constexpr int BM = 128, BN = 128, BK = 64;
+  constexpr int MI = 4, NI = 4;
+  constexpr int IMG = BK * 128;             // elements per operand image
+  constexpr int STAGE_E = 2 * IMG;
+  constexpr int EPI_LD = BN + 4;
+  constexpr int EPI_E = (BM / 2) * EPI_LD * 2;
+  constexpr int SMEM_E = STAGES * STAGE_E > EPI_E ? STAGES * STAGE_E : EPI_E;
+  __shared__ __attribute__((aligned(1024))) u16 smem[SMEM_E];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3, r16 = lane & 15;
+
+  const int per_split = a.tiles_o * a.tiles_k;
+  const int nwg = per_split * a.splits;
+  const int orig = blockIdx.x, xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int z = wg / per_split, rem = wg - z * per_split;
+  const int tk = rem % a.tiles_k, to = rem / a.tiles_k;
+  const int o0 = to * BM, n0 = tk * BN;
+  const int64_t r_begin = (int64_t)z * a.rows_per_split;
+  int64_t r_end = r_begin + a.rows_per_split;
+  if (r_end > a.M) r_end = a.M;
+  const int nk = r_end > r_begin ? (int)((r_end - r_begin + BK - 1) / BK) : 0;
+
+  // per-lane staging descriptors: instruction i stages rows 4*(wave*4+i) + (lane>>4)
+  const u16* zero = reinterpret_cast<const u16*>(g_zero_line);
+  const int pc = lane & 15;
+  int R[4], t_i[4], a_col[4], b_j[4], b_c[4];
+  int64_t base_i[4];
+  bool a_ok[4], b_ok[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    R[i] = (wave * 4 + i) * 4 + (lane >> 4);
+    const int lc = pc ^ ((R[i] & 7) << 1);
+    a_col[i] = o0 + lc * 8;
+    a_ok[i] = a_col[i] < a.Cout;
+    const int kk = n0 + lc * 8;
+    b_ok[i] = kk < a.Kp;
+    b_j[i] = kk / a.Cin;
+    b_c[i] = kk - b_j[i] * a.Cin;
+    const int64_t m = r_begin + R[i];
+    const int64_t s = m / a.T;
+    t_i[i] = (int)(m - s * a.T);
+    base_i[i] = s * a.T;
+  }
+
+  auto issue = [&](int kt, int stage) {
+    u16* As = smem + stage * STAGE_E;
+    u16* Bs = As + IMG;
+    const int64_t k0 = r_begin + (int64_t)kt * BK;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t m = k0 + R[i];
+      const bool mok = m < r_end;
+      const u16* sa = (mok && a_ok[i]) ? a.dy + m * a.ldy + a_col[i] : zero;
+      glds16(sa, As + (wave * 4 + i) * 4 * 128);
+      const int tt = t_i[i] + b_j[i] - a.pad;
+      const u16* sb = (mok && b_ok[i] && tt >= 0 && tt < a.T)
+                          ? a.x + (base_i[i] + tt) * a.ldx + b_c[i] : zero;
+      glds16(sb, Bs + (wave * 4 + i) * 4 * 128);
+      t_i[i] += BK;
+      while (t_i[i] >= a.T) {
+        t_i[i] -= (int)a.T;
+        base_i[i] += a.T;
+      }
+    }
+  };
+
+  f32x4 acc[MI][NI], accb[MI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+    accb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const bool do_bias = a.bslab != nullptr && tk == 0 && wn == 0;  // wave-uniform
+  bf16x8g ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = (__bf16)1.0f;
+
+  // transposed fragment: 16 columns at col0, k-step ks; rows {4g+q} and {16+4g+q}
+  const int swz = ((4 * g + q) & 7) << 1;
+  auto tr_frag = [&](const u16* img, int col0, int ks) -> bf16x8g {
+    const int lc = (col0 >> 3) + (p >> 1);
+    const int off = (ks * 32 + 4 * g + q) * 128 + ((lc ^ swz) << 3) + ((p & 1) << 2);
+    const s16x4g lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4g*)(img + off));
+    const s16x4g hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4g*)(img + off + 16 * 128));
+    return __builtin_bit_cast(bf16x8g, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+  };
+  auto compute = [&](int stage) {
+    const u16* As = smem + stage * STAGE_E;
+    const u16* Bs = As + IMG;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8g fa[MI], fb[NI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) fa[i] = tr_frag(As, wm * 64 + i * 16, ks);
+#pragma unroll
+      for (int j = 0; j < NI; ++j) fb[j] = tr_frag(Bs, wn * 64 + j * 16, ks);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      if (do_bias) {
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+          accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], ones, accb[i], 0, 0, 0);
+      }
+    }
+  };
+
+  if constexpr (STAGES == 1) {
+    for (int kt = 0; kt < nk; ++kt) {
+      issue(kt, 0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      compute(0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+  } else {
+    if (nk > 0) issue(0, 0);
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt + 1 < nk) {
+        issue(kt + 1, (kt + 1) & 1);
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();
+      compute(kt & 1);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+  }
+
+  if (do_bias && r16 == 0) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int o = o0 + wm * 64 + i * 16 + 4 * g + r;
+        if (o < a.Cout) a.bslab[(int64_t)z * a.Cout + o] = accb[i][r];
+      }
+  }
+  // slab tile through LDS: rows o, 8 consecutive kk per thread (32-B stores)
+  float* Cs = reinterpret_cast<float*>(smem);
+  float* slab = a.slab + (int64_t)z * a.Cout * a.Kp;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (wm == h) {
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            Cs[(i * 16 + 4 * g + r) * EPI_LD + wn * 64 + j * 16 + r16] = acc[i][j][r];
+    }
+    __syncthreads();
+    const int cc = (tid & 15) * 8;
+    const int kk = n0 + cc;
+#pragma unroll
+    for (int pp = 0; pp < 4; ++pp) {
+      const int rr = pp * 16 + (tid >> 4);
+      const int o = o0 + h * 64 + rr;
+      if (o < a.Cout && kk < a.Kp) {
+        float* dst = slab + (int64_t)o * a.Kp + kk;
+        *reinterpret_cast<f32x4*>(dst) = *reinterpret_cast<const f32x4*>(Cs + rr * EPI_LD + cc);
+        *reinterpret_cast<f32x4*>(dst + 4) = *reinterpret_cast<const f32x4*>(Cs + rr * EPI_LD + cc + 4);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// dw[o][c][j] (+)= sum_z slab[z][o][j*Cin + c]; db[o] += sum_z bslab[z][o].  Split order is
+// fixed (bitwise reproducible).  taps == 1: the layouts coincide, 4 consecutive elements per
+// thread.  taps > 1: one block per (o, 64-channel chunk); slab rows are read as 256-B runs
+// per tap and the [c][j] block is written contiguously.
+__global__ __launch_bounds__(256) void wgrad_reduce_k1(const float* __restrict__ slab,
+                                                       const float* __restrict__ bslab, int splits,
+                                                       int Cout, int64_t total, float* dw, float* db) {
+  const int64_t i4 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i4 < total) {
+    f32x4 s = ld4(slab + i4);
+    for (int zz = 1; zz < splits; ++zz) s += ld4(slab + zz * total + i4);
+    st4(dw + i4, ld4(dw + i4) + s);
+  }
+  if (db && blockIdx.x == 0) {
+    for (int o = threadIdx.x; o < Cout; o += 256) {
+      float b = 0.f;
+      for (int zz = 0; zz < splits; ++zz) b += bslab[(int64_t)zz * Cout + o];
+      db[o] += b;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void wgrad_reduce_taps(const float* __restrict__ slab,
+                                                         const float* __restrict__ bslab,
+                                                         int splits, int Cout, int Cin, int taps,
+                                                         float* dw, float* db) {
+  __shared__ float tile[64 * 33];
+  const int o = blockIdx.y, c0 = blockIdx.x * 64;
+  const int64_t Kp = (int64_t)taps * Cin, total = (int64_t)Cout * Kp;
+  const int nc = Cin - c0 < 64 ? Cin - c0 : 64;
+  for (int jb = 0; jb < taps; jb += 32) {
+    const int nj = taps - jb < 32 ? taps - jb : 32;
+    for (int e = threadIdx.x; e < 64 * nj; e += 256) {
+      const int jj = e >> 6, c = e & 63;
+      if (c < nc) {
+        const int64_t off = (int64_t)o * Kp + (int64_t)(jb + jj) * Cin + c0 + c;
+        float s = slab[off];
+        for (int zz = 1; zz < splits; ++zz) s += slab[zz * total + off];
+        tile[c * 33 + jj] = s;
+      }
+    }
+    __syncthreads();
+    float* out = dw + ((int64_t)o * Cin + c0) * taps;
+    for (int e = threadIdx.x; e < nc * nj; e += 256) {
+      const int c = e / nj, jj = e - c * nj;
+      out[(int64_t)c * taps + jb + jj] += tile[c * 33 + jj];
+    }
+    __syncthreads();
+  }
+  if (db && blockIdx.x == 0 && threadIdx.x == 0) {
+    float s = 0.f;
+    for (int zz = 0; zz < splits; ++zz) s += bslab[(int64_t)zz * Cout + o];
+    db[o] += s;
+  }
+}
+
+int conv_wgrad_glds_launch(const void* dy, int64_t ldy, const void* x, int64_t ldx, float* dw,
+                           float* db, int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out,
+                           int taps, int pad, int splits, float* ws, hipStream_t st) {
+  FS2_CHECK_ARG(c_in % 8 == 0 && c_out % 8 == 0 && ldx % 8 == 0 && ldy % 8 == 0 &&
+                    ((uintptr_t)dy & 15) == 0 && ((uintptr_t)x & 15) == 0,
+                "fs2_conv_wgrad(bf16): channel counts / strides must be multiples of 8, operands 16-B aligned");
+  if (g_wvariant < 0) {
+    const char* e = getenv("FS2_WGRAD_STAGES");
+    g_wvariant = (e && e[0] == '2') ? 2 : 1;
+  }
+  int64_t rps = (rows + splits - 1) / splits;
+  rps = (rps + 63) / 64 * 64;
+  const int64_t Kp = taps * c_in;
+  float* bslab = db ? ws + splits * c_out * Kp : nullptr;
+  WgradGlds a{(const u16*)dy, ldy, (const u16*)x, ldx, ws, bslab, rows, seq_len, (int)c_in,
+              (int)c_out, taps, pad, (int)Kp, rps, (int)((c_out + 127) / 128),
+              (int)((Kp + 127) / 128), splits};
+  const unsigned grid = (unsigned)(a.tiles_o * a.tiles_k * splits);
+  if (g_wvariant == 1) conv_wgrad_tn_glds<1><<<grid, 256, 0, st>>>(a);
+  else conv_wgrad_tn_glds<2><<<grid, 256, 0, st>>>(a);
+  if (taps == 1) {
+    const int64_t total = c_out * c_in;  // multiple of 64 (both channel counts % 8 == 0)
+    wgrad_reduce_k1<<<(unsigned)((total / 4 + 255) / 256), 256, 0, st>>>(ws, bslab, splits,
+                                                                       (int)c_out, total, dw, db);
+  } else {
+    dim3 rg((unsigned)((c_in + 63) / 64), (unsigned)c_out);
+    wgrad_reduce_taps<<<rg, 256, 0, st>>>(ws, bslab, splits, (int)c_out, (int)c_in, taps, dw, db);
+  }
+  return launch_status("fs2_conv_wgrad(bf16)");
+}
+
+static int g_variant = -1;  // FS2_GEMM_STAGES: 1 or 2 (default: 2 for K >= 4096, else 1)
+
+template <int BM, int BN, int S>
+static void launch_nt(const GldsArgs& a, bool tapaligned, hipStream_t st) {
+  const unsigned grid = (unsigned)(a.tiles_m * a.tiles_n);
+  if (tapaligned) conv_gemm_nt_glds<BM, BN, S, true><<<grid, 256, 0, st>>>(a);
+  else conv_gemm_nt_glds<BM, BN, S, false><<<grid, 256, 0, st>>>(a);
+}
+
+int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, int64_t ldy,
+                          int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out, int taps,
+                          int pad, const float* bias, int flags, const void* aux, int64_t ld_aux,
+                          hipStream_t st) {
+  FS2_CHECK_ARG(c_in % 8 == 0 && ldx % 8 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)wk & 15) == 0,
+                "fs2_conv_gemm(bf16): c_in/ldx must be multiples of 8 and operands 16-B aligned");
+  if (g_variant < 0) {
+    const char* e = getenv("FS2_GEMM_STAGES");
+    g_variant = (e && e[0] == '2') ? 2 : (e && e[0] == '1') ? 1 : 0;
+  }
+  const int stages = g_variant ? g_variant : (taps * c_in >= 4096 ? 2 : 1);
+  const int K = (int)(taps * c_in);
+  const bool out_bf16 = flags & FS2_EPI_OUT_BF16, aux_bf16 = flags & FS2_EPI_AUX_BF16;
+  const int yb = out_bf16 ? 2 : 4, ab = aux_bf16 ? 2 : 4;
+  const bool uses_aux = flags & (FS2_EPI_ADD_AUX | FS2_EPI_RELU_MASK_AUX);
+  const int vec = c_out % 8 == 0 && ldy % 8 == 0 && ((uintptr_t)y % 16) == 0 &&
+                  (!(flags & FS2_EPI_BIAS) || ((uintptr_t)bias % 16) == 0) &&
+                  (!uses_aux || (ld_aux % 8 == 0 && ((uintptr_t)aux % 16) == 0));
+  (void)yb;
+  (void)ab;
+  GldsArgs a{(const u16*)x, ldx, (const u16*)wk, y, ldy, rows, seq_len, (int)c_in, (int)c_out,
+             taps, pad, K, bias, flags, aux, ld_aux, 0, 0, vec};
+  const bool tapaligned = c_in % 64 == 0;
+  const int64_t big = ((rows + 127) / 128) * ((c_out + 127) / 128);
+  if (big >= 512) {
+    a.tiles_m = (int)((rows + 127) / 128);
+    a.tiles_n = (int)((c_out + 127) / 128);
+    if (stages == 2) launch_nt<128, 128, 2>(a, tapaligned, st);
+    else launch_nt<128, 128, 1>(a, tapaligned, st);
+  } else if (big >= 128) {
+    a.tiles_m = (int)((rows + 127) / 128);
+    a.tiles_n = (int)((c_out + 63) / 64);
+    if (stages == 2) launch_nt<128, 64, 2>(a, tapaligned, st);
+    else launch_nt<128, 64, 1>(a, tapaligned, st);
+  } else {
+    a.tiles_m = (int)((rows + 63) / 64);
+    a.tiles_n = (int)((c_out + 63) / 64);
+    if (stages == 2) launch_nt<64, 64, 2>(a, tapaligned, st);
+    else launch_nt<64, 64, 1>(a, tapaligned, st);
+  }
+  return launch_status("fs2_conv_gemm(bf16)");
+}
+
+}  // namespace fs2

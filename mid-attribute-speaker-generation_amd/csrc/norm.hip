@@ -379,15 +379,14 @@ int fs2_ln_bwd(int dtype, const float* dout, const float* ddot, const float* dot
   ln_bwd_f32<<<(unsigned)nblk, 256, 0, st>>>(a);
   int rc = launch_status("fs2_ln_bwd");
   if (rc) return rc;
-  if (dgamma && (rc = colsum_final_launch(ws, nblk, LN_D, dgamma, 1, st))) return rc;
-  if (dbeta && (rc = colsum_final_launch(ws + nblk * LN_D, nblk, LN_D, dbeta, 1, st))) return rc;
-  if (ddot && dw_dot && (rc = colsum_final_launch(ws + 2 * nblk * LN_D, nblk, LN_D, dw_dot, 1, st)))
-    return rc;
-  if (ddot && db_dot && (rc = colsum_final_launch(ws + 4 * nblk * LN_D, nblk, 1, db_dot, 1, st)))
-    return rc;
-  if (dbias_in && (rc = colsum_final_launch(ws + 3 * nblk * LN_D, nblk, LN_D, dbias_in, 1, st)))
-    return rc;
-  return FS2_OK;
+  ColsumJobs jobs{};
+  jobs.acc = 1;
+  if (dgamma) jobs.add(ws, nblk, LN_D, dgamma);
+  if (dbeta) jobs.add(ws + nblk * LN_D, nblk, LN_D, dbeta);
+  if (ddot && dw_dot) jobs.add(ws + 2 * nblk * LN_D, nblk, LN_D, dw_dot);
+  if (ddot && db_dot) jobs.add(ws + 4 * nblk * LN_D, nblk, 1, db_dot);
+  if (dbias_in) jobs.add(ws + 3 * nblk * LN_D, nblk, LN_D, dbias_in);
+  return colsum_final_multi_launch(jobs, st);
 }
 
 int64_t fs2_bn_ws_bytes(int64_t rows, int64_t c) {

@@ -77,14 +77,15 @@ def weight_prep(w, c_out, c_in, taps, w_fwd=None, w_bwd=None):
     lib.fs2_conv_weight_prep(code(dt), ptr(w), c_out, c_in, taps, ptr(w_fwd), ptr(w_bwd), stream())
 
 
-def conv_wgrad(dy, x, dw, rows, seq_len, c_in, c_out, taps, pad):
-    _dev(dy, x, dw)
+def conv_wgrad(dy, x, dw, rows, seq_len, c_in, c_out, taps, pad, db=None):
+    """dw (+)= conv weight gradient; db (+)= column sums of dy when given (same launch)."""
+    _dev(dy, x, dw, db)
     if dy.dtype != x.dtype:
         raise RuntimeError(f"conv_wgrad operand dtypes differ: {dy.dtype} vs {x.dtype}")
     n = lib.fs2_conv_wgrad_ws_bytes(rows, c_in, c_out, taps)
     w = ws(n, dy.device)
-    lib.fs2_conv_wgrad(code(dy.dtype), ptr(dy), c_out, ptr(x), c_in, ptr(dw), rows, seq_len, c_in,
-                       c_out, taps, pad, ptr(w), n, stream())
+    lib.fs2_conv_wgrad(code(dy.dtype), ptr(dy), c_out, ptr(x), c_in, ptr(dw), ptr(db), rows,
+                       seq_len, c_in, c_out, taps, pad, ptr(w), n, stream())
 
 
 def colsum(x, rows, cols, out, accumulate=True):

@@ -292,8 +292,7 @@ class FFTBlock(nn.Module):
         K.conv_wgrad(dy2_c, h, _g(w2.weight), M, T, w2.c_in, d, w2.k, w2.padding)
         dh = K.conv_gemm(dy2_c, w2._w_bwd, M, T, d, w2.c_in, w2.k, w2.padding,
                          flags=K.EPI_RELU_MASK_AUX, aux=h, out_dtype=cdt)
-        K.colsum(dh, M, w1.c_out, _g(w1.bias))
-        K.conv_wgrad(dh, x1_c, _g(w1.weight), M, T, d, w1.c_out, w1.k, w1.padding)
+        K.conv_wgrad(dh, x1_c, _g(w1.weight), M, T, d, w1.c_out, w1.k, w1.padding, db=_g(w1.bias))
         K.conv_gemm(dh, w1._w_bwd, M, T, w1.c_out, d, w1.k, w1.padding, flags=K.EPI_ADD_AUX,
                     aux=dx1, out=dx1)
         # LN1 -> fc -> attention -> QKV
@@ -306,8 +305,7 @@ class FFTBlock(nn.Module):
         K.conv_wgrad(dy1_c, o, _g(a.fc.weight), M, T, hd, d, 1, 0)
         do = K.conv_gemm(dy1_c, a.fc._w_bwd, M, T, d, hd, 1, 0, out_dtype=cdt)
         dqkv = K.attn_bwd(qkv, o, do, lse, lens, B, T, a.n_head, a.d_k, 1.0 / math.sqrt(a.d_k))
-        K.colsum(dqkv, M, n3, self._qkv_gb)
-        K.conv_wgrad(dqkv, x_c, self._qkv_gw, M, T, d, n3, 1, 0)
+        K.conv_wgrad(dqkv, x_c, self._qkv_gw, M, T, d, n3, 1, 0, db=self._qkv_gb)
         K.conv_gemm(dqkv, q._w_bwd, M, T, n3, d, 1, 0, flags=K.EPI_ADD_AUX, aux=dx, out=dx)
         return dx
 
@@ -495,9 +493,8 @@ class PostNet(nn.Module):
             dz, dz_t = K.bn_bwd(d, z, mean, rstd, bn.weight, bn.bias, _g(bn.weight), _g(bn.bias),
                                 i < n - 1, p, ctx.seed, self.site + i, copy=ctx.copy)
             dz_c = _t(dz, dz_t)
-            K.colsum(dz, M, conv.c_out, _g(conv.bias))
             K.conv_wgrad(dz_c, a_c, _g(conv.weight), M, T, conv.c_in, conv.c_out, conv.k,
-                         conv.padding)
+                         conv.padding, db=_g(conv.bias))
             if i > 0:
                 d = K.conv_gemm(dz_c, conv._w_bwd, M, T, conv.c_out, conv.c_in, conv.k, conv.padding)
             else:
@@ -765,8 +762,7 @@ class MelHeadFn(torch.autograd.Function):
             dm = d_out
         ctx.notify(postnet_param_order(m.postnet))
         dm_c = K.cast_bf16(dm) if ctx.copy is not None else dm
-        K.colsum(dm, M, n_mel, _g(lin.bias))
-        K.conv_wgrad(dm_c, x_c, _g(lin.weight), M, T, lin.in_features, n_mel, 1, 0)
+        K.conv_wgrad(dm_c, x_c, _g(lin.weight), M, T, lin.in_features, n_mel, 1, 0, db=_g(lin.bias))
         dx = K.conv_gemm(dm_c, lin._w_bwd, M, T, n_mel, lin.in_features, 1, 0)
         ctx.notify([lin.weight, lin.bias])
         fctx.saved = None
@@ -849,14 +845,12 @@ class FastSpeech2(nn.Module):
                 v.prep(cdt, jobs)
             self.postnet.prep(cdt, jobs)
             _linear_prep(self.mel_linear, cdt, jobs=jobs)
-            rows, first = [], 0
-            for (w, co, ci, k, wf, wb) in jobs:
-                rows.append([w, co, ci, k, wf, wb, first, first + co * ci * k])
-                first += co * ci * k
+            rows = [[w, co, ci, k, wf, wb, 0, 0] for (w, co, ci, k, wf, wb) in jobs]
+            assert max(r[3] for r in rows) <= 9
             table = torch.tensor(rows, dtype=torch.int64).to(self._arena.flat.device)
-            self._prep = (cdt, table, len(rows), first)
-        cdt, table, n, total = self._prep
-        K.lib.fs2_weight_prep_batch(K.code(cdt), K.ptr(table), n, total, K.stream())
+            self._prep = (cdt, table, len(rows), max(r[1] for r in rows), max(r[2] for r in rows))
+        cdt, table, n, max_co, max_ci = self._prep
+        K.lib.fs2_weight_prep_batch(K.code(cdt), K.ptr(table), n, max_co, max_ci, K.stream())
 
     # -- forward ----------------------------------------------------------------------
     def forward(self, speakers, texts, src_lens, max_src_len, mels=None, mel_lens=None,

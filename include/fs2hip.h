@@ -63,10 +63,23 @@ int fs2_conv_gemm(int dtype, const void* x, int64_t ldx, const void* wk, void* y
 int fs2_conv_weight_prep(int dtype, const float* w, int64_t c_out, int64_t c_in, int taps,
                          void* w_fwd, void* w_bwd, void* stream);
 /* The same for every layer of the model in one launch: jobs (device, int64) holds
- * n_jobs rows {w, c_out, c_in, taps, w_fwd, w_bwd, 0, 0}; max_c_out / max_c_in bound the
- * rows' c_out / c_in; taps <= 9.                                                       */
-int fs2_weight_prep_batch(int dtype, const int64_t* jobs, int n_jobs, int64_t max_c_out,
-                          int64_t max_c_in, void* stream);
+ * n_jobs rows {w, c_out, c_in, taps, w_fwd, w_bwd, first, end}: the job's tiles
+ * [first, end) of ceil(c_out/64) * ceil(c_in/CT) tiles, numbered consecutively over the
+ * jobs, CT = fs2_weight_prep_tile_channels(dtype); n_tiles = end of the last job; taps <= 9. */
+int fs2_weight_prep_tile_channels(int dtype);
+int fs2_weight_prep_batch(int dtype, const int64_t* jobs, int n_jobs, int64_t n_tiles,
+                          void* stream);
+
+/* Kernel-selection knobs for benchmarking (0 = automatic choice, the default):
+ *   FS2_TUNE_GEMM_STAGES   fwd/dX LDS stages (1 or 2)
+ *   FS2_TUNE_WGRAD_STAGES  weight-gradient LDS stages (1 or 2)
+ *   FS2_TUNE_WGRAD_TILE    weight-gradient tile width (64 or 128)
+ *   FS2_TUNE_WGRAD_SPLITS  weight-gradient row splits (1..64)
+ *   FS2_TUNE_LEGACY_GEMM   1 = the register-staged bf16 kernels of round 1
+ * Process-wide; query workspace sizes after setting.                                 */
+enum { FS2_TUNE_GEMM_STAGES = 0, FS2_TUNE_WGRAD_STAGES = 1, FS2_TUNE_WGRAD_TILE = 2,
+       FS2_TUNE_WGRAD_SPLITS = 3, FS2_TUNE_LEGACY_GEMM = 4, FS2_TUNE_COUNT = 5 };
+int fs2_set_tuning(int knob, int value);
 
 /* Weight (and optionally bias) gradient, accumulated into the fp32 master-gradient layout:
  *   dw[o, c, j] += sum_r dy[r, o] * x[r + j - pad, c]
@@ -108,7 +121,8 @@ int fs2_attn_bwd(int dtype, const void* qkv, const void* o, const void* d_o, con
  * and optionally a per-row dot with a Linear(256 -> 1): dot_out[r] = padded ? 0 : out.w + b.
  *   SubLayers.py:54-55,91-93 + Layers.py:25,28   (p_in = dropout, res = residual, masked)
  *   model/modules.py:209-250                      (p_out = dropout, dot = linear_layer)
- * xhat/rstd are saved for the backward.  out_t: optional extra copy in `dtype`.       */
+ * xhat/rstd are saved for the backward (not written for masked rows outside dot mode,
+ * whose backward is zero).  out_t: optional extra copy in `dtype`.                    */
 int fs2_ln_fwd(int dtype, const float* y, const float* res, const float* gamma, const float* beta,
                float* out, void* out_t, float* xhat, float* rstd, const int64_t* lens,
                int64_t seq_len, int64_t rows, int d, float p_in, float p_out, uint64_t seed,
@@ -116,22 +130,24 @@ int fs2_ln_fwd(int dtype, const float* y, const float* res, const float* gamma, 
                float* dot_out, void* stream);
 /* Backward of fs2_ln_fwd.  Upstream gradient is dout (per element) or, in dot mode,
  * ddot (per row).  Produces dy (gradient w.r.t. y before dropout, times (relu_y > 0) when
- * relu_y != NULL), optionally adds dz into dres (+=), and accumulates dgamma, dbeta and
+ * relu_y != NULL), optionally adds dz into dres (dres_add 1: +=, 0: =), and accumulates dgamma, dbeta and
  * (dot mode) dw_dot/db_dot into fp32 gradients; dbias_in (nullable) += sum over rows of
  * dy — the bias gradient of the layer that produced y, fused here instead of a separate
- * column sum.  ws >= fs2_ln_bwd_ws_bytes(rows, d).                                   */
+ * column sum.  dy may be NULL when the dtype copy dy_t is requested.
+ * ws >= fs2_ln_bwd_ws_bytes(rows, d).                                                 */
 int64_t fs2_ln_bwd_ws_bytes(int64_t rows, int d);
 int fs2_ln_bwd(int dtype, const float* dout, const float* ddot, const float* dot_w,
                const float* xhat, const float* rstd, const float* gamma, const float* beta,
                const int64_t* lens, int64_t seq_len, int64_t rows, int d, float p_in, float p_out,
                uint64_t seed, uint64_t site_in, uint64_t site_out, const float* relu_y, float* dy,
-               void* dy_t, float* dres, float* dgamma, float* dbeta, float* dw_dot, float* db_dot,
-               float* dbias_in, float* ws, int64_t ws_bytes, void* stream);
+               void* dy_t, float* dres, int dres_add, float* dgamma, float* dbeta, float* dw_dot,
+               float* db_dot, float* dbias_in, float* ws, int64_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------- BatchNorm (PostNet)
  * Training-mode BatchNorm1d over all rows (padded frames included) + optional tanh +
  * dropout (transformer/Layers.py:129-137).  Stats are exact two-pass (mean, then centred
- * sum of squares); running stats updated with momentum, unbiased variance.           */
+ * sum of squares); running stats updated with momentum, unbiased variance.  c % 4 == 0.
+ * out / dz may be NULL when the bf16 copy (out_t / dz_t) is requested.               */
 int64_t fs2_bn_ws_bytes(int64_t rows, int64_t c);
 int fs2_bn_fwd(int dtype, const float* z, int64_t rows, int64_t c, const float* gamma,
                const float* beta, float eps, float momentum, float* running_mean,
@@ -154,9 +170,12 @@ int fs2_embedding_fwd(const int64_t* ids, const float* table, int64_t n, int d, 
 /* mask[b, t] = t >= lens[b]  (get_mask_from_lengths, utils/tools.py:155-163), 1 byte.   */
 int fs2_length_mask(const int64_t* lens, int64_t batch, int64_t max_len, uint8_t* mask,
                     void* stream);
-/* dtable[ids[i]] += dout[i]  for ids[i] != padding_idx (padding_idx < 0: none).       */
+/* dtable[ids[i]] += dout[i]  for ids[i] != padding_idx (padding_idx < 0: none); dtable
+ * has n_table rows.  Fixed summation order (chunk partials in ws, no atomics).
+ * ws_bytes >= fs2_embedding_bwd_ws_bytes(n, d, n_table) (also for fs2_bucket_embed_bwd). */
+int64_t fs2_embedding_bwd_ws_bytes(int64_t n, int d, int64_t n_table);
 int fs2_embedding_bwd(const float* dout, const int64_t* ids, int64_t n, int d, int padding_idx,
-                      float* dtable, void* stream);
+                      float* dtable, int64_t n_table, float* ws, int64_t ws_bytes, void* stream);
 /* out[b, t] = x[b, t] + table[ids[b]] over all t (model/fastspeech2.py:81-84).        */
 int fs2_rowvec_add_fwd(const float* x, const int64_t* ids, const float* table, int64_t batch,
                        int64_t seq_len, int d, float* out, void* out_t, void* stream);
@@ -168,7 +187,7 @@ int fs2_bucket_embed_fwd(const float* x, const void* values, int values_dtype, c
                          int n_bins, const float* table, int64_t rows, int d, float* out,
                          void* out_t, int32_t* idx, void* stream);
 int fs2_bucket_embed_bwd(const float* dout, const int32_t* idx, int64_t rows, int d,
-                         float* dtable, void* stream);
+                         float* dtable, int64_t n_table, float* ws, int64_t ws_bytes, void* stream);
 int fs2_bucketize(const void* values, int values_dtype, const float* bins, int n_bins,
                   int64_t n, int32_t* idx, void* stream);
 

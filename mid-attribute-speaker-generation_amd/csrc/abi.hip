@@ -6,6 +6,8 @@
 
 namespace fs2 {
 
+int g_tune[FS2_TUNE_COUNT] = {0, 0, 0, 0, 0};
+
 static thread_local char g_err[512] = "";
 
 void set_error(const char* fmt, ...) {
@@ -65,6 +67,12 @@ extern "C" {
 const char* fs2_last_error(void) { return g_err; }
 
 int fs2_abi_version(void) { return 1; }
+
+int fs2_set_tuning(int knob, int value) {
+  FS2_CHECK_ARG(knob >= 0 && knob < FS2_TUNE_COUNT, "fs2_set_tuning: unknown knob %d", knob);
+  g_tune[knob] = value;
+  return FS2_OK;
+}
 
 int fs2_fill(float* x, int64_t n, float value, void* stream) {
   if (n <= 0) return FS2_OK;

@@ -17,6 +17,8 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 namespace fs2 {
 
+extern int g_tune[FS2_TUNE_COUNT];  // fs2_set_tuning knobs (abi.hip)
+
 // ------------------------------------------------------------------ error reporting
 void set_error(const char* fmt, ...);
 int launch_status(const char* what);
@@ -60,7 +62,7 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
                           hipStream_t st);
 int conv_wgrad_glds_launch(const void* dy, int64_t ldy, const void* x, int64_t ldx, float* dw,
                            float* db, int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out,
-                           int taps, int pad, int splits, float* ws, hipStream_t st);
+                           int taps, int pad, int splits, int tile, float* ws, hipStream_t st);
 int conv_wgrad_bf16_launch(const void* dy, int64_t ldy, const void* x, int64_t ldx, float* slab,
                            int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out, int taps,
                            int pad, int splits, hipStream_t st);

@@ -27,14 +27,87 @@ __global__ void encoder_embed(const int64_t* texts, const int64_t* accents, cons
   }
 }
 
-__global__ void embedding_bwd(const float* dout, const int64_t* ids, int64_t n, int d, int pad_idx,
-                              float* dtab) {
-  const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int lane = threadIdx.x & 63;
-  if (r >= n) return;
-  const int64_t id = ids[r];
-  if (id == pad_idx) return;
-  for (int c = lane; c < d; c += 64) atomicAdd(dtab + id * d + c, dout[r * d + c]);
+// Deterministic scatter-add of rows by id (embedding backward), skew-proof.
+// Pass 1: block (id, chunk) lists, in row order, the rows of its 1024-row chunk that carry
+// `id` (wave ballots + prefix popcounts), then sums them (4 row lanes x 4 channels per
+// thread, loads unrolled) into ws[chunk][id].  Pass 2 adds the chunk partials to the table
+// row in chunk order.  No atomics; a table row hit by every row costs n/1024 blocks.
+constexpr int IA_CHUNK = 1024;
+
+template <typename I>
+__global__ __launch_bounds__(256) void index_add_partial(const float* __restrict__ dout,
+                                                         const I* __restrict__ ids, int64_t n,
+                                                         int d, int n_table, float* ws) {
+  __shared__ int list[IA_CHUNK];
+  __shared__ int wcnt[4][4];
+  __shared__ f32x4 red[4][64];
+  const int id = blockIdx.x, chunk = blockIdx.y;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t r0 = (int64_t)chunk * IA_CHUNK;
+  bool match[4];
+  uint64_t mask[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int64_t r = r0 + wave * 256 + k * 64 + lane;
+    match[k] = r < n && (int64_t)ids[r] == id;
+    mask[k] = __ballot(match[k]);
+    if (lane == 0) wcnt[wave][k] = __popcll(mask[k]);
+  }
+  __syncthreads();
+  int base = 0;
+  for (int w = 0; w < wave; ++w)
+    for (int k = 0; k < 4; ++k) base += wcnt[w][k];
+  int count = 0;
+  for (int w = 0; w < 4; ++w)
+    for (int k = 0; k < 4; ++k) count += wcnt[w][k];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask[k] >> 32),
+                                                __builtin_amdgcn_mbcnt_lo((uint32_t)mask[k], 0));
+    if (match[k]) list[base + below] = wave * 256 + k * 64 + lane;
+    base += __popcll(mask[k]);
+  }
+  __syncthreads();
+  const int tx = lane, ty = wave;
+  for (int c0 = 0; c0 < d; c0 += 256) {
+    const int c = c0 + 4 * tx;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    if (c < d) {
+#pragma unroll 8
+      for (int i = ty; i < count; i += 4) acc += ld4(dout + (r0 + list[i]) * d + c);
+    }
+    red[ty][tx] = acc;
+    __syncthreads();
+    if (ty == 0 && c < d)
+      st4(ws + ((int64_t)chunk * n_table + id) * d + c,
+          ((red[0][tx] + red[1][tx]) + red[2][tx]) + red[3][tx]);
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(256) void index_add_final(const float* __restrict__ ws, int nchunks,
+                                                       int n_table, int d, int64_t pad_idx,
+                                                       float* dtab) {
+  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;  // float4 index into the table
+  const int64_t total4 = (int64_t)n_table * d / 4;
+  if (q >= total4) return;
+  const int64_t row = q * 4 / d;
+  if (row == pad_idx) return;
+  f32x4 s = ld4(ws + q * 4);
+  for (int ch = 1; ch < nchunks; ++ch) s += ld4(ws + ((int64_t)ch * n_table * d) + q * 4);
+  st4(dtab + q * 4, ld4(dtab + q * 4) + s);
+}
+
+template <typename I>
+static int index_add_launch(const float* dout, const I* ids, int64_t n, int d, int64_t pad_idx,
+                            float* dtab, int64_t n_table, float* ws, hipStream_t st) {
+  const int64_t nchunks = (n + IA_CHUNK - 1) / IA_CHUNK;
+  dim3 grid((unsigned)n_table, (unsigned)nchunks);
+  index_add_partial<I><<<grid, 256, 0, st>>>(dout, ids, n, d, (int)n_table, ws);
+  const int64_t total4 = n_table * d / 4;
+  index_add_final<<<(unsigned)((total4 + 255) / 256), 256, 0, st>>>(ws, (int)nchunks, (int)n_table,
+                                                                    d, pad_idx, dtab);
+  return launch_status("index_add");
 }
 
 __global__ void rowvec_add(const float* x, const int64_t* ids, const float* tab, int64_t rows,
@@ -50,13 +123,30 @@ __global__ void rowvec_add(const float* x, const int64_t* ids, const float* tab,
   }
 }
 
-// dtab[ids[b]] += sum_t dout[b, t]   (one block per utterance, thread per channel)
-__global__ void rowvec_add_bwd(const float* dout, const int64_t* ids, int64_t T, int d, float* dtab) {
-  const int64_t b = blockIdx.x;
-  for (int c = threadIdx.x; c < d; c += blockDim.x) {
-    float s = 0.f;
-    for (int64_t t = 0; t < T; ++t) s += dout[(b * T + t) * d + c];
-    atomicAdd(dtab + ids[b] * d + c, s);
+// dtab[ids[b]] += sum_t dout[b, t].  One block per utterance; the block of the FIRST
+// utterance carrying an id sums every utterance with that id (in utterance order, frames in
+// 4 row lanes combined in lane order), so repeated speakers need no atomics.
+__global__ __launch_bounds__(256) void rowvec_add_bwd(const float* __restrict__ dout,
+                                                      const int64_t* __restrict__ ids, int64_t batch,
+                                                      int64_t T, int d, float* dtab) {
+  __shared__ f32x4 red[4][64];
+  const int64_t b = blockIdx.x, id = ids[b];
+  for (int64_t j = 0; j < b; ++j)
+    if (ids[j] == id) return;  // block-uniform: an earlier utterance owns this id
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int c0 = 0; c0 < d; c0 += 256) {
+    const int c = c0 + 4 * tx;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    if (c < d)
+      for (int64_t bb = b; bb < batch; ++bb) {
+        if (ids[bb] != id) continue;
+        for (int64_t t = ty; t < T; t += 4) acc += ld4(dout + (bb * T + t) * d + c);
+      }
+    red[ty][tx] = acc;
+    __syncthreads();
+    if (ty == 0 && c < d)
+      st4(dtab + id * d + c, ld4(dtab + id * d + c) + (((red[0][tx] + red[1][tx]) + red[2][tx]) + red[3][tx]));
+    __syncthreads();
   }
 }
 
@@ -92,14 +182,6 @@ template <typename V>
 __global__ void bucketize_k(const V* vals, const float* bins, int nb, int64_t n, int32_t* idx) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) idx[i] = lower_bound<V>(bins, nb, vals[i]);
-}
-
-__global__ void bucket_embed_bwd(const float* dout, const int32_t* idx, int64_t rows, int d, float* dtab) {
-  const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int lane = threadIdx.x & 63;
-  if (r >= rows) return;
-  const int64_t k = idx[r];
-  for (int c = lane; c < d; c += 64) atomicAdd(dtab + k * d + c, dout[r * d + c]);
 }
 
 // ------------------------------------------------------------------ LengthRegulator
@@ -238,11 +320,18 @@ int fs2_length_mask(const int64_t* lens, int64_t batch, int64_t max_len, uint8_t
   return launch_status("fs2_length_mask");
 }
 
+int64_t fs2_embedding_bwd_ws_bytes(int64_t n, int d, int64_t n_table) {
+  return ((n + IA_CHUNK - 1) / IA_CHUNK) * n_table * d * 4;
+}
+
 int fs2_embedding_bwd(const float* dout, const int64_t* ids, int64_t n, int d, int padding_idx,
-                      float* dtable, void* stream) {
-  if (n == 0) return FS2_OK;
-  embedding_bwd<<<rows_grid(n), 256, 0, as_stream(stream)>>>(dout, ids, n, d, padding_idx, dtable);
-  return launch_status("fs2_embedding_bwd");
+                      float* dtable, int64_t n_table, float* ws, int64_t ws_bytes, void* stream) {
+  FS2_CHECK_ARG(d % 4 == 0, "fs2_embedding_bwd: d must be a multiple of 4");
+  FS2_CHECK_ARG(ws_bytes >= fs2_embedding_bwd_ws_bytes(n, d, n_table),
+                "fs2_embedding_bwd: workspace too small");
+  if (n == 0 || n_table == 0) return FS2_OK;
+  return index_add_launch<int64_t>(dout, ids, n, d, padding_idx, dtable, n_table, ws,
+                                   as_stream(stream));
 }
 
 int fs2_rowvec_add_fwd(const float* x, const int64_t* ids, const float* table, int64_t batch,
@@ -258,7 +347,8 @@ int fs2_rowvec_add_fwd(const float* x, const int64_t* ids, const float* table, i
 int fs2_rowvec_add_bwd(const float* dout, const int64_t* ids, int64_t batch, int64_t seq_len,
                        int d, float* dtable, void* stream) {
   if (batch == 0) return FS2_OK;
-  rowvec_add_bwd<<<(unsigned)batch, 256, 0, as_stream(stream)>>>(dout, ids, seq_len, d, dtable);
+  FS2_CHECK_ARG(d % 4 == 0, "fs2_rowvec_add_bwd: d must be a multiple of 4");
+  rowvec_add_bwd<<<(unsigned)batch, 256, 0, as_stream(stream)>>>(dout, ids, batch, seq_len, d, dtable);
   return launch_status("fs2_rowvec_add_bwd");
 }
 
@@ -282,10 +372,12 @@ int fs2_bucket_embed_fwd(const float* x, const void* values, int values_dtype, c
 }
 
 int fs2_bucket_embed_bwd(const float* dout, const int32_t* idx, int64_t rows, int d,
-                         float* dtable, void* stream) {
-  if (rows == 0) return FS2_OK;
-  bucket_embed_bwd<<<rows_grid(rows), 256, 0, as_stream(stream)>>>(dout, idx, rows, d, dtable);
-  return launch_status("fs2_bucket_embed_bwd");
+                         float* dtable, int64_t n_table, float* ws, int64_t ws_bytes, void* stream) {
+  FS2_CHECK_ARG(d % 4 == 0, "fs2_bucket_embed_bwd: d must be a multiple of 4");
+  FS2_CHECK_ARG(ws_bytes >= fs2_embedding_bwd_ws_bytes(rows, d, n_table),
+                "fs2_bucket_embed_bwd: workspace too small");
+  if (rows == 0 || n_table == 0) return FS2_OK;
+  return index_add_launch<int32_t>(dout, idx, rows, d, -1, dtable, n_table, ws, as_stream(stream));
 }
 
 int fs2_bucketize(const void* values, int values_dtype, const float* bins, int n_bins, int64_t n,

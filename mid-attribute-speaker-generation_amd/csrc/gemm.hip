@@ -374,18 +374,28 @@ int colsum_final_launch(const float* part, int64_t nparts, int64_t cols, float* 
   return launch_status("colsum_final");
 }
 
+// Weight-gradient decomposition (measured on the step's shapes, scripts/wgrad_sweep.py):
+// 128-wide tiles with <= 8 row splits for the large k>1 products, 64-wide tiles with 4..24
+// splits (>= 8 k-tiles of 64 rows each) for the small ones, ~1024 blocks where possible.
+static int wgrad_tile(int64_t rows, int64_t c_in, int64_t c_out, int taps) {
+  (void)rows;
+  if (g_tune[FS2_TUNE_WGRAD_TILE]) return g_tune[FS2_TUNE_WGRAD_TILE] == 64 ? 64 : 128;
+  return (int64_t)taps * c_in * c_out >= (1 << 20) ? 128 : 64;
+}
+
 static int wgrad_splits(int64_t rows, int64_t c_in, int64_t c_out, int taps) {
+  if (g_tune[FS2_TUNE_WGRAD_SPLITS]) {
+    const int s = g_tune[FS2_TUNE_WGRAD_SPLITS];
+    return s < 1 ? 1 : s > 64 ? 64 : s;
+  }
   const int64_t Kp = (int64_t)taps * c_in;
-  const int64_t tiles = ((c_out + 127) / 128) * ((Kp + 127) / 128);
-  // ~640 blocks (2-3 per CU), >= 4 k-tiles of 64 rows per split, and the fp32 slabs
-  // (written once, read once by the reduction) kept to ~24 MB unless that leaves < 4 splits.
-  int64_t s = (640 + tiles - 1) / tiles;
-  const int64_t slab = c_out * Kp * 4;
-  int64_t max_s = rows / 256;
-  const int64_t mem_s = (24 << 20) / slab > 4 ? (24 << 20) / slab : 4;
-  if (max_s > mem_s) max_s = mem_s;
-  if (s > max_s) s = max_s;
-  if (s > 64) s = 64;
+  const int bt = wgrad_tile(rows, c_in, c_out, taps);
+  const int64_t tiles = ((c_out + bt - 1) / bt) * ((Kp + bt - 1) / bt);
+  int64_t s = (1024 + tiles - 1) / tiles;
+  const int64_t hi = bt == 128 ? 8 : 24;
+  if (s > hi) s = hi;
+  if (s < 4) s = 4;
+  if (s > rows / 512) s = rows / 512;
   if (s < 1) s = 1;
   return (int)s;
 }
@@ -460,14 +470,9 @@ int fs2_conv_wgrad(int dtype, const void* dy, int64_t ldy, const void* x, int64_
                   "fs2_conv_wgrad: workspace too small");
     if (rows == 0) return FS2_OK;
     const int S = wgrad_splits(rows, c_in, c_out, taps);
-    static int old = -1;
-    if (old < 0) {
-      const char* e = getenv("FS2_GEMM_OLD");
-      old = e && e[0] == '1';
-    }
-    if (!old)
+    if (!g_tune[FS2_TUNE_LEGACY_GEMM])
       return conv_wgrad_glds_launch(dy, ldy, x, ldx, dw, db, rows, seq_len, c_in, c_out, taps, pad,
-                                    S, ws, as_stream(stream));
+                                    S, wgrad_tile(rows, c_in, c_out, taps), ws, as_stream(stream));
     int rc = conv_wgrad_bf16_launch(dy, ldy, x, ldx, ws, rows, seq_len, c_in, c_out, taps, pad, S,
                                     as_stream(stream));
     if (rc) return rc;

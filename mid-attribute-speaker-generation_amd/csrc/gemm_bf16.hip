@@ -297,25 +297,32 @@ __global__ void weight_prep_bf16(const float* w, int Cout, int Cin, int taps, u1
   }
 }
 
-// All layers' re-layouts in one launch.  jobs[j] = {src, c_out, c_in, taps, w_fwd, w_bwd, -, -}
-// (int64).  Block (x, j) re-lays out one tile of job j: 64 output channels x CT input channels
-// x all taps.  The source rows are read as contiguous CT*taps runs into LDS (already cast),
-// then w_fwd is written as CT-long runs per (o, tap) and w_bwd as 64-long runs per (c, tap).
+// All layers' re-layouts in one launch.  jobs[j] = {src, c_out, c_in, taps, w_fwd, w_bwd,
+// first tile, end tile} (int64); a job has ceil(c_out/64) x ceil(c_in/CT) tiles, numbered
+// consecutively over the jobs (CT = fs2_weight_prep_tile_channels).  Block b re-lays out
+// one tile: 64 output channels x CT input channels x all taps.  The source rows are read as
+// contiguous CT*taps runs into LDS (already cast), then w_fwd is written as CT-long runs per
+// (o, tap) and w_bwd as 64-long runs per (c, tap).
 template <typename OutT>
-__global__ __launch_bounds__(256) void weight_prep_tiles(const int64_t* __restrict__ jobs,
-                                                         int tiles_c_max) {
+__global__ __launch_bounds__(256) void weight_prep_tiles(const int64_t* __restrict__ jobs, int n_jobs) {
   constexpr int CT = sizeof(OutT) == 2 ? 32 : 16;
   constexpr int MAXT = 9;
   constexpr int LD = CT * MAXT + 1;  // odd row stride (in OutT units of 2 or 4 B)
   __shared__ OutT tile[64 * LD];
-  const int64_t* jb = jobs + (int64_t)blockIdx.y * 8;
+  int lo = 0, hi = n_jobs - 1;
+  while (lo < hi) {  // last job whose first tile <= blockIdx.x
+    const int mid = (lo + hi + 1) >> 1;
+    if (jobs[mid * 8 + 6] <= (int64_t)blockIdx.x) lo = mid;
+    else hi = mid - 1;
+  }
+  const int64_t* jb = jobs + (int64_t)lo * 8;
   const float* w = (const float*)jb[0];
   const int Cout = (int)jb[1], Cin = (int)jb[2], taps = (int)jb[3];
   OutT* wf = (OutT*)jb[4];
   OutT* wb = (OutT*)jb[5];
-  const int tc = blockIdx.x % tiles_c_max, to = blockIdx.x / tiles_c_max;
+  const int t = (int)(blockIdx.x - jb[6]), tiles_c = (Cin + CT - 1) / CT;
+  const int tc = t % tiles_c, to = t / tiles_c;
   const int o0 = to * 64, c0 = tc * CT;
-  if (o0 >= Cout || c0 >= Cin) return;
   const int no = Cout - o0 < 64 ? Cout - o0 : 64;
   const int nc = Cin - c0 < CT ? Cin - c0 : CT;
   const int run = nc * taps;  // contiguous source elements per row
@@ -370,12 +377,7 @@ int conv_gemm_bf16_launch(const void* x, int64_t ldx, const void* wk, void* y, i
                           int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out, int taps,
                           int pad, const float* bias, int flags, const void* aux, int64_t ld_aux,
                           hipStream_t st) {
-  static int old = -1;
-  if (old < 0) {
-    const char* e = getenv("FS2_GEMM_OLD");
-    old = e && e[0] == '1';
-  }
-  if (!old)
+  if (!g_tune[FS2_TUNE_LEGACY_GEMM])
     return conv_gemm_glds_launch(x, ldx, wk, y, ldy, rows, seq_len, c_in, c_out, taps, pad, bias,
                                  flags, aux, ld_aux, st);
   FS2_CHECK_ARG(c_in % 8 == 0 && ldx % 8 == 0, "fs2_conv_gemm(bf16): c_in/ldx must be multiples of 8");
@@ -425,16 +427,15 @@ int colsum_bf16_launch(const void* x, int64_t ldx, int64_t rows, int64_t cols, f
 
 }  // namespace fs2
 
-extern "C" int fs2_weight_prep_batch(int dtype, const int64_t* jobs, int n_jobs, int64_t max_c_out,
-                                     int64_t max_c_in, void* stream) {
-  if (n_jobs <= 0 || max_c_out <= 0 || max_c_in <= 0) return FS2_OK;
-  const int ct = dtype == FS2_BF16 ? 32 : 16;
-  const int tiles_c = (int)((max_c_in + ct - 1) / ct);
-  dim3 grid((unsigned)(tiles_c * ((max_c_out + 63) / 64)), (unsigned)n_jobs);
+extern "C" int fs2_weight_prep_tile_channels(int dtype) { return dtype == FS2_BF16 ? 32 : 16; }
+
+extern "C" int fs2_weight_prep_batch(int dtype, const int64_t* jobs, int n_jobs, int64_t n_tiles,
+                                     void* stream) {
+  if (n_jobs <= 0 || n_tiles <= 0) return FS2_OK;
   if (dtype == FS2_BF16)
-    fs2::weight_prep_tiles<unsigned short><<<grid, 256, 0, as_stream(stream)>>>(jobs, tiles_c);
+    fs2::weight_prep_tiles<unsigned short><<<(unsigned)n_tiles, 256, 0, as_stream(stream)>>>(jobs, n_jobs);
   else if (dtype == FS2_F32)
-    fs2::weight_prep_tiles<float><<<grid, 256, 0, as_stream(stream)>>>(jobs, tiles_c);
+    fs2::weight_prep_tiles<float><<<(unsigned)n_tiles, 256, 0, as_stream(stream)>>>(jobs, n_jobs);
   else {
     fs2::set_error("fs2_weight_prep_batch: dtype %d not built", dtype);
     return FS2_ERR_DTYPE;

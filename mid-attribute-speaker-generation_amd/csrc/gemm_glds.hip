@@ -310,8 +310,6 @@ __global__ __launch_bounds__(256) void conv_gemm_nt_glds(GldsArgs a) {
   }
 }
 
-static int g_wvariant = -1;  // FS2_WGRAD_STAGES: 1 or 2 (default 1)
-
 // ------------------------------------------------------------------------ weight gradient
 //   slab[z][o][kk] = sum_{m in split z} dy[m, o] * x~[m, kk],  x~[m, j*Cin + c] = x[m + j - pad, c]
 //   bslab[z][o]    = sum_{m in split z} dy[m, o]            (bias gradient, optional)
@@ -340,11 +338,14 @@ struct WgradGlds {
 typedef short s16x4g __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4g lds_s16x4g;
 
-template <int STAGES>
+template <int BT, int STAGES>
 __global__ __launch_bounds__(256) void conv_wgrad_tn_glds(WgradGlds a) {
-  constexpr int BM = 128, BN = 128, BK = 64;
-  constexpr int MI = 4, NI = 4;
-  constexpr int IMG = BK * 128;             // elements per operand image
+  constexpr int BM = BT, BN = BT, BK = 64;  // BT = 128 or 64 (o and kk tile widths)
+  constexpr int MI = BM / 32, NI = BN / 32;
+  constexpr int NCH = BT / 8;               // 16-B chunks per image row
+  constexpr int RPI = 64 / NCH;             // image rows per glds wave-instruction
+  constexpr int IPW = BK / RPI / 4;         // glds per wave per operand per tile
+  constexpr int IMG = BK * BT;              // elements per operand image
   constexpr int STAGE_E = 2 * IMG;
   constexpr int EPI_LD = BN + 4;
   constexpr int EPI_E = (BM / 2) * EPI_LD * 2;
@@ -368,16 +369,20 @@ __global__ __launch_bounds__(256) void conv_wgrad_tn_glds(WgradGlds a) {
   if (r_end > a.M) r_end = a.M;
   const int nk = r_end > r_begin ? (int)((r_end - r_begin + BK - 1) / BK) : 0;
 
-  // per-lane staging descriptors: instruction i stages rows 4*(wave*4+i) + (lane>>4)
+  // per-lane staging descriptors: instruction i stages rows RPI*(wave*IPW+i) + lane/NCH.
+  // Chunk swizzle f(R): 256-B rows (BT 128) (R & 7) << 1; 128-B rows (BT 64)
+  // ((R >> 1) & 3) << 1 -- either way a 32-lane transposed read (8 rows x 2 chunks) hits
+  // 16 distinct 16-B bank slots.
+  auto swz_of = [](int R) { return BT == 128 ? (R & 7) << 1 : ((R >> 1) & 3) << 1; };
   const u16* zero = reinterpret_cast<const u16*>(g_zero_line);
-  const int pc = lane & 15;
-  int R[4], t_i[4], a_col[4], b_j[4], b_c[4];
-  int64_t base_i[4];
-  bool a_ok[4], b_ok[4];
+  const int pc = lane % NCH;
+  int R[IPW], t_i[IPW], a_col[IPW], b_j[IPW], b_c[IPW];
+  int64_t base_i[IPW];
+  bool a_ok[IPW], b_ok[IPW];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    R[i] = (wave * 4 + i) * 4 + (lane >> 4);
-    const int lc = pc ^ ((R[i] & 7) << 1);
+  for (int i = 0; i < IPW; ++i) {
+    R[i] = (wave * IPW + i) * RPI + lane / NCH;
+    const int lc = pc ^ swz_of(R[i]);
     a_col[i] = o0 + lc * 8;
     a_ok[i] = a_col[i] < a.Cout;
     const int kk = n0 + lc * 8;
@@ -395,15 +400,15 @@ __global__ __launch_bounds__(256) void conv_wgrad_tn_glds(WgradGlds a) {
     u16* Bs = As + IMG;
     const int64_t k0 = r_begin + (int64_t)kt * BK;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < IPW; ++i) {
       const int64_t m = k0 + R[i];
       const bool mok = m < r_end;
       const u16* sa = (mok && a_ok[i]) ? a.dy + m * a.ldy + a_col[i] : zero;
-      glds16(sa, As + (wave * 4 + i) * 4 * 128);
+      glds16(sa, As + (wave * IPW + i) * RPI * BT);
       const int tt = t_i[i] + b_j[i] - a.pad;
       const u16* sb = (mok && b_ok[i] && tt >= 0 && tt < a.T)
                           ? a.x + (base_i[i] + tt) * a.ldx + b_c[i] : zero;
-      glds16(sb, Bs + (wave * 4 + i) * 4 * 128);
+      glds16(sb, Bs + (wave * IPW + i) * RPI * BT);
       t_i[i] += BK;
       while (t_i[i] >= a.T) {
         t_i[i] -= (int)a.T;
@@ -425,12 +430,12 @@ __global__ __launch_bounds__(256) void conv_wgrad_tn_glds(WgradGlds a) {
   for (int e = 0; e < 8; ++e) ones[e] = (__bf16)1.0f;
 
   // transposed fragment: 16 columns at col0, k-step ks; rows {4g+q} and {16+4g+q}
-  const int swz = ((4 * g + q) & 7) << 1;
+  const int swz = swz_of(4 * g + q);
   auto tr_frag = [&](const u16* img, int col0, int ks) -> bf16x8g {
     const int lc = (col0 >> 3) + (p >> 1);
-    const int off = (ks * 32 + 4 * g + q) * 128 + ((lc ^ swz) << 3) + ((p & 1) << 2);
+    const int off = (ks * 32 + 4 * g + q) * BT + ((lc ^ swz) << 3) + ((p & 1) << 2);
     const s16x4g lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4g*)(img + off));
-    const s16x4g hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4g*)(img + off + 16 * 128));
+    const s16x4g hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4g*)(img + off + 16 * BT));
     return __builtin_bit_cast(bf16x8g, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
   };
   auto compute = [&](int stage) {
@@ -440,9 +445,9 @@ __global__ __launch_bounds__(256) void conv_wgrad_tn_glds(WgradGlds a) {
     for (int ks = 0; ks < 2; ++ks) {
       bf16x8g fa[MI], fb[NI];
 #pragma unroll
-      for (int i = 0; i < MI; ++i) fa[i] = tr_frag(As, wm * 64 + i * 16, ks);
+      for (int i = 0; i < MI; ++i) fa[i] = tr_frag(As, wm * (BM / 2) + i * 16, ks);
 #pragma unroll
-      for (int j = 0; j < NI; ++j) fb[j] = tr_frag(Bs, wn * 64 + j * 16, ks);
+      for (int j = 0; j < NI; ++j) fb[j] = tr_frag(Bs, wn * (BN / 2) + j * 16, ks);
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -470,7 +475,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_tn_glds(WgradGlds a) {
     for (int kt = 0; kt < nk; ++kt) {
       if (kt + 1 < nk) {
         issue(kt + 1, (kt + 1) & 1);
-        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        if constexpr (IPW == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
@@ -486,7 +492,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_tn_glds(WgradGlds a) {
     for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int o = o0 + wm * 64 + i * 16 + 4 * g + r;
+        const int o = o0 + wm * (BM / 2) + i * 16 + 4 * g + r;
         if (o < a.Cout) a.bslab[(int64_t)z * a.Cout + o] = accb[i][r];
       }
   }
@@ -502,15 +508,16 @@ __global__ __launch_bounds__(256) void conv_wgrad_tn_glds(WgradGlds a) {
         for (int j = 0; j < NI; ++j)
 #pragma unroll
           for (int r = 0; r < 4; ++r)
-            Cs[(i * 16 + 4 * g + r) * EPI_LD + wn * 64 + j * 16 + r16] = acc[i][j][r];
+            Cs[(i * 16 + 4 * g + r) * EPI_LD + wn * (BN / 2) + j * 16 + r16] = acc[i][j][r];
     }
     __syncthreads();
-    const int cc = (tid & 15) * 8;
+    constexpr int TPR = BN / 8, RPP = 256 / TPR;
+    const int cc = (tid % TPR) * 8;
     const int kk = n0 + cc;
 #pragma unroll
-    for (int pp = 0; pp < 4; ++pp) {
-      const int rr = pp * 16 + (tid >> 4);
-      const int o = o0 + h * 64 + rr;
+    for (int pp = 0; pp < (BM / 2) / RPP; ++pp) {
+      const int rr = pp * RPP + tid / TPR;
+      const int o = o0 + h * (BM / 2) + rr;
       if (o < a.Cout && kk < a.Kp) {
         float* dst = slab + (int64_t)o * a.Kp + kk;
         *reinterpret_cast<f32x4*>(dst) = *reinterpret_cast<const f32x4*>(Cs + rr * EPI_LD + cc);
@@ -528,12 +535,20 @@ __global__ __launch_bounds__(256) void conv_wgrad_tn_glds(WgradGlds a) {
 __global__ __launch_bounds__(256) void wgrad_reduce_k1(const float* __restrict__ slab,
                                                        const float* __restrict__ bslab, int splits,
                                                        int Cout, int64_t total, float* dw, float* db) {
-  const int64_t i4 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  // 64 float4 columns x 4 split groups: group y sums splits y, y+4, ... in order, then the
+  // 4 group sums are added in group order (fixed order, bitwise reproducible)
+  __shared__ f32x4 red[4][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int64_t i4 = ((int64_t)blockIdx.x * 64 + tx) * 4;
+  f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
   if (i4 < total) {
-    f32x4 s = ld4(slab + i4);
-    for (int zz = 1; zz < splits; ++zz) s += ld4(slab + zz * total + i4);
-    st4(dw + i4, ld4(dw + i4) + s);
+#pragma unroll 4
+    for (int zz = ty; zz < splits; zz += 4) s += ld4(slab + zz * total + i4);
   }
+  red[ty][tx] = s;
+  __syncthreads();
+  if (ty == 0 && i4 < total)
+    st4(dw + i4, ld4(dw + i4) + (((red[0][tx] + red[1][tx]) + red[2][tx]) + red[3][tx]));
   if (db && blockIdx.x == 0) {
     for (int o = threadIdx.x; o < Cout; o += 256) {
       float b = 0.f;
@@ -579,28 +594,30 @@ __global__ __launch_bounds__(256) void wgrad_reduce_taps(const float* __restrict
 
 int conv_wgrad_glds_launch(const void* dy, int64_t ldy, const void* x, int64_t ldx, float* dw,
                            float* db, int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out,
-                           int taps, int pad, int splits, float* ws, hipStream_t st) {
+                           int taps, int pad, int splits, int tile, float* ws, hipStream_t st) {
   FS2_CHECK_ARG(c_in % 8 == 0 && c_out % 8 == 0 && ldx % 8 == 0 && ldy % 8 == 0 &&
                     ((uintptr_t)dy & 15) == 0 && ((uintptr_t)x & 15) == 0,
                 "fs2_conv_wgrad(bf16): channel counts / strides must be multiples of 8, operands 16-B aligned");
-  if (g_wvariant < 0) {
-    const char* e = getenv("FS2_WGRAD_STAGES");
-    g_wvariant = (e && e[0] == '2') ? 2 : 1;
-  }
   int64_t rps = (rows + splits - 1) / splits;
   rps = (rps + 63) / 64 * 64;
   const int64_t Kp = taps * c_in;
   float* bslab = db ? ws + splits * c_out * Kp : nullptr;
   WgradGlds a{(const u16*)dy, ldy, (const u16*)x, ldx, ws, bslab, rows, seq_len, (int)c_in,
-              (int)c_out, taps, pad, (int)Kp, rps, (int)((c_out + 127) / 128),
-              (int)((Kp + 127) / 128), splits};
+              (int)c_out, taps, pad, (int)Kp, rps, (int)((c_out + tile - 1) / tile),
+              (int)((Kp + tile - 1) / tile), splits};
   const unsigned grid = (unsigned)(a.tiles_o * a.tiles_k * splits);
-  if (g_wvariant == 1) conv_wgrad_tn_glds<1><<<grid, 256, 0, st>>>(a);
-  else conv_wgrad_tn_glds<2><<<grid, 256, 0, st>>>(a);
+  const int stages = g_tune[FS2_TUNE_WGRAD_STAGES] == 2 ? 2 : 1;
+  if (tile == 128) {
+    if (stages == 2) conv_wgrad_tn_glds<128, 2><<<grid, 256, 0, st>>>(a);
+    else conv_wgrad_tn_glds<128, 1><<<grid, 256, 0, st>>>(a);
+  } else {
+    if (stages == 2) conv_wgrad_tn_glds<64, 2><<<grid, 256, 0, st>>>(a);
+    else conv_wgrad_tn_glds<64, 1><<<grid, 256, 0, st>>>(a);
+  }
   if (taps == 1) {
     const int64_t total = c_out * c_in;  // multiple of 64 (both channel counts % 8 == 0)
-    wgrad_reduce_k1<<<(unsigned)((total / 4 + 255) / 256), 256, 0, st>>>(ws, bslab, splits,
-                                                                       (int)c_out, total, dw, db);
+    wgrad_reduce_k1<<<(unsigned)((total / 4 + 63) / 64), 256, 0, st>>>(ws, bslab, splits,
+                                                                     (int)c_out, total, dw, db);
   } else {
     dim3 rg((unsigned)((c_in + 63) / 64), (unsigned)c_out);
     wgrad_reduce_taps<<<rg, 256, 0, st>>>(ws, bslab, splits, (int)c_out, (int)c_in, taps, dw, db);
@@ -608,7 +625,6 @@ int conv_wgrad_glds_launch(const void* dy, int64_t ldy, const void* x, int64_t l
   return launch_status("fs2_conv_wgrad(bf16)");
 }
 
-static int g_variant = -1;  // FS2_GEMM_STAGES: 1 or 2 (default: 2 for K >= 4096, else 1)
 
 template <int BM, int BN, int S>
 static void launch_nt(const GldsArgs& a, bool tapaligned, hipStream_t st) {
@@ -623,20 +639,13 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
                           hipStream_t st) {
   FS2_CHECK_ARG(c_in % 8 == 0 && ldx % 8 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)wk & 15) == 0,
                 "fs2_conv_gemm(bf16): c_in/ldx must be multiples of 8 and operands 16-B aligned");
-  if (g_variant < 0) {
-    const char* e = getenv("FS2_GEMM_STAGES");
-    g_variant = (e && e[0] == '2') ? 2 : (e && e[0] == '1') ? 1 : 0;
-  }
-  const int stages = g_variant ? g_variant : (taps * c_in >= 4096 ? 2 : 1);
   const int K = (int)(taps * c_in);
-  const bool out_bf16 = flags & FS2_EPI_OUT_BF16, aux_bf16 = flags & FS2_EPI_AUX_BF16;
-  const int yb = out_bf16 ? 2 : 4, ab = aux_bf16 ? 2 : 4;
+  // long reductions keep the next tile's DMA in flight across the barrier
+  const int stages = g_tune[FS2_TUNE_GEMM_STAGES] ? g_tune[FS2_TUNE_GEMM_STAGES] : (K >= 4096 ? 2 : 1);
   const bool uses_aux = flags & (FS2_EPI_ADD_AUX | FS2_EPI_RELU_MASK_AUX);
   const int vec = c_out % 8 == 0 && ldy % 8 == 0 && ((uintptr_t)y % 16) == 0 &&
                   (!(flags & FS2_EPI_BIAS) || ((uintptr_t)bias % 16) == 0) &&
                   (!uses_aux || (ld_aux % 8 == 0 && ((uintptr_t)aux % 16) == 0));
-  (void)yb;
-  (void)ab;
   GldsArgs a{(const u16*)x, ldx, (const u16*)wk, y, ldy, rows, seq_len, (int)c_in, (int)c_out,
              taps, pad, K, bias, flags, aux, ld_aux, 0, 0, vec};
   const bool tapaligned = c_in % 64 == 0;

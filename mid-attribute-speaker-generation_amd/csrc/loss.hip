@@ -233,64 +233,89 @@ __global__ void gmm_logprob(const float* e, const float* pi, const float* mu, co
   }
 }
 
-// one thread per head output; loops over the batch in order (deterministic)
-__global__ void gmm_head_bwd(const float* meta, const float* e, const float* pi, const float* mu,
-                             const float* sigma, const float* sigma_pre, const float* resp,
-                             const float* g, int64_t B, int in_dim, int K, int D, float* dw_pi,
-                             float* db_pi, float* dw_s, float* db_s, float* dw_mu, float* db_mu) {
+// dL/dz of the pi head output (b, k): through log_softmax, clamp, normalisation, softmax
+FS2_DEV float gmm_pi_gz(const float* pi, const float* resp, const float* g, int64_t b, int K, int k) {
+  float lm[16], pn[16], sm[16], dpn[16];
+  const float* p = pi + b * K;
+  log_mix(p, K, lm, pn, sm);
+  const float eps = 1.1920928955078125e-07f;
+  float S = 0.f;
+  for (int j = 0; j < K; ++j) S += p[j];
+  for (int j = 0; j < K; ++j) {
+    const float dl = g[b] * resp[b * K + j] - sm[j] * g[b];
+    const bool in = pn[j] >= eps && pn[j] <= 1.f - eps;
+    const float c = fminf(fmaxf(pn[j], eps), 1.f - eps);
+    dpn[j] = in ? dl / c : 0.f;
+  }
+  float t = 0.f;
+  for (int j = 0; j < K; ++j) t += dpn[j] * p[j];
+  float dot = 0.f, dpk = 0.f;
+  for (int j = 0; j < K; ++j) {
+    const float dpj = dpn[j] / S - t / (S * S);
+    dot += p[j] * dpj;
+    if (j == k) dpk = dpj;
+  }
+  return p[k] * (dpk - dot);
+}
+
+// Blocks 0..: one thread per mu / sigma head output, looping over the batch in order.
+// Last block: the pi head -- (b, k) gradients for a chunk of the batch into LDS, then one
+// thread per (k, input) sums the chunk in batch order.  Deterministic throughout.
+__global__ __launch_bounds__(256) void gmm_head_bwd(const float* meta, const float* e,
+                                                    const float* pi, const float* mu,
+                                                    const float* sigma, const float* sigma_pre,
+                                                    const float* resp, const float* g, int64_t B,
+                                                    int in_dim, int K, int D, float* dw_pi,
+                                                    float* db_pi, float* dw_s, float* db_s,
+                                                    float* dw_mu, float* db_mu) {
   const int KD = K * D;
-  const int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (o >= 2 * KD + K) return;
+  if (blockIdx.x == gridDim.x - 1) {
+    __shared__ float gzs[256];
+    const int CH = 256 / K, t = threadIdx.x;
+    const int k_acc = t / (in_dim + 1), i_acc = t - k_acc * (in_dim + 1);
+    float acc = 0.f;
+    for (int64_t b0 = 0; b0 < B; b0 += CH) {
+      const int64_t b = b0 + t / K;
+      if (t < CH * K && b < B) gzs[t] = gmm_pi_gz(pi, resp, g, b, K, t % K);
+      __syncthreads();
+      if (k_acc < K) {
+        for (int64_t bb = b0; bb < b0 + CH && bb < B; ++bb) {
+          const float gz = gzs[(bb - b0) * K + k_acc];
+          acc += i_acc < in_dim ? gz * meta[bb * in_dim + i_acc] : gz;
+        }
+      }
+      __syncthreads();
+    }
+    if (k_acc < K) {
+      if (i_acc < in_dim) dw_pi[k_acc * in_dim + i_acc] += acc;
+      else db_pi[k_acc] += acc;
+    }
+    return;
+  }
+  const int o = blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= 2 * KD) return;
+  const int kd = o < KD ? o : o - KD;
+  const int k = kd / D, dd = kd - k * D;
   float acc_w[8] = {0, 0, 0, 0, 0, 0, 0, 0}, acc_b = 0.f;
   for (int64_t b = 0; b < B; ++b) {
+    const int64_t idx = b * KD + kd;
+    const float gg = g[b] * resp[b * K + k];
+    const float sg = sigma[idx], df = e[b * D + dd] - mu[idx];
     float gz;
-    if (o < 2 * KD) {
-      const int64_t kd = o % KD;
-      const int k = (int)(kd / D);
-      const int64_t idx = b * KD + kd;
-      const float gg = g[b] * resp[b * K + k];
-      const float sg = sigma[idx], df = e[b * D + (kd % D)] - mu[idx];
-      if (o < KD) {  // mu
-        gz = gg * df / (sg * sg);
-      } else {  // sigma through softplus
-        const float dsg = gg * (df * df / (sg * sg * sg) - 1.f / sg);
-        const float x = sigma_pre[idx];
-        gz = dsg * (x > 20.f ? 1.f : 1.f / (1.f + expf(-x)));
-      }
-    } else {  // pi through log_softmax, clamp, normalisation and softmax
-      const int k = (int)(o - 2 * KD);
-      float lm[16], pn[16], sm[16], dpn[16];
-      const float* p = pi + b * K;
-      log_mix(p, K, lm, pn, sm);
-      const float eps = 1.1920928955078125e-07f;
-      float S = 0.f;
-      for (int j = 0; j < K; ++j) S += p[j];
-      for (int j = 0; j < K; ++j) {
-        const float dl = g[b] * resp[b * K + j] - sm[j] * g[b];
-        const bool in = pn[j] >= eps && pn[j] <= 1.f - eps;
-        const float c = fminf(fmaxf(pn[j], eps), 1.f - eps);
-        dpn[j] = in ? dl / c : 0.f;
-      }
-      float t = 0.f;
-      for (int j = 0; j < K; ++j) t += dpn[j] * p[j];
-      float dot = 0.f, dpk = 0.f;
-      for (int j = 0; j < K; ++j) {
-        const float dpj = dpn[j] / S - t / (S * S);
-        dot += p[j] * dpj;
-        if (j == k) dpk = dpj;
-      }
-      gz = p[k] * (dpk - dot);
+    if (o < KD) {  // mu
+      gz = gg * df / (sg * sg);
+    } else {  // sigma through softplus
+      const float dsg = gg * (df * df / (sg * sg * sg) - 1.f / sg);
+      const float x = sigma_pre[idx];
+      gz = dsg * (x > 20.f ? 1.f : 1.f / (1.f + expf(-x)));
     }
     for (int i = 0; i < in_dim; ++i) acc_w[i] += gz * meta[b * in_dim + i];
     acc_b += gz;
   }
-  float *dw, *db;
-  int64_t row;
-  if (o < KD) { dw = dw_mu; db = db_mu; row = o; }
-  else if (o < 2 * KD) { dw = dw_s; db = db_s; row = o - KD; }
-  else { dw = dw_pi; db = db_pi; row = o - 2 * KD; }
-  for (int i = 0; i < in_dim; ++i) dw[row * in_dim + i] += acc_w[i];
-  db[row] += acc_b;
+  float* dw = o < KD ? dw_mu : dw_s;
+  float* db = o < KD ? db_mu : db_s;
+  for (int i = 0; i < in_dim; ++i) dw[kd * in_dim + i] += acc_w[i];
+  db[kd] += acc_b;
 }
 
 __global__ void mean_k(const float* x, int64_t n, float* out, const float* den) {
@@ -420,8 +445,9 @@ int fs2_gmm_head_bwd(const float* meta, const float* e, const float* pi, const f
                      float* dw_pi, float* db_pi, float* dw_sigma, float* db_sigma, float* dw_mu,
                      float* db_mu, void* stream) {
   FS2_CHECK_ARG(k >= 1 && k <= 16 && in_dim >= 1 && in_dim <= 8, "fs2_gmm_head_bwd: k <= 16, in_dim <= 8");
-  const int64_t n = 2LL * k * d + k;
-  gmm_head_bwd<<<(unsigned)((n + 255) / 256), 256, 0, as_stream(stream)>>>(
+  FS2_CHECK_ARG(k * (in_dim + 1) <= 256, "fs2_gmm_head_bwd: k * (in_dim + 1) <= 256");
+  const int64_t n = 2LL * k * d;
+  gmm_head_bwd<<<(unsigned)((n + 255) / 256 + 1), 256, 0, as_stream(stream)>>>(
       meta, e, pi, mu, sigma, sigma_pre, resp, g_logp, batch, in_dim, k, d, dw_pi, db_pi, dw_sigma,
       db_sigma, dw_mu, db_mu);
   return launch_status("fs2_gmm_head_bwd");

@@ -6,7 +6,7 @@
 // (SubLayers.py:54-55,91-93), padded-row zeroing after it (Layers.py:25,28), dropout
 // after it and the Linear(256 -> 1) head of the variance predictor (modules.py:209-250).
 // Backward recomputes nothing but the dropout masks: xhat and rstd are saved.
-// Affine/linear-head gradients are reduced per 64-row block in registers + LDS and then
+// Affine/linear-head gradients are reduced per 32-row block in registers + LDS and then
 // summed over blocks in a fixed order (bitwise reproducible).
 //
 // BatchNorm: two-pass column statistics over every (utterance, frame) row, padded frames
@@ -18,7 +18,7 @@
 namespace fs2 {
 
 constexpr int LN_D = 256;
-constexpr int LN_ROWS = 64;  // rows per block in the backward (16 per wave)
+constexpr int LN_ROWS = 32;  // rows per block in the backward (8 per wave)
 
 struct LnFwd {
   const float* y;
@@ -49,6 +49,12 @@ __global__ __launch_bounds__(256) void ln_fwd_f32(LnFwd a) {
   const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= a.rows) return;
   const int64_t e0 = r * LN_D + 4 * lane;
+  const bool pad = row_padded(a.lens, a.T, r);
+  if (pad && !a.dot_out) {  // masked row: output 0; xhat/rstd are never read (bwd skips it)
+    st4(a.out + e0, f32x4{0.f, 0.f, 0.f, 0.f});
+    if (a.out_t) st4_bf16(a.out_t + e0, f32x4{0.f, 0.f, 0.f, 0.f});
+    return;
+  }
   f32x4 z = ld4(a.y + e0);
   if (a.p_in > 0.f) z *= dropout4(a.seed, a.site_in, (uint64_t)e0, a.p_in);
   if (a.res) z += ld4(a.res + e0);
@@ -59,9 +65,7 @@ __global__ __launch_bounds__(256) void ln_fwd_f32(LnFwd a) {
   const f32x4 xh = c * rs;
   f32x4 u = xh * ld4(a.gamma + 4 * lane) + ld4(a.beta + 4 * lane);
   if (a.p_out > 0.f) u *= dropout4(a.seed, a.site_out, (uint64_t)e0, a.p_out);
-  const bool pad = row_padded(a.lens, a.T, r);
-  if (pad && !a.dot_out) u = f32x4{0.f, 0.f, 0.f, 0.f};  // dot mode masks only the head output
-  st4(a.out + e0, u);
+  st4(a.out + e0, u);  // (dot mode masks only the head output)
   if (a.out_t) st4_bf16(a.out_t + e0, u);
   st4(a.xhat + e0, xh);
   if (lane == 0) a.rstd[r] = rs;
@@ -87,6 +91,7 @@ struct LnBwd {
   const float* relu_y;
   float* dy;
   float* dres;
+  int dres_add;  // 1: dres += dz ; 0: dres = dz
   float* part;  // [3][nblk][256] dgamma, dbeta, dw_dot partials, then [nblk] db_dot partials
   int64_t nblk;
   unsigned short* dy_t;  // optional bf16 copy of dy
@@ -107,19 +112,24 @@ __global__ __launch_bounds__(256) void ln_bwd_f32(LnBwd a) {
     const int64_t r = rbeg + i;
     if (r >= a.rows) break;
     const int64_t e0 = r * LN_D + 4 * lane;
-    const bool pad = row_padded(a.lens, a.T, r);
+    if (row_padded(a.lens, a.T, r)) {  // masked row: zero upstream gradient, nothing to add
+      if (a.dres && !a.dres_add) st4(a.dres + e0, f32x4{0.f, 0.f, 0.f, 0.f});
+      if (a.dy) st4(a.dy + e0, f32x4{0.f, 0.f, 0.f, 0.f});
+      if (a.dy_t) st4_bf16(a.dy_t + e0, f32x4{0.f, 0.f, 0.f, 0.f});
+      continue;
+    }
     const f32x4 xh = ld4(a.xhat + e0);
     const f32x4 mo = a.p_out > 0.f ? dropout4(a.seed, a.site_out, (uint64_t)e0, a.p_out)
                                    : f32x4{1.f, 1.f, 1.f, 1.f};
     f32x4 du;
     if (a.ddot) {
-      const float gr = pad ? 0.f : a.ddot[r];
+      const float gr = a.ddot[r];
       du = gr * w;
       const f32x4 u = (xh * gam + bet) * mo;
       pw += gr * u;
       pdb += gr;
     } else {
-      du = pad ? f32x4{0.f, 0.f, 0.f, 0.f} : ld4(a.dout + e0);
+      du = ld4(a.dout + e0);
     }
     du *= mo;
     pg += du * xh;
@@ -129,7 +139,7 @@ __global__ __launch_bounds__(256) void ln_bwd_f32(LnBwd a) {
     const float m2 =
         wave_sum(dxh.x * xh.x + dxh.y * xh.y + dxh.z * xh.z + dxh.w * xh.w) * (1.f / LN_D);
     const f32x4 dz = a.rstd[r] * (dxh - m1 - xh * m2);
-    if (a.dres) st4(a.dres + e0, ld4(a.dres + e0) + dz);
+    if (a.dres) st4(a.dres + e0, a.dres_add ? ld4(a.dres + e0) + dz : dz);
     f32x4 dy = dz;
     if (a.p_in > 0.f) dy *= dropout4(a.seed, a.site_in, (uint64_t)e0, a.p_in);
     if (a.relu_y) {
@@ -139,7 +149,7 @@ __global__ __launch_bounds__(256) void ln_bwd_f32(LnBwd a) {
       dy.z = yv.z > 0.f ? dy.z : 0.f;
       dy.w = yv.w > 0.f ? dy.w : 0.f;
     }
-    st4(a.dy + e0, dy);
+    if (a.dy) st4(a.dy + e0, dy);
     if (a.dy_t) st4_bf16(a.dy_t + e0, dy);
     py += dy;  // bias gradient of the layer that produced y (fused colsum)
   }
@@ -156,29 +166,33 @@ __global__ __launch_bounds__(256) void ln_bwd_f32(LnBwd a) {
 }
 
 // ------------------------------------------------------------------ BatchNorm
-constexpr int BN_ROWS = 256;
+constexpr int BN_ROWS = 64;
 
-// MODE 0: sum z ; MODE 1: sum (z - mean)^2
+// Column partial sums over BN_ROWS-row chunks, 4 consecutive channels per lane (16-B loads):
+// block (x, y) covers channels [256x, 256x+256) of rows [BN_ROWS*y, BN_ROWS*(y+1)), four row
+// lanes summed in lane order.  MODE 0: sum z ; MODE 1: sum (z - mean)^2
 template <int MODE>
-__global__ void bn_partial(const float* z, const float* mean, int64_t rows, int64_t c, float* part) {
-  const int64_t col = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
-  const int ry = threadIdx.x >> 6;
+__global__ __launch_bounds__(256) void bn_partial(const float* z, const float* mean, int64_t rows,
+                                                  int64_t c, float* part) {
+  const int tx = threadIdx.x & 63, ry = threadIdx.x >> 6;
+  const int64_t col = ((int64_t)blockIdx.x * 64 + tx) * 4;
   const int64_t r0 = (int64_t)blockIdx.y * BN_ROWS;
-  __shared__ float red[4][64];
-  float s = 0.f;
+  __shared__ f32x4 red[4][64];
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
   if (col < c) {
-    const float mu = MODE == 1 ? mean[col] : 0.f;
+    const f32x4 mu = MODE == 1 ? ld4(mean + col) : f32x4{0.f, 0.f, 0.f, 0.f};
     const int64_t r1 = r0 + BN_ROWS < rows ? r0 + BN_ROWS : rows;
+#pragma unroll 4
     for (int64_t r = r0 + ry; r < r1; r += 4) {
-      const float v = z[r * c + col];
-      s += MODE == 0 ? v : (v - mu) * (v - mu);
+      const f32x4 v = ld4(z + r * c + col);
+      if (MODE == 0) s += v;
+      else s += (v - mu) * (v - mu);
     }
   }
-  red[ry][threadIdx.x & 63] = s;
+  red[ry][tx] = s;
   __syncthreads();
   if (ry == 0 && col < c)
-    part[(int64_t)blockIdx.y * c + col] =
-        red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+    st4(part + (int64_t)blockIdx.y * c + col, ((red[0][tx] + red[1][tx]) + red[2][tx]) + red[3][tx]);
 }
 
 // in-order column sum of partial rows: 64 columns x 16 lanes per block (see colsum_final)
@@ -224,63 +238,70 @@ __global__ __launch_bounds__(1024) void bn_var_final(const float* part, int64_t 
   if (rv) rv[col] = (1.f - mom) * rv[col] + mom * (rows > 1 ? s / (float)(rows - 1) : var);
 }
 
-__global__ void bn_apply(const float* z, const float* mean, const float* rstd, const float* gamma,
-                         const float* beta, int64_t rows, int64_t c, int act_tanh, float p,
-                         uint64_t seed, uint64_t site, const float* res, float* out,
-                         unsigned short* out_t) {
-  const int64_t n = rows * c;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n;
-       e += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t col = e % c;
-    float v = (z[e] - mean[col]) * rstd[col] * gamma[col] + beta[col];
-    if (act_tanh) v = tanhf(v);
-    if (p > 0.f) v *= dropout1(seed, site, (uint64_t)e, p);
-    if (res) v += res[e];
-    out[e] = v;
-    if (out_t) out_t[e] = to_bf16(v);
+// out = act(BN(z)) * dropout (+ res), 4 consecutive elements (same row) per lane
+__global__ __launch_bounds__(256) void bn_apply(const float* z, const float* mean, const float* rstd,
+                                                const float* gamma, const float* beta, int64_t n4,
+                                                int c, int act_tanh, float p, uint64_t seed,
+                                                uint64_t site, const float* res, float* out,
+                                                unsigned short* out_t) {
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4;
+       q += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e0 = q * 4;
+    const int col = (int)(e0 % c);
+    f32x4 v = (ld4(z + e0) - ld4(mean + col)) * ld4(rstd + col) * ld4(gamma + col) + ld4(beta + col);
+    if (act_tanh) v = f32x4{tanhf(v.x), tanhf(v.y), tanhf(v.z), tanhf(v.w)};
+    if (p > 0.f) v *= dropout4(seed, site, (uint64_t)e0, p);
+    if (res) v += ld4(res + e0);
+    if (out) st4(out + e0, v);
+    if (out_t) st4_bf16(out_t + e0, v);
   }
 }
 
-// g = dout * mask * act'(a);  partial sums of g and g * xhat
-FS2_DEV float bn_g(const float* dout, const float* z, float mu, float rs, float ga, float be,
-                   int act_tanh, float p, uint64_t seed, uint64_t site, int64_t e, float* xh_out) {
-  const float xh = (z[e] - mu) * rs;
+// g = dout * mask * act'(a) for 4 consecutive elements; also returns xhat
+FS2_DEV f32x4 bn_g4(const float* dout, const float* z, f32x4 mu, f32x4 rs, f32x4 ga, f32x4 be,
+                    int act_tanh, float p, uint64_t seed, uint64_t site, int64_t e0, f32x4* xh_out) {
+  const f32x4 xh = (ld4(z + e0) - mu) * rs;
   *xh_out = xh;
-  float g = dout[e];
-  if (p > 0.f) g *= dropout1(seed, site, (uint64_t)e, p);
+  f32x4 g = ld4(dout + e0);
+  if (p > 0.f) g *= dropout4(seed, site, (uint64_t)e0, p);
   if (act_tanh) {
-    const float t = tanhf(xh * ga + be);
+    const f32x4 a = xh * ga + be;
+    const f32x4 t = {tanhf(a.x), tanhf(a.y), tanhf(a.z), tanhf(a.w)};
     g *= 1.f - t * t;
   }
   return g;
 }
 
-__global__ void bn_bwd_partial(const float* dout, const float* z, const float* mean,
-                               const float* rstd, const float* gamma, const float* beta,
-                               int64_t rows, int64_t c, int act_tanh, float p, uint64_t seed,
-                               uint64_t site, float* part_g, float* part_gx) {
-  const int64_t col = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
-  const int ry = threadIdx.x >> 6;
+__global__ __launch_bounds__(256) void bn_bwd_partial(const float* dout, const float* z,
+                                                      const float* mean, const float* rstd,
+                                                      const float* gamma, const float* beta,
+                                                      int64_t rows, int64_t c, int act_tanh,
+                                                      float p, uint64_t seed, uint64_t site,
+                                                      float* part_g, float* part_gx) {
+  const int tx = threadIdx.x & 63, ry = threadIdx.x >> 6;
+  const int64_t col = ((int64_t)blockIdx.x * 64 + tx) * 4;
   const int64_t r0 = (int64_t)blockIdx.y * BN_ROWS;
-  __shared__ float red[2][4][64];
-  float sg = 0.f, sgx = 0.f;
+  __shared__ f32x4 red[2][4][64];
+  f32x4 sg = {0.f, 0.f, 0.f, 0.f}, sgx = sg;
   if (col < c) {
-    const float mu = mean[col], rs = rstd[col], ga = gamma[col], be = beta[col];
+    const f32x4 mu = ld4(mean + col), rs = ld4(rstd + col), ga = ld4(gamma + col),
+                be = ld4(beta + col);
     const int64_t r1 = r0 + BN_ROWS < rows ? r0 + BN_ROWS : rows;
     for (int64_t r = r0 + ry; r < r1; r += 4) {
-      float xh;
-      const float g = bn_g(dout, z, mu, rs, ga, be, act_tanh, p, seed, site, r * c + col, &xh);
+      f32x4 xh;
+      const f32x4 g = bn_g4(dout, z, mu, rs, ga, be, act_tanh, p, seed, site, r * c + col, &xh);
       sg += g;
       sgx += g * xh;
     }
   }
-  red[0][ry][threadIdx.x & 63] = sg;
-  red[1][ry][threadIdx.x & 63] = sgx;
+  red[0][ry][tx] = sg;
+  red[1][ry][tx] = sgx;
   __syncthreads();
   if (ry == 0 && col < c) {
-    const int t = threadIdx.x;
-    part_g[(int64_t)blockIdx.y * c + col] = red[0][0][t] + red[0][1][t] + red[0][2][t] + red[0][3][t];
-    part_gx[(int64_t)blockIdx.y * c + col] = red[1][0][t] + red[1][1][t] + red[1][2][t] + red[1][3][t];
+    st4(part_g + (int64_t)blockIdx.y * c + col,
+        ((red[0][0][tx] + red[0][1][tx]) + red[0][2][tx]) + red[0][3][tx]);
+    st4(part_gx + (int64_t)blockIdx.y * c + col,
+        ((red[1][0][tx] + red[1][1][tx]) + red[1][2][tx]) + red[1][3][tx]);
   }
 }
 
@@ -299,21 +320,24 @@ __global__ __launch_bounds__(1024) void bn_bwd_final(const float* part_g, const 
   if (dgamma) dgamma[col] += sgx;
 }
 
-__global__ void bn_bwd_apply(const float* dout, const float* z, const float* mean, const float* rstd,
-                             const float* gamma, const float* beta, const float* sums, int64_t rows,
-                             int64_t c, int act_tanh, float p, uint64_t seed, uint64_t site,
-                             float* dz, unsigned short* dz_t) {
-  const int64_t n = rows * c;
+__global__ __launch_bounds__(256) void bn_bwd_apply(const float* dout, const float* z,
+                                                    const float* mean, const float* rstd,
+                                                    const float* gamma, const float* beta,
+                                                    const float* sums, int64_t n4, int64_t rows,
+                                                    int c, int act_tanh, float p, uint64_t seed,
+                                                    uint64_t site, float* dz, unsigned short* dz_t) {
   const float inv_m = 1.f / (float)rows;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n;
-       e += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t col = e % c;
-    float xh;
-    const float g = bn_g(dout, z, mean[col], rstd[col], gamma[col], beta[col], act_tanh, p, seed,
-                         site, e, &xh);
-    const float v = gamma[col] * rstd[col] * (g - sums[col] * inv_m - xh * sums[c + col] * inv_m);
-    dz[e] = v;
-    if (dz_t) dz_t[e] = to_bf16(v);
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4;
+       q += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e0 = q * 4;
+    const int col = (int)(e0 % c);
+    const f32x4 ga = ld4(gamma + col), rs = ld4(rstd + col);
+    f32x4 xh;
+    const f32x4 g = bn_g4(dout, z, ld4(mean + col), rs, ga, ld4(beta + col), act_tanh, p, seed,
+                          site, e0, &xh);
+    const f32x4 v = ga * rs * (g - ld4(sums + col) * inv_m - xh * ld4(sums + c + col) * inv_m);
+    if (dz) st4(dz + e0, v);
+    if (dz_t) st4_bf16(dz_t + e0, v);
   }
 }
 
@@ -363,8 +387,8 @@ int fs2_ln_bwd(int dtype, const float* dout, const float* ddot, const float* dot
                const float* xhat, const float* rstd, const float* gamma, const float* beta,
                const int64_t* lens, int64_t seq_len, int64_t rows, int d, float p_in, float p_out,
                uint64_t seed, uint64_t site_in, uint64_t site_out, const float* relu_y, float* dy,
-               void* dy_t, float* dres, float* dgamma, float* dbeta, float* dw_dot, float* db_dot,
-               float* dbias_in, float* ws, int64_t ws_bytes, void* stream) {
+               void* dy_t, float* dres, int dres_add, float* dgamma, float* dbeta, float* dw_dot,
+               float* db_dot, float* dbias_in, float* ws, int64_t ws_bytes, void* stream) {
   if (int rc = copy_dtype_ok(dtype, "fs2_ln_bwd")) return rc;
   FS2_CHECK_ARG(d == LN_D, "fs2_ln_bwd: only d = 256 is supported (got %d)", d);
   FS2_CHECK_ARG((dout != nullptr) != (ddot != nullptr), "fs2_ln_bwd: give exactly one of dout/ddot");
@@ -374,7 +398,7 @@ int fs2_ln_bwd(int dtype, const float* dout, const float* ddot, const float* dot
   hipStream_t st = as_stream(stream);
   const int64_t nblk = (rows + LN_ROWS - 1) / LN_ROWS;
   LnBwd a{dout, ddot, dot_w, xhat, rstd, gamma, beta, lens, seq_len, rows, p_in, p_out, seed,
-          site_in, site_out, relu_y, dy, dres, ws, nblk,
+          site_in, site_out, relu_y, dy, dres, dres_add, ws, nblk,
           dtype == FS2_BF16 ? (unsigned short*)dy_t : nullptr};
   ln_bwd_f32<<<(unsigned)nblk, 256, 0, st>>>(a);
   int rc = launch_status("fs2_ln_bwd");
@@ -404,16 +428,18 @@ int fs2_bn_fwd(int dtype, const float* z, int64_t rows, int64_t c, const float* 
   FS2_CHECK_ARG(ws_bytes >= fs2_bn_ws_bytes(rows, c), "fs2_bn_fwd: workspace too small");
   hipStream_t st = as_stream(stream);
   const int64_t nparts = (rows + BN_ROWS - 1) / BN_ROWS;
-  dim3 grid((unsigned)((c + 63) / 64), (unsigned)nparts);
+  FS2_CHECK_ARG(c % 4 == 0, "fs2_bn_fwd: channel count must be a multiple of 4");
+  dim3 grid((unsigned)((c + 255) / 256), (unsigned)nparts);
   const unsigned cg = (unsigned)((c + 63) / 64);
   bn_partial<0><<<grid, 256, 0, st>>>(z, nullptr, rows, c, ws);
   bn_mean_final<<<cg, 1024, 0, st>>>(ws, nparts, rows, c, mean);
   bn_partial<1><<<grid, 256, 0, st>>>(z, mean, rows, c, ws);
   bn_var_final<<<cg, 1024, 0, st>>>(ws, nparts, rows, c, eps, momentum, mean, running_mean,
                                    running_var, rstd);
-  bn_apply<<<ew_grid(rows * c), 256, 0, st>>>(z, mean, rstd, gamma, beta, rows, c, act_tanh, p,
-                                              seed, site, res, out,
-                                              dtype == FS2_BF16 ? (unsigned short*)out_t : nullptr);
+  unsigned short* ot = dtype == FS2_BF16 ? (unsigned short*)out_t : nullptr;
+  FS2_CHECK_ARG(out || ot, "fs2_bn_fwd: no output requested");
+  bn_apply<<<ew_grid(rows * c / 4), 256, 0, st>>>(z, mean, rstd, gamma, beta, rows * c / 4, (int)c,
+                                                  act_tanh, p, seed, site, res, out, ot);
   return launch_status("fs2_bn_fwd");
 }
 
@@ -429,14 +455,17 @@ int fs2_bn_bwd(int dtype, const float* dout, const float* z, const float* mean, 
   float* part_g = ws;
   float* part_gx = ws + nparts * c;
   float* sums = ws + 2 * nparts * c;
-  dim3 grid((unsigned)((c + 63) / 64), (unsigned)nparts);
+  FS2_CHECK_ARG(c % 4 == 0, "fs2_bn_bwd: channel count must be a multiple of 4");
+  unsigned short* zt = dtype == FS2_BF16 ? (unsigned short*)dz_t : nullptr;
+  FS2_CHECK_ARG(dz || zt, "fs2_bn_bwd: no output requested");
+  dim3 grid((unsigned)((c + 255) / 256), (unsigned)nparts);
   bn_bwd_partial<<<grid, 256, 0, st>>>(dout, z, mean, rstd, gamma, beta, rows, c, act_tanh, p,
                                        seed, site, part_g, part_gx);
   bn_bwd_final<<<(unsigned)((c + 63) / 64), 1024, 0, st>>>(part_g, part_gx, nparts, c, sums,
                                                              dgamma, dbeta);
-  bn_bwd_apply<<<ew_grid(rows * c), 256, 0, st>>>(dout, z, mean, rstd, gamma, beta, sums, rows, c,
-                                                  act_tanh, p, seed, site, dz,
-                                                  dtype == FS2_BF16 ? (unsigned short*)dz_t : nullptr);
+  bn_bwd_apply<<<ew_grid(rows * c / 4), 256, 0, st>>>(dout, z, mean, rstd, gamma, beta, sums,
+                                                      rows * c / 4, rows, (int)c, act_tanh, p,
+                                                      seed, site, dz, zt);
   return launch_status("fs2_bn_bwd");
 }
 

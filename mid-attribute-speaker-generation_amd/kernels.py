@@ -144,28 +144,31 @@ def ln_fwd(y, gamma, beta, res=None, lens=None, seq_len=1, p_in=0.0, p_out=0.0, 
 
 def ln_bwd(xhat, rstd, gamma, beta, dgamma, dbeta, dout=None, ddot=None, dot_w=None,
            dw_dot=None, db_dot=None, lens=None, seq_len=1, p_in=0.0, p_out=0.0, seed=0,
-           site_in=0, site_out=0, relu_y=None, dres=None, copy=None, dbias_in=None):
-    """Returns (dy fp32, dy compute copy or None); dbias_in (+)= column sums of dy."""
+           site_in=0, site_out=0, relu_y=None, dres=None, copy=None, dbias_in=None,
+           dres_add=True):
+    """Returns (dy fp32, dy compute copy or None); dbias_in (+)= column sums of dy.
+    With a compute copy the fp32 dy is not produced (None): only the copy feeds the GEMMs."""
     _dev(xhat, rstd, gamma, beta, dout, ddot, dot_w, relu_y, dres, lens)
     rows, d = xhat.shape
-    dy = torch.empty_like(xhat)
+    dy = torch.empty_like(xhat) if copy is None else None
     dy_t = _copy(xhat.shape, copy, xhat.device)
     n = lib.fs2_ln_bwd_ws_bytes(rows, d)
     w = ws(n, xhat.device)
     lib.fs2_ln_bwd(BF16 if copy is not None else F32, ptr(dout), ptr(ddot), ptr(dot_w), ptr(xhat),
                    ptr(rstd), ptr(gamma), ptr(beta), ptr(lens), seq_len, rows, d, p_in, p_out,
                    seed, site_in, site_out, ptr(relu_y), ptr(dy), ptr(dy_t), ptr(dres),
-                   ptr(dgamma), ptr(dbeta), ptr(dw_dot), ptr(db_dot), ptr(dbias_in), ptr(w), n,
+                   int(dres_add), ptr(dgamma), ptr(dbeta), ptr(dw_dot), ptr(db_dot), ptr(dbias_in), ptr(w), n,
                    stream())
     return dy, dy_t
 
 
 # ------------------------------------------------------------------ BatchNorm
 def bn_fwd(z, gamma, beta, running_mean, running_var, act_tanh, p, seed, site, res=None,
-           eps=1e-5, momentum=0.1, copy=None):
+           eps=1e-5, momentum=0.1, copy=None, want_out=True):
+    """(out fp32 or None when only the copy is wanted, out copy or None, mean, rstd)."""
     _dev(z, gamma, beta, running_mean, running_var, res)
     rows, c = z.shape
-    out = torch.empty_like(z)
+    out = torch.empty_like(z) if (want_out or copy is None) else None
     out_t = _copy(z.shape, copy, z.device)
     mean = torch.empty(c, dtype=torch.float32, device=z.device)
     rstd = torch.empty(c, dtype=torch.float32, device=z.device)
@@ -181,7 +184,7 @@ def bn_fwd(z, gamma, beta, running_mean, running_var, act_tanh, p, seed, site, r
 def bn_bwd(dout, z, mean, rstd, gamma, beta, dgamma, dbeta, act_tanh, p, seed, site, copy=None):
     _dev(dout, z, mean, rstd, gamma, beta, dgamma, dbeta)
     rows, c = z.shape
-    dz = torch.empty_like(z)
+    dz = torch.empty_like(z) if copy is None else None  # with a copy only it feeds the GEMMs
     dz_t = _copy(z.shape, copy, z.device)
     n = lib.fs2_bn_ws_bytes(rows, c)
     w = ws(n, z.device)
@@ -211,8 +214,10 @@ def embedding_fwd(ids, table):
 
 def embedding_bwd(dout, ids, dtable, padding_idx=-1):
     _dev(dout, ids, dtable)
+    n = lib.fs2_embedding_bwd_ws_bytes(ids.numel(), dtable.shape[1], dtable.shape[0])
+    w = ws(n, dout.device)
     lib.fs2_embedding_bwd(ptr(dout), ptr(ids), ids.numel(), dtable.shape[1], padding_idx,
-                          ptr(dtable), stream())
+                          ptr(dtable), dtable.shape[0], ptr(w), n, stream())
 
 
 def length_mask(lens, max_len):
@@ -257,7 +262,10 @@ def bucket_embed(x, values, bins, table, copy=None):
 
 def bucket_embed_bwd(dout, idx, dtable):
     _dev(dout, idx, dtable)
-    lib.fs2_bucket_embed_bwd(ptr(dout), ptr(idx), idx.numel(), dout.shape[1], ptr(dtable), stream())
+    n = lib.fs2_embedding_bwd_ws_bytes(idx.numel(), dout.shape[1], dtable.shape[0])
+    w = ws(n, dout.device)
+    lib.fs2_bucket_embed_bwd(ptr(dout), ptr(idx), idx.numel(), dout.shape[1], ptr(dtable),
+                             dtable.shape[0], ptr(w), n, stream())
 
 
 def bucketize(values, bins):

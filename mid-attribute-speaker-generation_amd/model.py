@@ -283,10 +283,10 @@ class FFTBlock(nn.Module):
         w1, w2 = f.w_1, f.w_2
         ln2, ln1 = f.layer_norm, a.layer_norm
         # LN2 (masked; dropout before the residual add): dx1 starts as dz2
-        dx1 = K.zeros((M, d), x_c.device)
+        dx1 = torch.empty((M, d), dtype=torch.float32, device=x_c.device)
         dy2, dy2_t = K.ln_bwd(xh2, rs2, ln2.weight, ln2.bias, _g(ln2.weight), _g(ln2.bias),
                               dout=dx2, lens=lens, seq_len=T, p_in=p, seed=seed,
-                              site_in=self.site + 1, dres=dx1, copy=ctx.copy,
+                              site_in=self.site + 1, dres=dx1, dres_add=False, copy=ctx.copy,
                               dbias_in=_g(w2.bias))
         dy2_c = _t(dy2, dy2_t)
         K.conv_wgrad(dy2_c, h, _g(w2.weight), M, T, w2.c_in, d, w2.k, w2.padding)
@@ -296,10 +296,11 @@ class FFTBlock(nn.Module):
         K.conv_gemm(dh, w1._w_bwd, M, T, w1.c_out, d, w1.k, w1.padding, flags=K.EPI_ADD_AUX,
                     aux=dx1, out=dx1)
         # LN1 -> fc -> attention -> QKV
-        dx = K.zeros((M, d), x_c.device)
+        dx = torch.empty((M, d), dtype=torch.float32, device=x_c.device)
         dy1, dy1_t = K.ln_bwd(xh1, rs1, ln1.weight, ln1.bias, _g(ln1.weight), _g(ln1.bias),
                               dout=dx1, lens=lens, seq_len=T, p_in=p, seed=seed,
-                              site_in=self.site, dres=dx, copy=ctx.copy, dbias_in=_g(a.fc.bias))
+                              site_in=self.site, dres=dx, dres_add=False, copy=ctx.copy,
+                              dbias_in=_g(a.fc.bias))
         dy1_c = _t(dy1, dy1_t)
         hd = a.n_head * a.d_k
         K.conv_wgrad(dy1_c, o, _g(a.fc.weight), M, T, hd, d, 1, 0)
@@ -474,7 +475,7 @@ class PostNet(nn.Module):
             last = i == n - 1
             out, out_t, mean, rstd = K.bn_fwd(z, bn.weight, bn.bias, rm, rv, not last, p, ctx.seed,
                                               self.site + i, res=x if last else None,
-                                              copy=None if last else ctx.copy)
+                                              copy=None if last else ctx.copy, want_out=last)
             if self.training:
                 K.add_i64_(bn.num_batches_tracked, 1)
             saved.append((a_c, z, mean, rstd))
@@ -845,12 +846,17 @@ class FastSpeech2(nn.Module):
                 v.prep(cdt, jobs)
             self.postnet.prep(cdt, jobs)
             _linear_prep(self.mel_linear, cdt, jobs=jobs)
-            rows = [[w, co, ci, k, wf, wb, 0, 0] for (w, co, ci, k, wf, wb) in jobs]
-            assert max(r[3] for r in rows) <= 9
+            ct = K.lib.fs2_weight_prep_tile_channels(K.code(cdt))
+            rows, first = [], 0
+            for (w, co, ci, k, wf, wb) in jobs:
+                assert k <= 9
+                n = -(-co // 64) * -(-ci // ct)
+                rows.append([w, co, ci, k, wf, wb, first, first + n])
+                first += n
             table = torch.tensor(rows, dtype=torch.int64).to(self._arena.flat.device)
-            self._prep = (cdt, table, len(rows), max(r[1] for r in rows), max(r[2] for r in rows))
-        cdt, table, n, max_co, max_ci = self._prep
-        K.lib.fs2_weight_prep_batch(K.code(cdt), K.ptr(table), n, max_co, max_ci, K.stream())
+            self._prep = (cdt, table, len(rows), first)
+        cdt, table, n, n_tiles = self._prep
+        K.lib.fs2_weight_prep_batch(K.code(cdt), K.ptr(table), n, n_tiles, K.stream())
 
     # -- forward ----------------------------------------------------------------------
     def forward(self, speakers, texts, src_lens, max_src_len, mels=None, mel_lens=None,

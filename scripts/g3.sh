@@ -1,0 +1,5 @@
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 300 python -m pytest tests/test_gpu_kernels.py -q -x -k "conv" > gpurun_out/t_conv.log 2>&1 || { tail -40 gpurun_out/t_conv.log; exit 1; }
+tail -1 gpurun_out/t_conv.log
+timeout -k 10 400 python scripts/wgrad_sweep.py

@@ -1,0 +1,60 @@
+"""Sweep the weight-gradient decomposition knobs (tile, stages, splits) on the step's shapes."""
+import importlib
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+K = importlib.import_module("mid-attribute-speaker-generation_amd.kernels")
+dev = "cuda:0"
+TILE, STAGES, SPLITS = 2, 1, 3
+WSHAPES = [
+    ("dec conv1 k9 dW", 24576, 512, 256, 1024, 9),
+    ("dec conv2 k1 dW", 24576, 512, 1024, 256, 1),
+    ("dec qkv dW", 24576, 512, 256, 768, 1),
+    ("dec fc dW", 24576, 512, 256, 256, 1),
+    ("enc conv1 k9 dW", 6144, 128, 256, 1024, 9),
+    ("enc qkv dW", 6144, 128, 256, 768, 1),
+    ("enc fc dW", 6144, 128, 256, 256, 1),
+    ("postnet k5 dW", 24576, 512, 512, 512, 5),
+    ("vp k3 dW", 6144, 128, 256, 256, 3),
+]
+
+
+def timeit(run, n=15):
+    for _ in range(3):
+        run()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(n):
+        run()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / n * 1e3
+
+
+for name, M, T, cin, cout, k in WSHAPES:
+    x = torch.randn(M, cin, device=dev).to(torch.bfloat16)
+    dy = torch.randn(M, cout, device=dev).to(torch.bfloat16)
+    dw = torch.zeros(cout, cin, k, device=dev)
+    db = torch.zeros(cout, device=dev)
+    run = lambda: K.conv_wgrad(dy, x, dw, M, T, cin, cout, k, (k - 1) // 2, db=db)
+    res = []
+    for tile in (0, 64, 128):
+        for st in (1, 2):
+            for sp in (0, 4, 8, 16, 24, 32, 48, 64):
+                if tile == 0 and sp:
+                    continue
+                K.lib.fs2_set_tuning(TILE, tile)
+                K.lib.fs2_set_tuning(STAGES, st)
+                K.lib.fs2_set_tuning(SPLITS, sp)
+                res.append((timeit(run), tile, st, sp))
+    K.lib.fs2_set_tuning(TILE, 0)
+    K.lib.fs2_set_tuning(STAGES, 0)
+    K.lib.fs2_set_tuning(SPLITS, 0)
+    auto = [r for r in res if r[1] == 0 and r[2] == 1][0]
+    best = sorted(res)[:3]
+    fl = 2 * M * cout * cin * k
+    print(f"{name:18s} auto {auto[0]:7.1f}us ({fl / auto[0] / 1e6:5.0f} TF) | best " +
+          "  ".join(f"{t:7.1f}us tile{ti} st{s} sp{p}" for t, ti, s, p in best))

@@ -153,6 +153,10 @@ def test_layernorm(mode):
         dy, _ = K.ln_bwd(xh, rs, g, bta, dg, db, dout=dout, lens=lens, seq_len=T, dres=dres, **kw)
         close(dy, yr.grad)
         close(dres, rr.grad)
+        dres2 = torch.full((M, d), 7.0, device=DEV)  # overwrite mode ignores the old contents
+        K.ln_bwd(xh, rs, g, bta, dg.clone(), db.clone(), dout=dout, lens=lens, seq_len=T,
+                 dres=dres2, dres_add=False, **kw)
+        close(dres2, rr.grad)
     elif mode == "dot":
         wr, wbr = w.clone().requires_grad_(), wb.clone().requires_grad_()
         ref = (F.layer_norm(yr, (d,), gr, br, 1e-5) @ wr + wbr).masked_fill(pad, 0)
@@ -377,7 +381,9 @@ def test_norm_copies_bf16():
     assert out_t.dtype == torch.bfloat16 and torch.equal(out_t, out.to(torch.bfloat16))
     dg, db = torch.zeros(d, device=DEV), torch.zeros(d, device=DEV)
     dy, dy_t = K.ln_bwd(xh, rs, g, b, dg, db, dout=rnd(M, d, seed=5), copy=torch.bfloat16)
-    assert torch.equal(dy_t, dy.to(torch.bfloat16))
+    assert dy is None  # only the compute copy is produced
+    dy32, _ = K.ln_bwd(xh, rs, g, b, dg.clone(), db.clone(), dout=rnd(M, d, seed=5))
+    assert torch.equal(dy_t, dy32.to(torch.bfloat16))
     z = rnd(M, 512, seed=6)
     o2, o2_t, mean, rstd = K.bn_fwd(z, torch.ones(512, device=DEV), torch.zeros(512, device=DEV),
                                     None, None, True, 0.0, 0, 0, copy=torch.bfloat16)

@@ -34,6 +34,11 @@ K = importlib.import_module("mid-attribute-speaker-generation_amd.kernels")
 TR = importlib.import_module("mid-attribute-speaker-generation_amd.train")
 
 PEAK = {"f32": (157.3, "TFLOP/s"), "bf16": (2500.0, "TFLOP/s")}
+# compulsory bytes of one decoder k=9 launch, bf16 operands: fwd reads x (N x 256) + W, writes
+# h (N x 1024); dX reads dh (N x 1024) + W, reads and writes dx1 fp32 (N x 256); averaged
+_N = 24576
+ALG_BYTES = round(((_N * 256 * 2 + 1024 * 2304 * 2 + _N * 1024 * 2) +
+                   (_N * 1024 * 2 + 1024 * 2304 * 2 + 2 * _N * 256 * 4)) / 2)
 
 
 class ConvTimer:
@@ -68,6 +73,67 @@ class ConvTimer:
         return float(np.sum(self.flops)), float(np.sum(ms)) / 1e3, len(ms)
 
 
+PROBE_SHAPES = [  # the decoder's k=9 launches: forward (h = conv(x1)) and data gradient
+    (24576, 512, 256, 1024, 9, "fwd"), (24576, 512, 1024, 256, 9, "dx")]
+
+
+def probe_conv(reps=10):
+    """The dominant kernel's launches alone (same shapes / epilogues as the step), for the
+    PMC passes of ``hbm_traffic``."""
+    dev = torch.device("cuda", 0)
+    for M_, T_, cin, cout, k, kind in PROBE_SHAPES:
+        x = torch.randn(M_, cin, device=dev).to(torch.bfloat16)
+        w = (torch.randn(cout * cin * k, device=dev) * 0.02).to(torch.bfloat16)
+        if kind == "fwd":
+            b = torch.randn(cout, device=dev)
+            run = lambda: K.conv_gemm(x, w, M_, T_, cin, cout, k, 4, bias=b, flags=K.EPI_RELU,
+                                      out_dtype=torch.bfloat16)
+        else:
+            aux = torch.randn(M_, cout, device=dev)
+            run = lambda: K.conv_gemm(x, w, M_, T_, cin, cout, k, 4, flags=K.EPI_ADD_AUX,
+                                      aux=aux, out=aux)
+        for _ in range(reps):
+            run()
+    torch.cuda.synchronize()
+
+
+def hbm_traffic(timeout=300):
+    """Per-launch memory-side bytes of the k=9 conv GEMM from rocprofv3 PMC counters:
+    FETCH_SIZE and WRITE_SIZE (KiB) in separate passes (they do not fit one TCC pass),
+    FETCH_SIZE doubled (gfx950 reports half the bytes of 16-B-per-lane streaming reads;
+    MI355X_MICROARCH.md, HBM).  These count L2 misses, Infinity-Cache hits included."""
+    import csv
+    import glob
+    import shutil
+    import subprocess
+    import tempfile
+    prof = shutil.which("rocprofv3")
+    if prof is None:
+        return None, "rocprofv3 not found"
+    per = {}
+    with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as tmp:
+        for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+            d = os.path.join(tmp, ctr)
+            cmd = [prof, "--pmc", ctr, "-d", d, "-o", "probe", "--output-format", "csv", "--",
+                   sys.executable, os.path.abspath(__file__), "--probe-conv"]
+            try:
+                r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout)
+            except subprocess.TimeoutExpired:
+                return None, f"{ctr} pass timed out"
+            files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+            if r.returncode != 0 or not files:
+                return None, f"{ctr} pass failed (rc {r.returncode})"
+            vals = []
+            for row in csv.DictReader(open(files[0])):
+                if "conv_gemm_nt" in row.get("Kernel_Name", "") and row.get("Counter_Name") == ctr:
+                    vals.append(float(row["Counter_Value"]))
+            if not vals:
+                return None, f"{ctr}: no conv_gemm_nt dispatches"
+            per[ctr] = float(np.mean(vals))
+    # both counters are in KiB
+    return (per["FETCH_SIZE"] * 2.0 + per["WRITE_SIZE"]) * 1024.0, per
+
+
 def cpu_baseline(batch_np, steps=2):
     from oracle import fs2_cpu
     n_thr = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
@@ -98,7 +164,12 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["f32", "bf16"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC passes")
+    ap.add_argument("--probe-conv", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.probe_conv:
+        probe_conv()
+        return
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -154,6 +225,14 @@ def main():
                     "frac": round(ach / peak, 4), "traffic": None,
                     "kernel": "conv_gemm_nt (FFN Conv1d k=9, fwd + dX)",
                     "per_launch_flop": round(flops / n), "avg_launch_ms": round(secs / n * 1e3, 4)}
+            if world == 1 and args.dtype == "bf16" and not args.no_traffic:
+                traffic, detail = hbm_traffic()
+                if traffic is not None:
+                    roof["traffic"] = round(traffic)
+                    roof["traffic_unit"] = "bytes/launch (FETCH_SIZE x2 + WRITE_SIZE, PMC)"
+                    roof["traffic_algorithmic"] = ALG_BYTES
+                else:
+                    roof["traffic_note"] = detail
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(batch_np)

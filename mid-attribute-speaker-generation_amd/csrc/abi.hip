@@ -6,7 +6,7 @@
 
 namespace fs2 {
 
-int g_tune[FS2_TUNE_COUNT] = {0, 0, 0, 0, 0};
+int g_tune[FS2_TUNE_COUNT] = {};
 
 static thread_local char g_err[512] = "";
 

@@ -45,7 +45,8 @@ struct GldsArgs {
   const void* aux;
   int64_t ld_aux;
   int tiles_m, tiles_n;
-  int vec;  // 8-wide epilogue legal (N, ldy, ld_aux multiples of 8; aligned pointers)
+  int vec;    // 8-wide epilogue legal (N, ldy, ld_aux multiples of 8; aligned pointers)
+  int group;  // n-tiles per tile group (see the block order below)
 };
 
 FS2_DEV void glds16(const void* src, u16* lds_wave_base) {
@@ -80,7 +81,12 @@ __global__ __launch_bounds__(256) void conv_gemm_nt_glds(GldsArgs a) {
   const int nwg = a.tiles_m * a.tiles_n;
   const int orig = blockIdx.x, xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
-  const int tn = wg % a.tiles_n, tm = wg / a.tiles_n;
+  // tile order: groups of `group` n-tiles (a weight slice that stays L2-resident), m-tiles
+  // within a group, n fastest -- each XCD's contiguous share streams its A rows once per group
+  const int gfull = a.tiles_m * a.group;
+  const int ng = wg / gfull, rem = wg - ng * gfull;
+  const int gsz = a.tiles_n - ng * a.group < a.group ? a.tiles_n - ng * a.group : a.group;
+  const int tm = rem / gsz, tn = ng * a.group + (rem - (rem / gsz) * gsz);
   const int64_t m0 = (int64_t)tm * BM;
   const int n0 = tn * BN;
 
@@ -627,7 +633,11 @@ int conv_wgrad_glds_launch(const void* dy, int64_t ldy, const void* x, int64_t l
 
 
 template <int BM, int BN, int S>
-static void launch_nt(const GldsArgs& a, bool tapaligned, hipStream_t st) {
+static void launch_nt(GldsArgs a, bool tapaligned, hipStream_t st) {
+  // n-tiles per group: all of them by default (measured: smaller weight-slice groups did not
+  // pay on the step's shapes and multiplied the A re-reads of the long-K data gradient)
+  const int g = g_tune[FS2_TUNE_NT_GROUP] > 0 ? g_tune[FS2_TUNE_NT_GROUP] : a.tiles_n;
+  a.group = g > a.tiles_n ? a.tiles_n : g;
   const unsigned grid = (unsigned)(a.tiles_m * a.tiles_n);
   if (tapaligned) conv_gemm_nt_glds<BM, BN, S, true><<<grid, 256, 0, st>>>(a);
   else conv_gemm_nt_glds<BM, BN, S, false><<<grid, 256, 0, st>>>(a);
@@ -647,7 +657,7 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
                   (!(flags & FS2_EPI_BIAS) || ((uintptr_t)bias % 16) == 0) &&
                   (!uses_aux || (ld_aux % 8 == 0 && ((uintptr_t)aux % 16) == 0));
   GldsArgs a{(const u16*)x, ldx, (const u16*)wk, y, ldy, rows, seq_len, (int)c_in, (int)c_out,
-             taps, pad, K, bias, flags, aux, ld_aux, 0, 0, vec};
+             taps, pad, K, bias, flags, aux, ld_aux, 0, 0, vec, 1};
   const bool tapaligned = c_in % 64 == 0;
   const int64_t big = ((rows + 127) / 128) * ((c_out + 127) / 128);
   if (big >= 512) {

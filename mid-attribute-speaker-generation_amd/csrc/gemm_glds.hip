@@ -61,6 +61,47 @@ FS2_DEV u16 fbv(float f) {
   return *reinterpret_cast<u16*>(&b);
 }
 
+// Wait until at most `ahead` tiles of PER LDS-DMA instructions each are still in flight.
+template <int PER>
+FS2_DEV void vm_wait_tiles(int ahead) {
+  switch (ahead) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER) : "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * PER) : "memory"); break;
+  }
+}
+
+// The k-loop.  STAGES == 1: load; vmcnt(0); barrier; MFMA; barrier.  STAGES >= 2: a ring of
+// LDS stages with STAGES-1 tiles issued ahead; per tile: counted vmcnt (the tile landed, later
+// ones may stay in flight), ONE raw barrier (the tile is visible to every wave AND every wave
+// has finished the previous tile, whose slot the refill below overwrites), refill, MFMA.
+template <int STAGES, int PER, typename Issue, typename Compute>
+FS2_DEV void kloop(int nk, Issue&& issue, Compute&& compute) {
+  if constexpr (STAGES == 1) {
+    for (int kt = 0; kt < nk; ++kt) {
+      issue(kt, 0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      compute(0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+  } else {
+    for (int t = 0; t < STAGES - 1 && t < nk; ++t) issue(t, t);
+    for (int kt = 0; kt < nk; ++kt) {
+      const int ahead = nk - 1 - kt < STAGES - 2 ? nk - 1 - kt : STAGES - 2;
+      vm_wait_tiles<PER>(ahead);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
+      compute(kt % STAGES);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+}
+
 template <int BM, int BN, int STAGES, bool TAPALIGNED>
 __global__ __launch_bounds__(256) void conv_gemm_nt_glds(GldsArgs a) {
   constexpr int BK = 64;
@@ -185,33 +226,7 @@ __global__ __launch_bounds__(256) void conv_gemm_nt_glds(GldsArgs a) {
     }
   };
 
-  if constexpr (STAGES == 1) {
-    for (int kt = 0; kt < nk; ++kt) {
-      issue(kt, 0);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      compute(0);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-    }
-  } else {
-    issue(0, 0);
-    for (int kt = 0; kt < nk; ++kt) {
-      if (kt + 1 < nk) {
-        issue(kt + 1, (kt + 1) & 1);
-        if constexpr (AW + BW == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        else if constexpr (AW + BW == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-        else if constexpr (AW + BW == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      __builtin_amdgcn_s_barrier();
-      compute(kt & 1);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-    }
-  }
+  kloop<STAGES, AW + BW>(nk, issue, compute);
 
   // ---- epilogue through LDS, one half (wm) at a time
   float* Cs = reinterpret_cast<float*>(smem);
@@ -467,31 +482,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_tn_glds(WgradGlds a) {
     }
   };
 
-  if constexpr (STAGES == 1) {
-    for (int kt = 0; kt < nk; ++kt) {
-      issue(kt, 0);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      compute(0);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-    }
-  } else {
-    if (nk > 0) issue(0, 0);
-    for (int kt = 0; kt < nk; ++kt) {
-      if (kt + 1 < nk) {
-        issue(kt + 1, (kt + 1) & 1);
-        if constexpr (IPW == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      __builtin_amdgcn_s_barrier();
-      compute(kt & 1);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-    }
-  }
+  kloop<STAGES, 2 * IPW>(nk, issue, compute);
 
   if (do_bias && r16 == 0) {
 #pragma unroll
@@ -612,14 +603,25 @@ int conv_wgrad_glds_launch(const void* dy, int64_t ldy, const void* x, int64_t l
               (int)c_out, taps, pad, (int)Kp, rps, (int)((c_out + tile - 1) / tile),
               (int)((Kp + tile - 1) / tile), splits};
   const unsigned grid = (unsigned)(a.tiles_o * a.tiles_k * splits);
-  const int stages = g_tune[FS2_TUNE_WGRAD_STAGES] == 2 ? 2 : 1;
+  const int stages = g_tune[FS2_TUNE_WGRAD_STAGES] >= 1 && g_tune[FS2_TUNE_WGRAD_STAGES] <= 4
+                         ? g_tune[FS2_TUNE_WGRAD_STAGES] : (tile == 128 ? 1 : 2);
+#define FS2_WG(BT, S) conv_wgrad_tn_glds<BT, S><<<grid, 256, 0, st>>>(a)
   if (tile == 128) {
-    if (stages == 2) conv_wgrad_tn_glds<128, 2><<<grid, 256, 0, st>>>(a);
-    else conv_wgrad_tn_glds<128, 1><<<grid, 256, 0, st>>>(a);
+    switch (stages) {
+      case 2: FS2_WG(128, 2); break;
+      case 3: FS2_WG(128, 3); break;
+      case 4: FS2_WG(128, 4); break;
+      default: FS2_WG(128, 1);
+    }
   } else {
-    if (stages == 2) conv_wgrad_tn_glds<64, 2><<<grid, 256, 0, st>>>(a);
-    else conv_wgrad_tn_glds<64, 1><<<grid, 256, 0, st>>>(a);
+    switch (stages) {
+      case 2: FS2_WG(64, 2); break;
+      case 3: FS2_WG(64, 3); break;
+      case 4: FS2_WG(64, 4); break;
+      default: FS2_WG(64, 1);
+    }
   }
+#undef FS2_WG
   if (taps == 1) {
     const int64_t total = c_out * c_in;  // multiple of 64 (both channel counts % 8 == 0)
     wgrad_reduce_k1<<<(unsigned)((total / 4 + 63) / 64), 256, 0, st>>>(ws, bslab, splits,
@@ -650,8 +652,10 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
   FS2_CHECK_ARG(c_in % 8 == 0 && ldx % 8 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)wk & 15) == 0,
                 "fs2_conv_gemm(bf16): c_in/ldx must be multiples of 8 and operands 16-B aligned");
   const int K = (int)(taps * c_in);
-  // long reductions keep the next tile's DMA in flight across the barrier
-  const int stages = g_tune[FS2_TUNE_GEMM_STAGES] ? g_tune[FS2_TUNE_GEMM_STAGES] : (K >= 4096 ? 2 : 1);
+  // LDS stages (scripts/nt_sweep.py): 128x128 tiles run 3-4 blocks per CU and overlap one
+  // another's load phase with one stage; the smaller-grid tilings prefetch (2 stages, 4 for
+  // 64x64 tiles with K >= 4096, where each block walks 144 k-tiles)
+  const int tune = g_tune[FS2_TUNE_GEMM_STAGES];
   const bool uses_aux = flags & (FS2_EPI_ADD_AUX | FS2_EPI_RELU_MASK_AUX);
   const int vec = c_out % 8 == 0 && ldy % 8 == 0 && ((uintptr_t)y % 16) == 0 &&
                   (!(flags & FS2_EPI_BIAS) || ((uintptr_t)bias % 16) == 0) &&
@@ -660,22 +664,30 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
              taps, pad, K, bias, flags, aux, ld_aux, 0, 0, vec, 1};
   const bool tapaligned = c_in % 64 == 0;
   const int64_t big = ((rows + 127) / 128) * ((c_out + 127) / 128);
+#define FS2_NT(BM_, BN_)                                                  \
+  switch (stages) {                                                       \
+    case 2: launch_nt<BM_, BN_, 2>(a, tapaligned, st); break;             \
+    case 3: launch_nt<BM_, BN_, 3>(a, tapaligned, st); break;             \
+    case 4: launch_nt<BM_, BN_, 4>(a, tapaligned, st); break;             \
+    default: launch_nt<BM_, BN_, 1>(a, tapaligned, st);                   \
+  }
   if (big >= 512) {
     a.tiles_m = (int)((rows + 127) / 128);
     a.tiles_n = (int)((c_out + 127) / 128);
-    if (stages == 2) launch_nt<128, 128, 2>(a, tapaligned, st);
-    else launch_nt<128, 128, 1>(a, tapaligned, st);
+    const int stages = tune ? tune : 1;
+    FS2_NT(128, 128)
   } else if (big >= 128) {
     a.tiles_m = (int)((rows + 127) / 128);
     a.tiles_n = (int)((c_out + 63) / 64);
-    if (stages == 2) launch_nt<128, 64, 2>(a, tapaligned, st);
-    else launch_nt<128, 64, 1>(a, tapaligned, st);
+    const int stages = tune ? tune : 2;
+    FS2_NT(128, 64)
   } else {
     a.tiles_m = (int)((rows + 63) / 64);
     a.tiles_n = (int)((c_out + 63) / 64);
-    if (stages == 2) launch_nt<64, 64, 2>(a, tapaligned, st);
-    else launch_nt<64, 64, 1>(a, tapaligned, st);
+    const int stages = tune ? tune : (K >= 4096 ? 4 : 2);
+    FS2_NT(64, 64)
   }
+#undef FS2_NT
   return launch_status("fs2_conv_gemm(bf16)");
 }
 

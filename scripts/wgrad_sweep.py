@@ -42,8 +42,8 @@ for name, M, T, cin, cout, k in WSHAPES:
     run = lambda: K.conv_wgrad(dy, x, dw, M, T, cin, cout, k, (k - 1) // 2, db=db)
     res = []
     for tile in (0, 64, 128):
-        for st in (1, 2):
-            for sp in (0, 4, 8, 16, 24, 32, 48, 64):
+        for st in (1, 2, 3, 4):
+            for sp in (0, 4, 8, 16, 24, 32):
                 if tile == 0 and sp:
                     continue
                 K.lib.fs2_set_tuning(TILE, tile)

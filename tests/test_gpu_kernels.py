@@ -390,3 +390,38 @@ def test_norm_copies_bf16():
     assert torch.equal(o2_t, o2.to(torch.bfloat16))
     x = rnd(M, d, seed=7)
     assert torch.equal(K.cast_bf16(x), x.to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("stages", [1, 2, 3, 4])
+@pytest.mark.parametrize("B,T,cin,cout,k", [(2, 70, 256, 512, 9), (3, 50, 80, 256, 5),
+                                            (1, 200, 512, 80, 5)])
+def test_conv_gemm_bf16_pipeline_depths(stages, B, T, cin, cout, k):
+    """Every LDS-stage count of the bf16 fwd/dX and weight-gradient kernels (the automatic
+    choice uses 1 or 2) against fp32 math on the same bf16 data; knob reset afterwards."""
+    pad = (k - 1) // 2
+    x = bf(rnd(B * T, cin, seed=21))
+    w = bf(rnd(cout, cin, k, scale=1 / math.sqrt(cin * k), seed=22)).float()
+    b = rnd(cout, seed=23)
+    wf = torch.empty(cout * cin * k, device=DEV, dtype=torch.bfloat16)
+    wb = torch.empty(cout * cin * k, device=DEV, dtype=torch.bfloat16)
+    K.weight_prep(w, cout, cin, k, wf, wb)
+    dy = bf(rnd(B * T, cout, seed=24))
+    xr, wr = x.float().clone().requires_grad_(), w.clone().requires_grad_()
+    ref = ref_conv(xr, wr, b, B, T, pad)
+    ref.backward(dy.float())
+    try:
+        for knob in (0, 1):  # FS2_TUNE_GEMM_STAGES, FS2_TUNE_WGRAD_STAGES
+            K.lib.fs2_set_tuning(knob, stages)
+        for tile in (64, 128):
+            K.lib.fs2_set_tuning(2, tile)  # FS2_TUNE_WGRAD_TILE
+            y = K.conv_gemm(x, wf, B * T, T, cin, cout, k, pad, bias=b)
+            close(y, ref.detach(), 1e-5)
+            dx = K.conv_gemm(dy, wb, B * T, T, cout, cin, k, pad)
+            close(dx, xr.grad, 1e-5)
+            dw, db = torch.zeros_like(w), torch.zeros(cout, device=DEV)
+            K.conv_wgrad(dy, x, dw, B * T, T, cin, cout, k, pad, db=db)
+            close(dw, wr.grad, 1e-5)
+            close(db, dy.float().sum(0), 1e-5)
+    finally:
+        for knob in (0, 1, 2):
+            K.lib.fs2_set_tuning(knob, 0)

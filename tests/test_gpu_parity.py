@@ -237,3 +237,25 @@ def test_bf16_step_tracks_fp32():
     for a, b in zip(runs[torch.bfloat16], runs[torch.float32]):
         close(a, b, 2e-2, "bf16 vs fp32 losses")
     assert runs[torch.bfloat16][-1][0] < runs[torch.bfloat16][0][0]
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_step_bitwise_reproducible(dt):
+    """No floating-point atomics anywhere: two runs of 2 steps (dropout on) from the same
+    weights and seed give bitwise-identical weights, Adam moments and BN running stats."""
+    pp, mc, tc, path = PKG.config.load_configs("JVS-VCTK")
+    finals = []
+    for _ in range(2):
+        model = M.FastSpeech2(pp, mc, path, device=DEV, compute_dtype=dt)
+        PKG.seeded.load_seeded_(model)
+        model.train()
+        model.seed(77)
+        tr = T.Trainer(model, pp, mc, tc)
+        batch = PKG.data.to_device(PKG.data.syn_batch(8, 32, seed=5), DEV)
+        for _ in range(2):
+            tr.step(batch)
+        torch.cuda.synchronize()
+        finals.append((model.arena().flat.clone(), tr.opt.m.clone(), tr.opt.v.clone(),
+                       model.postnet.convolutions[2][1].running_var.clone()))
+    for a, b in zip(*finals):
+        assert torch.equal(a, b)

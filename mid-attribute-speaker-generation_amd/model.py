@@ -120,9 +120,27 @@ class StepCtx:
         self.cdt = cdt
         self.copy = None if cdt == torch.float32 else cdt  # bf16 compute copies wanted?
         self.hook = None  # gradient-ready callback (data-parallel bucketed all-reduce)
+        self.side = None  # stream for the weight-gradient GEMMs (off the critical path)
 
     def p(self, p):
         return float(p) if self.drop else 0.0
+
+    def wgrad(self, dy, x, dw, rows, seq_len, c_in, c_out, taps, pad, db=None):
+        """Weight (+bias) gradient GEMM.  Nothing in the backward waits for it, so with a
+        side stream it runs concurrently with the data-gradient chain on the main stream
+        (the small GEMMs of a block fill the GPU together); ``join`` orders it back."""
+        if self.side is None:
+            return K.conv_wgrad(dy, x, dw, rows, seq_len, c_in, c_out, taps, pad, db=db)
+        self.side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(self.side):
+            K.conv_wgrad(dy, x, dw, rows, seq_len, c_in, c_out, taps, pad, db=db)
+        dy.record_stream(self.side)
+        x.record_stream(self.side)
+
+    def join(self):
+        """Make the current stream wait for every weight-gradient GEMM issued so far."""
+        if self.side is not None:
+            torch.cuda.current_stream().wait_stream(self.side)
 
     def notify(self, params):
         """Tell the gradient hook that these parameters' gradients are final."""
@@ -289,10 +307,10 @@ class FFTBlock(nn.Module):
                               site_in=self.site + 1, dres=dx1, dres_add=False, copy=ctx.copy,
                               dbias_in=_g(w2.bias))
         dy2_c = _t(dy2, dy2_t)
-        K.conv_wgrad(dy2_c, h, _g(w2.weight), M, T, w2.c_in, d, w2.k, w2.padding)
+        ctx.wgrad(dy2_c, h, _g(w2.weight), M, T, w2.c_in, d, w2.k, w2.padding)
         dh = K.conv_gemm(dy2_c, w2._w_bwd, M, T, d, w2.c_in, w2.k, w2.padding,
                          flags=K.EPI_RELU_MASK_AUX, aux=h, out_dtype=cdt)
-        K.conv_wgrad(dh, x1_c, _g(w1.weight), M, T, d, w1.c_out, w1.k, w1.padding, db=_g(w1.bias))
+        ctx.wgrad(dh, x1_c, _g(w1.weight), M, T, d, w1.c_out, w1.k, w1.padding, db=_g(w1.bias))
         K.conv_gemm(dh, w1._w_bwd, M, T, w1.c_out, d, w1.k, w1.padding, flags=K.EPI_ADD_AUX,
                     aux=dx1, out=dx1)
         # LN1 -> fc -> attention -> QKV
@@ -303,10 +321,10 @@ class FFTBlock(nn.Module):
                               dbias_in=_g(a.fc.bias))
         dy1_c = _t(dy1, dy1_t)
         hd = a.n_head * a.d_k
-        K.conv_wgrad(dy1_c, o, _g(a.fc.weight), M, T, hd, d, 1, 0)
+        ctx.wgrad(dy1_c, o, _g(a.fc.weight), M, T, hd, d, 1, 0)
         do = K.conv_gemm(dy1_c, a.fc._w_bwd, M, T, d, hd, 1, 0, out_dtype=cdt)
         dqkv = K.attn_bwd(qkv, o, do, lse, lens, B, T, a.n_head, a.d_k, 1.0 / math.sqrt(a.d_k))
-        K.conv_wgrad(dqkv, x_c, self._qkv_gw, M, T, d, n3, 1, 0, db=self._qkv_gb)
+        ctx.wgrad(dqkv, x_c, self._qkv_gw, M, T, d, n3, 1, 0, db=self._qkv_gb)
         K.conv_gemm(dqkv, q._w_bwd, M, T, n3, d, 1, 0, flags=K.EPI_ADD_AUX, aux=dx, out=dx)
         return dx
 
@@ -404,13 +422,13 @@ class VariancePredictor(nn.Module):
                               p_out=p, seed=seed, site_out=self.site + 1, relu_y=h2,
                               copy=ctx.copy, dbias_in=_g(c2.bias))
         dh2_c = _t(dh2, dh2_t)
-        K.conv_wgrad(dh2_c, u1_c, _g(c2.weight), M, T, c2.c_in, c2.c_out, c2.k, c2.padding)
+        ctx.wgrad(dh2_c, u1_c, _g(c2.weight), M, T, c2.c_in, c2.c_out, c2.k, c2.padding)
         du1 = K.conv_gemm(dh2_c, c2._w_bwd, M, T, c2.c_out, c2.c_in, c2.k, c2.padding)
         dh1, dh1_t = K.ln_bwd(xh1, rs1, ln1.weight, ln1.bias, _g(ln1.weight), _g(ln1.bias),
                               dout=du1, p_out=p, seed=seed, site_out=self.site, relu_y=h1,
                               copy=ctx.copy, dbias_in=_g(c1.bias))
         dh1_c = _t(dh1, dh1_t)
-        K.conv_wgrad(dh1_c, x_c, _g(c1.weight), M, T, c1.c_in, c1.c_out, c1.k, c1.padding)
+        ctx.wgrad(dh1_c, x_c, _g(c1.weight), M, T, c1.c_in, c1.c_out, c1.k, c1.padding)
         K.conv_gemm(dh1_c, c1._w_bwd, M, T, c1.c_out, c1.c_in, c1.k, c1.padding,
                     flags=K.EPI_ADD_AUX, aux=dx_acc, out=dx_acc)
 
@@ -494,7 +512,7 @@ class PostNet(nn.Module):
             dz, dz_t = K.bn_bwd(d, z, mean, rstd, bn.weight, bn.bias, _g(bn.weight), _g(bn.bias),
                                 i < n - 1, p, ctx.seed, self.site + i, copy=ctx.copy)
             dz_c = _t(dz, dz_t)
-            K.conv_wgrad(dz_c, a_c, _g(conv.weight), M, T, conv.c_in, conv.c_out, conv.k,
+            ctx.wgrad(dz_c, a_c, _g(conv.weight), M, T, conv.c_in, conv.c_out, conv.k,
                          conv.padding, db=_g(conv.bias))
             if i > 0:
                 d = K.conv_gemm(dz_c, conv._w_bwd, M, T, conv.c_out, conv.c_in, conv.k, conv.padding)
@@ -656,6 +674,7 @@ class EncoderFn(torch.autograd.Function):
         texts, accents = fctx.ids
         K.embedding_bwd(dx, texts, _g(enc.src_word_emb.weight), 0)
         K.embedding_bwd(dx, accents, _g(enc.src_accent_emb.weight), 0)
+        fctx.ctx.join()  # last block of the backward: every weight gradient is final after this
         fctx.ctx.notify([enc.src_accent_emb.weight, enc.src_word_emb.weight])
         fctx.saved = None
         return (None,) * 8
@@ -763,7 +782,7 @@ class MelHeadFn(torch.autograd.Function):
             dm = d_out
         ctx.notify(postnet_param_order(m.postnet))
         dm_c = K.cast_bf16(dm) if ctx.copy is not None else dm
-        K.conv_wgrad(dm_c, x_c, _g(lin.weight), M, T, lin.in_features, n_mel, 1, 0, db=_g(lin.bias))
+        ctx.wgrad(dm_c, x_c, _g(lin.weight), M, T, lin.in_features, n_mel, 1, 0, db=_g(lin.bias))
         dx = K.conv_gemm(dm_c, lin._w_bwd, M, T, n_mel, lin.in_features, 1, 0)
         ctx.notify([lin.weight, lin.bias])
         fctx.saved = None
@@ -809,6 +828,8 @@ class FastSpeech2(nn.Module):
         self._arena = None
         self._prep = None
         self._hooks = {"grad": None}  # gradient-ready callback, see StepCtx.notify
+        self.overlap_wgrad = True  # weight-gradient GEMMs on a side stream (StepCtx.wgrad)
+        self._side = None
         self.to(device)
 
     # -- plumbing ---------------------------------------------------------------------
@@ -828,6 +849,19 @@ class FastSpeech2(nn.Module):
             self.speaker_enc._tok = self._token
             self.speaker_enc._model_hooks = self._hooks
         return self._arena
+
+    def side_stream(self):
+        """The weight-gradient stream (None when overlap is off)."""
+        if not self.overlap_wgrad:
+            return None
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=self.encoder.position_enc.device)
+        return self._side
+
+    def join_side(self):
+        """Make the current stream wait for all weight-gradient work issued so far."""
+        if self._side is not None:
+            torch.cuda.current_stream().wait_stream(self._side)
 
     def seed(self, s):
         """Seed the per-step dropout stream (Philox keys are drawn from it)."""
@@ -871,6 +905,7 @@ class FastSpeech2(nn.Module):
         ctx = StepCtx(self._seed_rng.integers(0, 2 ** 62), self.training, self.dropout,
                       self.compute_dtype)
         ctx.hook = self._hooks["grad"]
+        ctx.side = self.side_stream() if self.training else None
         B, Ts = texts.shape
         max_src_len = int(max_src_len)
         max_mel_len = int(max_mel_len)

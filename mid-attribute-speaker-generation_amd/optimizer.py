@@ -69,6 +69,7 @@ class ScheduledOptim:
     def __init__(self, model, train_config, model_config, current_step):
         oc = train_config["optimizer"]
         self.arena = model.arena()
+        self._join = getattr(model, "join_side", None)  # weight-gradient stream
         self.betas = tuple(float(b) for b in oc["betas"])
         self.eps = float(oc["eps"])
         wd = float(oc["weight_decay"])
@@ -116,11 +117,15 @@ class ScheduledOptim:
     def clip_grad_norm_(self, max_norm):
         """Global L2 norm of all gradients; the clip is applied inside the next ``step``.
         Returns the (pre-clip) norm as a 0-dim device tensor, like torch's clip_grad_norm_."""
+        if self._join is not None:
+            self._join()
         K.grad_norm(self.arena.grad, float(max_norm), self.norm_coef)
         self._clip_pending = True
         return self.norm_coef[0]
 
     def step(self):
+        if self._join is not None:
+            self._join()
         self.adam_steps += 1
         b1, b2 = self.betas
         t = self.adam_steps

@@ -60,6 +60,7 @@ class GradBuckets:
             self.ranges.append((arena.offsets[idxs[0]],
                                 arena.offsets[last] + arena.params[last].numel()))
         self.sizes = [len(idxs) for idxs in buckets]
+        self.join = None
         del index
         self.reset()
 
@@ -69,6 +70,8 @@ class GradBuckets:
         self.works = []
 
     def _launch(self, b):
+        if self.join is not None:
+            self.join()  # weight gradients computed on the side stream are part of the bucket
         s, e = self.ranges[b]
         self.works.append(dist.all_reduce(self.arena.grad[s:e], group=self.group, async_op=True))
 
@@ -106,6 +109,7 @@ class Trainer:
             with torch.no_grad():  # identical initial weights on every rank
                 dist.broadcast(arena.flat, src=0, group=process_group)
             self.buckets = GradBuckets(arena, process_group, bucket_bytes)
+            self.buckets.join = model.join_side
             model._hooks["grad"] = self.buckets.ready
 
     def _global_denominators(self, batch):

@@ -18,7 +18,9 @@
  *     r / seq_len.  Padding masks are given as per-utterance lengths (int64), a row being
  *     padding when (r % seq_len) >= lens[r / seq_len] (utils/tools.py:155-163).
  *   - dropout is counter-based (Philox4x32-10 keyed by seed, site, element index): the
- *     backward entry points regenerate the forward mask from the same (seed, site).
+ *     backward entry points regenerate the forward mask from the same (seed, site).  The
+ *     seed is read from DEVICE memory (`const uint64_t* seed`, NULL when p == 0), so a
+ *     captured HIP graph of the step draws a new seed per replay (fs2_seed_next).
  */
 #ifndef FS2HIP_H
 #define FS2HIP_H
@@ -127,8 +129,9 @@ int fs2_attn_bwd(int dtype, const void* qkv, const void* o, const void* d_o, con
  * whose backward is zero).  out_t: optional extra copy in `dtype`.                    */
 int fs2_ln_fwd(int dtype, const float* y, const float* res, const float* gamma, const float* beta,
                float* out, void* out_t, float* xhat, float* rstd, const int64_t* lens,
-               int64_t seq_len, int64_t rows, int d, float p_in, float p_out, uint64_t seed,
-               uint64_t site_in, uint64_t site_out, const float* dot_w, const float* dot_b,
+               int64_t seq_len, int64_t rows, int d, float p_in, float p_out,
+               const uint64_t* seed, uint64_t site_in, uint64_t site_out, const float* dot_w,
+               const float* dot_b,
                float* dot_out, void* stream);
 /* Backward of fs2_ln_fwd.  Upstream gradient is dout (per element) or, in dot mode,
  * ddot (per row).  Produces dy (gradient w.r.t. y before dropout, times (relu_y > 0) when
@@ -141,7 +144,8 @@ int64_t fs2_ln_bwd_ws_bytes(int64_t rows, int d);
 int fs2_ln_bwd(int dtype, const float* dout, const float* ddot, const float* dot_w,
                const float* xhat, const float* rstd, const float* gamma, const float* beta,
                const int64_t* lens, int64_t seq_len, int64_t rows, int d, float p_in, float p_out,
-               uint64_t seed, uint64_t site_in, uint64_t site_out, const float* relu_y, float* dy,
+               const uint64_t* seed, uint64_t site_in, uint64_t site_out, const float* relu_y,
+               float* dy,
                void* dy_t, float* dres, int dres_add, float* dgamma, float* dbeta, float* dw_dot,
                float* db_dot, float* dbias_in, float* ws, int64_t ws_bytes, void* stream);
 
@@ -154,11 +158,13 @@ int64_t fs2_bn_ws_bytes(int64_t rows, int64_t c);
 int fs2_bn_fwd(int dtype, const float* z, int64_t rows, int64_t c, const float* gamma,
                const float* beta, float eps, float momentum, float* running_mean,
                float* running_var, float* mean, float* rstd, int act_tanh, float p,
-               uint64_t seed, uint64_t site, const float* res, float* out, void* out_t, float* ws,
+               const uint64_t* seed, uint64_t site, const float* res, float* out, void* out_t,
+               float* ws,
                int64_t ws_bytes, void* stream);
 int fs2_bn_bwd(int dtype, const float* dout, const float* z, const float* mean, const float* rstd,
                const float* gamma, const float* beta, int64_t rows, int64_t c, int act_tanh,
-               float p, uint64_t seed, uint64_t site, float* dz, void* dz_t, float* dgamma,
+               float p, const uint64_t* seed, uint64_t site, float* dz, void* dz_t,
+               float* dgamma,
                float* dbeta, float* ws, int64_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------- embeddings, adaptor
@@ -271,7 +277,19 @@ int fs2_grad_norm(const float* g, int64_t n, float max_norm, float* norm_coef, f
                   int64_t ws_bytes, void* stream);
 int fs2_adam_step(float* p, const float* g, float* m, float* v, int64_t n, const float* norm_coef,
                   float lr, float beta1, float beta2, float eps, float bias_corr1,
-                  float bias_corr2_sqrt, void* stream);
+                  float bias_corr2_sqrt, const float* hyper, void* stream);
+/* Device-side ScheduledOptim.step_and_update_lr (model/optimizer.py:33-51): steps (device,
+ * int64[2] = [current_step, adam t]) are incremented (current_step only when advance_lr;
+ * step() without the LR update passes 0) and hyper (device, float[3]) set to
+ * [lr, 1 - beta1^t, sqrt(1 - beta2^t)], lr = init_lr * min(s^-0.5, warmup^-1.5 * s) *
+ * rate^#{anneal < s}; fs2_adam_step reads hyper when it is non-NULL.  anneal_steps_host is
+ * a host array (<= 3 entries, copied into the launch).  Together with fs2_seed_next
+ * (state = device uint64[3] {base, counter, current seed}; current = splitmix64 of the
+ * incremented counter) the whole step is a fixed launch sequence: graph-capturable.     */
+int fs2_sched_step(int64_t* steps, float* hyper, double init_lr, int64_t n_warmup,
+                   const int64_t* anneal_steps_host, int n_anneal, double anneal_rate, double beta1,
+                   double beta2, int advance_lr, void* stream);
+int fs2_seed_next(uint64_t* state, void* stream);
 int fs2_fill(float* x, int64_t n, float value, void* stream);
 /* y = bf16(x), round to nearest even (compute copies for the bf16 path)              */
 int fs2_cast_bf16(const float* x, void* y, int64_t n, void* stream);

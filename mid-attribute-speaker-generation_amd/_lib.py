@@ -22,6 +22,7 @@ _CT = {
     "int64_t": ctypes.c_int64,
     "uint64_t": ctypes.c_uint64,
     "float": ctypes.c_float,
+    "double": ctypes.c_double,
     "const char*": ctypes.c_char_p,
 }
 

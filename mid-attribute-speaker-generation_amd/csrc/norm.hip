@@ -31,7 +31,8 @@ struct LnFwd {
   const int64_t* lens;
   int64_t T, rows;
   float p_in, p_out;
-  uint64_t seed, site_in, site_out;
+  const uint64_t* seed;  // device (read once per thread; NULL when no dropout)
+  uint64_t site_in, site_out;
   const float* dot_w;
   const float* dot_b;
   float* dot_out;
@@ -55,8 +56,9 @@ __global__ __launch_bounds__(256) void ln_fwd_f32(LnFwd a) {
     if (a.out_t) st4_bf16(a.out_t + e0, f32x4{0.f, 0.f, 0.f, 0.f});
     return;
   }
+  const uint64_t seed = a.seed ? *a.seed : 0ull;
   f32x4 z = ld4(a.y + e0);
-  if (a.p_in > 0.f) z *= dropout4(a.seed, a.site_in, (uint64_t)e0, a.p_in);
+  if (a.p_in > 0.f) z *= dropout4(seed, a.site_in, (uint64_t)e0, a.p_in);
   if (a.res) z += ld4(a.res + e0);
   const float mean = wave_sum(z.x + z.y + z.z + z.w) * (1.f / LN_D);
   const f32x4 c = z - mean;
@@ -64,7 +66,7 @@ __global__ __launch_bounds__(256) void ln_fwd_f32(LnFwd a) {
   const float rs = 1.f / sqrtf(var + 1e-5f);
   const f32x4 xh = c * rs;
   f32x4 u = xh * ld4(a.gamma + 4 * lane) + ld4(a.beta + 4 * lane);
-  if (a.p_out > 0.f) u *= dropout4(a.seed, a.site_out, (uint64_t)e0, a.p_out);
+  if (a.p_out > 0.f) u *= dropout4(seed, a.site_out, (uint64_t)e0, a.p_out);
   st4(a.out + e0, u);  // (dot mode masks only the head output)
   if (a.out_t) st4_bf16(a.out_t + e0, u);
   st4(a.xhat + e0, xh);
@@ -87,7 +89,8 @@ struct LnBwd {
   const int64_t* lens;
   int64_t T, rows;
   float p_in, p_out;
-  uint64_t seed, site_in, site_out;
+  const uint64_t* seed;
+  uint64_t site_in, site_out;
   const float* relu_y;
   float* dy;
   float* dres;
@@ -107,6 +110,7 @@ __global__ __launch_bounds__(256) void ln_bwd_f32(LnBwd a) {
   if (a.ddot) w = ld4(a.dot_w + 4 * lane);
   f32x4 pg = {0.f, 0.f, 0.f, 0.f}, pb = pg, pw = pg, py = pg;
   float pdb = 0.f;
+  const uint64_t seed = a.seed ? *a.seed : 0ull;
   const int64_t rbeg = (int64_t)blockIdx.x * LN_ROWS;
   for (int i = wave; i < LN_ROWS; i += 4) {
     const int64_t r = rbeg + i;
@@ -119,7 +123,7 @@ __global__ __launch_bounds__(256) void ln_bwd_f32(LnBwd a) {
       continue;
     }
     const f32x4 xh = ld4(a.xhat + e0);
-    const f32x4 mo = a.p_out > 0.f ? dropout4(a.seed, a.site_out, (uint64_t)e0, a.p_out)
+    const f32x4 mo = a.p_out > 0.f ? dropout4(seed, a.site_out, (uint64_t)e0, a.p_out)
                                    : f32x4{1.f, 1.f, 1.f, 1.f};
     f32x4 du;
     if (a.ddot) {
@@ -141,7 +145,7 @@ __global__ __launch_bounds__(256) void ln_bwd_f32(LnBwd a) {
     const f32x4 dz = a.rstd[r] * (dxh - m1 - xh * m2);
     if (a.dres) st4(a.dres + e0, a.dres_add ? ld4(a.dres + e0) + dz : dz);
     f32x4 dy = dz;
-    if (a.p_in > 0.f) dy *= dropout4(a.seed, a.site_in, (uint64_t)e0, a.p_in);
+    if (a.p_in > 0.f) dy *= dropout4(seed, a.site_in, (uint64_t)e0, a.p_in);
     if (a.relu_y) {
       const f32x4 yv = ld4(a.relu_y + e0);
       dy.x = yv.x > 0.f ? dy.x : 0.f;
@@ -241,9 +245,10 @@ __global__ __launch_bounds__(1024) void bn_var_final(const float* part, int64_t 
 // out = act(BN(z)) * dropout (+ res), 4 consecutive elements (same row) per lane
 __global__ __launch_bounds__(256) void bn_apply(const float* z, const float* mean, const float* rstd,
                                                 const float* gamma, const float* beta, int64_t n4,
-                                                int c, int act_tanh, float p, uint64_t seed,
+                                                int c, int act_tanh, float p, const uint64_t* seed_p,
                                                 uint64_t site, const float* res, float* out,
                                                 unsigned short* out_t) {
+  const uint64_t seed = seed_p ? *seed_p : 0ull;
   for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4;
        q += (int64_t)gridDim.x * blockDim.x) {
     const int64_t e0 = q * 4;
@@ -276,8 +281,9 @@ __global__ __launch_bounds__(256) void bn_bwd_partial(const float* dout, const f
                                                       const float* mean, const float* rstd,
                                                       const float* gamma, const float* beta,
                                                       int64_t rows, int64_t c, int act_tanh,
-                                                      float p, uint64_t seed, uint64_t site,
-                                                      float* part_g, float* part_gx) {
+                                                      float p, const uint64_t* seed_p,
+                                                      uint64_t site, float* part_g, float* part_gx) {
+  const uint64_t seed = seed_p ? *seed_p : 0ull;
   const int tx = threadIdx.x & 63, ry = threadIdx.x >> 6;
   const int64_t col = ((int64_t)blockIdx.x * 64 + tx) * 4;
   const int64_t r0 = (int64_t)blockIdx.y * BN_ROWS;
@@ -324,8 +330,10 @@ __global__ __launch_bounds__(256) void bn_bwd_apply(const float* dout, const flo
                                                     const float* mean, const float* rstd,
                                                     const float* gamma, const float* beta,
                                                     const float* sums, int64_t n4, int64_t rows,
-                                                    int c, int act_tanh, float p, uint64_t seed,
-                                                    uint64_t site, float* dz, unsigned short* dz_t) {
+                                                    int c, int act_tanh, float p,
+                                                    const uint64_t* seed_p, uint64_t site, float* dz,
+                                                    unsigned short* dz_t) {
+  const uint64_t seed = seed_p ? *seed_p : 0ull;
   const float inv_m = 1.f / (float)rows;
   for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4;
        q += (int64_t)gridDim.x * blockDim.x) {
@@ -363,8 +371,9 @@ static int copy_dtype_ok(int dtype, const char* what) {
 
 int fs2_ln_fwd(int dtype, const float* y, const float* res, const float* gamma, const float* beta,
                float* out, void* out_t, float* xhat, float* rstd, const int64_t* lens,
-               int64_t seq_len, int64_t rows, int d, float p_in, float p_out, uint64_t seed,
-               uint64_t site_in, uint64_t site_out, const float* dot_w, const float* dot_b,
+               int64_t seq_len, int64_t rows, int d, float p_in, float p_out,
+               const uint64_t* seed, uint64_t site_in, uint64_t site_out, const float* dot_w,
+               const float* dot_b,
                float* dot_out, void* stream) {
   if (int rc = copy_dtype_ok(dtype, "fs2_ln_fwd")) return rc;
   FS2_CHECK_ARG(d == LN_D, "fs2_ln_fwd: only d = 256 is supported (got %d)", d);
@@ -386,7 +395,8 @@ int64_t fs2_ln_bwd_ws_bytes(int64_t rows, int d) {
 int fs2_ln_bwd(int dtype, const float* dout, const float* ddot, const float* dot_w,
                const float* xhat, const float* rstd, const float* gamma, const float* beta,
                const int64_t* lens, int64_t seq_len, int64_t rows, int d, float p_in, float p_out,
-               uint64_t seed, uint64_t site_in, uint64_t site_out, const float* relu_y, float* dy,
+               const uint64_t* seed, uint64_t site_in, uint64_t site_out, const float* relu_y,
+               float* dy,
                void* dy_t, float* dres, int dres_add, float* dgamma, float* dbeta, float* dw_dot,
                float* db_dot, float* dbias_in, float* ws, int64_t ws_bytes, void* stream) {
   if (int rc = copy_dtype_ok(dtype, "fs2_ln_bwd")) return rc;
@@ -421,7 +431,8 @@ int64_t fs2_bn_ws_bytes(int64_t rows, int64_t c) {
 int fs2_bn_fwd(int dtype, const float* z, int64_t rows, int64_t c, const float* gamma,
                const float* beta, float eps, float momentum, float* running_mean,
                float* running_var, float* mean, float* rstd, int act_tanh, float p,
-               uint64_t seed, uint64_t site, const float* res, float* out, void* out_t, float* ws,
+               const uint64_t* seed, uint64_t site, const float* res, float* out, void* out_t,
+               float* ws,
                int64_t ws_bytes, void* stream) {
   if (int rc = copy_dtype_ok(dtype, "fs2_bn_fwd")) return rc;
   FS2_CHECK_ARG(rows > 0 && c > 0, "fs2_bn_fwd: empty input");
@@ -445,7 +456,8 @@ int fs2_bn_fwd(int dtype, const float* z, int64_t rows, int64_t c, const float* 
 
 int fs2_bn_bwd(int dtype, const float* dout, const float* z, const float* mean, const float* rstd,
                const float* gamma, const float* beta, int64_t rows, int64_t c, int act_tanh,
-               float p, uint64_t seed, uint64_t site, float* dz, void* dz_t, float* dgamma,
+               float p, const uint64_t* seed, uint64_t site, float* dz, void* dz_t,
+               float* dgamma,
                float* dbeta, float* ws, int64_t ws_bytes, void* stream) {
   if (int rc = copy_dtype_ok(dtype, "fs2_bn_bwd")) return rc;
   FS2_CHECK_ARG(rows > 0 && c > 0, "fs2_bn_bwd: empty input");

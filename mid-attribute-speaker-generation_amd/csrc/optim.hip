@@ -53,7 +53,13 @@ __global__ __launch_bounds__(1024) void norm_final(const float* part, int np, fl
 
 __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                             float* __restrict__ v, int64_t n, const float* __restrict__ norm_coef,
-                            float lr, float b1, float b2, float eps, float bc1, float bc2s) {
+                            float lr, float b1, float b2, float eps, float bc1, float bc2s,
+                            const float* __restrict__ hyper) {
+  if (hyper) {  // device-side schedule (fs2_sched_step): [lr, 1 - b1^t, sqrt(1 - b2^t)]
+    lr = hyper[0];
+    bc1 = hyper[1];
+    bc2s = hyper[2];
+  }
   const float coef = norm_coef ? norm_coef[1] : 1.f;
   const float step = lr / bc1;
   const int64_t n4 = n / 4;
@@ -80,6 +86,35 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, 
       v[i] = b2 * v[i] + (1.f - b2) * gv * gv;
       p[i] -= step * m[i] / (sqrtf(v[i]) / bc2s + eps);
     }
+}
+
+// ScheduledOptim.step_and_update_lr on the device (model/optimizer.py:33-51): one step of
+// the counters [lr step, Adam t] and the hyper-parameters [lr, 1 - b1^t, sqrt(1 - b2^t)],
+// in double like the host's numpy arithmetic, so a captured graph replays the schedule.
+__global__ void sched_step_kernel(int64_t* steps, float* hyper, double init_lr, int64_t warmup,
+                                  int64_t a0, int64_t a1, int64_t a2, int n_anneal, double rate,
+                                  double b1, double b2, int advance_lr) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const int64_t s = advance_lr ? ++steps[0] : steps[0];
+  const int64_t t = ++steps[1];
+  double sc = fmin(pow((double)s, -0.5), pow((double)warmup, -1.5) * (double)s);
+  const int64_t an[3] = {a0, a1, a2};
+  for (int i = 0; i < n_anneal && i < 3; ++i)
+    if (s > an[i]) sc *= rate;
+  hyper[0] = (float)(init_lr * sc);
+  hyper[1] = (float)(1.0 - pow(b1, (double)t));
+  hyper[2] = (float)sqrt(1.0 - pow(b2, (double)t));
+}
+
+// Per-step dropout seed: state = [base, counter, current]; current = splitmix64 of
+// (base, ++counter).
+__global__ void seed_next_kernel(uint64_t* st) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const uint64_t c = ++st[1];
+  uint64_t z = st[0] + 0x9E3779B97F4A7C15ull * c;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  st[2] = z ^ (z >> 31);
 }
 
 __global__ void add_i64(int64_t* x, int64_t n, int64_t v) {
@@ -110,7 +145,7 @@ int fs2_grad_norm(const float* g, int64_t n, float max_norm, float* norm_coef, f
 
 int fs2_adam_step(float* p, const float* g, float* m, float* v, int64_t n, const float* norm_coef,
                   float lr, float beta1, float beta2, float eps, float bias_corr1,
-                  float bias_corr2_sqrt, void* stream) {
+                  float bias_corr2_sqrt, const float* hyper, void* stream) {
   FS2_CHECK_ARG((((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) == 0,
                 "fs2_adam_step: buffers must be 16-B aligned");
   if (n == 0) return FS2_OK;
@@ -119,8 +154,25 @@ int fs2_adam_step(float* p, const float* g, float* m, float* v, int64_t n, const
   if (blocks < 1) blocks = 1;
   adam_kernel<<<(unsigned)blocks, 256, 0, as_stream(stream)>>>(p, g, m, v, n, norm_coef, lr, beta1,
                                                                beta2, eps, bias_corr1,
-                                                               bias_corr2_sqrt);
+                                                               bias_corr2_sqrt, hyper);
   return launch_status("fs2_adam_step");
+}
+
+int fs2_sched_step(int64_t* steps, float* hyper, double init_lr, int64_t n_warmup,
+                   const int64_t* anneal_steps_host, int n_anneal, double anneal_rate, double beta1,
+                   double beta2, int advance_lr, void* stream) {
+  FS2_CHECK_ARG(n_anneal >= 0 && n_anneal <= 3, "fs2_sched_step: at most 3 anneal steps");
+  int64_t an[3] = {0, 0, 0};
+  for (int i = 0; i < n_anneal; ++i) an[i] = anneal_steps_host[i];
+  sched_step_kernel<<<1, 64, 0, as_stream(stream)>>>(steps, hyper, init_lr, n_warmup, an[0], an[1],
+                                                     an[2], n_anneal, anneal_rate, beta1, beta2,
+                                                     advance_lr);
+  return launch_status("fs2_sched_step");
+}
+
+int fs2_seed_next(uint64_t* state, void* stream) {
+  seed_next_kernel<<<1, 64, 0, as_stream(stream)>>>(state);
+  return launch_status("fs2_seed_next");
 }
 
 int fs2_add_i64(int64_t* x, int64_t n, int64_t value, void* stream) {

@@ -8,6 +8,8 @@ compute in fp32 and can emit a bf16 *compute copy* of their output (``copy=torch
 for the next GEMM.  There is no PyTorch-math fallback: a wrong input raises, a missing
 library raises.
 """
+import ctypes
+
 import torch
 
 from ._lib import lib
@@ -41,6 +43,16 @@ def code(dtype):
         return _CODE[dtype]
     except KeyError:
         raise RuntimeError(f"unsupported compute dtype {dtype}") from None
+
+
+def seed_arg(seed, device):
+    """Dropout seed as the device pointer the kernels read: a device int64 tensor is passed
+    through (the model's per-step seed), a host int is uploaded (tests, one-off calls)."""
+    if torch.is_tensor(seed):
+        if not seed.is_cuda or seed.dtype != torch.int64:
+            raise RuntimeError("seed tensor must be a CUDA int64 tensor")
+        return seed
+    return torch.tensor([int(seed) & (2 ** 63 - 1)], dtype=torch.int64, device=device)
 
 
 def ws(nbytes, device):
@@ -136,9 +148,10 @@ def ln_fwd(y, gamma, beta, res=None, lens=None, seq_len=1, p_in=0.0, p_out=0.0, 
     xhat = torch.empty_like(y)
     rstd = torch.empty(rows, dtype=torch.float32, device=y.device)
     dot = torch.empty(rows, dtype=torch.float32, device=y.device) if dot_w is not None else None
+    sd = seed_arg(seed, y.device) if (p_in > 0 or p_out > 0) else None
     lib.fs2_ln_fwd(BF16 if copy is not None else F32, ptr(y), ptr(res), ptr(gamma), ptr(beta),
                    ptr(out), ptr(out_t), ptr(xhat), ptr(rstd), ptr(lens), seq_len, rows, d, p_in,
-                   p_out, seed, site_in, site_out, ptr(dot_w), ptr(dot_b), ptr(dot), stream())
+                   p_out, ptr(sd), site_in, site_out, ptr(dot_w), ptr(dot_b), ptr(dot), stream())
     return out, out_t, xhat, rstd, dot
 
 
@@ -154,11 +167,12 @@ def ln_bwd(xhat, rstd, gamma, beta, dgamma, dbeta, dout=None, ddot=None, dot_w=N
     dy_t = _copy(xhat.shape, copy, xhat.device)
     n = lib.fs2_ln_bwd_ws_bytes(rows, d)
     w = ws(n, xhat.device)
+    sd = seed_arg(seed, xhat.device) if (p_in > 0 or p_out > 0) else None
     lib.fs2_ln_bwd(BF16 if copy is not None else F32, ptr(dout), ptr(ddot), ptr(dot_w), ptr(xhat),
                    ptr(rstd), ptr(gamma), ptr(beta), ptr(lens), seq_len, rows, d, p_in, p_out,
-                   seed, site_in, site_out, ptr(relu_y), ptr(dy), ptr(dy_t), ptr(dres),
-                   int(dres_add), ptr(dgamma), ptr(dbeta), ptr(dw_dot), ptr(db_dot), ptr(dbias_in), ptr(w), n,
-                   stream())
+                   ptr(sd), site_in, site_out, ptr(relu_y), ptr(dy), ptr(dy_t), ptr(dres),
+                   int(dres_add), ptr(dgamma), ptr(dbeta), ptr(dw_dot), ptr(db_dot), ptr(dbias_in),
+                   ptr(w), n, stream())
     return dy, dy_t
 
 
@@ -174,9 +188,10 @@ def bn_fwd(z, gamma, beta, running_mean, running_var, act_tanh, p, seed, site, r
     rstd = torch.empty(c, dtype=torch.float32, device=z.device)
     n = lib.fs2_bn_ws_bytes(rows, c)
     w = ws(n, z.device)
+    sd = seed_arg(seed, z.device) if p > 0 else None
     lib.fs2_bn_fwd(BF16 if copy is not None else F32, ptr(z), rows, c, ptr(gamma), ptr(beta), eps,
                    momentum, ptr(running_mean), ptr(running_var), ptr(mean), ptr(rstd),
-                   int(act_tanh), p, seed, site, ptr(res), ptr(out), ptr(out_t), ptr(w), n,
+                   int(act_tanh), p, ptr(sd), site, ptr(res), ptr(out), ptr(out_t), ptr(w), n,
                    stream())
     return out, out_t, mean, rstd
 
@@ -188,9 +203,10 @@ def bn_bwd(dout, z, mean, rstd, gamma, beta, dgamma, dbeta, act_tanh, p, seed, s
     dz_t = _copy(z.shape, copy, z.device)
     n = lib.fs2_bn_ws_bytes(rows, c)
     w = ws(n, z.device)
+    sd = seed_arg(seed, z.device) if p > 0 else None
     lib.fs2_bn_bwd(BF16 if copy is not None else F32, ptr(dout), ptr(z), ptr(mean), ptr(rstd),
-                   ptr(gamma), ptr(beta), rows, c, int(act_tanh), p, seed, site, ptr(dz), ptr(dz_t),
-                   ptr(dgamma), ptr(dbeta), ptr(w), n, stream())
+                   ptr(gamma), ptr(beta), rows, c, int(act_tanh), p, ptr(sd), site, ptr(dz),
+                   ptr(dz_t), ptr(dgamma), ptr(dbeta), ptr(w), n, stream())
     return dz, dz_t
 
 
@@ -398,9 +414,26 @@ def grad_norm(g, max_norm, norm_coef):
     lib.fs2_grad_norm(ptr(g), g.numel(), float(max_norm), ptr(norm_coef), ptr(w), n, stream())
 
 
-def adam_step(p, g, m, v, norm_coef, lr, beta1, beta2, eps, bc1, bc2_sqrt):
+def adam_step(p, g, m, v, norm_coef, lr, beta1, beta2, eps, bc1, bc2_sqrt, hyper=None):
+    """Adam over flat buffers; with ``hyper`` (device [lr, bc1, bc2_sqrt], see sched_step) the
+    scalar lr/bc1/bc2_sqrt arguments are ignored."""
     lib.fs2_adam_step(ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), ptr(norm_coef), float(lr),
-                      float(beta1), float(beta2), float(eps), float(bc1), float(bc2_sqrt), stream())
+                      float(beta1), float(beta2), float(eps), float(bc1), float(bc2_sqrt),
+                      ptr(hyper), stream())
+
+
+def sched_step(steps, hyper, init_lr, n_warmup, anneal_steps, anneal_rate, beta1, beta2,
+               advance_lr=True):
+    """Device-side LR schedule + Adam bias corrections for one step (fs2_sched_step)."""
+    an = (ctypes.c_int64 * 3)(*[int(a) for a in anneal_steps][:3])
+    lib.fs2_sched_step(ptr(steps), ptr(hyper), float(init_lr), int(n_warmup), ctypes.addressof(an),
+                       len(anneal_steps), float(anneal_rate), float(beta1), float(beta2),
+                       int(advance_lr), stream())
+
+
+def seed_next(state):
+    """state: device int64[3] {base, counter, current}; advances the per-step dropout seed."""
+    lib.fs2_seed_next(ptr(state), stream())
 
 
 def fill_(t, value):

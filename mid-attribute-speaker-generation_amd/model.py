@@ -115,7 +115,7 @@ class StepCtx:
     site id per dropout call, assigned at construction)."""
 
     def __init__(self, seed, training, dropout, cdt=torch.float32):
-        self.seed = int(seed)
+        self.seed = seed  # device int64[1] tensor (or a host int when no dropout runs)
         self.drop = bool(training and dropout)
         self.cdt = cdt
         self.copy = None if cdt == torch.float32 else cdt  # bf16 compute copies wanted?
@@ -824,7 +824,8 @@ class FastSpeech2(nn.Module):
         self.postnet.site = site
         self.dropout = True
         self.compute_dtype = compute_dtype
-        self._seed_rng = np.random.default_rng(0)
+        self._seed_base = 0
+        self._seed_state = None  # device int64[3] {base, counter, current}, fs2_seed_next
         self._arena = None
         self._prep = None
         self._hooks = {"grad": None}  # gradient-ready callback, see StepCtx.notify
@@ -864,8 +865,17 @@ class FastSpeech2(nn.Module):
             torch.cuda.current_stream().wait_stream(self._side)
 
     def seed(self, s):
-        """Seed the per-step dropout stream (Philox keys are drawn from it)."""
-        self._seed_rng = np.random.default_rng(s)
+        """Seed the per-step dropout stream: step i's Philox key is splitmix64(s, i), drawn on
+        the device (fs2_seed_next) so a captured step graph draws a fresh key per replay."""
+        self._seed_base = int(s) & (2 ** 63 - 1)
+        self._seed_state = None
+
+    def _step_seed(self):
+        if self._seed_state is None:
+            self._seed_state = torch.tensor([self._seed_base, 0, 0], dtype=torch.int64,
+                                            device=self.encoder.position_enc.device)
+        K.seed_next(self._seed_state)
+        return self._seed_state[2:3].clone()  # this forward's key (backward re-reads it)
 
     def prep_weights(self):
         """Re-lay out (and cast) every weight for the GEMMs: one batched launch per step; the
@@ -902,8 +912,8 @@ class FastSpeech2(nn.Module):
             raise ValueError("accents are required in training (transformer/Models.py:101)")
         self.arena()
         self.prep_weights()
-        ctx = StepCtx(self._seed_rng.integers(0, 2 ** 62), self.training, self.dropout,
-                      self.compute_dtype)
+        seed = self._step_seed() if (self.training and self.dropout) else 0
+        ctx = StepCtx(seed, self.training, self.dropout, self.compute_dtype)
         ctx.hook = self._hooks["grad"]
         ctx.side = self.side_stream() if self.training else None
         B, Ts = texts.shape

@@ -7,7 +7,6 @@ reads the gradients (one pass over 34.7 M gradients instead of three).  ``_optim
 exposes a torch.optim.Adam-compatible ``state_dict``/``load_state_dict``/``param_groups``
 so checkpoints (``train.py:276-285``) round-trip with the reference's format.
 """
-import math
 
 import numpy as np
 import torch
@@ -55,6 +54,7 @@ class _AdamView:
                 o.v[off:off + n].copy_(st["exp_avg_sq"].reshape(-1))
                 steps = int(float(st["step"]))
         o.adam_steps = steps
+        o._sync_counters()
         for k in ("lr", "betas", "eps", "weight_decay"):
             if k in sd["param_groups"][0]:
                 self.param_groups[0][k] = sd["param_groups"][0][k]
@@ -87,11 +87,28 @@ class ScheduledOptim:
         self.current_step = current_step
         self.init_lr = np.power(model_config["transformer"]["encoder_hidden"], -0.5)
         self._optimizer = _AdamView(self, list(model.parameters()), self.betas, self.eps, wd)
+        # device mirrors of the counters and the per-step hyper-parameters: the kernels read
+        # these, so the step is a fixed launch sequence (HIP-graph capturable)
+        self._dev_steps = torch.zeros(2, dtype=torch.int64, device=dev)
+        self._hyper = torch.zeros(3, dtype=torch.float32, device=dev)
+        self._sync_counters()
+
+    def _sync_counters(self):
+        """Host counters -> device mirrors (construction, checkpoint load)."""
+        self._dev_steps.copy_(torch.tensor([int(self.current_step), int(self.adam_steps)],
+                                           dtype=torch.int64))
+
+    def host_advance(self, update_lr=True):
+        """Advance the host-side counters exactly as one replayed (graph-captured) step did
+        on the device."""
+        if update_lr:
+            self._update_learning_rate()
+        self.adam_steps += 1
 
     # -- reference API ------------------------------------------------------------------
     def step_and_update_lr(self):
-        self._update_learning_rate()
-        self.step()
+        self._update_learning_rate()  # host mirror (param_groups lr, checkpoints)
+        self.step(_advance_lr=True)
 
     def zero_grad(self):
         self.arena.zero_grad()
@@ -123,15 +140,15 @@ class ScheduledOptim:
         self._clip_pending = True
         return self.norm_coef[0]
 
-    def step(self):
+    def step(self, _advance_lr=False):
         if self._join is not None:
             self._join()
         self.adam_steps += 1
         b1, b2 = self.betas
-        t = self.adam_steps
-        lr = float(self._optimizer.param_groups[0]["lr"])
+        K.sched_step(self._dev_steps, self._hyper, self.init_lr, self.n_warmup_steps,
+                     self.anneal_steps, self.anneal_rate, b1, b2, advance_lr=_advance_lr)
         K.adam_step(self.arena.flat, self.arena.grad, self.m, self.v,
-                    self.norm_coef if self._clip_pending else None, lr, b1, b2, self.eps,
-                    1.0 - b1 ** t, math.sqrt(1.0 - b2 ** t))
+                    self.norm_coef if self._clip_pending else None, 0.0, b1, b2, self.eps,
+                    1.0, 1.0, hyper=self._hyper)
         self._clip_pending = False
         self.arena.version += 1

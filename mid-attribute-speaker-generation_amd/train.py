@@ -92,11 +92,21 @@ class GradBuckets:
 
 
 class Trainer:
-    """Model + loss + optimiser for one rank (``world_size`` 1 = plain single-GPU)."""
+    """Model + loss + optimiser for one rank (``world_size`` 1 = plain single-GPU).
+
+    ``graph=True`` (single process): the first ``step`` runs eagerly and captures the whole
+    step -- forward, both backwards, clip, Adam + schedule, zero_grad -- into one HIP graph;
+    later steps copy the batch into the graph's static inputs and replay it.  Every per-step
+    quantity the kernels read (dropout key, LR, Adam bias corrections, BN counters) lives in
+    device memory, so a replay is exactly an eager step; the returned tensors are the graph's
+    static outputs (overwritten by the next replay).  A batch of another shape re-captures.
+    """
 
     def __init__(self, model, preprocess_config, model_config, train_config, current_step=0,
-                 process_group=None, bucket_bytes=32 << 20):
+                 process_group=None, bucket_bytes=32 << 20, graph=False):
         self.model = model
+        self.graph_mode = bool(graph)
+        self._graph = None
         self.Loss = FastSpeech2Loss(preprocess_config, model_config)
         self.eLoss = SpeakerMetaEncLoss(preprocess_config, model_config)
         self.opt = ScheduledOptim(model, train_config, model_config, current_step)
@@ -119,7 +129,41 @@ class Trainer:
         dist.all_reduce(counts, group=self.pg)
         return counts
 
+    def _shape_key(self, batch):
+        return tuple(tuple(b.shape) if torch.is_tensor(b) else b for b in batch)
+
+    def _graph_step(self, batch):
+        key = self._shape_key(batch)
+        if self._graph is not None and key == self._graph_key:
+            for s, b in zip(self._static, batch):
+                if torch.is_tensor(b):
+                    s.copy_(b)
+            self._graph.replay()
+            self.opt.host_advance()
+            return self._graph_out
+        # eager step (this call's step), then capture the next one
+        out = train_step(self.model, self.opt, self.Loss, self.eLoss, batch, self.clip)
+        self._static = tuple(b.clone() if torch.is_tensor(b) else b for b in batch)
+        host = (self.opt.current_step, self.opt.adam_steps,
+                self.opt._optimizer.param_groups[0]["lr"])
+        overlap = self.model.overlap_wgrad
+        self.model.overlap_wgrad = False  # one stream inside the captured graph
+        g = torch.cuda.CUDAGraph()
+        try:
+            with torch.cuda.graph(g):
+                self._graph_out = train_step(self.model, self.opt, self.Loss, self.eLoss,
+                                             self._static, self.clip)
+        finally:
+            self.model.overlap_wgrad = overlap
+            # capture recorded kernels without running them: undo its host-side bookkeeping
+            self.opt.current_step, self.opt.adam_steps = host[0], host[1]
+            self.opt._optimizer.param_groups[0]["lr"] = host[2]
+        self._graph, self._graph_key = g, key
+        return out
+
     def step(self, batch):
+        if self.graph_mode and self.world == 1:
+            return self._graph_step(batch)
         if self.world > 1:
             glob = self._global_denominators(batch)
             self.Loss.denoms = glob[0:2]

@@ -259,3 +259,27 @@ def test_step_bitwise_reproducible(dt):
                        model.postnet.convolutions[2][1].running_var.clone()))
     for a, b in zip(*finals):
         assert torch.equal(a, b)
+
+
+def test_graph_replay_matches_eager():
+    """Trainer(graph=True): step 1 eager + capture, steps 2-4 replays of the captured step.
+    With dropout ON (device-side per-step keys) the weights, Adam moments, LR and losses
+    after 4 steps equal an eager Trainer's bitwise."""
+    pp, mc, tc, path = PKG.config.load_configs("JVS-VCTK")
+    res = []
+    for graph in (False, True):
+        model = M.FastSpeech2(pp, mc, path, device=DEV, compute_dtype=torch.bfloat16)
+        PKG.seeded.load_seeded_(model)
+        model.train()
+        model.seed(11)
+        model.overlap_wgrad = False  # same summation schedule on both sides
+        tr = T.Trainer(model, pp, mc, tc, graph=graph)
+        batch = PKG.data.to_device(PKG.data.syn_batch(8, 32, seed=4), DEV)
+        losses = [torch.stack(list(tr.step(batch)[0])).clone() for _ in range(4)]
+        torch.cuda.synchronize()
+        res.append((model.arena().flat.clone(), tr.opt.m.clone(), torch.stack(losses),
+                    tr.opt._optimizer.param_groups[0]["lr"], tr.opt.adam_steps,
+                    model.postnet.convolutions[0][1].num_batches_tracked.item()))
+    (fe, me, le, lre, te, ne), (fg, mg, lg, lrg, tg, ng) = res
+    assert torch.equal(fe, fg) and torch.equal(me, mg) and torch.equal(le, lg)
+    assert lre == lrg and te == tg == 4 and ne == ng == 4

@@ -178,9 +178,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC passes")
-    ap.add_argument("--no-graph", action="store_true",
-                    help="eager steps (default at N=1: the step is captured once into a HIP "
-                         "graph and replayed)")
+    ap.add_argument("--graph", action="store_true",
+                    help="N=1: capture the step once into a HIP graph and replay it (measured "
+                         "slower than eager here: replay serialises the weight-gradient stream)")
     ap.add_argument("--probe-conv", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.probe_conv:
@@ -200,7 +200,7 @@ def main():
     model = M.FastSpeech2(pp, mc, path, device=dev, compute_dtype=cdt)
     model.train()
     model.seed(1234 + rank)
-    use_graph = world == 1 and not args.no_graph
+    use_graph = world == 1 and args.graph
     trainer = TR.Trainer(model, pp, mc, tc, graph=use_graph)
     batch_np = PKG.data.syn_batch(args.batch, args.src_len, seed=rank)
     batch = PKG.data.to_device(batch_np, dev)

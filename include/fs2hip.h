@@ -290,6 +290,9 @@ int fs2_sched_step(int64_t* steps, float* hyper, double init_lr, int64_t n_warmu
                    const int64_t* anneal_steps_host, int n_anneal, double anneal_rate, double beta1,
                    double beta2, int advance_lr, void* stream);
 int fs2_seed_next(uint64_t* state, void* stream);
+/* Stream ordering: work queued on `waiter` after this call starts only after everything
+ * queued on `signaler` so far (event record + stream wait; host-side, not a launch).  */
+int fs2_stream_wait(void* waiter, void* signaler);
 int fs2_fill(float* x, int64_t n, float value, void* stream);
 /* y = bf16(x), round to nearest even (compute copies for the bf16 path)              */
 int fs2_cast_bf16(const float* x, void* y, int64_t n, void* stream);

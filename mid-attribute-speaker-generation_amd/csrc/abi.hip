@@ -74,6 +74,30 @@ int fs2_set_tuning(int knob, int value) {
   return FS2_OK;
 }
 
+// Cross-stream ordering without host objects: a ring of timing-free events; a wait binds to
+// the record made just before it, so re-recording a ring slot later is harmless.
+int fs2_stream_wait(void* waiter, void* signaler) {
+  static hipEvent_t ring[64];
+  static int next = 0;
+  static bool init = false;
+  if (!init) {
+    for (auto& e : ring)
+      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+        set_error("fs2_stream_wait: hipEventCreate failed");
+        return FS2_ERR_LAUNCH;
+      }
+    init = true;
+  }
+  hipEvent_t ev = ring[next];
+  next = (next + 1) & 63;
+  if (hipEventRecord(ev, as_stream(signaler)) != hipSuccess ||
+      hipStreamWaitEvent(as_stream(waiter), ev, 0) != hipSuccess) {
+    set_error("fs2_stream_wait: event record/wait failed");
+    return FS2_ERR_LAUNCH;
+  }
+  return FS2_OK;
+}
+
 int fs2_fill(float* x, int64_t n, float value, void* stream) {
   if (n <= 0) return FS2_OK;
   fill_kernel<<<grid_for(n), 256, 0, as_stream(stream)>>>(x, n, value);

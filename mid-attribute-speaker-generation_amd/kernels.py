@@ -21,8 +21,14 @@ EPI_BIAS, EPI_RELU, EPI_ADD_AUX, EPI_RELU_MASK_AUX, EPI_OUT_BF16, EPI_AUX_BF16 =
 _CODE = {torch.float32: F32, torch.bfloat16: BF16}
 
 
+_DEV_INDEX = []
+
+
 def stream():
-    return torch.cuda.current_stream().cuda_stream
+    """Raw handle of the calling thread's current HIP stream (one device per process)."""
+    if not _DEV_INDEX:
+        _DEV_INDEX.append(torch.cuda.current_device())
+    return torch._C._cuda_getCurrentRawStream(_DEV_INDEX[0])
 
 
 def ptr(t):
@@ -89,15 +95,23 @@ def weight_prep(w, c_out, c_in, taps, w_fwd=None, w_bwd=None):
     lib.fs2_conv_weight_prep(code(dt), ptr(w), c_out, c_in, taps, ptr(w_fwd), ptr(w_bwd), stream())
 
 
-def conv_wgrad(dy, x, dw, rows, seq_len, c_in, c_out, taps, pad, db=None):
-    """dw (+)= conv weight gradient; db (+)= column sums of dy when given (same launch)."""
+def conv_wgrad(dy, x, dw, rows, seq_len, c_in, c_out, taps, pad, db=None, ws_buf=None,
+               on_stream=None):
+    """dw (+)= conv weight gradient; db (+)= column sums of dy when given (same launch).
+    ``ws_buf``: caller-owned fp32 workspace (else one is allocated on the current stream)."""
     _dev(dy, x, dw, db)
     if dy.dtype != x.dtype:
         raise RuntimeError(f"conv_wgrad operand dtypes differ: {dy.dtype} vs {x.dtype}")
     n = lib.fs2_conv_wgrad_ws_bytes(rows, c_in, c_out, taps)
-    w = ws(n, dy.device)
+    if ws_buf is not None:
+        if ws_buf.numel() * 4 < n:
+            raise RuntimeError("conv_wgrad: workspace too small")
+        w, n = ws_buf, ws_buf.numel() * 4
+    else:
+        w = ws(n, dy.device)
     lib.fs2_conv_wgrad(code(dy.dtype), ptr(dy), c_out, ptr(x), c_in, ptr(dw), ptr(db), rows,
-                       seq_len, c_in, c_out, taps, pad, ptr(w), n, stream())
+                       seq_len, c_in, c_out, taps, pad, ptr(w), n,
+                       stream() if on_stream is None else on_stream)
 
 
 def colsum(x, rows, cols, out, accumulate=True):

@@ -121,6 +121,8 @@ class StepCtx:
         self.copy = None if cdt == torch.float32 else cdt  # bf16 compute copies wanted?
         self.hook = None  # gradient-ready callback (data-parallel bucketed all-reduce)
         self.side = None  # stream for the weight-gradient GEMMs (off the critical path)
+        self.ws_cache = None  # dict holding the side stream's shared split-K workspace
+        self.keep = []  # operands read by side-stream work, released at the next join
 
     def p(self, p):
         return float(p) if self.drop else 0.0
@@ -131,16 +133,27 @@ class StepCtx:
         (the small GEMMs of a block fill the GPU together); ``join`` orders it back."""
         if self.side is None:
             return K.conv_wgrad(dy, x, dw, rows, seq_len, c_in, c_out, taps, pad, db=db)
-        self.side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(self.side):
-            K.conv_wgrad(dy, x, dw, rows, seq_len, c_in, c_out, taps, pad, db=db)
-        dy.record_stream(self.side)
-        x.record_stream(self.side)
+        # one workspace for every side-stream weight gradient (they run in stream order);
+        # allocated on the main stream and only grown outside graph capture, so nothing is
+        # allocated on the side stream (a captured graph owns only main-stream allocations)
+        need = K.lib.fs2_conv_wgrad_ws_bytes(rows, c_in, c_out, taps) // 4 + 1
+        ws = self.ws_cache.get("wgrad")
+        if ws is None or ws.numel() < need:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("weight-gradient workspace must be sized before capture")
+            K.lib.fs2_stream_wait(K.stream(), self.side.cuda_stream)  # old buffer drained
+            ws = self.ws_cache["wgrad"] = torch.empty(need, dtype=torch.float32, device=dy.device)
+        side = self.side.cuda_stream
+        K.lib.fs2_stream_wait(side, K.stream())
+        K.conv_wgrad(dy, x, dw, rows, seq_len, c_in, c_out, taps, pad, db=db, ws_buf=ws,
+                     on_stream=side)
+        self.keep.append((dy, x))  # not freed (reusable by the main stream) before the join
 
     def join(self):
         """Make the current stream wait for every weight-gradient GEMM issued so far."""
         if self.side is not None:
-            torch.cuda.current_stream().wait_stream(self.side)
+            K.lib.fs2_stream_wait(K.stream(), self.side.cuda_stream)
+            self.keep.clear()
 
     def notify(self, params):
         """Tell the gradient hook that these parameters' gradients are final."""
@@ -831,6 +844,7 @@ class FastSpeech2(nn.Module):
         self._hooks = {"grad": None}  # gradient-ready callback, see StepCtx.notify
         self.overlap_wgrad = True  # weight-gradient GEMMs on a side stream (StepCtx.wgrad)
         self._side = None
+        self._ws_cache = {}
         self.to(device)
 
     # -- plumbing ---------------------------------------------------------------------
@@ -862,7 +876,7 @@ class FastSpeech2(nn.Module):
     def join_side(self):
         """Make the current stream wait for all weight-gradient work issued so far."""
         if self._side is not None:
-            torch.cuda.current_stream().wait_stream(self._side)
+            K.lib.fs2_stream_wait(K.stream(), self._side.cuda_stream)
 
     def seed(self, s):
         """Seed the per-step dropout stream: step i's Philox key is splitmix64(s, i), drawn on
@@ -916,6 +930,7 @@ class FastSpeech2(nn.Module):
         ctx = StepCtx(seed, self.training, self.dropout, self.compute_dtype)
         ctx.hook = self._hooks["grad"]
         ctx.side = self.side_stream() if self.training else None
+        ctx.ws_cache = self._ws_cache
         B, Ts = texts.shape
         max_src_len = int(max_src_len)
         max_mel_len = int(max_mel_len)

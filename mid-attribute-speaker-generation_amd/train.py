@@ -146,15 +146,12 @@ class Trainer:
         self._static = tuple(b.clone() if torch.is_tensor(b) else b for b in batch)
         host = (self.opt.current_step, self.opt.adam_steps,
                 self.opt._optimizer.param_groups[0]["lr"])
-        overlap = self.model.overlap_wgrad
-        self.model.overlap_wgrad = False  # one stream inside the captured graph
         g = torch.cuda.CUDAGraph()
-        try:
+        try:  # the weight-gradient side stream joins the capture (parallel graph branches)
             with torch.cuda.graph(g):
                 self._graph_out = train_step(self.model, self.opt, self.Loss, self.eLoss,
                                              self._static, self.clip)
         finally:
-            self.model.overlap_wgrad = overlap
             # capture recorded kernels without running them: undo its host-side bookkeeping
             self.opt.current_step, self.opt.adam_steps = host[0], host[1]
             self.opt._optimizer.param_groups[0]["lr"] = host[2]

@@ -272,7 +272,6 @@ def test_graph_replay_matches_eager():
         PKG.seeded.load_seeded_(model)
         model.train()
         model.seed(11)
-        model.overlap_wgrad = False  # same summation schedule on both sides
         tr = T.Trainer(model, pp, mc, tc, graph=graph)
         batch = PKG.data.to_device(PKG.data.syn_batch(8, 32, seed=4), DEV)
         losses = [torch.stack(list(tr.step(batch)[0])).clone() for _ in range(4)]

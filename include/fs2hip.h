@@ -54,10 +54,17 @@ int fs2_abi_version(void);
  * data gradient is the same call on dy with w_bwd (flipped taps, transposed channels).
  * Replaces nn.Conv1d / nn.Linear forward and their input-gradient:
  *   transformer/SubLayers.py:39-41,53,85-89 ; model/modules.py:289-296 ;
- *   transformer/Layers.py:59-64 ; model/fastspeech2.py:25-28,109.                       */
+ *   transformer/Layers.py:59-64 ; model/fastspeech2.py:25-28,109.
+ * lens (nullable, device int64[rows / seq_len]): row r = b*seq_len + t is padding when
+ * t >= lens[b].  With lens, output tiles made only of padding rows are not computed: they
+ * are written as if their rows were zero and there were no bias (aux under ADD_AUX, 0
+ * otherwise) -- for the FFT blocks, whose padded rows are masked (Layers.py:25,28) or carry
+ * zero gradient.  fs2_conv_wgrad skips 64-row k-tiles made only of padding rows (their dy
+ * rows must be zero).  The fp32 path ignores lens.                                     */
 int fs2_conv_gemm(int dtype, const void* x, int64_t ldx, const void* wk, void* y, int64_t ldy,
                   int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out, int taps, int pad,
-                  const float* bias, int flags, const void* aux, int64_t ld_aux, void* stream);
+                  const int64_t* lens, const float* bias, int flags, const void* aux,
+                  int64_t ld_aux, void* stream);
 
 /* Weight re-layout (and cast for bf16) of a (c_out, c_in, taps) fp32 master weight:
  *   w_fwd[o, j*c_in + c]        = w[o, c, j]
@@ -94,7 +101,7 @@ int fs2_set_tuning(int knob, int value);
 int64_t fs2_conv_wgrad_ws_bytes(int64_t rows, int64_t c_in, int64_t c_out, int taps);
 int fs2_conv_wgrad(int dtype, const void* dy, int64_t ldy, const void* x, int64_t ldx, float* dw,
                    float* db, int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out, int taps,
-                   int pad, float* ws, int64_t ws_bytes, void* stream);
+                   int pad, const int64_t* lens, float* ws, int64_t ws_bytes, void* stream);
 
 /* Column sums (bias / LayerNorm-affine / BatchNorm gradients):
  *   out[c] (+)= sum_r x[r, c]   in a fixed order (partials in ws, then in-order sum).   */

@@ -54,15 +54,16 @@ int colsum_launch(const float* x, int64_t ldx, int64_t rows, int64_t cols, float
 // bf16 launchers (gemm_bf16.hip)
 int conv_gemm_bf16_launch(const void* x, int64_t ldx, const void* wk, void* y, int64_t ldy,
                           int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out, int taps,
-                          int pad, const float* bias, int flags, const void* aux, int64_t ld_aux,
-                          hipStream_t st);
+                          int pad, const int64_t* lens, const float* bias, int flags,
+                          const void* aux, int64_t ld_aux, hipStream_t st);
 int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, int64_t ldy,
                           int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out, int taps,
-                          int pad, const float* bias, int flags, const void* aux, int64_t ld_aux,
-                          hipStream_t st);
+                          int pad, const int64_t* lens, const float* bias, int flags,
+                          const void* aux, int64_t ld_aux, hipStream_t st);
 int conv_wgrad_glds_launch(const void* dy, int64_t ldy, const void* x, int64_t ldx, float* dw,
                            float* db, int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out,
-                           int taps, int pad, int splits, int tile, float* ws, hipStream_t st);
+                           int taps, int pad, const int64_t* lens, int splits, int tile, float* ws,
+                           hipStream_t st);
 int conv_wgrad_bf16_launch(const void* dy, int64_t ldy, const void* x, int64_t ldx, float* slab,
                            int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out, int taps,
                            int pad, int splits, hipStream_t st);

@@ -408,7 +408,8 @@ extern "C" {
 
 int fs2_conv_gemm(int dtype, const void* x, int64_t ldx, const void* wk, void* y, int64_t ldy,
                   int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out, int taps, int pad,
-                  const float* bias, int flags, const void* aux, int64_t ld_aux, void* stream) {
+                  const int64_t* lens, const float* bias, int flags, const void* aux,
+                  int64_t ld_aux, void* stream) {
   FS2_CHECK_ARG(rows >= 0 && seq_len > 0 && taps >= 1 && pad >= 0 && pad < taps,
                 "fs2_conv_gemm: bad geometry");
   FS2_CHECK_ARG(!(flags & FS2_EPI_BIAS) || bias, "fs2_conv_gemm: bias flag without bias");
@@ -416,8 +417,8 @@ int fs2_conv_gemm(int dtype, const void* x, int64_t ldx, const void* wk, void* y
                 "fs2_conv_gemm: aux flag without aux");
   if (rows == 0) return FS2_OK;
   if (dtype == FS2_BF16)
-    return conv_gemm_bf16_launch(x, ldx, wk, y, ldy, rows, seq_len, c_in, c_out, taps, pad, bias,
-                                 flags, aux, ld_aux, as_stream(stream));
+    return conv_gemm_bf16_launch(x, ldx, wk, y, ldy, rows, seq_len, c_in, c_out, taps, pad, lens,
+                                 bias, flags, aux, ld_aux, as_stream(stream));
   if (dtype != FS2_F32) {
     set_error("fs2_conv_gemm: dtype %d not built", dtype);
     return FS2_ERR_DTYPE;
@@ -463,7 +464,7 @@ int64_t fs2_conv_wgrad_ws_bytes(int64_t rows, int64_t c_in, int64_t c_out, int t
 
 int fs2_conv_wgrad(int dtype, const void* dy, int64_t ldy, const void* x, int64_t ldx, float* dw,
                    float* db, int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out, int taps,
-                   int pad, float* ws, int64_t ws_bytes, void* stream) {
+                   int pad, const int64_t* lens, float* ws, int64_t ws_bytes, void* stream) {
   const int64_t slab_floats = (int64_t)wgrad_splits(rows, c_in, c_out, taps) * c_out * taps * c_in;
   if (dtype == FS2_BF16) {
     FS2_CHECK_ARG(ws_bytes >= fs2_conv_wgrad_ws_bytes(rows, c_in, c_out, taps),
@@ -472,7 +473,8 @@ int fs2_conv_wgrad(int dtype, const void* dy, int64_t ldy, const void* x, int64_
     const int S = wgrad_splits(rows, c_in, c_out, taps);
     if (!g_tune[FS2_TUNE_LEGACY_GEMM])
       return conv_wgrad_glds_launch(dy, ldy, x, ldx, dw, db, rows, seq_len, c_in, c_out, taps, pad,
-                                    S, wgrad_tile(rows, c_in, c_out, taps), ws, as_stream(stream));
+                                    lens, S, wgrad_tile(rows, c_in, c_out, taps), ws,
+                                    as_stream(stream));
     int rc = conv_wgrad_bf16_launch(dy, ldy, x, ldx, ws, rows, seq_len, c_in, c_out, taps, pad, S,
                                     as_stream(stream));
     if (rc) return rc;

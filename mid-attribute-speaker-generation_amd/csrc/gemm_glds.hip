@@ -47,7 +47,17 @@ struct GldsArgs {
   int tiles_m, tiles_n;
   int vec;    // 8-wide epilogue legal (N, ldy, ld_aux multiples of 8; aligned pointers)
   int group;  // n-tiles per tile group (see the block order below)
+  const int64_t* lens;  // optional utterance lengths: all-padding row tiles are not computed
 };
+
+// Are rows [r0, r1) all padding (t >= lens[b] for r = b*T + t)?  Scalar, block-uniform.
+FS2_DEV bool rows_all_padding(const int64_t* lens, int64_t T, int64_t r0, int64_t r1) {
+  int64_t s = r0 / T;
+  if (r0 - s * T < lens[s]) return false;
+  for (++s; s * T < r1; ++s)
+    if (lens[s] > 0) return false;
+  return true;
+}
 
 FS2_DEV void glds16(const void* src, u16* lds_wave_base) {
   __builtin_amdgcn_global_load_lds(
@@ -130,6 +140,7 @@ __global__ __launch_bounds__(256) void conv_gemm_nt_glds(GldsArgs a) {
   const int tm = rem / gsz, tn = ng * a.group + (rem - (rem / gsz) * gsz);
   const int64_t m0 = (int64_t)tm * BM;
   const int n0 = tn * BN;
+  const bool skip = a.lens && rows_all_padding(a.lens, a.T, m0, m0 + BM < a.M ? m0 + BM : a.M);
 
   // ---- per-lane source descriptors (fixed over the k loop)
   const int lrow = lane >> 3;  // row within the 8-row piece
@@ -226,7 +237,7 @@ __global__ __launch_bounds__(256) void conv_gemm_nt_glds(GldsArgs a) {
     }
   };
 
-  kloop<STAGES, AW + BW>(nk, issue, compute);
+  if (!skip) kloop<STAGES, AW + BW>(nk, issue, compute);
 
   // ---- epilogue through LDS, one half (wm) at a time
   float* Cs = reinterpret_cast<float*>(smem);
@@ -261,7 +272,7 @@ __global__ __launch_bounds__(256) void conv_gemm_nt_glds(GldsArgs a) {
         v[e + 4] = hi[e];
       }
       if (a.vec) {
-        if (a.flags & FS2_EPI_BIAS) {
+        if ((a.flags & FS2_EPI_BIAS) && !skip) {
           const f32x4 b0 = *reinterpret_cast<const f32x4*>(a.bias + n);
           const f32x4 b1 = *reinterpret_cast<const f32x4*>(a.bias + n + 4);
 #pragma unroll
@@ -314,7 +325,7 @@ __global__ __launch_bounds__(256) void conv_gemm_nt_glds(GldsArgs a) {
         for (int e = 0; e < 8; ++e) {
           if (n + e >= a.N) break;
           float x = v[e];
-          if (a.flags & FS2_EPI_BIAS) x += a.bias[n + e];
+          if ((a.flags & FS2_EPI_BIAS) && !skip) x += a.bias[n + e];
           float av = 0.f;
           if (a.flags & (FS2_EPI_ADD_AUX | FS2_EPI_RELU_MASK_AUX))
             av = aux_bf16 ? bfv(((const u16*)a.aux)[m * a.ld_aux + n + e])
@@ -354,6 +365,7 @@ struct WgradGlds {
   int Cin, Cout, taps, pad, Kp;
   int64_t rows_per_split;
   int tiles_o, tiles_k, splits;
+  const int64_t* lens;  // optional: 64-row k-tiles made only of padding rows are skipped
 };
 
 typedef short s16x4g __attribute__((ext_vector_type(4)));
@@ -371,7 +383,10 @@ __global__ __launch_bounds__(256) void conv_wgrad_tn_glds(WgradGlds a) {
   constexpr int EPI_LD = BN + 4;
   constexpr int EPI_E = (BM / 2) * EPI_LD * 2;
   constexpr int SMEM_E = STAGES * STAGE_E > EPI_E ? STAGES * STAGE_E : EPI_E;
-  __shared__ __attribute__((aligned(1024))) u16 smem[SMEM_E];
+  constexpr int MAXKT = 1024;  // k-tile list (skipping all-padding tiles) lives after the ring
+  __shared__ __attribute__((aligned(1024))) u16 smem[SMEM_E + MAXKT + 64];
+  short* ktl = reinterpret_cast<short*>(smem + SMEM_E);
+  int* wcnt = reinterpret_cast<int*>(smem + SMEM_E + MAXKT);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -388,7 +403,33 @@ __global__ __launch_bounds__(256) void conv_wgrad_tn_glds(WgradGlds a) {
   const int64_t r_begin = (int64_t)z * a.rows_per_split;
   int64_t r_end = r_begin + a.rows_per_split;
   if (r_end > a.M) r_end = a.M;
-  const int nk = r_end > r_begin ? (int)((r_end - r_begin + BK - 1) / BK) : 0;
+  const int nk_all = r_end > r_begin ? (int)((r_end - r_begin + BK - 1) / BK) : 0;
+  // ordered list of the split's k-tiles that hold at least one real row (wave ballots +
+  // prefix popcounts; skipped tiles add exact zeros, so the sums are unchanged bitwise)
+  const bool use_list = a.lens != nullptr && nk_all <= MAXKT;
+  int nk = nk_all;
+  if (use_list) {
+    int total = 0;
+    for (int c0 = 0; c0 < nk_all; c0 += 256) {
+      const int kt = c0 + tid;
+      bool v = false;
+      if (kt < nk_all) {
+        const int64_t q0 = r_begin + (int64_t)kt * BK;
+        v = !rows_all_padding(a.lens, a.T, q0, q0 + BK < r_end ? q0 + BK : r_end);
+      }
+      const uint64_t mask = __ballot(v);
+      if (lane == 0) wcnt[wave] = __popcll(mask);
+      __syncthreads();
+      int before = total;
+      for (int w = 0; w < wave; ++w) before += wcnt[w];
+      const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
+      if (v) ktl[before + below] = (short)kt;
+      for (int w = 0; w < 4; ++w) total += wcnt[w];
+      __syncthreads();
+    }
+    nk = total;
+  }
 
   // per-lane staging descriptors: instruction i stages rows RPI*(wave*IPW+i) + lane/NCH.
   // Chunk swizzle f(R): 256-B rows (BT 128) (R & 7) << 1; 128-B rows (BT 64)
@@ -416,12 +457,21 @@ __global__ __launch_bounds__(256) void conv_wgrad_tn_glds(WgradGlds a) {
     base_i[i] = s * a.T;
   }
 
+  int cur_tile = 0;  // the k-tile whose rows t_i / base_i describe
   auto issue = [&](int kt, int stage) {
     u16* As = smem + stage * STAGE_E;
     u16* Bs = As + IMG;
-    const int64_t k0 = r_begin + (int64_t)kt * BK;
+    const int tile = use_list ? (int)ktl[kt] : kt;
+    const int adv = (tile - cur_tile) * BK;
+    cur_tile = tile;
+    const int64_t k0 = r_begin + (int64_t)tile * BK;
 #pragma unroll
     for (int i = 0; i < IPW; ++i) {
+      t_i[i] += adv;
+      while (t_i[i] >= a.T) {
+        t_i[i] -= (int)a.T;
+        base_i[i] += a.T;
+      }
       const int64_t m = k0 + R[i];
       const bool mok = m < r_end;
       const u16* sa = (mok && a_ok[i]) ? a.dy + m * a.ldy + a_col[i] : zero;
@@ -430,11 +480,6 @@ __global__ __launch_bounds__(256) void conv_wgrad_tn_glds(WgradGlds a) {
       const u16* sb = (mok && b_ok[i] && tt >= 0 && tt < a.T)
                           ? a.x + (base_i[i] + tt) * a.ldx + b_c[i] : zero;
       glds16(sb, Bs + (wave * IPW + i) * RPI * BT);
-      t_i[i] += BK;
-      while (t_i[i] >= a.T) {
-        t_i[i] -= (int)a.T;
-        base_i[i] += a.T;
-      }
     }
   };
 
@@ -591,7 +636,8 @@ __global__ __launch_bounds__(256) void wgrad_reduce_taps(const float* __restrict
 
 int conv_wgrad_glds_launch(const void* dy, int64_t ldy, const void* x, int64_t ldx, float* dw,
                            float* db, int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out,
-                           int taps, int pad, int splits, int tile, float* ws, hipStream_t st) {
+                           int taps, int pad, const int64_t* lens, int splits, int tile, float* ws,
+                           hipStream_t st) {
   FS2_CHECK_ARG(c_in % 8 == 0 && c_out % 8 == 0 && ldx % 8 == 0 && ldy % 8 == 0 &&
                     ((uintptr_t)dy & 15) == 0 && ((uintptr_t)x & 15) == 0,
                 "fs2_conv_wgrad(bf16): channel counts / strides must be multiples of 8, operands 16-B aligned");
@@ -601,7 +647,7 @@ int conv_wgrad_glds_launch(const void* dy, int64_t ldy, const void* x, int64_t l
   float* bslab = db ? ws + splits * c_out * Kp : nullptr;
   WgradGlds a{(const u16*)dy, ldy, (const u16*)x, ldx, ws, bslab, rows, seq_len, (int)c_in,
               (int)c_out, taps, pad, (int)Kp, rps, (int)((c_out + tile - 1) / tile),
-              (int)((Kp + tile - 1) / tile), splits};
+              (int)((Kp + tile - 1) / tile), splits, lens};
   const unsigned grid = (unsigned)(a.tiles_o * a.tiles_k * splits);
   const int stages = g_tune[FS2_TUNE_WGRAD_STAGES] >= 1 && g_tune[FS2_TUNE_WGRAD_STAGES] <= 4
                          ? g_tune[FS2_TUNE_WGRAD_STAGES] : (tile == 128 ? 1 : 2);
@@ -647,8 +693,8 @@ static void launch_nt(GldsArgs a, bool tapaligned, hipStream_t st) {
 
 int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, int64_t ldy,
                           int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out, int taps,
-                          int pad, const float* bias, int flags, const void* aux, int64_t ld_aux,
-                          hipStream_t st) {
+                          int pad, const int64_t* lens, const float* bias, int flags,
+                          const void* aux, int64_t ld_aux, hipStream_t st) {
   FS2_CHECK_ARG(c_in % 8 == 0 && ldx % 8 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)wk & 15) == 0,
                 "fs2_conv_gemm(bf16): c_in/ldx must be multiples of 8 and operands 16-B aligned");
   const int K = (int)(taps * c_in);
@@ -661,7 +707,7 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
                   (!(flags & FS2_EPI_BIAS) || ((uintptr_t)bias % 16) == 0) &&
                   (!uses_aux || (ld_aux % 8 == 0 && ((uintptr_t)aux % 16) == 0));
   GldsArgs a{(const u16*)x, ldx, (const u16*)wk, y, ldy, rows, seq_len, (int)c_in, (int)c_out,
-             taps, pad, K, bias, flags, aux, ld_aux, 0, 0, vec, 1};
+             taps, pad, K, bias, flags, aux, ld_aux, 0, 0, vec, 1, lens};
   const bool tapaligned = c_in % 64 == 0;
   const int64_t big = ((rows + 127) / 128) * ((c_out + 127) / 128);
 #define FS2_NT(BM_, BN_)                                                  \

@@ -71,9 +71,10 @@ def _copy(shape, copy, device):
 
 # ------------------------------------------------------------------ GEMM / conv
 def conv_gemm(x, wk, rows, seq_len, c_in, c_out, taps, pad, bias=None, flags=0, aux=None,
-              out=None, ldx=None, out_dtype=torch.float32):
-    """y = conv(x) (+bias, epilogue flags); x/wk fp32 or bf16 (same), y fp32 or bf16."""
-    _dev(x, wk, bias, aux)
+              out=None, ldx=None, out_dtype=torch.float32, lens=None):
+    """y = conv(x) (+bias, epilogue flags); x/wk fp32 or bf16 (same), y fp32 or bf16.
+    ``lens``: all-padding row tiles are not computed (see fs2_conv_gemm)."""
+    _dev(x, wk, bias, aux, lens)
     if x.dtype != wk.dtype:
         raise RuntimeError(f"conv_gemm operand dtypes differ: {x.dtype} vs {wk.dtype}")
     if out is None:
@@ -85,7 +86,8 @@ def conv_gemm(x, wk, rows, seq_len, c_in, c_out, taps, pad, bias=None, flags=0, 
     if aux is not None and aux.dtype == torch.bfloat16:
         flags |= EPI_AUX_BF16
     lib.fs2_conv_gemm(code(x.dtype), ptr(x), ldx or c_in, ptr(wk), ptr(out), c_out, rows, seq_len,
-                      c_in, c_out, taps, pad, ptr(bias), flags, ptr(aux), c_out, stream())
+                      c_in, c_out, taps, pad, ptr(lens), ptr(bias), flags, ptr(aux), c_out,
+                      stream())
     return out
 
 
@@ -96,7 +98,7 @@ def weight_prep(w, c_out, c_in, taps, w_fwd=None, w_bwd=None):
 
 
 def conv_wgrad(dy, x, dw, rows, seq_len, c_in, c_out, taps, pad, db=None, ws_buf=None,
-               on_stream=None):
+               on_stream=None, lens=None):
     """dw (+)= conv weight gradient; db (+)= column sums of dy when given (same launch).
     ``ws_buf``: caller-owned fp32 workspace (else one is allocated on the current stream)."""
     _dev(dy, x, dw, db)
@@ -110,7 +112,7 @@ def conv_wgrad(dy, x, dw, rows, seq_len, c_in, c_out, taps, pad, db=None, ws_buf
     else:
         w = ws(n, dy.device)
     lib.fs2_conv_wgrad(code(dy.dtype), ptr(dy), c_out, ptr(x), c_in, ptr(dw), ptr(db), rows,
-                       seq_len, c_in, c_out, taps, pad, ptr(w), n,
+                       seq_len, c_in, c_out, taps, pad, ptr(lens), ptr(w), n,
                        stream() if on_stream is None else on_stream)
 
 

@@ -127,12 +127,13 @@ class StepCtx:
     def p(self, p):
         return float(p) if self.drop else 0.0
 
-    def wgrad(self, dy, x, dw, rows, seq_len, c_in, c_out, taps, pad, db=None):
+    def wgrad(self, dy, x, dw, rows, seq_len, c_in, c_out, taps, pad, db=None, lens=None):
         """Weight (+bias) gradient GEMM.  Nothing in the backward waits for it, so with a
         side stream it runs concurrently with the data-gradient chain on the main stream
         (the small GEMMs of a block fill the GPU together); ``join`` orders it back."""
         if self.side is None:
-            return K.conv_wgrad(dy, x, dw, rows, seq_len, c_in, c_out, taps, pad, db=db)
+            return K.conv_wgrad(dy, x, dw, rows, seq_len, c_in, c_out, taps, pad, db=db,
+                                lens=lens)
         # one workspace for every side-stream weight gradient (they run in stream order);
         # allocated on the main stream and only grown outside graph capture, so nothing is
         # allocated on the side stream (a captured graph owns only main-stream allocations)
@@ -146,7 +147,7 @@ class StepCtx:
         side = self.side.cuda_stream
         K.lib.fs2_stream_wait(side, K.stream())
         K.conv_wgrad(dy, x, dw, rows, seq_len, c_in, c_out, taps, pad, db=db, ws_buf=ws,
-                     on_stream=side)
+                     on_stream=side, lens=lens)
         self.keep.append((dy, x))  # not freed (reusable by the main stream) before the join
 
     def join(self):
@@ -287,17 +288,19 @@ class FFTBlock(nn.Module):
         n3 = q.out_features
         p = ctx.p(a.p)
         x_c = _t(x, x_t)
-        qkv = K.conv_gemm(x_c, q._w_fwd, M, T, d, n3, 1, 0, bias=self._qkv_b, out_dtype=ctx.cdt)
+        qkv = K.conv_gemm(x_c, q._w_fwd, M, T, d, n3, 1, 0, bias=self._qkv_b, out_dtype=ctx.cdt,
+                          lens=lens)
         o, lse = K.attn_fwd(qkv, lens, B, T, a.n_head, a.d_k, 1.0 / math.sqrt(a.d_k))
-        y1 = K.conv_gemm(o, a.fc._w_fwd, M, T, a.n_head * a.d_k, d, 1, 0, bias=a.fc.bias)
+        y1 = K.conv_gemm(o, a.fc._w_fwd, M, T, a.n_head * a.d_k, d, 1, 0, bias=a.fc.bias,
+                         lens=lens)
         x1, x1_t, xh1, rs1, _ = K.ln_fwd(y1, a.layer_norm.weight, a.layer_norm.bias, res=x,
                                          lens=lens, seq_len=T, p_in=p, seed=ctx.seed,
                                          site_in=self.site, copy=ctx.copy)
         w1, w2 = f.w_1, f.w_2
         x1_c = _t(x1, x1_t)
         h = K.conv_gemm(x1_c, w1._w_fwd, M, T, d, w1.c_out, w1.k, w1.padding, bias=w1.bias,
-                        flags=K.EPI_RELU, out_dtype=ctx.cdt)
-        y2 = K.conv_gemm(h, w2._w_fwd, M, T, w2.c_in, d, w2.k, w2.padding, bias=w2.bias)
+                        flags=K.EPI_RELU, out_dtype=ctx.cdt, lens=lens)
+        y2 = K.conv_gemm(h, w2._w_fwd, M, T, w2.c_in, d, w2.k, w2.padding, bias=w2.bias, lens=lens)
         x2, x2_t, xh2, rs2, _ = K.ln_fwd(y2, f.layer_norm.weight, f.layer_norm.bias, res=x1,
                                          lens=lens, seq_len=T, p_in=p, seed=ctx.seed,
                                          site_in=self.site + 1, copy=ctx.copy)
@@ -320,12 +323,13 @@ class FFTBlock(nn.Module):
                               site_in=self.site + 1, dres=dx1, dres_add=False, copy=ctx.copy,
                               dbias_in=_g(w2.bias))
         dy2_c = _t(dy2, dy2_t)
-        ctx.wgrad(dy2_c, h, _g(w2.weight), M, T, w2.c_in, d, w2.k, w2.padding)
+        ctx.wgrad(dy2_c, h, _g(w2.weight), M, T, w2.c_in, d, w2.k, w2.padding, lens=lens)
         dh = K.conv_gemm(dy2_c, w2._w_bwd, M, T, d, w2.c_in, w2.k, w2.padding,
-                         flags=K.EPI_RELU_MASK_AUX, aux=h, out_dtype=cdt)
-        ctx.wgrad(dh, x1_c, _g(w1.weight), M, T, d, w1.c_out, w1.k, w1.padding, db=_g(w1.bias))
+                         flags=K.EPI_RELU_MASK_AUX, aux=h, out_dtype=cdt, lens=lens)
+        ctx.wgrad(dh, x1_c, _g(w1.weight), M, T, d, w1.c_out, w1.k, w1.padding, db=_g(w1.bias),
+                  lens=lens)
         K.conv_gemm(dh, w1._w_bwd, M, T, w1.c_out, d, w1.k, w1.padding, flags=K.EPI_ADD_AUX,
-                    aux=dx1, out=dx1)
+                    aux=dx1, out=dx1, lens=lens)
         # LN1 -> fc -> attention -> QKV
         dx = torch.empty((M, d), dtype=torch.float32, device=x_c.device)
         dy1, dy1_t = K.ln_bwd(xh1, rs1, ln1.weight, ln1.bias, _g(ln1.weight), _g(ln1.bias),
@@ -334,11 +338,12 @@ class FFTBlock(nn.Module):
                               dbias_in=_g(a.fc.bias))
         dy1_c = _t(dy1, dy1_t)
         hd = a.n_head * a.d_k
-        ctx.wgrad(dy1_c, o, _g(a.fc.weight), M, T, hd, d, 1, 0)
-        do = K.conv_gemm(dy1_c, a.fc._w_bwd, M, T, d, hd, 1, 0, out_dtype=cdt)
+        ctx.wgrad(dy1_c, o, _g(a.fc.weight), M, T, hd, d, 1, 0, lens=lens)
+        do = K.conv_gemm(dy1_c, a.fc._w_bwd, M, T, d, hd, 1, 0, out_dtype=cdt, lens=lens)
         dqkv = K.attn_bwd(qkv, o, do, lse, lens, B, T, a.n_head, a.d_k, 1.0 / math.sqrt(a.d_k))
-        ctx.wgrad(dqkv, x_c, self._qkv_gw, M, T, d, n3, 1, 0, db=self._qkv_gb)
-        K.conv_gemm(dqkv, q._w_bwd, M, T, n3, d, 1, 0, flags=K.EPI_ADD_AUX, aux=dx, out=dx)
+        ctx.wgrad(dqkv, x_c, self._qkv_gw, M, T, d, n3, 1, 0, db=self._qkv_gb, lens=lens)
+        K.conv_gemm(dqkv, q._w_bwd, M, T, n3, d, 1, 0, flags=K.EPI_ADD_AUX, aux=dx, out=dx,
+                    lens=lens)
         return dx
 
 

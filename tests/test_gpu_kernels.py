@@ -425,3 +425,39 @@ def test_conv_gemm_bf16_pipeline_depths(stages, B, T, cin, cout, k):
     finally:
         for knob in (0, 1, 2):
             K.lib.fs2_set_tuning(knob, 0)
+
+
+def test_conv_gemm_bf16_padding_tiles():
+    """lens: all-padding 128-row tiles are written as zero rows (bias dropped) / aux, the
+    rest exactly as without lens; the weight gradient with zero dy at padded rows is
+    bitwise the same with and without skipping."""
+    B, T, cin, cout, k = 6, 512, 256, 1024, 9
+    lens = torch.tensor([512, 300, 129, 128, 1, 400], device=DEV)
+    pad_rows = (torch.arange(T, device=DEV)[None] >= lens[:, None]).reshape(-1)
+    x = bf(rnd(B * T, cin, seed=31)) * (~pad_rows)[:, None]
+    w = bf(rnd(cout, cin, k, scale=1 / math.sqrt(cin * k), seed=32)).float()
+    b = rnd(cout, seed=33)
+    wf = torch.empty(cout * cin * k, device=DEV, dtype=torch.bfloat16)
+    wb = torch.empty(cout * cin * k, device=DEV, dtype=torch.bfloat16)
+    K.weight_prep(w, cout, cin, k, wf, wb)
+    y0 = K.conv_gemm(x, wf, B * T, T, cin, cout, k, 4, bias=b)
+    y1 = K.conv_gemm(x, wf, B * T, T, cin, cout, k, 4, bias=b, lens=lens)
+    tile_pad = pad_rows.view(-1, 128).all(1).repeat_interleave(128)
+    assert tile_pad.sum() > 0
+    assert torch.equal(y1[~tile_pad], y0[~tile_pad])
+    assert torch.equal(y1[tile_pad], torch.zeros_like(y1[tile_pad]))
+    aux = rnd(B * T, cin, seed=34)
+    dy = bf(rnd(B * T, cout, seed=35)) * (~pad_rows)[:, None]
+    d0 = K.conv_gemm(dy, wb, B * T, T, cout, cin, k, 4, flags=K.EPI_ADD_AUX, aux=aux)
+    d1 = K.conv_gemm(dy, wb, B * T, T, cout, cin, k, 4, flags=K.EPI_ADD_AUX, aux=aux, lens=lens)
+    assert torch.equal(d1[~tile_pad], d0[~tile_pad]) and torch.equal(d1[tile_pad], aux[tile_pad])
+    for tile in (64, 128):
+        K.lib.fs2_set_tuning(2, tile)
+        try:
+            dw0, db0 = torch.zeros_like(w), torch.zeros(cout, device=DEV)
+            dw1, db1 = torch.zeros_like(w), torch.zeros(cout, device=DEV)
+            K.conv_wgrad(dy, x, dw0, B * T, T, cin, cout, k, 4, db=db0)
+            K.conv_wgrad(dy, x, dw1, B * T, T, cin, cout, k, 4, db=db1, lens=lens)
+        finally:
+            K.lib.fs2_set_tuning(2, 0)
+        assert torch.equal(dw0, dw1) and torch.equal(db0, db1)

@@ -12,7 +12,7 @@ import re
 import torch  # noqa: F401  (load torch's HIP runtime before ours)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "csrc", "libfs2hip.so")
+LIB_PATH = os.environ.get("FS2HIP_LIB") or os.path.join(_HERE, "csrc", "libfs2hip.so")
 HEADER = os.path.join(os.path.dirname(_HERE), "include", "fs2hip.h")
 if not os.path.exists(HEADER):  # installed layout: header shipped next to csrc/
     HEADER = os.path.join(_HERE, "csrc", "fs2hip.h")

@@ -32,16 +32,23 @@ FS2_DEV u16 f2bf(float f) {
   return *reinterpret_cast<u16*>(&b);
 }
 
-// 64 x 128 bf16 tile, rows r0.., row stride ld (elements) in global, LDS stride LDS_LD
-template <int LDS_LD>
-FS2_DEV void load_tile(u16* dst, const u16* base, int64_t ld, int r0, int nrows, int tid) {
+// register-staged copy of a 64 x 128 tile: load into 4 x 16 B per thread (issued before the
+// MFMA work on the previous tile, so the global latency overlaps it), store after a barrier
+FS2_DEV void load_regs(uint4 (&r)[4], const u16* base, int64_t ld, int r0, int nrows, int tid) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int c = tid + i * 256, row = c >> 4, col = (c & 15) * 8;
-    const int r = r0 + row;
-    uint4 v = r < nrows ? *reinterpret_cast<const uint4*>(base + (int64_t)r * ld + col)
-                        : make_uint4(0u, 0u, 0u, 0u);
-    *reinterpret_cast<uint4*>(&dst[row * LDS_LD + col]) = v;
+    const int rr = r0 + row;
+    r[i] = rr < nrows ? *reinterpret_cast<const uint4*>(base + (int64_t)rr * ld + col)
+                      : make_uint4(0u, 0u, 0u, 0u);
+  }
+}
+template <int LDS_LD>
+FS2_DEV void store_regs(u16* dst, const uint4 (&r)[4], int tid) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = tid + i * 256, row = c >> 4, col = (c & 15) * 8;
+    *reinterpret_cast<uint4*>(&dst[row * LDS_LD + col]) = r[i];
   }
 }
 
@@ -125,11 +132,20 @@ __global__ __launch_bounds__(256) void attn_fwd_bf16(const u16* __restrict__ qkv
   for (int i = 0; i < 8; ++i) oacc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nkt = (L + QB - 1) / QB;
+  const u16* kbase = base + (int64_t)H * DH + h * DH;
+  const u16* vbase = base + 2LL * H * DH + h * DH;
+  uint4 kr[4], vr[4];
+  load_regs(kr, kbase, ld, 0, T, tid);
+  load_regs(vr, vbase, ld, 0, T, tid);
   for (int kt = 0; kt < nkt; ++kt) {
     __syncthreads();
-    load_tile<LDR>(Ks, base + (int64_t)H * DH + h * DH, ld, kt * QB, T, tid);
-    load_tile<LDT>(Vs, base + 2LL * H * DH + h * DH, ld, kt * QB, T, tid);
+    store_regs<LDR>(Ks, kr, tid);
+    store_regs<LDT>(Vs, vr, tid);
     __syncthreads();
+    if (kt + 1 < nkt) {  // next tile's loads in flight during this tile's MFMAs
+      load_regs(kr, kbase, ld, (kt + 1) * QB, T, tid);
+      load_regs(vr, vbase, ld, (kt + 1) * QB, T, tid);
+    }
     f32x4 s[4];
     float mt = -INFINITY;
 #pragma unroll
@@ -226,11 +242,20 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_bf16(const u16* __restrict__ 
   for (int i = 0; i < 8; ++i) dq[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nkt = (L + QB - 1) / QB;
+  const u16* kbase = base + (int64_t)H * DH + h * DH;
+  const u16* vbase = base + 2LL * H * DH + h * DH;
+  uint4 kr[4], vr[4];
+  load_regs(kr, kbase, ld, 0, T, tid);
+  load_regs(vr, vbase, ld, 0, T, tid);
   for (int kt = 0; kt < nkt; ++kt) {
     __syncthreads();
-    load_tile<LDR>(Ks, base + (int64_t)H * DH + h * DH, ld, kt * QB, T, tid);
-    load_tile<LDR>(Vs, base + 2LL * H * DH + h * DH, ld, kt * QB, T, tid);
+    store_regs<LDR>(Ks, kr, tid);
+    store_regs<LDR>(Vs, vr, tid);
     __syncthreads();
+    if (kt + 1 < nkt) {
+      load_regs(kr, kbase, ld, (kt + 1) * QB, T, tid);
+      load_regs(vr, vbase, ld, (kt + 1) * QB, T, tid);
+    }
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       f32x4 dsv[2];
@@ -297,16 +322,30 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_bf16(const u16* __restrict_
   for (int i = 0; i < 8; ++i) dk[i] = dv[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nqt = (L + QB - 1) / QB;
-  for (int qt = 0; qt < nqt; ++qt) {
-    __syncthreads();
-    load_tile<LDR>(Qs, base + h * DH, ld, qt * QB, T, tid);
-    load_tile<LDR>(Ds, d_o + (int64_t)b * T * ldo + h * DH, ldo, qt * QB, T, tid);
+  const u16* qbase = base + h * DH;
+  const u16* dobase = d_o + (int64_t)b * T * ldo + h * DH;
+  uint4 qr[4], dr[4];
+  float lr_ = 0.f, dl_ = 0.f;
+  auto load_q = [&](int qt) {
+    load_regs(qr, qbase, ld, qt * QB, T, tid);
+    load_regs(dr, dobase, ldo, qt * QB, T, tid);
     if (tid < QB) {
       const int qq = qt * QB + tid;
-      lse_s[tid] = qq < T ? lse[(int64_t)bh * T + qq] : 0.f;
-      del_s[tid] = qq < T ? delta[(int64_t)bh * T + qq] : 0.f;
+      lr_ = qq < T ? lse[(int64_t)bh * T + qq] : 0.f;
+      dl_ = qq < T ? delta[(int64_t)bh * T + qq] : 0.f;
+    }
+  };
+  load_q(0);
+  for (int qt = 0; qt < nqt; ++qt) {
+    __syncthreads();
+    store_regs<LDR>(Qs, qr, tid);
+    store_regs<LDR>(Ds, dr, tid);
+    if (tid < QB) {
+      lse_s[tid] = lr_;
+      del_s[tid] = dl_;
     }
     __syncthreads();
+    if (qt + 1 < nqt) load_q(qt + 1);
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       f32x4 pp[2], dsv[2];

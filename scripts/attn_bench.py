@@ -1,0 +1,40 @@
+"""Time the bf16 attention kernels on the decoder/encoder shapes with SYN-48 lengths."""
+import importlib
+import math
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+PKG = importlib.import_module("mid-attribute-speaker-generation_amd")
+K = importlib.import_module("mid-attribute-speaker-generation_amd.kernels")
+dev = "cuda:0"
+b = PKG.data.syn_batch(48, 128, seed=0)
+
+
+def timeit(run, n=20):
+    for _ in range(3):
+        run()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(n):
+        run()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / n * 1e3
+
+
+for name, T, lens in (("decoder", 512, np.asarray(b[7])), ("encoder", 128, np.asarray(b[4]))):
+    B, H, dh = 48, 2, 128
+    L = torch.tensor(lens, device=dev)
+    qkv = (torch.randn(B * T, 3 * H * dh, device=dev) * 0.5).to(torch.bfloat16)
+    o, lse = K.attn_fwd(qkv, L, B, T, H, dh, 1 / math.sqrt(dh))
+    do = torch.randn(B * T, H * dh, device=dev).to(torch.bfloat16)
+    tf = timeit(lambda: K.attn_fwd(qkv, L, B, T, H, dh, 1 / math.sqrt(dh)))
+    tb = timeit(lambda: K.attn_bwd(qkv, o, do, lse, L, B, T, H, dh, 1 / math.sqrt(dh)))
+    kv = np.ceil(lens / 64) * 64
+    fl = float(np.sum(4.0 * H * kv * kv * dh))
+    print(f"{name}: fwd {tf:6.1f} us ({fl / tf / 1e6:5.0f} TF)  bwd {tb:6.1f} us "
+          f"({2.5 * fl / tb / 1e6:5.0f} TF)", flush=True)

@@ -9,9 +9,10 @@ rank (B = 48, 128 phonemes x 512 frames padded) with inputs resi
 value = valid mel frames of all ranks per second (max-over-ranks time, weak scaling).
 
 The JSON line also carries
-  roofline     the FFN Conv1d(k=9) implicit GEMM (the dominant kernel: 75% of the FFT-block
-               FLOPs), achieved FLOP/s from HIP events around its launches inside the timed
-               region, against the dense MFMA peak of the compute dtype;
+  roofline     the decoder FFN Conv1d(256->1024, k=9) forward implicit GEMM (the dominant
+               kernel: the k=9 convs are 75% of the FFT-block FLOPs), achieved FLOP/s from HIP
+               events around its launches inside the timed region, against the dense MFMA
+               peak of the compute dtype;
   cpu_baseline the CPU oracle (oracle/fs2_cpu.py, a restatement of the reference step) timed
                on this host's cores on a bounded sample (rank 0, N = 1 only).
 """
@@ -34,15 +35,17 @@ K = importlib.import_module("mid-attribute-speaker-generation_amd.kernels")
 TR = importlib.import_module("mid-attribute-speaker-generation_amd.train")
 
 PEAK = {"f32": (157.3, "TFLOP/s"), "bf16": (2500.0, "TFLOP/s")}
-# compulsory bytes of one decoder k=9 launch, bf16 operands: fwd reads x (N x 256) + W, writes
-# h (N x 1024); dX reads dh (N x 1024) + W, reads and writes dx1 fp32 (N x 256); averaged
+# compulsory bytes of one decoder FFN Conv1d(256 -> 1024, k=9) forward launch, bf16 operands:
+# read x (N x 256) and the re-laid-out weight (1024 x 9*256), write h (N x 1024)
 _N = 24576
-ALG_BYTES = round(((_N * 256 * 2 + 1024 * 2304 * 2 + _N * 1024 * 2) +
-                   (_N * 1024 * 2 + 1024 * 2304 * 2 + 2 * _N * 256 * 4)) / 2)
+ALG_BYTES = _N * 256 * 2 + 1024 * 2304 * 2 + _N * 1024 * 2
 
 
 class ConvTimer:
-    """HIP events around every k=9 conv GEMM launch (forward and data-gradient).
+    """HIP events around every decoder FFN Conv1d(256 -> 1024, k=9) forward launch (the
+    dominant kernel; 6 launches per step at SYN-48, each a 24,576 x 1,024 x 2,304 implicit
+    GEMM, grid 1,536 tiles of 128 x 128 -- the only launch of that grid in the step, so the
+    rocprofv3 trace isolates the same launches: scripts/kshape.py).
 
     Eager steps: events are recorded around the launches of the timed steps.  Graph replay:
     the event records are captured into the step graph next to the kernels (``capture``
@@ -53,14 +56,15 @@ class ConvTimer:
         self.on = False
         self.capture = False
         self.events, self.flops = [], []
+        self.rows = 0  # padded mel frames of the batch (the decoder's rows)
         self._orig = K.conv_gemm
 
     def install(self):
         orig = self._orig
 
         def timed(x, wk, rows, seq_len, c_in, c_out, taps, pad, **kw):
-            rec = taps == 9 and (self.on or (self.capture and
-                                             torch.cuda.is_current_stream_capturing()))
+            rec = (taps == 9 and c_out > c_in and rows == self.rows and
+                   (self.on or (self.capture and torch.cuda.is_current_stream_capturing())))
             if not rec:
                 return orig(x, wk, rows, seq_len, c_in, c_out, taps, pad, **kw)
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -86,8 +90,8 @@ class ConvTimer:
         return float(np.sum(self.flops)), float(np.sum(ms)) / 1e3, len(ms)
 
 
-PROBE_SHAPES = [  # the decoder's k=9 launches: forward (h = conv(x1)) and data gradient
-    (24576, 512, 256, 1024, 9, "fwd"), (24576, 512, 1024, 256, 9, "dx")]
+PROBE_SHAPES = [  # the decoder's FFN k=9 forward launch (h = relu(conv(x1) + b))
+    (24576, 512, 256, 1024, 9, "fwd")]
 
 
 def probe_conv(reps=10):
@@ -208,6 +212,7 @@ def main():
     padded_local = int(args.batch * batch_np[8])
 
     timer = ConvTimer()
+    timer.rows = padded_local
     if not args.no_roofline:
         timer.install()
         timer.capture = use_graph
@@ -249,7 +254,7 @@ def main():
             ach = flops / secs / 1e12
             roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": unit,
                     "frac": round(ach / peak, 4), "traffic": None,
-                    "kernel": "conv_gemm_nt (FFN Conv1d k=9, fwd + dX)",
+                    "kernel": "conv_gemm_nt_glds<128,128> (decoder FFN Conv1d 256->1024 k=9, forward)",
                     "per_launch_flop": round(flops / n), "avg_launch_ms": round(secs / n * 1e3, 4)}
             if world == 1 and args.dtype == "bf16" and not args.no_traffic:
                 traffic, detail = hbm_traffic()

@@ -168,6 +168,13 @@ int fs2_bn_fwd(int dtype, const float* z, int64_t rows, int64_t c, const float* 
                const uint64_t* seed, uint64_t site, const float* res, float* out, void* out_t,
                float* ws,
                int64_t ws_bytes, void* stream);
+/* Eval-mode BatchNorm1d (transformer/Layers.py:129-137 under model.eval()): normalise with
+ * the running statistics, no dropout, no statistics update; mean / rstd (c floats each)
+ * receive running_mean and 1/sqrt(running_var + eps).                                 */
+int fs2_bn_eval_fwd(int dtype, const float* z, int64_t rows, int64_t c, const float* gamma,
+                    const float* beta, float eps, const float* running_mean,
+                    const float* running_var, float* mean, float* rstd, int act_tanh,
+                    const float* res, float* out, void* out_t, void* stream);
 int fs2_bn_bwd(int dtype, const float* dout, const float* z, const float* mean, const float* rstd,
                const float* gamma, const float* beta, int64_t rows, int64_t c, int act_tanh,
                float p, const uint64_t* seed, uint64_t site, float* dz, void* dz_t,
@@ -211,6 +218,9 @@ int fs2_bucketize(const void* values, int values_dtype, const float* bins, int n
  * (uncropped).  dur_dtype: 0 = int64, 1 = f32.                                       */
 int fs2_lr_index(const void* durations, int dur_dtype, int64_t batch, int64_t src_len,
                  int32_t* cum, int64_t* mel_len, void* stream);
+/* Inference durations (model/modules.py:132-135):
+ * out = clamp(round_half_even(exp(log_d) - 1) * d_control, min = 0), f32 (NaN propagates). */
+int fs2_duration_round(const float* log_d, int64_t n, float d_control, float* out, void* stream);
 /* src[b, t] = i with cum[i-1] <= t < cum[i], or -1 past mel_len (bit-exact index map). */
 int fs2_lr_source(const int32_t* cum, int64_t batch, int64_t src_len, int64_t out_len,
                   int32_t* src, void* stream);

@@ -412,6 +412,24 @@ int fs2_lr_index(const void* durations, int dur_dtype, int64_t batch, int64_t sr
   return launch_status("fs2_lr_index");
 }
 
+// torch.clamp(torch.round(torch.exp(log_d) - 1) * d_control, min=0): round half to even
+// (rintf under the default rounding mode); a NaN stays NaN as in torch.clamp
+__global__ void duration_round(const float* log_d, int64_t n, float d_control, float* out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float v = rintf(expf(log_d[i]) - 1.f) * d_control;
+    out[i] = v < 0.f ? 0.f : v;
+  }
+}
+
+int fs2_duration_round(const float* log_d, int64_t n, float d_control, float* out, void* stream) {
+  if (n == 0) return FS2_OK;
+  FS2_CHECK_ARG(n > 0 && log_d && out, "fs2_duration_round: bad arguments");
+  duration_round<<<(unsigned)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096), 256, 0,
+                   as_stream(stream)>>>(log_d, n, d_control, out);
+  return launch_status("fs2_duration_round");
+}
+
 int fs2_lr_source(const int32_t* cum, int64_t batch, int64_t src_len, int64_t out_len,
                   int32_t* src, void* stream) {
   const int64_t n = batch * out_len;

@@ -454,6 +454,32 @@ int fs2_bn_fwd(int dtype, const float* z, int64_t rows, int64_t c, const float* 
   return launch_status("fs2_bn_fwd");
 }
 
+// eval-mode statistics: mean = running_mean, rstd = 1 / sqrt(running_var + eps)
+__global__ void bn_eval_stats(const float* rm, const float* rv, int64_t c, float eps, float* mean,
+                              float* rstd) {
+  const int64_t col = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (col >= c) return;
+  mean[col] = rm[col];
+  rstd[col] = 1.f / sqrtf(rv[col] + eps);
+}
+
+int fs2_bn_eval_fwd(int dtype, const float* z, int64_t rows, int64_t c, const float* gamma,
+                    const float* beta, float eps, const float* running_mean,
+                    const float* running_var, float* mean, float* rstd, int act_tanh,
+                    const float* res, float* out, void* out_t, void* stream) {
+  if (int rc = copy_dtype_ok(dtype, "fs2_bn_eval_fwd")) return rc;
+  FS2_CHECK_ARG(rows > 0 && c > 0 && c % 4 == 0, "fs2_bn_eval_fwd: bad shape (c % 4 == 0)");
+  FS2_CHECK_ARG(running_mean && running_var && mean && rstd, "fs2_bn_eval_fwd: null statistics");
+  hipStream_t st = as_stream(stream);
+  unsigned short* ot = dtype == FS2_BF16 ? (unsigned short*)out_t : nullptr;
+  FS2_CHECK_ARG(out || ot, "fs2_bn_eval_fwd: no output requested");
+  bn_eval_stats<<<(unsigned)((c + 255) / 256), 256, 0, st>>>(running_mean, running_var, c, eps,
+                                                             mean, rstd);
+  bn_apply<<<ew_grid(rows * c / 4), 256, 0, st>>>(z, mean, rstd, gamma, beta, rows * c / 4, (int)c,
+                                                  act_tanh, 0.f, nullptr, 0, res, out, ot);
+  return launch_status("fs2_bn_eval_fwd");
+}
+
 int fs2_bn_bwd(int dtype, const float* dout, const float* z, const float* mean, const float* rstd,
                const float* gamma, const float* beta, int64_t rows, int64_t c, int act_tanh,
                float p, const uint64_t* seed, uint64_t site, float* dz, void* dz_t,

@@ -212,6 +212,21 @@ def bn_fwd(z, gamma, beta, running_mean, running_var, act_tanh, p, seed, site, r
     return out, out_t, mean, rstd
 
 
+def bn_eval_fwd(z, gamma, beta, running_mean, running_var, act_tanh, res=None, eps=1e-5,
+                copy=None, want_out=True):
+    """Eval-mode BatchNorm1d (running statistics, no dropout): (out or None, out copy or None)."""
+    _dev(z, gamma, beta, running_mean, running_var, res)
+    rows, c = z.shape
+    out = torch.empty_like(z) if (want_out or copy is None) else None
+    out_t = _copy(z.shape, copy, z.device)
+    mean = torch.empty(c, dtype=torch.float32, device=z.device)
+    rstd = torch.empty(c, dtype=torch.float32, device=z.device)
+    lib.fs2_bn_eval_fwd(BF16 if copy is not None else F32, ptr(z), rows, c, ptr(gamma), ptr(beta),
+                        eps, ptr(running_mean), ptr(running_var), ptr(mean), ptr(rstd),
+                        int(act_tanh), ptr(res), ptr(out), ptr(out_t), stream())
+    return out, out_t
+
+
 def bn_bwd(dout, z, mean, rstd, gamma, beta, dgamma, dbeta, act_tanh, p, seed, site, copy=None):
     _dev(dout, z, mean, rstd, gamma, beta, dgamma, dbeta)
     rows, c = z.shape
@@ -321,6 +336,17 @@ def lr_index(durations):
     mel_len = torch.empty(B, dtype=torch.int64, device=durations.device)
     lib.fs2_lr_index(ptr(durations), dt, B, Ts, ptr(cum), ptr(mel_len), stream())
     return cum, mel_len
+
+
+def duration_round(log_d, d_control=1.0):
+    """Inference durations: clamp(round(exp(log_d) - 1) * d_control, min=0) (f32)."""
+    _dev(log_d)
+    if log_d.dtype != torch.float32:
+        raise RuntimeError(f"log durations must be float32, got {log_d.dtype}")
+    x = log_d.contiguous()
+    out = torch.empty_like(x)
+    lib.fs2_duration_round(ptr(x), x.numel(), float(d_control), ptr(out), stream())
+    return out
 
 
 def lr_source(cum, out_len):
@@ -467,6 +493,13 @@ def add(a, b, out=None):
     out = torch.empty_like(a) if out is None else out
     lib.fs2_add(ptr(out), ptr(a), ptr(b), a.numel(), stream())
     return out
+
+
+def scale_(t, value):
+    """t *= value in place (f32)."""
+    _dev(t)
+    lib.fs2_scale(ptr(t), t.numel(), float(value), stream())
+    return t
 
 
 def add_i64_(t, value):

@@ -495,8 +495,7 @@ class PostNet(nn.Module):
     def fwd(self, x, x_t, B, T, ctx):
         """x: (M, n_mel) mel_linear output; returns postnet(x) + x."""
         if not self.training:
-            raise NotImplementedError("eval-mode PostNet (running-stat BatchNorm) is part of the "
-                                      "inference path, SURVEY.md §8f row f1")
+            return self.fwd_eval(x, x_t, T, ctx.copy), None
         M = x.shape[0]
         a_c = _t(x, x_t)
         saved = []
@@ -517,6 +516,23 @@ class PostNet(nn.Module):
             saved.append((a_c, z, mean, rstd))
             a_c = _t(out, out_t)
         return out, (saved, p, ctx, T)
+
+    def fwd_eval(self, x, x_t, T, copy):
+        """Eval mode: BatchNorm on the running statistics, no dropout, no stat update."""
+        M = x.shape[0]
+        a_c = _t(x, x_t)
+        n = len(self.convolutions)
+        out = None
+        for i, layer in enumerate(self.convolutions):
+            conv, bn = layer[0].conv, layer[1]
+            z = K.conv_gemm(a_c, conv._w_fwd, M, T, conv.c_in, conv.c_out, conv.k, conv.padding,
+                            bias=conv.bias)
+            last = i == n - 1
+            out, out_t = K.bn_eval_fwd(z, bn.weight, bn.bias, bn.running_mean, bn.running_var,
+                                       not last, res=x if last else None,
+                                       copy=None if last else copy, want_out=last)
+            a_c = _t(out, out_t)
+        return out
 
     def bwd(self, dout, saved, dx_acc):
         """dout: grad of postnet(x) + x; adds the postnet input grad into ``dx_acc``."""
@@ -925,10 +941,17 @@ class FastSpeech2(nn.Module):
     def forward(self, speakers, texts, src_lens, max_src_len, mels=None, mel_lens=None,
                 max_mel_len=None, p_targets=None, e_targets=None, d_targets=None,
                 p_control=1.0, e_control=1.0, d_control=1.0, accents=None, speaker_meta=None):
-        if p_targets is None or e_targets is None or d_targets is None or mel_lens is None:
-            raise NotImplementedError("inference branch (no targets) is SURVEY.md §8f row f1")
         if accents is None:
-            raise ValueError("accents are required in training (transformer/Models.py:101)")
+            raise ValueError("accents are required (transformer/Models.py:101)")
+        teacher = not (p_targets is None or e_targets is None or d_targets is None or
+                       mel_lens is None)
+        if not (self.training and teacher):
+            if self.training and torch.is_grad_enabled():
+                raise ValueError("training needs p/e/d targets and mel_lens (train.py:145); "
+                                 "run inference under torch.no_grad() or model.eval()")
+            return self._forward_infer(speakers, texts, src_lens, max_src_len, mel_lens,
+                                       max_mel_len, p_targets, e_targets, d_targets, p_control,
+                                       e_control, d_control, accents, speaker_meta=speaker_meta)
         self.arena()
         self.prep_weights()
         seed = self._step_seed() if (self.training and self.dropout) else 0
@@ -958,6 +981,133 @@ class FastSpeech2(nn.Module):
         output, postnet_output = MelHeadFn.apply(tok, x, x_t, self, B, T_dec, ctx)
         return (output, postnet_output, p, e, log_d, d_targets, src_masks, mel_masks, src_lens,
                 mel_len, gmm, speaker_emb_s)
+
+    # -- inference ----------------------------------------------------------------------
+    def _posenc(self, T):
+        """Decoder position table for T frames: ``position_enc`` (1001 rows) or, past
+        ``max_seq_len`` in eval mode, a fresh table of T rows (Models.py:160-165)."""
+        tab = self.decoder.position_enc
+        if T <= tab.shape[1]:
+            return tab
+        cache = self.__dict__.setdefault("_long_posenc", {})
+        n = 1 << (T - 1).bit_length()  # power-of-two buckets (rows depend on position only)
+        if n not in cache:
+            cache.clear()
+            cache[n] = sinusoid_table(n, self.decoder.d).to(tab.device)[None]
+        return cache[n]
+
+    def _forward_infer(self, speakers, texts, src_lens, max_src_len, mel_lens, max_mel_len,
+                       p_targets, e_targets, d_targets, p_control, e_control, d_control, accents,
+                       speaker_meta=None, speaker_vec=None):
+        """Forward without autograd: ``model/fastspeech2.py:52-174`` under ``torch.no_grad()``
+        (evaluate.py, synthesize.py), any of the p/e/d targets optional.
+
+        * pitch / energy without a target: prediction * control, bucketized
+          (``modules.py:80-100``); energy uses ``p_control`` (``modules.py:124``, quirk kept,
+          so ``e_control`` is accepted and unused as in the reference);
+        * durations without a target: ``fs2_duration_round`` then the LengthRegulator; the
+          frame count max(mel_len) is the one device->host read (``utils/tools.py:157``);
+        * eval-mode decoder past ``max_seq_len``: no truncation, fresh position table
+          (``Models.py:160-165``); training mode truncates to ``max_seq_len``;
+        * eval-mode PostNet: BatchNorm on the running statistics.
+        """
+        del e_control  # modules.py:124 passes p_control to the energy branch
+        self.arena()
+        self.prep_weights()
+        ctx = StepCtx(0, False, False, self.compute_dtype)  # no dropout outside training
+        ctx.ws_cache = self._ws_cache
+        B, Ts = texts.shape
+        max_src_len = int(max_src_len)
+        assert Ts == max_src_len, "texts must be padded to max_src_len"
+        src_lens = src_lens.contiguous().long()
+        src_masks = K.length_mask(src_lens, Ts)
+        va, enc, dec = self.variance_adaptor, self.encoder, self.decoder
+        with torch.no_grad():
+            x, x_t = K.encoder_embed(texts.contiguous(), accents.contiguous(),
+                                     enc.src_word_emb.weight, enc.src_accent_emb.weight,
+                                     enc.position_enc, B, Ts, enc.d, copy=ctx.copy)
+            for layer in enc.layer_stack:
+                x, x_t, _ = layer.fwd(x, x_t, src_lens, B, Ts, ctx)
+            if speaker_vec is None:
+                ids, table = speakers.contiguous(), self.speaker_emb.weight
+                speaker_emb_s = K.embedding_fwd(ids, table)
+            else:  # synthesize_from_speaker_emb: one (1 or B, d) vector per utterance
+                table = speaker_vec.detach().float().contiguous().view(-1, enc.d)
+                ids = torch.arange(B, device=table.device) if table.shape[0] == B else \
+                    torch.zeros(B, dtype=torch.int64, device=table.device)
+                speaker_emb_s = None
+            gmm = self.speaker_enc(speaker_meta) if speaker_meta is not None else None
+            x0, x0_t = K.rowvec_add(x, ids, table, B, Ts, copy=ctx.copy)
+            log_d, _ = va.duration_predictor.fwd(x0, x0_t, src_lens, B, Ts, ctx)
+            p, _ = va.pitch_predictor.fwd(x0, x0_t, src_lens, B, Ts, ctx)
+            if p_targets is None:
+                if p_control != 1.0:
+                    K.scale_(p, p_control)
+                p_vals = p
+            else:
+                p_vals = p_targets
+            x1, x1_t, _ = K.bucket_embed(x0, p_vals.contiguous().view(-1), va.pitch_bins,
+                                         va.pitch_embedding.weight, copy=ctx.copy)
+            e, _ = va.energy_predictor.fwd(x1, x1_t, src_lens, B, Ts, ctx)
+            if e_targets is None:
+                if p_control != 1.0:
+                    K.scale_(e, p_control)
+                e_vals = e
+            else:
+                e_vals = e_targets
+            x2, _, _ = K.bucket_embed(x1, e_vals.contiguous().view(-1), va.energy_bins,
+                                      va.energy_embedding.weight)
+            if d_targets is not None:
+                if mel_lens is None:
+                    raise ValueError("d_targets without mel_lens: the decoder has no mask "
+                                     "(model/fastspeech2.py:71-75)")
+                d_rounded = d_targets
+                cum, mel_len = K.lr_index(d_targets.contiguous())
+                dec_lens = mel_lens.contiguous().long()
+                T = int(max_mel_len) if max_mel_len is not None else int(mel_len.max())
+            else:
+                d_rounded = K.duration_round(log_d, d_control)
+                cum, mel_len = K.lr_index(d_rounded)
+                dec_lens = mel_len
+                T_mask = int(mel_len.max())  # get_mask_from_lengths(mel_len), modules.py:137
+                T = T_mask if max_mel_len is None else int(max_mel_len)
+                if T > T_mask:
+                    raise ValueError(f"max_mel_len {T} exceeds the predicted length {T_mask}: "
+                                     "the reference's decoder mask would not broadcast")
+            T_dec = T if (not self.training and T > dec.max_seq_len) else min(T, dec.max_seq_len)
+            mel_masks = K.length_mask(dec_lens, T_dec)
+            x, x_t = K.lr_expand(x2, cum, T_dec, posenc=self._posenc(T_dec), copy=ctx.copy)
+            for layer in dec.layer_stack:
+                x, x_t, _ = layer.fwd(x, x_t, dec_lens, B, T_dec, ctx)
+            lin = self.mel_linear
+            M = B * T_dec
+            out = K.conv_gemm(_t(x, x_t), lin._w_fwd, M, T_dec, lin.in_features,
+                              lin.out_features, 1, 0, bias=lin.bias)
+            out_t = K.cast_bf16(out) if ctx.copy is not None else None
+            post, _ = self.postnet.fwd(out, out_t, B, T_dec, ctx)
+        out, post = out.view(B, T_dec, -1), post.view(B, T_dec, -1)
+        head = (out, post, p, e, log_d, d_rounded, src_masks, mel_masks, src_lens, mel_len)
+        if speaker_vec is not None:
+            return head
+        return head + (gmm, speaker_emb_s)
+
+    def synthesize_from_speaker_emb(self, speakers, texts, src_lens, max_src_len, mels=None,
+                                    mel_lens=None, max_mel_len=None, p_targets=None,
+                                    e_targets=None, d_targets=None, p_control=1.0, e_control=1.0,
+                                    d_control=1.0, accents=None, speaker_emb=None):
+        """``model/fastspeech2.py:186-303``: the forward with a given speaker embedding (e.g.
+        drawn by ``speaker_gen`` / a mid-attribute GMM) in place of the speaker table;
+        ``speakers`` is unused, as in the reference.  Returns the 10-tuple."""
+        if speaker_emb is None:
+            raise ValueError("speaker_emb is required")
+        if accents is None:
+            raise ValueError("accents are required (transformer/Models.py:101)")
+        if not torch.is_tensor(speaker_emb):
+            speaker_emb = torch.as_tensor(np.asarray(speaker_emb), dtype=torch.float32)
+        dev = self.encoder.position_enc.device
+        return self._forward_infer(None, texts, src_lens, max_src_len, mel_lens, max_mel_len,
+                                   p_targets, e_targets, d_targets, p_control, e_control,
+                                   d_control, accents, speaker_vec=speaker_emb.to(dev))
 
     def speaker_gen(self, speaker_meta, seed=None):
         """``model/fastspeech2.py:176-180``: one embedding drawn from the attribute prior."""

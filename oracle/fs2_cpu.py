@@ -141,7 +141,7 @@ class Encoder(nn.Module):
 
 
 class Decoder(nn.Module):
-    """``transformer/Models.py:115-183`` (training branch: truncate to max_seq_len)."""
+    """``transformer/Models.py:115-183`` (truncate to max_seq_len, except in eval mode)."""
 
     def __init__(self, config):
         super().__init__()
@@ -154,6 +154,13 @@ class Decoder(nn.Module):
             for _ in range(config["transformer"]["decoder_layer"]))
 
     def forward(self, x, pad):
+        if not self.training and x.shape[1] > self.max_seq_len:
+            # Models.py:160-165: eval past max_seq_len, fresh table, no truncation
+            T = x.shape[1]
+            x = x + sinusoid_table(T, x.shape[2])[None, :T]
+            for layer in self.layer_stack:
+                x = layer(x, pad)
+            return x, pad
         T = min(x.shape[1], self.max_seq_len)
         x = x[:, :T] + self.position_enc[:, :T]
         pad = pad[:, :T]
@@ -357,6 +364,23 @@ class FastSpeech2(nn.Module):
         out = self.mel_linear(x)
         post = self.postnet(out) + out
         return (out, post, p, e, log_d, d_r, src_pad, mel_pad, src_lens, mel_lens, gmm, spk)
+
+    def synthesize_from_speaker_emb(self, speakers, texts, src_lens, max_src_len, mels=None,
+                                    mel_lens=None, max_mel_len=None, p_targets=None,
+                                    e_targets=None, d_targets=None, p_control=1.0, e_control=1.0,
+                                    d_control=1.0, accents=None, speaker_emb=None):
+        # model/fastspeech2.py:186-303 (multi_speaker, no JDIT): 10-tuple
+        src_pad = mask_from_lengths(src_lens, max_src_len)
+        mel_pad = mask_from_lengths(mel_lens, max_mel_len) if mel_lens is not None else None
+        x = self.encoder(texts, src_pad, accents)
+        x = x + speaker_emb.unsqueeze(1).expand(-1, max_src_len, -1)
+        x, p, e, log_d, d_r, mel_lens, mel_pad = self.variance_adaptor(
+            x, src_pad, mel_pad, max_mel_len, p_targets, e_targets, d_targets,
+            p_control, e_control, d_control)
+        x, mel_pad = self.decoder(x, mel_pad)
+        out = self.mel_linear(x)
+        post = self.postnet(out) + out
+        return (out, post, p, e, log_d, d_r, src_pad, mel_pad, src_lens, mel_lens)
 
 
 # ---------------------------------------------------------------------------------------

@@ -13,6 +13,9 @@ Fixtures:
   g3_bucket.npz    bucketize KATs and the 255-entry pitch/energy bins
   g4_ops.npz       per-module fwd outputs / input grads / weight-grad checksums
   g5_step_*.npz    3-step training trajectories (losses, eloss, grad norm, lr, output sums)
+  g6_infer.npz     eval-mode forward (synthesize.py / evaluate.py): predicted durations with
+                   controls, teacher-forced eval, synthesize_from_speaker_emb, and a decoder
+                   longer than max_seq_len (fresh position table)
 """
 import importlib
 import os
@@ -223,13 +226,89 @@ def g5(fs2, loss_mod, B, Ts, steps=3, seed=0):
     print("g5", B, Ts, res["s0.losses"], res["s2.losses"])
 
 
+def infer_overrides(model_prefix=""):
+    """Fixture-only weight overrides for the eval-mode cases (applied identically to every
+    implementation under test): a duration-head bias so predicted durations are a few
+    frames per phoneme instead of ~0, and non-trivial PostNet BatchNorm running stats."""
+    rng = np.random.default_rng(6)
+    ov = {model_prefix + "variance_adaptor.duration_predictor.linear_layer.bias":
+          np.array([np.log(4.0)], np.float32)}
+    chans = [512, 512, 512, 512, 80]
+    for i, c in enumerate(chans):
+        ov[f"{model_prefix}postnet.convolutions.{i}.1.running_mean"] = \
+            (0.1 * rng.standard_normal(c)).astype(np.float32)
+        ov[f"{model_prefix}postnet.convolutions.{i}.1.running_var"] = \
+            (0.5 + rng.random(c)).astype(np.float32)
+    return ov
+
+
+def _apply(model, ov):
+    sd = model.state_dict()
+    with torch.no_grad():
+        for k, v in ov.items():
+            sd[k].copy_(torch.from_numpy(v))
+
+
+def g6(fs2, loss_mod):
+    pp, mc, tc, path = PKG.config.load_configs("JVS-VCTK")
+    torch.manual_seed(0)
+    model = fs2.FastSpeech2(pp, mc, path)
+    seeded(model)
+    ov = infer_overrides()
+    _apply(model, ov)
+    model.eval()
+    res = {"ov." + k: v for k, v in ov.items()}
+
+    def record(tag, out):
+        for i, name in enumerate(("out", "post", "p", "e", "log_d", "d_r")):
+            res[f"{tag}.{name}"] = out[i].detach().float().numpy()
+        res[f"{tag}.mel_mask"] = out[7].numpy()
+        res[f"{tag}.mel_lens"] = out[9].numpy()
+
+    b = PKG.data.to_device(PKG.data.syn_batch(3, 16, seed=0), "cpu")
+    with torch.no_grad():
+        # A: synthesize.py -- no targets, unit controls
+        record("A", model(b[2], b[3], b[4], b[5], accents=b[13], speaker_meta=b[12]))
+        # B: controls (energy follows p_control: modules.py:124)
+        record("B", model(b[2], b[3], b[4], b[5], p_control=1.3, e_control=0.7, d_control=1.2,
+                          accents=b[13], speaker_meta=b[12]))
+        # C: evaluate.py -- teacher-forced forward in eval mode, plus the loss 6-tuple
+        out = model(*(b[2:12]), accents=b[13], speaker_meta=b[12])
+        record("C", out)
+        losses = loss_mod.FastSpeech2Loss(pp, mc)(b[:12], out[:-2])
+        res["C.losses"] = np.array([float(l) for l in losses])
+        # D: examples_gen_distri.py -- given speaker embedding, B = 1
+        b1 = PKG.data.to_device(PKG.data.syn_batch(1, 20, seed=5), "cpu")
+        emb = torch.from_numpy(np.random.default_rng(7).standard_normal((1, 256))
+                               .astype(np.float32) * 0.5)
+        res["D.emb"] = emb.numpy()
+        record("D", model.synthesize_from_speaker_emb(None, b1[3], b1[4], b1[5], accents=b1[13],
+                                                      speaker_emb=emb))
+        # E: decoder longer than max_seq_len (eval: fresh position table, no truncation)
+        bl = PKG.data.to_device(PKG.data.syn_batch(1, 128, seed=9), "cpu")
+        model.variance_adaptor.duration_predictor.linear_layer.bias.fill_(float(np.log(9.5)))
+        out = model(bl[2], bl[3], bl[4], bl[5], accents=bl[13], speaker_meta=bl[12])
+        res["E.dur_bias"] = np.array([np.log(9.5)], np.float32)
+        res["E.mel_lens"] = out[9].numpy()
+        res["E.d_r"] = out[5].numpy()
+        res["E.post_probe"] = out[1][:, ::13, ::5].numpy()
+        res["E.post_sum"] = np.array([out[1].double().sum(), out[1].double().abs().sum()])
+        print("g6: mel lens A", res["A.mel_lens"], "B", res["B.mel_lens"], "D",
+              res["D.mel_lens"], "E", res["E.mel_lens"])
+    np.savez_compressed(os.path.join(OUT, "g6_infer.npz"), **res)
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     fs2, loss_mod, mods, layers = import_reference()
     no_dropout()
     torch.set_num_threads(8)
+    if "--only-g6" in sys.argv:
+        g6(fs2, loss_mod)
+        return
     g1_g2_g3(mods)
     g4(fs2, loss_mod, mods, layers)
+    g6(fs2, loss_mod)
     sizes = [(3, 16), (8, 32)] + ([(48, 128)] if "--full" in sys.argv else [])
     for B, Ts in sizes:
         g5(fs2, loss_mod, B, Ts)

@@ -461,3 +461,37 @@ def test_conv_gemm_bf16_padding_tiles():
         finally:
             K.lib.fs2_set_tuning(2, 0)
         assert torch.equal(dw0, dw1) and torch.equal(db0, db1)
+
+
+@pytest.mark.parametrize("act,res", [(True, False), (False, True)])
+def test_batchnorm_eval(act, res):
+    """Eval-mode BatchNorm1d (running statistics, no update) vs F.batch_norm(training=False)."""
+    M, c = 333, 80 if res else 512
+    z = rnd(M, c, seed=11) * 2 - 0.5
+    g, b = 1 + 0.1 * rnd(c, seed=12), 0.1 * rnd(c, seed=13)
+    rm, rv = 0.2 * rnd(c, seed=14), 0.5 + rnd(c, seed=15).abs()
+    rm0, rv0 = rm.clone(), rv.clone()
+    r = rnd(M, c, seed=16) if res else None
+    out, out_t = K.bn_eval_fwd(z, g, b, rm, rv, act, res=r, copy=torch.bfloat16)
+    ref = F.batch_norm(z, rm.clone(), rv.clone(), g, b, training=False, eps=1e-5)
+    if act:
+        ref = torch.tanh(ref)
+    if res:
+        ref = ref + r
+    close(out, ref, 2e-6)
+    close(out_t.float(), ref, 1e-2)
+    assert torch.equal(rm, rm0) and torch.equal(rv, rv0)
+
+
+def test_duration_round_golden():
+    """Inference durations (modules.py:132-135) bit-exact vs the reference (G2) and vs
+    torch on random log-durations, incl. control scaling and the clamp."""
+    g = load_golden("g2_round.npz")
+    got = K.duration_round(torch.from_numpy(g["log_d"]).to(DEV))
+    np.testing.assert_array_equal(got.cpu().numpy(), g["rounded"])
+    x = rnd(4097, scale=1.5, seed=21)
+    for c in (1.0, 1.3, 0.5):
+        want = torch.clamp(torch.round(torch.exp(x) - 1) * c, min=0)
+        got = K.duration_round(x, c)
+        # exp may differ by an ulp between libraries; only exact .5 ties could flip
+        assert (got != want).sum().item() <= 1

@@ -164,3 +164,54 @@ def test_g5_train_trajectory(no_dropout, B, Ts):
         o, po = out[0].detach().double(), out[1].detach().double()
         np.testing.assert_allclose([o.sum(), o.abs().sum(), po.sum(), po.abs().sum()],
                                    g[f"s{s}.out_sum"], rtol=1e-4)
+
+
+def _g6_model(g):
+    m, _ = fs2_cpu.build("JVS-VCTK")
+    sd = m.state_dict()
+    with torch.no_grad():
+        for k in g.files:
+            if k.startswith("ov."):
+                sd[k[3:]].copy_(torch.from_numpy(g[k]))
+    m.eval()
+    return m
+
+
+def _g6_check(g, tag, out, rtol=1e-4):
+    for i, name in enumerate(("out", "post", "p", "e", "log_d")):
+        want = g[f"{tag}.{name}"]
+        got = out[i].detach().numpy()
+        assert got.shape == want.shape, (tag, name, got.shape, want.shape)
+        np.testing.assert_allclose(got, want, rtol=0, atol=rtol * max(np.abs(want).max(), 1e-6),
+                                   err_msg=f"{tag}.{name}")
+    np.testing.assert_array_equal(out[5].numpy(), g[f"{tag}.d_r"])
+    np.testing.assert_array_equal(out[7].numpy(), g[f"{tag}.mel_mask"])
+    np.testing.assert_array_equal(out[9].numpy(), g[f"{tag}.mel_lens"])
+
+
+def test_g6_inference_oracle():
+    """Eval-mode forward of the oracle == the reference's (synthesize / evaluate / given
+    speaker embedding / decoder past max_seq_len)."""
+    g = load_golden("g6_infer.npz")
+    fs2_cpu.DROPOUT["enabled"] = True  # eval mode must switch dropout off by itself
+    m = _g6_model(g)
+    b = PKG.data.to_device(PKG.data.syn_batch(3, 16, seed=0), "cpu")
+    with torch.no_grad():
+        _g6_check(g, "A", m(b[2], b[3], b[4], b[5], accents=b[13], speaker_meta=b[12]))
+        _g6_check(g, "B", m(b[2], b[3], b[4], b[5], p_control=1.3, e_control=0.7, d_control=1.2,
+                            accents=b[13], speaker_meta=b[12]))
+        out = m(*(b[2:12]), accents=b[13], speaker_meta=b[12])
+        _g6_check(g, "C", out)
+        np.testing.assert_allclose(np.array([float(l) for l in fs2_cpu.fs2_loss(b[:12], out[:-2])]),
+                                   g["C.losses"], rtol=1e-5)
+        b1 = PKG.data.to_device(PKG.data.syn_batch(1, 20, seed=5), "cpu")
+        _g6_check(g, "D", m.synthesize_from_speaker_emb(None, b1[3], b1[4], b1[5], accents=b1[13],
+                                                        speaker_emb=torch.from_numpy(g["D.emb"])))
+        bl = PKG.data.to_device(PKG.data.syn_batch(1, 128, seed=9), "cpu")
+        m.variance_adaptor.duration_predictor.linear_layer.bias.fill_(float(g["E.dur_bias"][0]))
+        out = m(bl[2], bl[3], bl[4], bl[5], accents=bl[13], speaker_meta=bl[12])
+    assert out[1].shape[1] > 1000  # the eval-mode branch past max_seq_len ran
+    np.testing.assert_array_equal(out[9].numpy(), g["E.mel_lens"])
+    np.testing.assert_array_equal(out[5].numpy(), g["E.d_r"])
+    np.testing.assert_allclose(out[1][:, ::13, ::5].numpy(), g["E.post_probe"], rtol=0,
+                               atol=1e-4 * np.abs(g["E.post_probe"]).max())

@@ -284,6 +284,40 @@ int fs2_gmm_head_bwd(const float* meta, const float* e, const float* pi, const f
 int fs2_gmm_sample(const float* pi, const float* mu, const float* sigma, int64_t batch, int k,
                    int d, uint64_t seed, uint64_t offset, float* out, int32_t* comp, void* stream);
 
+/* ---------------------------------------------------------------- mid-attribute GMMs
+ * model/distributions.py (off the training step).
+ * Mixtures are (k, d) rows of mu / sd (Normal scale) plus k weights.
+ *
+ * InterpolateGMM (12-77).  fs2_gmm_w2_cost: cost[i*kb+j] = the reference's _w2sq (64-77)
+ * incl. its elementwise-diagonal quirk, ||mu_a-mu_b||^2 + sum(va + vb - 2 sa^3 sb), double.
+ * fs2_ot_emd: exact transport plan (replaces ot.emd, 22: the f32 weights taken as float64,
+ * b rescaled to a's mass), one-thread
+ * transportation simplex; status[0] = iterations or -1 at max_iter.  k <= 16.
+ * fs2_gmm_interpolate (23-62): pi[n] = plan.flat[n] / sum (n = i*kb + j), component
+ * n = j*ka + i: mu = (1-t) mu_a[i] + t mu_b[j], sd = ((1-t) sd_a[i] + t sd_b[j])^2.      */
+int fs2_gmm_w2_cost(const float* mu_a, const float* sd_a, int ka, const float* mu_b,
+                    const float* sd_b, int kb, int d, double* cost, void* stream);
+int fs2_ot_emd(const float* a, const float* b, const double* cost, int ka, int kb,
+               int max_iter, double* plan, int* status, void* stream);
+int fs2_gmm_interpolate(const double* plan, const float* mu_a, const float* sd_a, int ka,
+                        const float* mu_b, const float* sd_b, int kb, int d, double t, float* pi,
+                        float* mu, float* sd, void* stream);
+/* BarycenterGMM (79-192).  m mixtures of k components (one per metadata combination).
+ * fs2_gmm_barycenter_positions: k^m (<= 4096) or -1.  fs2_gmm_barycenter (136-163): mean and
+ * 60-step fixed-point std of every position of product(range(k), repeat=m), fp32 in the
+ * reference's operation order (rate: m floats).  fs2_gmm_bary_mix (165-184): nearest
+ * barycenter of each of the m*k original components, weights rate_i * pi_ij (rate: m
+ * doubles) summed per barycenter in first-use order, normalised; n_used[0] = number of
+ * components written to used / pi_out / mu_out / sd_out (capacity m*k).  m*k <= 64.      */
+int64_t fs2_gmm_barycenter_positions(int m, int k);
+int fs2_gmm_barycenter(const float* mu, const float* sd, int m, int k, int d, const float* rate,
+                       int iters, float* bmean, float* bstd, void* stream);
+int64_t fs2_gmm_bary_mix_ws_bytes(int m, int k);
+int fs2_gmm_bary_mix(const float* pi, const float* mu, const float* sd, int m, int k, int d,
+                     const double* rate, const float* bmean, const float* bstd, int* n_used,
+                     int* used, float* pi_out, float* mu_out, float* sd_out, double* ws,
+                     int64_t ws_bytes, void* stream);
+
 /* ---------------------------------------------------------------- optimiser
  * clip_grad_norm_ + Adam over one flat fp32 parameter buffer (train.py:202,
  * model/optimizer.py:10-51).  fs2_grad_norm writes norm_coef[0] = ||g||_2 and

@@ -506,3 +506,71 @@ def add_i64_(t, value):
     _dev(t)
     lib.fs2_add_i64(ptr(t), t.numel(), int(value), stream())
     return t
+
+
+# ------------------------------------------------------------------ mid-attribute GMMs
+def gmm_w2_cost(mu_a, sd_a, mu_b, sd_b):
+    """(ka, kb) float64 cost of InterpolateGMM._w2sq (distributions.py:64-77)."""
+    _dev(mu_a, sd_a, mu_b, sd_b)
+    ka, d = mu_a.shape
+    kb = mu_b.shape[0]
+    cost = torch.empty(ka, kb, dtype=torch.float64, device=mu_a.device)
+    lib.fs2_gmm_w2_cost(ptr(mu_a), ptr(sd_a), ka, ptr(mu_b), ptr(sd_b), kb, d, ptr(cost), stream())
+    return cost
+
+
+def ot_emd(a, b, cost, max_iter=10000):
+    """Exact OT plan (ot.emd): (plan float64 (ka, kb), status int32[1] = iterations or -1)."""
+    _dev(a, b, cost)
+    ka, kb = cost.shape
+    plan = torch.empty(ka, kb, dtype=torch.float64, device=cost.device)
+    status = torch.empty(1, dtype=torch.int32, device=cost.device)
+    lib.fs2_ot_emd(ptr(a), ptr(b), ptr(cost), ka, kb, int(max_iter), ptr(plan), ptr(status),
+                   stream())
+    return plan, status
+
+
+def gmm_interpolate(plan, mu_a, sd_a, mu_b, sd_b, t):
+    _dev(plan, mu_a, sd_a, mu_b, sd_b)
+    ka, d = mu_a.shape
+    kb = mu_b.shape[0]
+    n = ka * kb
+    pi = torch.empty(n, dtype=torch.float32, device=mu_a.device)
+    mu = torch.empty(n, d, dtype=torch.float32, device=mu_a.device)
+    sd = torch.empty(n, d, dtype=torch.float32, device=mu_a.device)
+    lib.fs2_gmm_interpolate(ptr(plan), ptr(mu_a), ptr(sd_a), ka, ptr(mu_b), ptr(sd_b), kb, d,
+                            float(t), ptr(pi), ptr(mu), ptr(sd), stream())
+    return pi, mu, sd
+
+
+def gmm_barycenter(mu, sd, rate32, iters=60):
+    """Barycenter mean/std of every position of product(range(k), repeat=m)."""
+    _dev(mu, sd, rate32)
+    m, k, d = mu.shape
+    n_pos = lib.fs2_gmm_barycenter_positions(m, k)
+    if n_pos <= 0:
+        raise RuntimeError(f"{k}^{m} barycenter positions exceed the kernel's limit")
+    bm = torch.empty(n_pos, d, dtype=torch.float32, device=mu.device)
+    bs = torch.empty(n_pos, d, dtype=torch.float32, device=mu.device)
+    lib.fs2_gmm_barycenter(ptr(mu), ptr(sd), m, k, d, ptr(rate32), int(iters), ptr(bm), ptr(bs),
+                           stream())
+    return bm, bs
+
+
+def gmm_bary_mix(pi, mu, sd, rate64, bm, bs):
+    """Nearest-barycenter mixture: (n_used int32[1], used, pi, mu, sd) with capacity m*k
+    (rows past n_used are unwritten)."""
+    _dev(pi, mu, sd, rate64, bm, bs)
+    m, k, d = mu.shape
+    dev = mu.device
+    n_used = torch.empty(1, dtype=torch.int32, device=dev)
+    used = torch.empty(m * k, dtype=torch.int32, device=dev)
+    pi_o = torch.empty(m * k, dtype=torch.float32, device=dev)
+    mu_o = torch.empty(m * k, d, dtype=torch.float32, device=dev)
+    sd_o = torch.empty(m * k, d, dtype=torch.float32, device=dev)
+    n = lib.fs2_gmm_bary_mix_ws_bytes(m, k)
+    w = torch.empty(max(n // 8, 1), dtype=torch.float64, device=dev)
+    lib.fs2_gmm_bary_mix(ptr(pi), ptr(mu), ptr(sd), m, k, d, ptr(rate64), ptr(bm), ptr(bs),
+                         ptr(n_used), ptr(used), ptr(pi_o), ptr(mu_o), ptr(sd_o), ptr(w), n,
+                         stream())
+    return n_used, used, pi_o, mu_o, sd_o

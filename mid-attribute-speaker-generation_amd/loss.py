@@ -79,6 +79,26 @@ class GMMMeanLogProbFn(torch.autograd.Function):
         return None, None, None, None
 
 
+class _Mix:
+    def __init__(self, pi):
+        self.probs = pi
+
+
+class _Normal:
+    def __init__(self, mu, sigma):
+        self.loc = self.mean = mu
+        self.scale = self.stddev = sigma
+
+    @property
+    def variance(self):
+        return self.scale.pow(2)
+
+
+class _Comp:
+    def __init__(self, mu, sigma):
+        self.base_dist = _Normal(mu, sigma)
+
+
 class GMMPrior:
     """The reference's ``MixtureSameFamily(Categorical(pi), Independent(Normal(mu, sigma), 1))``
     (``model/fastspeech2.py:336-341``) as device tensors, with HIP log_prob / sample."""
@@ -86,6 +106,17 @@ class GMMPrior:
     def __init__(self, pi, mu, sigma, sigma_pre=None, meta=None, head=None):
         self.pi, self.mu, self.sigma = pi, mu, sigma
         self.sigma_pre, self.meta, self.head = sigma_pre, meta, head
+
+    # torch.distributions-shaped read access used by the reference's callers
+    # (model/distributions.py:14-19, 88-90): .mixture_distribution.probs,
+    # .component_distribution.base_dist.{loc, scale, mean, stddev, variance}
+    @property
+    def mixture_distribution(self):
+        return _Mix(self.pi)
+
+    @property
+    def component_distribution(self):
+        return _Comp(self.mu, self.sigma)
 
     def log_prob(self, e):
         logp, _, _ = K.gmm_logprob(e.detach().contiguous().float(), self.pi, self.mu, self.sigma)

@@ -563,6 +563,7 @@ class SpeakerMetaEncoder(nn.Module):
 
     def __init__(self, preprocess_config, model_config):
         super().__init__()
+        self.metadata_list = preprocess_config["speaker_generation"]["metadata"]
         self.input_dim = cfg.meta_dim(preprocess_config)
         self.K = model_config["speaker_generation"]["GMM_mixtures"]
         self.D = model_config["transformer"]["encoder_hidden"]

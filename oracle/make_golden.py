@@ -16,6 +16,11 @@ Fixtures:
   g6_infer.npz     eval-mode forward (synthesize.py / evaluate.py): predicted durations with
                    controls, teacher-forced eval, synthesize_from_speaker_emb, and a decoder
                    longer than max_seq_len (fresh position table)
+  g7_gmm_ops.npz   mid-attribute GMM operations (model/distributions.py): InterpolateGMM
+                   cost / OT plan / mixture at two rates, BarycenterGMM at two rate vectors.
+                   POT is absent: ``ot.emd`` is stubbed by the same LP solved with scipy's
+                   HiGHS (unique optimum); BarycenterGMM's ``_print`` TypeError is bypassed
+                   by letting ``_barycenter_gaussians`` accept and ignore the kwarg.
 """
 import importlib
 import os
@@ -298,6 +303,64 @@ def g6(fs2, loss_mod):
     np.savez_compressed(os.path.join(OUT, "g6_infer.npz"), **res)
 
 
+def g7(fs2):
+    from oracle import gmm_ops
+    sys.modules["ot"].emd = lambda a, b, M: gmm_ops.emd(a, b, np.asarray(M, np.float64))
+    sys.modules["model"].FastSpeech2 = fs2.FastSpeech2
+    dist = importlib.import_module("model.distributions")
+    orig = dist.BarycenterGMM._barycenter_gaussians
+    dist.BarycenterGMM._barycenter_gaussians = lambda self, _print=True: orig(self)
+    pp, mc, tc, path = PKG.config.load_configs("JVS-VCTK")
+    torch.manual_seed(0)
+    model = fs2.FastSpeech2(pp, mc, path)
+    seeded(model)
+    # spread the per-metadata mixtures apart (fixture-only: seeded heads give near-equal ones)
+    rng = np.random.default_rng(7)
+    ov = {}
+    with torch.no_grad():
+        for name in ("pi_linear.0.weight", "sigma_linear.0.weight", "mu_linear.weight"):
+            p_ = dict(model.speaker_enc.named_parameters())[name]
+            scale = {"pi": 1.5, "sigma": 0.6, "mu": 1.0}[name.split("_")[0]]
+            p_.add_(torch.from_numpy((scale * rng.standard_normal(tuple(p_.shape)))
+                                     .astype(np.float32)))
+            ov["speaker_enc." + name] = p_.detach().numpy().copy()
+    model.eval()
+    res = {"ov." + k: v for k, v in ov.items()}
+
+    def params(g):
+        return (g.mixture_distribution.probs.detach().numpy(),
+                g.component_distribution.base_dist.loc.detach().numpy(),
+                g.component_distribution.base_dist.scale.detach().numpy())
+
+    meta_a = torch.tensor([[1.0, 0.0, 1.0, 0.0]])
+    meta_b = torch.tensor([[0.0, 1.0, 0.0, 1.0]])
+    ga, gb = model.speaker_distribution(meta_a), model.speaker_distribution(meta_b)
+    res["I.meta_a"], res["I.meta_b"] = meta_a.numpy(), meta_b.numpy()
+    for tag, g in (("a", ga), ("b", gb)):
+        res[f"I.pi_{tag}"], res[f"I.mu_{tag}"], res[f"I.sd_{tag}"] = params(g)
+    ig = dist.InterpolateGMM(ga, gb)
+    res["I.cost"] = np.array(ig.ot_Cost, np.float64)
+    res["I.plan"] = np.asarray(ig.ot_Matrix, np.float64)
+    for t in (0.5, 0.3):
+        if t != 0.5:
+            ig.interpolate_rate(t)
+        pi, mu, sd = params(ig)
+        res[f"I.t{t}.pi"] = pi.astype(np.float64)
+        res[f"I.t{t}.mu"] = mu.astype(np.float32)
+        res[f"I.t{t}.sd"] = sd.astype(np.float64)
+    bg = dist.BarycenterGMM(model)
+    for tag, rate in (("u", None), ("w", [0.5, 0.25, 0.125, 0.125])):
+        if rate is not None:
+            bg.barycenter_rate(rate, _print=False)
+        pi, mu, sd = params(bg)
+        res[f"G.{tag}.pi"], res[f"G.{tag}.mu"], res[f"G.{tag}.sd"] = pi, mu, sd
+        res[f"G.{tag}.rate"] = np.array(bg.rate, np.float64)
+    res["G.metas"] = np.stack([m.numpy()[0] for m in bg.original_distri.keys()])
+    print("g7: plan", res["I.plan"].round(4).tolist(), "barycenter comps",
+          res["G.u.pi"].shape, res["G.w.pi"].shape)
+    np.savez_compressed(os.path.join(OUT, "g7_gmm_ops.npz"), **res)
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     fs2, loss_mod, mods, layers = import_reference()
@@ -306,9 +369,13 @@ def main():
     if "--only-g6" in sys.argv:
         g6(fs2, loss_mod)
         return
+    if "--only-g7" in sys.argv:
+        g7(fs2)
+        return
     g1_g2_g3(mods)
     g4(fs2, loss_mod, mods, layers)
     g6(fs2, loss_mod)
+    g7(fs2)
     sizes = [(3, 16), (8, 32)] + ([(48, 128)] if "--full" in sys.argv else [])
     for B, Ts in sizes:
         g5(fs2, loss_mod, B, Ts)

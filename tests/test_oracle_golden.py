@@ -215,3 +215,43 @@ def test_g6_inference_oracle():
     np.testing.assert_array_equal(out[5].numpy(), g["E.d_r"])
     np.testing.assert_allclose(out[1][:, ::13, ::5].numpy(), g["E.post_probe"], rtol=0,
                                atol=1e-4 * np.abs(g["E.post_probe"]).max())
+
+
+def test_g7_interpolate_oracle():
+    """InterpolateGMM (distributions.py:12-77): quirk cost, OT plan, mixture at t=0.5/0.3."""
+    from oracle import gmm_ops
+    g = load_golden("g7_gmm_ops.npz")
+    a = [g[f"I.{n}_a"][0] for n in ("pi", "mu", "sd")]
+    b = [g[f"I.{n}_b"][0] for n in ("pi", "mu", "sd")]
+    cost = gmm_ops.interp_cost(a[1], a[2], b[1], b[2])
+    np.testing.assert_allclose(cost, g["I.cost"], rtol=1e-5)
+    plan = gmm_ops.emd(a[0], b[0], cost)
+    np.testing.assert_allclose(plan, g["I.plan"], rtol=0, atol=1e-9)
+    for t in (0.5, 0.3):
+        pi, mu, sd = gmm_ops.interp_mixture(plan, a[1], a[2], b[1], b[2], t)
+        np.testing.assert_allclose(pi, g[f"I.t{t}.pi"][0], rtol=1e-6)
+        np.testing.assert_array_equal(mu, g[f"I.t{t}.mu"][0])
+        np.testing.assert_allclose(sd, g[f"I.t{t}.sd"][0], rtol=1e-6)
+
+
+def test_g7_barycenter_oracle():
+    """BarycenterGMM (distributions.py:79-192): barycenters bit-exact (fp32, same op order),
+    nearest-barycenter weights, for the uniform and a weighted rate vector."""
+    from oracle import gmm_ops
+    g = load_golden("g7_gmm_ops.npz")
+    pp, _, _, _ = PKG.config.load_configs("JVS-VCTK")
+    metas = gmm_ops.meta_product(pp["speaker_generation"]["metadata"])
+    np.testing.assert_array_equal(metas, g["G.metas"])
+    m, _ = fs2_cpu.build("JVS-VCTK")
+    sd = m.state_dict()
+    with torch.no_grad():
+        for k in g.files:
+            if k.startswith("ov."):
+                sd[k[3:]].copy_(torch.from_numpy(g[k]))
+        gmm = m.speaker_enc(torch.from_numpy(metas))
+    pi, mu, sig = (gmm.pi.numpy(), gmm.mu.numpy(), gmm.sigma.numpy())
+    for tag in ("u", "w"):
+        used, p, bm, bs = gmm_ops.barycenter_mixture(pi, mu, sig, g[f"G.{tag}.rate"])
+        np.testing.assert_allclose(p, g[f"G.{tag}.pi"][0], rtol=1e-6)
+        np.testing.assert_allclose(bm, g[f"G.{tag}.mu"][0], rtol=0, atol=1e-6)
+        np.testing.assert_allclose(bs, g[f"G.{tag}.sd"][0], rtol=1e-6)

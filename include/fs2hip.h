@@ -86,10 +86,12 @@ int fs2_weight_prep_batch(int dtype, const int64_t* jobs, int n_jobs, int64_t n_
  *   FS2_TUNE_WGRAD_SPLITS  weight-gradient row splits (1..64)
  *   FS2_TUNE_LEGACY_GEMM   1 = the register-staged bf16 kernels of round 1
  *   FS2_TUNE_NT_GROUP      fwd/dX n-tiles per L2 tile group
+ *   FS2_TUNE_NT_HALO       fwd/dX Conv1d (taps > 1) halo kernel: 0 = where it applies
+ *                          (default), -1 = off (tap-major kernel), 2 = force 128-wide tiles
  * Process-wide; query workspace sizes after setting.                                 */
 enum { FS2_TUNE_GEMM_STAGES = 0, FS2_TUNE_WGRAD_STAGES = 1, FS2_TUNE_WGRAD_TILE = 2,
        FS2_TUNE_WGRAD_SPLITS = 3, FS2_TUNE_LEGACY_GEMM = 4, FS2_TUNE_NT_GROUP = 5,
-       FS2_TUNE_COUNT = 6 };
+       FS2_TUNE_NT_HALO = 6, FS2_TUNE_COUNT = 7 };
 int fs2_set_tuning(int knob, int value);
 
 /* Weight (and optionally bias) gradient, accumulated into the fp32 master-gradient layout:

@@ -112,6 +112,115 @@ FS2_DEV void kloop(int nk, Issue&& issue, Compute&& compute) {
   }
 }
 
+// Epilogue through LDS, one half (wm) at a time: bias, aux add, ReLU / ReLU-mask, bf16 cast
+// on 8-element row vectors (16-B / 32-B coalesced stores).  Shared by both NT kernels.
+template <int BM, int BN>
+FS2_DEV void nt_epilogue(const GldsArgs& a, f32x4 (&acc)[BM / 32][BN / 32], u16* smem, int64_t m0,
+                         int n0, bool skip, int tid, int wm, int wn, int g, int r16) {
+  constexpr int MI = BM / 32, NI = BN / 32;
+  constexpr int EPI_LD = BN + 4;
+  float* Cs = reinterpret_cast<float*>(smem);
+  const bool out_bf16 = a.flags & FS2_EPI_OUT_BF16, aux_bf16 = a.flags & FS2_EPI_AUX_BF16;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (wm == h) {
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            Cs[(i * 16 + 4 * g + r) * EPI_LD + wn * (BN / 2) + j * 16 + r16] = acc[i][j][r];
+    }
+    __syncthreads();
+    constexpr int TPR = BN / 8;           // threads per row
+    constexpr int RPP = 256 / TPR;        // rows per pass
+    const int cc = (tid % TPR) * 8;
+    const int n = n0 + cc;
+#pragma unroll
+    for (int p = 0; p < (BM / 2) / RPP; ++p) {
+      const int rr = p * RPP + tid / TPR;
+      const int64_t m = m0 + h * (BM / 2) + rr;
+      if (m >= a.M || n >= a.N) continue;
+      float v[8];
+      const f32x4 lo = *reinterpret_cast<const f32x4*>(Cs + rr * EPI_LD + cc);
+      const f32x4 hi = *reinterpret_cast<const f32x4*>(Cs + rr * EPI_LD + cc + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = lo[e];
+        v[e + 4] = hi[e];
+      }
+      if (a.vec) {
+        if ((a.flags & FS2_EPI_BIAS) && !skip) {
+          const f32x4 b0 = *reinterpret_cast<const f32x4*>(a.bias + n);
+          const f32x4 b1 = *reinterpret_cast<const f32x4*>(a.bias + n + 4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[e] += b0[e];
+            v[e + 4] += b1[e];
+          }
+        }
+        float av[8];
+        if (a.flags & (FS2_EPI_ADD_AUX | FS2_EPI_RELU_MASK_AUX)) {
+          if (aux_bf16) {
+            const uint4 raw = *reinterpret_cast<const uint4*>((const u16*)a.aux + m * a.ld_aux + n);
+            const uint32_t wv[4] = {raw.x, raw.y, raw.z, raw.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              av[2 * e] = __uint_as_float(wv[e] << 16);
+              av[2 * e + 1] = __uint_as_float(wv[e] & 0xffff0000u);
+            }
+          } else {
+            const float* ap = (const float*)a.aux + m * a.ld_aux + n;
+            const f32x4 a0 = *reinterpret_cast<const f32x4*>(ap);
+            const f32x4 a1 = *reinterpret_cast<const f32x4*>(ap + 4);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              av[e] = a0[e];
+              av[e + 4] = a1[e];
+            }
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          if (a.flags & FS2_EPI_ADD_AUX) v[e] += av[e];
+          if (a.flags & FS2_EPI_RELU) v[e] = fmaxf(v[e], 0.f);
+          if (a.flags & FS2_EPI_RELU_MASK_AUX) v[e] = av[e] > 0.f ? v[e] : 0.f;
+        }
+        if (out_bf16) {
+          uint4 o;
+          o.x = (uint32_t)fbv(v[0]) | ((uint32_t)fbv(v[1]) << 16);
+          o.y = (uint32_t)fbv(v[2]) | ((uint32_t)fbv(v[3]) << 16);
+          o.z = (uint32_t)fbv(v[4]) | ((uint32_t)fbv(v[5]) << 16);
+          o.w = (uint32_t)fbv(v[6]) | ((uint32_t)fbv(v[7]) << 16);
+          *reinterpret_cast<uint4*>((u16*)a.y + m * a.ldy + n) = o;
+        } else {
+          float* yp = (float*)a.y + m * a.ldy + n;
+          *reinterpret_cast<f32x4*>(yp) = f32x4{v[0], v[1], v[2], v[3]};
+          *reinterpret_cast<f32x4*>(yp + 4) = f32x4{v[4], v[5], v[6], v[7]};
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          if (n + e >= a.N) break;
+          float x = v[e];
+          if ((a.flags & FS2_EPI_BIAS) && !skip) x += a.bias[n + e];
+          float av = 0.f;
+          if (a.flags & (FS2_EPI_ADD_AUX | FS2_EPI_RELU_MASK_AUX))
+            av = aux_bf16 ? bfv(((const u16*)a.aux)[m * a.ld_aux + n + e])
+                          : ((const float*)a.aux)[m * a.ld_aux + n + e];
+          if (a.flags & FS2_EPI_ADD_AUX) x += av;
+          if (a.flags & FS2_EPI_RELU) x = fmaxf(x, 0.f);
+          if (a.flags & FS2_EPI_RELU_MASK_AUX) x = av > 0.f ? x : 0.f;
+          if (out_bf16) ((u16*)a.y)[m * a.ldy + n + e] = fbv(x);
+          else ((float*)a.y)[m * a.ldy + n + e] = x;
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
 template <int BM, int BN, int STAGES, bool TAPALIGNED>
 __global__ __launch_bounds__(256) void conv_gemm_nt_glds(GldsArgs a) {
   constexpr int BK = 64;
@@ -239,107 +348,119 @@ __global__ __launch_bounds__(256) void conv_gemm_nt_glds(GldsArgs a) {
 
   if (!skip) kloop<STAGES, AW + BW>(nk, issue, compute);
 
-  // ---- epilogue through LDS, one half (wm) at a time
-  float* Cs = reinterpret_cast<float*>(smem);
-  const bool out_bf16 = a.flags & FS2_EPI_OUT_BF16, aux_bf16 = a.flags & FS2_EPI_AUX_BF16;
+  nt_epilogue<BM, BN>(a, acc, smem, m0, n0, skip, tid, wm, wn, g, r16);
+}
+
+// ------------------------------------------------------------------------ halo variant
+// Conv1d with taps > 1, Cin % 64 == 0 and T % BM == 0 (every row tile lies inside one
+// utterance).  The reduction runs channel-block-major: for each 64-channel block the
+// BM + taps - 1 input rows of the tile and its tap halo (zero outside the utterance) are
+// staged in LDS ONCE, and tap j reads them at row offset j -- only the weight tile is
+// re-staged per tap.  Against the tap-major kernel above this removes (taps-1)/taps of the
+// A-operand LDS-DMA traffic: the k=9 FFN conv moves 18 KB instead of 32 KB per 64-deep step
+// of a 128 x 128 tile, and that traffic, not the MFMA, bounds the tap-major kernel
+// (per-CU vector-memory rate; profiles/).  LDS rows are swizzled chunk c -> c ^ (row & 7),
+// which keeps the 16-row fragment reads conflict-free at every row offset.
+template <int BM, int BN>
+__global__ __launch_bounds__(256, 4) void conv_gemm_halo(GldsArgs a) {
+  constexpr int BK = 64;
+  constexpr int MI = BM / 32, NI = BN / 32;
+  constexpr int HMAX = BM + 16;                     // halo rows allocated (taps <= 17)
+  constexpr int QMAX = (HMAX / 8 + 3) / 4;          // 8-row halo pieces per wave
+  constexpr int BW = BN / 32;                       // weight pieces per wave
+  constexpr int A_E = HMAX * BK, B_E = BN * BK;
+  constexpr int EPI_E = (BM / 2) * (BN + 4) * 2;
+  constexpr int SMEM_E = A_E + B_E > EPI_E ? A_E + B_E : EPI_E;
+  __shared__ __attribute__((aligned(1024))) u16 smem[SMEM_E];
+  u16* As = smem;
+  u16* Bs = smem + A_E;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int g = lane >> 4, r16 = lane & 15;
+
+  const int nwg = a.tiles_m * a.tiles_n;
+  const int orig = blockIdx.x, xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int gfull = a.tiles_m * a.group;
+  const int ng = wg / gfull, rem = wg - ng * gfull;
+  const int gsz = a.tiles_n - ng * a.group < a.group ? a.tiles_n - ng * a.group : a.group;
+  const int tm = rem / gsz, tn = ng * a.group + (rem - (rem / gsz) * gsz);
+  const int64_t m0 = (int64_t)tm * BM;
+  const int n0 = tn * BN;
+  const bool skip = a.lens && rows_all_padding(a.lens, a.T, m0, m0 + BM < a.M ? m0 + BM : a.M);
+
+  const int lrow = lane >> 3;
+  const u16* zero = reinterpret_cast<const u16*>(g_zero_line);
+  const int HR = BM + a.taps - 1, HP = (HR + 7) / 8;
+  const int64_t u0 = (m0 / a.T) * a.T, u1 = u0 + a.T < a.M ? u0 + a.T : a.M;
+  // halo piece p = wave + 4 q: rows h = 8 p + lrow, global row m0 - pad + h
+  const u16* h_src[QMAX];
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    if (wm == h) {
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < NI; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            Cs[(i * 16 + 4 * g + r) * EPI_LD + wn * (BN / 2) + j * 16 + r16] = acc[i][j][r];
-    }
-    __syncthreads();
-    constexpr int TPR = BN / 8;           // threads per row
-    constexpr int RPP = 256 / TPR;        // rows per pass
-    const int cc = (tid % TPR) * 8;
-    const int n = n0 + cc;
-#pragma unroll
-    for (int p = 0; p < (BM / 2) / RPP; ++p) {
-      const int rr = p * RPP + tid / TPR;
-      const int64_t m = m0 + h * (BM / 2) + rr;
-      if (m >= a.M || n >= a.N) continue;
-      float v[8];
-      const f32x4 lo = *reinterpret_cast<const f32x4*>(Cs + rr * EPI_LD + cc);
-      const f32x4 hi = *reinterpret_cast<const f32x4*>(Cs + rr * EPI_LD + cc + 4);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        v[e] = lo[e];
-        v[e + 4] = hi[e];
-      }
-      if (a.vec) {
-        if ((a.flags & FS2_EPI_BIAS) && !skip) {
-          const f32x4 b0 = *reinterpret_cast<const f32x4*>(a.bias + n);
-          const f32x4 b1 = *reinterpret_cast<const f32x4*>(a.bias + n + 4);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            v[e] += b0[e];
-            v[e + 4] += b1[e];
-          }
-        }
-        float av[8];
-        if (a.flags & (FS2_EPI_ADD_AUX | FS2_EPI_RELU_MASK_AUX)) {
-          if (aux_bf16) {
-            const uint4 raw = *reinterpret_cast<const uint4*>((const u16*)a.aux + m * a.ld_aux + n);
-            const uint32_t wv[4] = {raw.x, raw.y, raw.z, raw.w};
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              av[2 * e] = __uint_as_float(wv[e] << 16);
-              av[2 * e + 1] = __uint_as_float(wv[e] & 0xffff0000u);
-            }
-          } else {
-            const float* ap = (const float*)a.aux + m * a.ld_aux + n;
-            const f32x4 a0 = *reinterpret_cast<const f32x4*>(ap);
-            const f32x4 a1 = *reinterpret_cast<const f32x4*>(ap + 4);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              av[e] = a0[e];
-              av[e + 4] = a1[e];
-            }
-          }
-        }
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          if (a.flags & FS2_EPI_ADD_AUX) v[e] += av[e];
-          if (a.flags & FS2_EPI_RELU) v[e] = fmaxf(v[e], 0.f);
-          if (a.flags & FS2_EPI_RELU_MASK_AUX) v[e] = av[e] > 0.f ? v[e] : 0.f;
-        }
-        if (out_bf16) {
-          uint4 o;
-          o.x = (uint32_t)fbv(v[0]) | ((uint32_t)fbv(v[1]) << 16);
-          o.y = (uint32_t)fbv(v[2]) | ((uint32_t)fbv(v[3]) << 16);
-          o.z = (uint32_t)fbv(v[4]) | ((uint32_t)fbv(v[5]) << 16);
-          o.w = (uint32_t)fbv(v[6]) | ((uint32_t)fbv(v[7]) << 16);
-          *reinterpret_cast<uint4*>((u16*)a.y + m * a.ldy + n) = o;
-        } else {
-          float* yp = (float*)a.y + m * a.ldy + n;
-          *reinterpret_cast<f32x4*>(yp) = f32x4{v[0], v[1], v[2], v[3]};
-          *reinterpret_cast<f32x4*>(yp + 4) = f32x4{v[4], v[5], v[6], v[7]};
-        }
-      } else {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          if (n + e >= a.N) break;
-          float x = v[e];
-          if ((a.flags & FS2_EPI_BIAS) && !skip) x += a.bias[n + e];
-          float av = 0.f;
-          if (a.flags & (FS2_EPI_ADD_AUX | FS2_EPI_RELU_MASK_AUX))
-            av = aux_bf16 ? bfv(((const u16*)a.aux)[m * a.ld_aux + n + e])
-                          : ((const float*)a.aux)[m * a.ld_aux + n + e];
-          if (a.flags & FS2_EPI_ADD_AUX) x += av;
-          if (a.flags & FS2_EPI_RELU) x = fmaxf(x, 0.f);
-          if (a.flags & FS2_EPI_RELU_MASK_AUX) x = av > 0.f ? x : 0.f;
-          if (out_bf16) ((u16*)a.y)[m * a.ldy + n + e] = fbv(x);
-          else ((float*)a.y)[m * a.ldy + n + e] = x;
-        }
-      }
-    }
-    __syncthreads();
+  for (int q = 0; q < QMAX; ++q) {
+    const int h = (wave + 4 * q) * 8 + lrow;
+    const int64_t gr = m0 - a.pad + h;
+    const int lc = (lane & 7) ^ (h & 7);
+    h_src[q] = (gr >= u0 && gr < u1) ? a.x + gr * a.ldx + lc * 8 : nullptr;
   }
+  const u16* b_src[BW];
+#pragma unroll
+  for (int i = 0; i < BW; ++i) {
+    const int R = (wave * BW + i) * 8 + lrow;
+    const int n = n0 + R;
+    b_src[i] = n < a.N ? a.w + (int64_t)n * a.K + ((lane & 7) ^ (R & 7)) * 8 : nullptr;
+  }
+
+  f32x4 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int a_row = wm * (BM / 2) + r16;
+  const int b_row = wn * (BN / 2) + r16;
+  const int b_off[2] = {b_row * BK + ((0 + g) ^ (b_row & 7)) * 8, b_row * BK + ((4 + g) ^ (b_row & 7)) * 8};
+  if (!skip) {
+    const int ncb = a.Cin / BK;
+    for (int cb = 0; cb < ncb; ++cb) {
+      for (int j = 0; j < a.taps; ++j) {
+        if (j == 0) {
+#pragma unroll
+          for (int q = 0; q < QMAX; ++q) {
+            const int pc = wave + 4 * q;
+            if (pc < HP) glds16(h_src[q] ? h_src[q] + cb * BK : zero, As + pc * 8 * BK);
+          }
+        }
+        const int64_t k0 = (int64_t)j * a.Cin + cb * BK;
+#pragma unroll
+        for (int i = 0; i < BW; ++i)
+          glds16(b_src[i] ? b_src[i] + k0 : zero, Bs + (wave * BW + i) * 8 * BK);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        // fragment rows differ by multiples of 16, so one swizzle serves all of them
+        const int ha = a_row + j, sa = ha & 7;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          bf16x8g fa[MI], fb[NI];
+          const u16* pa = As + ha * BK + ((ks * 4 + g) ^ sa) * 8;
+          const u16* pb = Bs + b_off[ks];
+#pragma unroll
+          for (int i = 0; i < MI; ++i) fa[i] = *reinterpret_cast<const bf16x8g*>(pa + i * 16 * BK);
+#pragma unroll
+          for (int jj = 0; jj < NI; ++jj) fb[jj] = *reinterpret_cast<const bf16x8g*>(pb + jj * 16 * BK);
+#pragma unroll
+          for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int jj = 0; jj < NI; ++jj)
+              acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[jj], acc[i][jj], 0, 0, 0);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+      }
+    }
+  }
+  nt_epilogue<BM, BN>(a, acc, smem, m0, n0, skip, tid, wm, wn, g, r16);
 }
 
 // ------------------------------------------------------------------------ weight gradient
@@ -717,7 +838,20 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
     case 4: launch_nt<BM_, BN_, 4>(a, tapaligned, st); break;             \
     default: launch_nt<BM_, BN_, 1>(a, tapaligned, st);                   \
   }
-  if (big >= 512) {
+  // halo kernel (tile sizes as the tap-major choice below: 128x128 / 128x64 / 64x64 by grid;
+  // FS2_TUNE_NT_HALO = 2 forces 128 x 128).  Every row tile must lie inside one utterance.
+  const bool halo_wide = big >= 512 || g_tune[FS2_TUNE_NT_HALO] == 2;
+  const int halo_bm = halo_wide || big >= 128 ? 128 : 64;
+  if (taps > 1 && taps <= 17 && tapaligned && seq_len % halo_bm == 0 &&
+      g_tune[FS2_TUNE_NT_HALO] >= 0) {
+    a.tiles_m = (int)((rows + halo_bm - 1) / halo_bm);
+    a.tiles_n = (int)((c_out + (halo_wide ? 127 : 63)) / (halo_wide ? 128 : 64));
+    a.group = a.tiles_n;
+    const unsigned grid = (unsigned)(a.tiles_m * a.tiles_n);
+    if (halo_wide) conv_gemm_halo<128, 128><<<grid, 256, 0, st>>>(a);
+    else if (halo_bm == 128) conv_gemm_halo<128, 64><<<grid, 256, 0, st>>>(a);
+    else conv_gemm_halo<64, 64><<<grid, 256, 0, st>>>(a);
+  } else if (big >= 512) {
     a.tiles_m = (int)((rows + 127) / 128);
     a.tiles_n = (int)((c_out + 127) / 128);
     const int stages = tune ? tune : 1;

@@ -5,17 +5,16 @@
 Groups dispatches by (kernel name, grid size) -- one template instantiation serves several
 GEMM shapes, so the --stats summary averages unlike launches -- and prints total ms/step,
 launches/step and the average duration of each group.  The line tagged ROOFLINE is the
-launch set bench.py's `roofline` times with HIP events: conv_gemm_nt_glds<128,128,...> with
-1,536 workgroups is the decoder FFN Conv1d 256->1024 forward (k=9, K = 2,304) and the data
-gradient of its k=1 partner w_2 (same M x N, K = 256) -- the same grid, so the group is split
-at the widest gap of its sorted durations (the two clusters are ~7x apart) and the upper
-cluster is the k=9 forward.
+launch set bench.py's `roofline` times with HIP events: conv_gemm_halo<128,128> with 1,536
+workgroups is the decoder FFN Conv1d 256->1024 forward (k=9, K = 2,304), the only launch of
+that kernel and grid in the step (the earlier tap-major kernel shared its grid with the k=1
+data gradient of w_2, hence the widest-gap split below, kept for traces of that kernel).
 """
 import csv
 import sys
 from collections import defaultdict
 
-ROOF_NAME, ROOF_WGS = "conv_gemm_nt_glds<128, 128", 1536
+ROOF_NAME, ROOF_WGS = "conv_gemm_halo<128, 128>", 1536
 
 
 def main():

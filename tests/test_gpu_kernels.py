@@ -495,3 +495,44 @@ def test_duration_round_golden():
         got = K.duration_round(x, c)
         # exp may differ by an ulp between libraries; only exact .5 ties could flip
         assert (got != want).sum().item() <= 1
+
+
+@pytest.mark.parametrize("B,T,cin,cout,k", [(48, 128, 256, 1024, 9), (6, 512, 1024, 256, 9),
+                                            (4, 256, 512, 512, 5), (2, 64, 256, 256, 3),
+                                            (3, 128, 512, 80, 5), (8, 64, 1024, 256, 9)])
+def test_conv_gemm_bf16_halo(B, T, cin, cout, k):
+    """The channel-block-major halo kernel (Conv1d taps > 1, T a tile multiple) against fp32
+    math on the same bf16 data and against the tap-major kernel, at every tile width
+    (auto, forced 128-wide), with and without the all-padding tile skip."""
+    pad = (k - 1) // 2
+    x = bf(rnd(B * T, cin, seed=41))
+    w = bf(rnd(cout, cin, k, scale=1 / math.sqrt(cin * k), seed=42)).float()
+    b = rnd(cout, seed=43)
+    wf = torch.empty(cout * cin * k, device=DEV, dtype=torch.bfloat16)
+    wb = torch.empty(cout * cin * k, device=DEV, dtype=torch.bfloat16)
+    K.weight_prep(w, cout, cin, k, wf, wb)
+    ref = ref_conv(x.float(), w, b, B, T, pad)
+    lens = torch.tensor([T - (7 * u) % T for u in range(B)], device=DEV)
+    lens[-1] = 1
+    try:
+        K.lib.fs2_set_tuning(6, -1)  # FS2_TUNE_NT_HALO off: tap-major kernel
+        y_tm = K.conv_gemm(x, wf, B * T, T, cin, cout, k, pad, bias=b)
+        for mode in (0, 2):
+            K.lib.fs2_set_tuning(6, mode)
+            y = K.conv_gemm(x, wf, B * T, T, cin, cout, k, pad, bias=b)
+            close(y, ref, 1e-5)
+            close(y, y_tm, 1e-5)
+            yl = K.conv_gemm(x, wf, B * T, T, cin, cout, k, pad, bias=b, lens=lens)
+            keep = (yl != 0).any(1)  # rows of skipped (all-padding) tiles are zero
+            valid = (torch.arange(T, device=DEV)[None] < lens[:, None]).reshape(-1)
+            assert bool(keep[valid].all())
+            assert torch.equal(yl[keep], y[keep])
+            if cout % 8 == 0:
+                dy = bf(rnd(B * T, cout, seed=44))
+                xr, wr = x.float().clone().requires_grad_(), w.clone().requires_grad_()
+                ref_conv(xr, wr, b, B, T, pad).backward(dy.float())
+                aux = rnd(B * T, cin, seed=45)
+                dx = K.conv_gemm(dy, wb, B * T, T, cout, cin, k, pad, flags=K.EPI_ADD_AUX, aux=aux)
+                close(dx, xr.grad + aux, 1e-5)
+    finally:
+        K.lib.fs2_set_tuning(6, 0)

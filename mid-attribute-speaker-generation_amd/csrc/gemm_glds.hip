@@ -361,8 +361,8 @@ __global__ __launch_bounds__(256) void conv_gemm_nt_glds(GldsArgs a) {
 // of a 128 x 128 tile, and that traffic, not the MFMA, bounds the tap-major kernel
 // (per-CU vector-memory rate; profiles/).  LDS rows are swizzled chunk c -> c ^ (row & 7),
 // which keeps the 16-row fragment reads conflict-free at every row offset.
-template <int BM, int BN>
-__global__ __launch_bounds__(256, 4) void conv_gemm_halo(GldsArgs a) {
+template <int BM, int BN, int BST>
+__global__ __launch_bounds__(256, BST == 1 ? 4 : 3) void conv_gemm_halo(GldsArgs a) {
   constexpr int BK = 64;
   constexpr int MI = BM / 32, NI = BN / 32;
   constexpr int HMAX = BM + 16;                     // halo rows allocated (taps <= 17)
@@ -370,7 +370,7 @@ __global__ __launch_bounds__(256, 4) void conv_gemm_halo(GldsArgs a) {
   constexpr int BW = BN / 32;                       // weight pieces per wave
   constexpr int A_E = HMAX * BK, B_E = BN * BK;
   constexpr int EPI_E = (BM / 2) * (BN + 4) * 2;
-  constexpr int SMEM_E = A_E + B_E > EPI_E ? A_E + B_E : EPI_E;
+  constexpr int SMEM_E = A_E + BST * B_E > EPI_E ? A_E + BST * B_E : EPI_E;
   __shared__ __attribute__((aligned(1024))) u16 smem[SMEM_E];
   u16* As = smem;
   u16* Bs = smem + A_E;
@@ -421,43 +421,78 @@ __global__ __launch_bounds__(256, 4) void conv_gemm_halo(GldsArgs a) {
   const int a_row = wm * (BM / 2) + r16;
   const int b_row = wn * (BN / 2) + r16;
   const int b_off[2] = {b_row * BK + ((0 + g) ^ (b_row & 7)) * 8, b_row * BK + ((4 + g) ^ (b_row & 7)) * 8};
+  // step s = cb * taps + j: weight tile (tap j, channel block cb) into ring slot s % BST; the
+  // halo of channel block cb is staged at j == 0
+  auto issue_a = [&](int cb) {
+#pragma unroll
+    for (int q = 0; q < QMAX; ++q) {
+      const int pc = wave + 4 * q;
+      if (pc < HP) glds16(h_src[q] ? h_src[q] + cb * BK : zero, As + pc * 8 * BK);
+    }
+  };
+  auto issue_b = [&](int cb, int j, int slot) {
+    const int64_t k0 = (int64_t)j * a.Cin + cb * BK;
+#pragma unroll
+    for (int i = 0; i < BW; ++i)
+      glds16(b_src[i] ? b_src[i] + k0 : zero, Bs + slot * B_E + (wave * BW + i) * 8 * BK);
+  };
+  auto compute = [&](int j, int slot) {
+    // fragment rows differ by multiples of 16, so one swizzle serves all of them
+    const int ha = a_row + j, sa = ha & 7;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8g fa[MI], fb[NI];
+      const u16* pa = As + ha * BK + ((ks * 4 + g) ^ sa) * 8;
+      const u16* pb = Bs + slot * B_E + b_off[ks];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) fa[i] = *reinterpret_cast<const bf16x8g*>(pa + i * 16 * BK);
+#pragma unroll
+      for (int jj = 0; jj < NI; ++jj) fb[jj] = *reinterpret_cast<const bf16x8g*>(pb + jj * 16 * BK);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int jj = 0; jj < NI; ++jj)
+          acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[jj], acc[i][jj], 0, 0, 0);
+    }
+  };
   if (!skip) {
     const int ncb = a.Cin / BK;
-    for (int cb = 0; cb < ncb; ++cb) {
-      for (int j = 0; j < a.taps; ++j) {
-        if (j == 0) {
-#pragma unroll
-          for (int q = 0; q < QMAX; ++q) {
-            const int pc = wave + 4 * q;
-            if (pc < HP) glds16(h_src[q] ? h_src[q] + cb * BK : zero, As + pc * 8 * BK);
-          }
+    if constexpr (BST == 1) {
+      for (int cb = 0; cb < ncb; ++cb) {
+        for (int j = 0; j < a.taps; ++j) {
+          if (j == 0) issue_a(cb);
+          issue_b(cb, j, 0);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __builtin_amdgcn_s_barrier();
+          compute(j, 0);
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_s_barrier();
         }
-        const int64_t k0 = (int64_t)j * a.Cin + cb * BK;
-#pragma unroll
-        for (int i = 0; i < BW; ++i)
-          glds16(b_src[i] ? b_src[i] + k0 : zero, Bs + (wave * BW + i) * 8 * BK);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        // fragment rows differ by multiples of 16, so one swizzle serves all of them
-        const int ha = a_row + j, sa = ha & 7;
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-          bf16x8g fa[MI], fb[NI];
-          const u16* pa = As + ha * BK + ((ks * 4 + g) ^ sa) * 8;
-          const u16* pb = Bs + b_off[ks];
-#pragma unroll
-          for (int i = 0; i < MI; ++i) fa[i] = *reinterpret_cast<const bf16x8g*>(pa + i * 16 * BK);
-#pragma unroll
-          for (int jj = 0; jj < NI; ++jj) fb[jj] = *reinterpret_cast<const bf16x8g*>(pb + jj * 16 * BK);
-#pragma unroll
-          for (int i = 0; i < MI; ++i)
-#pragma unroll
-            for (int jj = 0; jj < NI; ++jj)
-              acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[jj], acc[i][jj], 0, 0, 0);
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
       }
+    } else {
+      // the next tap's weight tile is in flight during this tap's MFMAs; at a channel-block
+      // boundary the halo (single buffer) and the first weight tile are loaded after a barrier
+      issue_a(0);
+      issue_b(0, 0, 0);
+      int slot = 0;
+      for (int cb = 0; cb < ncb; ++cb) {
+        for (int j = 0; j < a.taps; ++j) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_s_barrier();
+          if (j + 1 < a.taps) issue_b(cb, j + 1, slot ^ 1);
+          compute(j, slot);
+          slot ^= 1;
+        }
+        if (cb + 1 < ncb) {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_s_barrier();
+          issue_a(cb + 1);
+          issue_b(cb + 1, 0, slot);
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
     }
   }
   nt_epilogue<BM, BN>(a, acc, smem, m0, n0, skip, tid, wm, wn, g, r16);
@@ -848,9 +883,15 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
     a.tiles_n = (int)((c_out + (halo_wide ? 127 : 63)) / (halo_wide ? 128 : 64));
     a.group = a.tiles_n;
     const unsigned grid = (unsigned)(a.tiles_m * a.tiles_n);
-    if (halo_wide) conv_gemm_halo<128, 128><<<grid, 256, 0, st>>>(a);
-    else if (halo_bm == 128) conv_gemm_halo<128, 64><<<grid, 256, 0, st>>>(a);
-    else conv_gemm_halo<64, 64><<<grid, 256, 0, st>>>(a);
+    if (g_tune[FS2_TUNE_NT_HALO] == 3) {  // single-buffered weight tile (A/B experiments)
+      if (halo_wide) conv_gemm_halo<128, 128, 1><<<grid, 256, 0, st>>>(a);
+      else if (halo_bm == 128) conv_gemm_halo<128, 64, 1><<<grid, 256, 0, st>>>(a);
+      else conv_gemm_halo<64, 64, 1><<<grid, 256, 0, st>>>(a);
+    } else {
+      if (halo_wide) conv_gemm_halo<128, 128, 2><<<grid, 256, 0, st>>>(a);
+      else if (halo_bm == 128) conv_gemm_halo<128, 64, 2><<<grid, 256, 0, st>>>(a);
+      else conv_gemm_halo<64, 64, 2><<<grid, 256, 0, st>>>(a);
+    }
   } else if (big >= 512) {
     a.tiles_m = (int)((rows + 127) / 128);
     a.tiles_n = (int)((c_out + 127) / 128);

@@ -161,7 +161,7 @@ int fs2_ln_bwd(int dtype, const float* dout, const float* ddot, const float* dot
 /* ---------------------------------------------------------------- BatchNorm (PostNet)
  * Training-mode BatchNorm1d over all rows (padded frames included) + optional tanh +
  * dropout (transformer/Layers.py:129-137).  Stats are exact two-pass (mean, then centred
- * sum of squares); running stats updated with momentum, unbiased variance.  c % 4 == 0.
+ * sum of squares); running stats updated with momentum, unbiased variance.  c % 8 == 0.
  * out / dz may be NULL when the bf16 copy (out_t / dz_t) is requested.               */
 int64_t fs2_bn_ws_bytes(int64_t rows, int64_t c);
 int fs2_bn_fwd(int dtype, const float* z, int64_t rows, int64_t c, const float* gamma,

@@ -124,15 +124,36 @@ FS2_DEV u32x4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint64_
 }
 FS2_DEV float u01(uint32_t x) { return (float)(x >> 8) * (1.0f / 16777216.0f); }
 
-// Keep-scale for 4 consecutive elements e0..e0+3 (e0 % 4 == 0) of dropout site `site`.
-// Returns 0 (dropped) or 1/(1-p) (kept) per element.
+// Dropout keep-scales.  One Philox-4x32-10 call serves 8 consecutive elements of a site
+// (counter = e >> 3): word w gives the 16-bit draws of elements 2w (low half) and 2w+1 (high
+// half); an element is dropped when its draw is below round(p * 65536), i.e. with
+// probability p to within 2^-17, and kept elements are scaled by 1/(1-p).  Kernels that own
+// 8 consecutive elements per lane call dropout8 (one Philox per lane); dropout4 / dropout1
+// give the same masks for narrower ownership.
+FS2_DEV uint32_t drop_thr16(float p) {
+  const float t = p * 65536.f + 0.5f;
+  return t >= 65536.f ? 65536u : (uint32_t)t;
+}
+FS2_DEV void dropout8(uint64_t seed, uint64_t site, uint64_t e0, float p, f32x4& lo, f32x4& hi) {
+  if (p <= 0.f) {
+    lo = hi = f32x4{1.f, 1.f, 1.f, 1.f};
+    return;
+  }
+  const uint64_t c = e0 >> 3;
+  const u32x4 r = philox((uint32_t)c, (uint32_t)(c >> 32), (uint32_t)site, (uint32_t)(site >> 32), seed);
+  const uint32_t th = drop_thr16(p);
+  const float s = 1.f / (1.f - p);
+  lo = f32x4{(r.x & 0xffffu) >= th ? s : 0.f, (r.x >> 16) >= th ? s : 0.f,
+             (r.y & 0xffffu) >= th ? s : 0.f, (r.y >> 16) >= th ? s : 0.f};
+  hi = f32x4{(r.z & 0xffffu) >= th ? s : 0.f, (r.z >> 16) >= th ? s : 0.f,
+             (r.w & 0xffffu) >= th ? s : 0.f, (r.w >> 16) >= th ? s : 0.f};
+}
+// 4 consecutive elements e0..e0+3 (e0 % 4 == 0): one half of the 8-element group
 FS2_DEV f32x4 dropout4(uint64_t seed, uint64_t site, uint64_t e0, float p) {
   if (p <= 0.f) return f32x4{1.f, 1.f, 1.f, 1.f};
-  uint64_t c = e0 >> 2;
-  u32x4 r = philox((uint32_t)c, (uint32_t)(c >> 32), (uint32_t)site, (uint32_t)(site >> 32), seed);
-  float s = 1.f / (1.f - p);
-  return f32x4{u01(r.x) >= p ? s : 0.f, u01(r.y) >= p ? s : 0.f, u01(r.z) >= p ? s : 0.f,
-               u01(r.w) >= p ? s : 0.f};
+  f32x4 lo, hi;
+  dropout8(seed, site, e0 & ~7ull, p, lo, hi);
+  return (e0 & 4) ? hi : lo;
 }
 FS2_DEV float dropout1(uint64_t seed, uint64_t site, uint64_t e, float p) {
   if (p <= 0.f) return 1.f;
@@ -157,6 +178,21 @@ FS2_DEV void st4_bf16(void* p, f32x4 v) {
   w.x = (uint32_t)to_bf16(v.x) | ((uint32_t)to_bf16(v.y) << 16);
   w.y = (uint32_t)to_bf16(v.z) | ((uint32_t)to_bf16(v.w) << 16);
   *reinterpret_cast<uint2*>(p) = w;
+}
+
+FS2_DEV void st8_bf16(void* p, f32x4 a, f32x4 b) {
+  uint4 w;
+  w.x = (uint32_t)to_bf16(a.x) | ((uint32_t)to_bf16(a.y) << 16);
+  w.y = (uint32_t)to_bf16(a.z) | ((uint32_t)to_bf16(a.w) << 16);
+  w.z = (uint32_t)to_bf16(b.x) | ((uint32_t)to_bf16(b.y) << 16);
+  w.w = (uint32_t)to_bf16(b.z) | ((uint32_t)to_bf16(b.w) << 16);
+  *reinterpret_cast<uint4*>(p) = w;
+}
+// sum over the 32 lanes of a half-wave (every lane gets the half's sum)
+FS2_DEV float half_sum(float v) {
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
 }
 
 }  // namespace fs2

@@ -1,7 +1,8 @@
 // LayerNorm (FFT blocks, variance predictors) and training-mode BatchNorm (PostNet).
 //
-// LayerNorm: one wave per 256-wide row, 4 consecutive channels per lane (one 16-B load,
-// one Philox call for the 4 dropout draws), wave-shuffle mean/variance.  The call-site
+// LayerNorm: one half-wave (32 lanes) per 256-wide row, 8 consecutive channels per lane
+// (two 16-B loads, ONE Philox call for the 8 dropout draws: dropout8), half-wave shuffle
+// mean/variance.  The call-site
 // epilogues of the reference are fused in: dropout + residual before the norm
 // (SubLayers.py:54-55,91-93), padded-row zeroing after it (Layers.py:25,28), dropout
 // after it and the Linear(256 -> 1) head of the variance predictor (modules.py:209-250).
@@ -18,7 +19,7 @@
 namespace fs2 {
 
 constexpr int LN_D = 256;
-constexpr int LN_ROWS = 32;  // rows per block in the backward (8 per wave)
+constexpr int LN_ROWS = 32;  // rows per block in the backward (4 row pairs per wave)
 
 struct LnFwd {
   const float* y;
@@ -45,36 +46,61 @@ FS2_DEV bool row_padded(const int64_t* lens, int64_t T, int64_t r) {
   return (r - b * T) >= lens[b];
 }
 
+// rows r = 8 * (blockIdx.x + k * gridDim.x) + half-wave index (grid-stride: the dropout key,
+// gamma and beta are fetched once per half-wave, not once per row)
 __global__ __launch_bounds__(256) void ln_fwd_f32(LnFwd a) {
-  const int lane = threadIdx.x & 63;
-  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (r >= a.rows) return;
-  const int64_t e0 = r * LN_D + 4 * lane;
+  const int hl = threadIdx.x & 31;  // lane within the row's half-wave
+  const uint64_t seed = a.seed ? *a.seed : 0ull;
+  const f32x4 ga0 = ld4(a.gamma + 8 * hl), ga1 = ld4(a.gamma + 8 * hl + 4);
+  const f32x4 be0 = ld4(a.beta + 8 * hl), be1 = ld4(a.beta + 8 * hl + 4);
+  for (int64_t r = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5); r < a.rows;
+       r += (int64_t)gridDim.x * 8) {
+  const int64_t e0 = r * LN_D + 8 * hl;
   const bool pad = row_padded(a.lens, a.T, r);
   if (pad && !a.dot_out) {  // masked row: output 0; xhat/rstd are never read (bwd skips it)
-    st4(a.out + e0, f32x4{0.f, 0.f, 0.f, 0.f});
-    if (a.out_t) st4_bf16(a.out_t + e0, f32x4{0.f, 0.f, 0.f, 0.f});
-    return;
+    const f32x4 zz = {0.f, 0.f, 0.f, 0.f};
+    st4(a.out + e0, zz);
+    st4(a.out + e0 + 4, zz);
+    if (a.out_t) st8_bf16(a.out_t + e0, zz, zz);
+    continue;
   }
-  const uint64_t seed = a.seed ? *a.seed : 0ull;
-  f32x4 z = ld4(a.y + e0);
-  if (a.p_in > 0.f) z *= dropout4(seed, a.site_in, (uint64_t)e0, a.p_in);
-  if (a.res) z += ld4(a.res + e0);
-  const float mean = wave_sum(z.x + z.y + z.z + z.w) * (1.f / LN_D);
-  const f32x4 c = z - mean;
-  const float var = wave_sum(c.x * c.x + c.y * c.y + c.z * c.z + c.w * c.w) * (1.f / LN_D);
+  f32x4 z0 = ld4(a.y + e0), z1 = ld4(a.y + e0 + 4);
+  if (a.p_in > 0.f) {
+    f32x4 m0, m1;
+    dropout8(seed, a.site_in, (uint64_t)e0, a.p_in, m0, m1);
+    z0 *= m0;
+    z1 *= m1;
+  }
+  if (a.res) {
+    z0 += ld4(a.res + e0);
+    z1 += ld4(a.res + e0 + 4);
+  }
+  const float mean = half_sum((z0.x + z0.y + z0.z + z0.w) + (z1.x + z1.y + z1.z + z1.w)) * (1.f / LN_D);
+  const f32x4 c0 = z0 - mean, c1 = z1 - mean;
+  const float var = half_sum((c0.x * c0.x + c0.y * c0.y + c0.z * c0.z + c0.w * c0.w) +
+                             (c1.x * c1.x + c1.y * c1.y + c1.z * c1.z + c1.w * c1.w)) * (1.f / LN_D);
   const float rs = 1.f / sqrtf(var + 1e-5f);
-  const f32x4 xh = c * rs;
-  f32x4 u = xh * ld4(a.gamma + 4 * lane) + ld4(a.beta + 4 * lane);
-  if (a.p_out > 0.f) u *= dropout4(seed, a.site_out, (uint64_t)e0, a.p_out);
-  st4(a.out + e0, u);  // (dot mode masks only the head output)
-  if (a.out_t) st4_bf16(a.out_t + e0, u);
-  st4(a.xhat + e0, xh);
-  if (lane == 0) a.rstd[r] = rs;
+  const f32x4 xh0 = c0 * rs, xh1 = c1 * rs;
+  f32x4 u0 = xh0 * ga0 + be0;
+  f32x4 u1 = xh1 * ga1 + be1;
+  if (a.p_out > 0.f) {
+    f32x4 m0, m1;
+    dropout8(seed, a.site_out, (uint64_t)e0, a.p_out, m0, m1);
+    u0 *= m0;
+    u1 *= m1;
+  }
+  st4(a.out + e0, u0);  // (dot mode masks only the head output)
+  st4(a.out + e0 + 4, u1);
+  if (a.out_t) st8_bf16(a.out_t + e0, u0, u1);
+  st4(a.xhat + e0, xh0);
+  st4(a.xhat + e0 + 4, xh1);
+  if (hl == 0) a.rstd[r] = rs;
   if (a.dot_out) {
-    const f32x4 w = ld4(a.dot_w + 4 * lane);
-    const float d = wave_sum(u.x * w.x + u.y * w.y + u.z * w.z + u.w * w.w);
-    if (lane == 0) a.dot_out[r] = pad ? 0.f : d + a.dot_b[0];
+    const f32x4 w0 = ld4(a.dot_w + 8 * hl), w1 = ld4(a.dot_w + 8 * hl + 4);
+    const float d = half_sum((u0.x * w0.x + u0.y * w0.y + u0.z * w0.z + u0.w * w0.w) +
+                             (u1.x * w1.x + u1.y * w1.y + u1.z * w1.z + u1.w * w1.w));
+    if (hl == 0) a.dot_out[r] = pad ? 0.f : d + a.dot_b[0];
+  }
   }
 }
 
@@ -100,73 +126,125 @@ struct LnBwd {
   unsigned short* dy_t;  // optional bf16 copy of dy
 };
 
+// Row pairs: half-wave h of a wave takes row 2i + h, 8 channels per lane.  Column partials
+// (8 per lane) are combined over the 8 half-waves of the block through LDS in a fixed order.
+template <bool DDOT>
 __global__ __launch_bounds__(256) void ln_bwd_f32(LnBwd a) {
-  __shared__ f32x4 red[4][4][64];
-  __shared__ float redb[4];
+  __shared__ f32x4 red[8][64];
+  __shared__ float redb[8];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const f32x4 gam = ld4(a.gamma + 4 * lane);
-  const f32x4 bet = ld4(a.beta + 4 * lane);
-  f32x4 w = {0.f, 0.f, 0.f, 0.f};
-  if (a.ddot) w = ld4(a.dot_w + 4 * lane);
-  f32x4 pg = {0.f, 0.f, 0.f, 0.f}, pb = pg, pw = pg, py = pg;
+  const int half = lane >> 5, hl = lane & 31, slot = wave * 2 + half;
+  const int c8 = 8 * hl;
+  const f32x4 gam0 = ld4(a.gamma + c8), gam1 = ld4(a.gamma + c8 + 4);
+  const f32x4 bet0 = ld4(a.beta + c8), bet1 = ld4(a.beta + c8 + 4);
+  const f32x4 zz = {0.f, 0.f, 0.f, 0.f};
+  f32x4 w0 = zz, w1 = zz;
+  if constexpr (DDOT) {
+    w0 = ld4(a.dot_w + c8);
+    w1 = ld4(a.dot_w + c8 + 4);
+  }
+  f32x4 pg0 = zz, pg1 = zz, pb0 = zz, pb1 = zz, pw0 = zz, pw1 = zz, py0 = zz, py1 = zz;
   float pdb = 0.f;
   const uint64_t seed = a.seed ? *a.seed : 0ull;
   const int64_t rbeg = (int64_t)blockIdx.x * LN_ROWS;
-  for (int i = wave; i < LN_ROWS; i += 4) {
-    const int64_t r = rbeg + i;
+#pragma unroll 1
+  for (int i = wave; i < LN_ROWS / 2; i += 4) {
+    const int64_t r = rbeg + 2 * i + half;
     if (r >= a.rows) break;
-    const int64_t e0 = r * LN_D + 4 * lane;
+    const int64_t e0 = r * LN_D + c8;
     if (row_padded(a.lens, a.T, r)) {  // masked row: zero upstream gradient, nothing to add
-      if (a.dres && !a.dres_add) st4(a.dres + e0, f32x4{0.f, 0.f, 0.f, 0.f});
-      if (a.dy) st4(a.dy + e0, f32x4{0.f, 0.f, 0.f, 0.f});
-      if (a.dy_t) st4_bf16(a.dy_t + e0, f32x4{0.f, 0.f, 0.f, 0.f});
+      if (a.dres && !a.dres_add) {
+        st4(a.dres + e0, zz);
+        st4(a.dres + e0 + 4, zz);
+      }
+      if (a.dy) {
+        st4(a.dy + e0, zz);
+        st4(a.dy + e0 + 4, zz);
+      }
+      if (a.dy_t) st8_bf16(a.dy_t + e0, zz, zz);
       continue;
     }
-    const f32x4 xh = ld4(a.xhat + e0);
-    const f32x4 mo = a.p_out > 0.f ? dropout4(seed, a.site_out, (uint64_t)e0, a.p_out)
-                                   : f32x4{1.f, 1.f, 1.f, 1.f};
-    f32x4 du;
-    if (a.ddot) {
+    const f32x4 xh0 = ld4(a.xhat + e0), xh1 = ld4(a.xhat + e0 + 4);
+    f32x4 mo0 = {1.f, 1.f, 1.f, 1.f}, mo1 = mo0;
+    if (a.p_out > 0.f) dropout8(seed, a.site_out, (uint64_t)e0, a.p_out, mo0, mo1);
+    f32x4 du0, du1;
+    if constexpr (DDOT) {
       const float gr = a.ddot[r];
-      du = gr * w;
-      const f32x4 u = (xh * gam + bet) * mo;
-      pw += gr * u;
+      du0 = gr * w0;
+      du1 = gr * w1;
+      pw0 += gr * ((xh0 * gam0 + bet0) * mo0);
+      pw1 += gr * ((xh1 * gam1 + bet1) * mo1);
       pdb += gr;
     } else {
-      du = ld4(a.dout + e0);
+      du0 = ld4(a.dout + e0);
+      du1 = ld4(a.dout + e0 + 4);
     }
-    du *= mo;
-    pg += du * xh;
-    pb += du;
-    const f32x4 dxh = du * gam;
-    const float m1 = wave_sum(dxh.x + dxh.y + dxh.z + dxh.w) * (1.f / LN_D);
-    const float m2 =
-        wave_sum(dxh.x * xh.x + dxh.y * xh.y + dxh.z * xh.z + dxh.w * xh.w) * (1.f / LN_D);
-    const f32x4 dz = a.rstd[r] * (dxh - m1 - xh * m2);
-    if (a.dres) st4(a.dres + e0, a.dres_add ? ld4(a.dres + e0) + dz : dz);
-    f32x4 dy = dz;
-    if (a.p_in > 0.f) dy *= dropout4(seed, a.site_in, (uint64_t)e0, a.p_in);
+    du0 *= mo0;
+    du1 *= mo1;
+    pg0 += du0 * xh0;
+    pg1 += du1 * xh1;
+    pb0 += du0;
+    pb1 += du1;
+    const f32x4 dxh0 = du0 * gam0, dxh1 = du1 * gam1;
+    const float m1 = half_sum((dxh0.x + dxh0.y + dxh0.z + dxh0.w) + (dxh1.x + dxh1.y + dxh1.z + dxh1.w)) *
+                     (1.f / LN_D);
+    const float m2 = half_sum((dxh0.x * xh0.x + dxh0.y * xh0.y + dxh0.z * xh0.z + dxh0.w * xh0.w) +
+                              (dxh1.x * xh1.x + dxh1.y * xh1.y + dxh1.z * xh1.z + dxh1.w * xh1.w)) *
+                     (1.f / LN_D);
+    const float rs = a.rstd[r];
+    const f32x4 dz0 = rs * (dxh0 - m1 - xh0 * m2), dz1 = rs * (dxh1 - m1 - xh1 * m2);
+    if (a.dres) {
+      st4(a.dres + e0, a.dres_add ? ld4(a.dres + e0) + dz0 : dz0);
+      st4(a.dres + e0 + 4, a.dres_add ? ld4(a.dres + e0 + 4) + dz1 : dz1);
+    }
+    f32x4 dy0 = dz0, dy1 = dz1;
+    if (a.p_in > 0.f) {
+      f32x4 mi0, mi1;
+      dropout8(seed, a.site_in, (uint64_t)e0, a.p_in, mi0, mi1);
+      dy0 *= mi0;
+      dy1 *= mi1;
+    }
     if (a.relu_y) {
-      const f32x4 yv = ld4(a.relu_y + e0);
-      dy.x = yv.x > 0.f ? dy.x : 0.f;
-      dy.y = yv.y > 0.f ? dy.y : 0.f;
-      dy.z = yv.z > 0.f ? dy.z : 0.f;
-      dy.w = yv.w > 0.f ? dy.w : 0.f;
+      const f32x4 y0 = ld4(a.relu_y + e0), y1 = ld4(a.relu_y + e0 + 4);
+      dy0 = f32x4{y0.x > 0.f ? dy0.x : 0.f, y0.y > 0.f ? dy0.y : 0.f, y0.z > 0.f ? dy0.z : 0.f,
+                  y0.w > 0.f ? dy0.w : 0.f};
+      dy1 = f32x4{y1.x > 0.f ? dy1.x : 0.f, y1.y > 0.f ? dy1.y : 0.f, y1.z > 0.f ? dy1.z : 0.f,
+                  y1.w > 0.f ? dy1.w : 0.f};
     }
-    if (a.dy) st4(a.dy + e0, dy);
-    if (a.dy_t) st4_bf16(a.dy_t + e0, dy);
-    py += dy;  // bias gradient of the layer that produced y (fused colsum)
+    if (a.dy) {
+      st4(a.dy + e0, dy0);
+      st4(a.dy + e0 + 4, dy1);
+    }
+    if (a.dy_t) st8_bf16(a.dy_t + e0, dy0, dy1);
+    py0 += dy0;  // bias gradient of the layer that produced y (fused colsum)
+    py1 += dy1;
   }
-  red[0][wave][lane] = pg;
-  red[1][wave][lane] = pb;
-  red[2][wave][lane] = pw;
-  red[3][wave][lane] = py;
-  if (lane == 0) redb[wave] = pdb;
+  // per kind: red[slot][q], f32x4 q covers channels 4q..4q+3 (lane hl owns q = 2hl, 2hl+1);
+  // wave 0 sums the 8 half-waves in slot order
+  auto flush = [&](f32x4 lo, f32x4 hi, int kind) {
+    red[slot][2 * hl] = lo;
+    red[slot][2 * hl + 1] = hi;
+    __syncthreads();
+    if (wave == 0) {
+      f32x4 sum = red[0][lane];
+#pragma unroll
+      for (int q = 1; q < 8; ++q) sum += red[q][lane];
+      st4(a.part + ((int64_t)kind * a.nblk + blockIdx.x) * LN_D + 4 * lane, sum);
+    }
+    __syncthreads();
+  };
+  flush(pg0, pg1, 0);
+  flush(pb0, pb1, 1);
+  if constexpr (DDOT) flush(pw0, pw1, 2);
+  flush(py0, py1, 3);
+  if (hl == 0) redb[slot] = pdb;
   __syncthreads();
-  const f32x4 s = red[wave][0][lane] + red[wave][1][lane] + red[wave][2][lane] + red[wave][3][lane];
-  st4(a.part + ((int64_t)wave * a.nblk + blockIdx.x) * LN_D + 4 * lane, s);
-  if (threadIdx.x == 0)
-    a.part[4 * a.nblk * LN_D + blockIdx.x] = redb[0] + redb[1] + redb[2] + redb[3];
+  if (threadIdx.x == 0) {
+    float b = redb[0];
+#pragma unroll
+    for (int q = 1; q < 8; ++q) b += redb[q];
+    a.part[4 * a.nblk * LN_D + blockIdx.x] = b;
+  }
 }
 
 // ------------------------------------------------------------------ BatchNorm
@@ -242,41 +320,64 @@ __global__ __launch_bounds__(1024) void bn_var_final(const float* part, int64_t 
   if (rv) rv[col] = (1.f - mom) * rv[col] + mom * (rows > 1 ? s / (float)(rows - 1) : var);
 }
 
-// out = act(BN(z)) * dropout (+ res), 4 consecutive elements (same row) per lane
+FS2_DEV f32x4 tanh4(f32x4 v) { return f32x4{tanhf(v.x), tanhf(v.y), tanhf(v.z), tanhf(v.w)}; }
+
+// out = act(BN(z)) * dropout (+ res), 8 consecutive elements (same row) per lane
 __global__ __launch_bounds__(256) void bn_apply(const float* z, const float* mean, const float* rstd,
-                                                const float* gamma, const float* beta, int64_t n4,
+                                                const float* gamma, const float* beta, int64_t n8,
                                                 int c, int act_tanh, float p, const uint64_t* seed_p,
                                                 uint64_t site, const float* res, float* out,
                                                 unsigned short* out_t) {
   const uint64_t seed = seed_p ? *seed_p : 0ull;
-  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n8;
        q += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t e0 = q * 4;
+    const int64_t e0 = q * 8;
     const int col = (int)(e0 % c);
-    f32x4 v = (ld4(z + e0) - ld4(mean + col)) * ld4(rstd + col) * ld4(gamma + col) + ld4(beta + col);
-    if (act_tanh) v = f32x4{tanhf(v.x), tanhf(v.y), tanhf(v.z), tanhf(v.w)};
-    if (p > 0.f) v *= dropout4(seed, site, (uint64_t)e0, p);
-    if (res) v += ld4(res + e0);
-    if (out) st4(out + e0, v);
-    if (out_t) st4_bf16(out_t + e0, v);
+    f32x4 v0 = (ld4(z + e0) - ld4(mean + col)) * ld4(rstd + col) * ld4(gamma + col) + ld4(beta + col);
+    f32x4 v1 = (ld4(z + e0 + 4) - ld4(mean + col + 4)) * ld4(rstd + col + 4) * ld4(gamma + col + 4) +
+               ld4(beta + col + 4);
+    if (act_tanh) {
+      v0 = tanh4(v0);
+      v1 = tanh4(v1);
+    }
+    if (p > 0.f) {
+      f32x4 m0, m1;
+      dropout8(seed, site, (uint64_t)e0, p, m0, m1);
+      v0 *= m0;
+      v1 *= m1;
+    }
+    if (res) {
+      v0 += ld4(res + e0);
+      v1 += ld4(res + e0 + 4);
+    }
+    if (out) {
+      st4(out + e0, v0);
+      st4(out + e0 + 4, v1);
+    }
+    if (out_t) st8_bf16(out_t + e0, v0, v1);
   }
 }
 
-// g = dout * mask * act'(a) for 4 consecutive elements; also returns xhat
-FS2_DEV f32x4 bn_g4(const float* dout, const float* z, f32x4 mu, f32x4 rs, f32x4 ga, f32x4 be,
-                    int act_tanh, float p, uint64_t seed, uint64_t site, int64_t e0, f32x4* xh_out) {
-  const f32x4 xh = (ld4(z + e0) - mu) * rs;
-  *xh_out = xh;
-  f32x4 g = ld4(dout + e0);
-  if (p > 0.f) g *= dropout4(seed, site, (uint64_t)e0, p);
-  if (act_tanh) {
-    const f32x4 a = xh * ga + be;
-    const f32x4 t = {tanhf(a.x), tanhf(a.y), tanhf(a.z), tanhf(a.w)};
-    g *= 1.f - t * t;
+// g = dout * mask * act'(a) for 8 consecutive elements (one Philox call); also returns xhat
+FS2_DEV void bn_g8(const float* dout, const float* z, const float* mean, const float* rstd,
+                   const float* gamma, const float* beta, int col, int act_tanh, float p,
+                   uint64_t seed, uint64_t site, int64_t e0, f32x4 (&g)[2], f32x4 (&xh)[2]) {
+  f32x4 m[2] = {{1.f, 1.f, 1.f, 1.f}, {1.f, 1.f, 1.f, 1.f}};
+  if (p > 0.f) dropout8(seed, site, (uint64_t)e0, p, m[0], m[1]);
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int cc = col + 4 * h;
+    xh[h] = (ld4(z + e0 + 4 * h) - ld4(mean + cc)) * ld4(rstd + cc);
+    g[h] = ld4(dout + e0 + 4 * h) * m[h];
+    if (act_tanh) {
+      const f32x4 t = tanh4(xh[h] * ld4(gamma + cc) + ld4(beta + cc));
+      g[h] *= 1.f - t * t;
+    }
   }
-  return g;
 }
 
+// column partials of g and g*xhat: block (x, y) covers channels [512x, 512x+512) (8 per
+// lane) of rows [BN_ROWS*y, BN_ROWS*(y+1)), four row lanes summed in lane order
 __global__ __launch_bounds__(256) void bn_bwd_partial(const float* dout, const float* z,
                                                       const float* mean, const float* rstd,
                                                       const float* gamma, const float* beta,
@@ -285,29 +386,37 @@ __global__ __launch_bounds__(256) void bn_bwd_partial(const float* dout, const f
                                                       uint64_t site, float* part_g, float* part_gx) {
   const uint64_t seed = seed_p ? *seed_p : 0ull;
   const int tx = threadIdx.x & 63, ry = threadIdx.x >> 6;
-  const int64_t col = ((int64_t)blockIdx.x * 64 + tx) * 4;
+  const int64_t col = ((int64_t)blockIdx.x * 64 + tx) * 8;
   const int64_t r0 = (int64_t)blockIdx.y * BN_ROWS;
-  __shared__ f32x4 red[2][4][64];
-  f32x4 sg = {0.f, 0.f, 0.f, 0.f}, sgx = sg;
+  __shared__ f32x4 red[2][4][128];
+  f32x4 sg[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}}, sgx[2] = {sg[0], sg[0]};
   if (col < c) {
-    const f32x4 mu = ld4(mean + col), rs = ld4(rstd + col), ga = ld4(gamma + col),
-                be = ld4(beta + col);
     const int64_t r1 = r0 + BN_ROWS < rows ? r0 + BN_ROWS : rows;
     for (int64_t r = r0 + ry; r < r1; r += 4) {
-      f32x4 xh;
-      const f32x4 g = bn_g4(dout, z, mu, rs, ga, be, act_tanh, p, seed, site, r * c + col, &xh);
-      sg += g;
-      sgx += g * xh;
+      f32x4 g[2], xh[2];
+      bn_g8(dout, z, mean, rstd, gamma, beta, (int)col, act_tanh, p, seed, site, r * c + col, g, xh);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        sg[h] += g[h];
+        sgx[h] += g[h] * xh[h];
+      }
     }
   }
-  red[0][ry][tx] = sg;
-  red[1][ry][tx] = sgx;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    red[0][ry][2 * tx + h] = sg[h];
+    red[1][ry][2 * tx + h] = sgx[h];
+  }
   __syncthreads();
   if (ry == 0 && col < c) {
-    st4(part_g + (int64_t)blockIdx.y * c + col,
-        ((red[0][0][tx] + red[0][1][tx]) + red[0][2][tx]) + red[0][3][tx]);
-    st4(part_gx + (int64_t)blockIdx.y * c + col,
-        ((red[1][0][tx] + red[1][1][tx]) + red[1][2][tx]) + red[1][3][tx]);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int q = 2 * tx + h;
+      st4(part_g + (int64_t)blockIdx.y * c + col + 4 * h,
+          ((red[0][0][q] + red[0][1][q]) + red[0][2][q]) + red[0][3][q]);
+      st4(part_gx + (int64_t)blockIdx.y * c + col + 4 * h,
+          ((red[1][0][q] + red[1][1][q]) + red[1][2][q]) + red[1][3][q]);
+    }
   }
 }
 
@@ -329,23 +438,29 @@ __global__ __launch_bounds__(1024) void bn_bwd_final(const float* part_g, const 
 __global__ __launch_bounds__(256) void bn_bwd_apply(const float* dout, const float* z,
                                                     const float* mean, const float* rstd,
                                                     const float* gamma, const float* beta,
-                                                    const float* sums, int64_t n4, int64_t rows,
+                                                    const float* sums, int64_t n8, int64_t rows,
                                                     int c, int act_tanh, float p,
                                                     const uint64_t* seed_p, uint64_t site, float* dz,
                                                     unsigned short* dz_t) {
   const uint64_t seed = seed_p ? *seed_p : 0ull;
   const float inv_m = 1.f / (float)rows;
-  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n8;
        q += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t e0 = q * 4;
+    const int64_t e0 = q * 8;
     const int col = (int)(e0 % c);
-    const f32x4 ga = ld4(gamma + col), rs = ld4(rstd + col);
-    f32x4 xh;
-    const f32x4 g = bn_g4(dout, z, ld4(mean + col), rs, ga, ld4(beta + col), act_tanh, p, seed,
-                          site, e0, &xh);
-    const f32x4 v = ga * rs * (g - ld4(sums + col) * inv_m - xh * ld4(sums + c + col) * inv_m);
-    if (dz) st4(dz + e0, v);
-    if (dz_t) st4_bf16(dz_t + e0, v);
+    f32x4 g[2], xh[2], v[2];
+    bn_g8(dout, z, mean, rstd, gamma, beta, col, act_tanh, p, seed, site, e0, g, xh);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int cc = col + 4 * h;
+      v[h] = ld4(gamma + cc) * ld4(rstd + cc) *
+             (g[h] - ld4(sums + cc) * inv_m - xh[h] * ld4(sums + c + cc) * inv_m);
+    }
+    if (dz) {
+      st4(dz + e0, v[0]);
+      st4(dz + e0 + 4, v[1]);
+    }
+    if (dz_t) st8_bf16(dz_t + e0, v[0], v[1]);
   }
 }
 
@@ -383,7 +498,9 @@ int fs2_ln_fwd(int dtype, const float* y, const float* res, const float* gamma, 
   LnFwd a{y, res, gamma, beta, out, xhat, rstd, lens, seq_len, rows, p_in, p_out, seed,
           site_in, site_out, dot_w, dot_b, dot_out,
           dtype == FS2_BF16 ? (unsigned short*)out_t : nullptr};
-  ln_fwd_f32<<<(unsigned)((rows + 3) / 4), 256, 0, as_stream(stream)>>>(a);
+  int64_t nb = (rows + 7) / 8;
+  if (nb > 2048) nb = 2048;  // 8 blocks per CU, grid-stride beyond
+  ln_fwd_f32<<<(unsigned)nb, 256, 0, as_stream(stream)>>>(a);
   return launch_status("fs2_ln_fwd");
 }
 
@@ -410,7 +527,8 @@ int fs2_ln_bwd(int dtype, const float* dout, const float* ddot, const float* dot
   LnBwd a{dout, ddot, dot_w, xhat, rstd, gamma, beta, lens, seq_len, rows, p_in, p_out, seed,
           site_in, site_out, relu_y, dy, dres, dres_add, ws, nblk,
           dtype == FS2_BF16 ? (unsigned short*)dy_t : nullptr};
-  ln_bwd_f32<<<(unsigned)nblk, 256, 0, st>>>(a);
+  if (ddot) ln_bwd_f32<true><<<(unsigned)nblk, 256, 0, st>>>(a);
+  else ln_bwd_f32<false><<<(unsigned)nblk, 256, 0, st>>>(a);
   int rc = launch_status("fs2_ln_bwd");
   if (rc) return rc;
   ColsumJobs jobs{};
@@ -439,7 +557,7 @@ int fs2_bn_fwd(int dtype, const float* z, int64_t rows, int64_t c, const float* 
   FS2_CHECK_ARG(ws_bytes >= fs2_bn_ws_bytes(rows, c), "fs2_bn_fwd: workspace too small");
   hipStream_t st = as_stream(stream);
   const int64_t nparts = (rows + BN_ROWS - 1) / BN_ROWS;
-  FS2_CHECK_ARG(c % 4 == 0, "fs2_bn_fwd: channel count must be a multiple of 4");
+  FS2_CHECK_ARG(c % 8 == 0, "fs2_bn_fwd: channel count must be a multiple of 8");
   dim3 grid((unsigned)((c + 255) / 256), (unsigned)nparts);
   const unsigned cg = (unsigned)((c + 63) / 64);
   bn_partial<0><<<grid, 256, 0, st>>>(z, nullptr, rows, c, ws);
@@ -449,7 +567,7 @@ int fs2_bn_fwd(int dtype, const float* z, int64_t rows, int64_t c, const float* 
                                    running_var, rstd);
   unsigned short* ot = dtype == FS2_BF16 ? (unsigned short*)out_t : nullptr;
   FS2_CHECK_ARG(out || ot, "fs2_bn_fwd: no output requested");
-  bn_apply<<<ew_grid(rows * c / 4), 256, 0, st>>>(z, mean, rstd, gamma, beta, rows * c / 4, (int)c,
+  bn_apply<<<ew_grid(rows * c / 8), 256, 0, st>>>(z, mean, rstd, gamma, beta, rows * c / 8, (int)c,
                                                   act_tanh, p, seed, site, res, out, ot);
   return launch_status("fs2_bn_fwd");
 }
@@ -468,14 +586,14 @@ int fs2_bn_eval_fwd(int dtype, const float* z, int64_t rows, int64_t c, const fl
                     const float* running_var, float* mean, float* rstd, int act_tanh,
                     const float* res, float* out, void* out_t, void* stream) {
   if (int rc = copy_dtype_ok(dtype, "fs2_bn_eval_fwd")) return rc;
-  FS2_CHECK_ARG(rows > 0 && c > 0 && c % 4 == 0, "fs2_bn_eval_fwd: bad shape (c % 4 == 0)");
+  FS2_CHECK_ARG(rows > 0 && c > 0 && c % 8 == 0, "fs2_bn_eval_fwd: bad shape (c % 8 == 0)");
   FS2_CHECK_ARG(running_mean && running_var && mean && rstd, "fs2_bn_eval_fwd: null statistics");
   hipStream_t st = as_stream(stream);
   unsigned short* ot = dtype == FS2_BF16 ? (unsigned short*)out_t : nullptr;
   FS2_CHECK_ARG(out || ot, "fs2_bn_eval_fwd: no output requested");
   bn_eval_stats<<<(unsigned)((c + 255) / 256), 256, 0, st>>>(running_mean, running_var, c, eps,
                                                              mean, rstd);
-  bn_apply<<<ew_grid(rows * c / 4), 256, 0, st>>>(z, mean, rstd, gamma, beta, rows * c / 4, (int)c,
+  bn_apply<<<ew_grid(rows * c / 8), 256, 0, st>>>(z, mean, rstd, gamma, beta, rows * c / 8, (int)c,
                                                   act_tanh, 0.f, nullptr, 0, res, out, ot);
   return launch_status("fs2_bn_eval_fwd");
 }
@@ -493,16 +611,16 @@ int fs2_bn_bwd(int dtype, const float* dout, const float* z, const float* mean, 
   float* part_g = ws;
   float* part_gx = ws + nparts * c;
   float* sums = ws + 2 * nparts * c;
-  FS2_CHECK_ARG(c % 4 == 0, "fs2_bn_bwd: channel count must be a multiple of 4");
+  FS2_CHECK_ARG(c % 8 == 0, "fs2_bn_bwd: channel count must be a multiple of 8");
   unsigned short* zt = dtype == FS2_BF16 ? (unsigned short*)dz_t : nullptr;
   FS2_CHECK_ARG(dz || zt, "fs2_bn_bwd: no output requested");
-  dim3 grid((unsigned)((c + 255) / 256), (unsigned)nparts);
+  dim3 grid((unsigned)((c + 511) / 512), (unsigned)nparts);
   bn_bwd_partial<<<grid, 256, 0, st>>>(dout, z, mean, rstd, gamma, beta, rows, c, act_tanh, p,
                                        seed, site, part_g, part_gx);
   bn_bwd_final<<<(unsigned)((c + 63) / 64), 1024, 0, st>>>(part_g, part_gx, nparts, c, sums,
                                                              dgamma, dbeta);
-  bn_bwd_apply<<<ew_grid(rows * c / 4), 256, 0, st>>>(dout, z, mean, rstd, gamma, beta, sums,
-                                                      rows * c / 4, rows, (int)c, act_tanh, p,
+  bn_bwd_apply<<<ew_grid(rows * c / 8), 256, 0, st>>>(dout, z, mean, rstd, gamma, beta, sums,
+                                                      rows * c / 8, rows, (int)c, act_tanh, p,
                                                       seed, site, dz, zt);
   return launch_status("fs2_bn_bwd");
 }

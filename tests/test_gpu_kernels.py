@@ -536,3 +536,29 @@ def test_conv_gemm_bf16_halo(B, T, cin, cout, k):
                 close(dx, xr.grad + aux, 1e-5)
     finally:
         K.lib.fs2_set_tuning(6, 0)
+
+
+@pytest.mark.parametrize("c,act", [(512, True), (80, False)])
+def test_batchnorm_dropout(c, act):
+    """PostNet BatchNorm with dropout (p = 0.5): keep-rate of the 16-bit Philox draws, and the
+    backward against autograd on the mask recovered from the forward output."""
+    M, p = 1000, 0.5
+    z = rnd(M, c, seed=11) * 2 + 0.5
+    g, b = 1 + 0.1 * rnd(c, seed=12), 0.1 * rnd(c, seed=13)
+    out, _, mean, rstd = K.bn_fwd(z, g, b, None, None, act, p, 7, 3)
+    keep = out != 0
+    frac = keep.float().mean().item()
+    assert abs(frac - (1 - p)) < 0.01, frac
+    zr, gr, br = z.clone().requires_grad_(), g.clone().requires_grad_(), b.clone().requires_grad_()
+    ref = F.batch_norm(zr, None, None, gr, br, training=True, eps=1e-5)
+    if act:
+        ref = torch.tanh(ref)
+    ref = ref * keep / (1 - p)
+    close(out, ref, 2e-5)
+    dout = rnd(M, c, seed=14)
+    ref.backward(dout)
+    dg, db = torch.zeros(c, device=DEV), torch.zeros(c, device=DEV)
+    dz, _ = K.bn_bwd(dout, z, mean, rstd, g, b, dg, db, act, p, 7, 3)
+    close(dz, zr.grad)
+    close(dg, gr.grad)
+    close(db, br.grad)

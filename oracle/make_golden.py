@@ -21,6 +21,11 @@ Fixtures:
                    POT is absent: ``ot.emd`` is stubbed by the same LP solved with scipy's
                    HiGHS (unique optimum); BarycenterGMM's ``_print`` TypeError is bypassed
                    by letting ``_barycenter_gaussians`` accept and ignore the kwarg.
+  g8_data.npz      data pipeline (dataset.py, utils/tools.py pad_1D/pad_2D): the reference's
+                   Dataset + ConcatDataset + collate_fn over the seeded synthetic corpora of
+                   tests/synth_corpus.py (one corpus with accent files, one without): two
+                   sorted/drop-last draws through the concatenation (14-tuples) and the
+                   accent-free corpus alone unsorted with its tail kept (13-tuples)
 """
 import importlib
 import os
@@ -361,8 +366,54 @@ def g7(fs2):
     np.savez_compressed(os.path.join(OUT, "g7_gmm_ops.npz"), **res)
 
 
+BATCH_FIELDS = ("ids", "raw_texts", "speakers", "texts", "src_lens", "max_src_len", "mels",
+                "mel_lens", "max_mel_len", "pitches", "energies", "durations", "speaker_meta",
+                "accents")
+
+
+def g8():
+    import tempfile
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from synth_corpus import make_corpora
+    ds_mod = importlib.import_module("dataset")  # the reference's dataset.py
+    res = {}
+    with tempfile.TemporaryDirectory() as root:
+        cfg_dir, corpora, pp, tc = make_corpora(root, seed=0)
+        dsets = []
+        for corpus in corpora:  # train.py:36-47
+            cfg = dict(corpus)
+            cfg["preprocessing"] = dict(pp, text=corpus["text"], accent=corpus["accent"])
+            dsets.append(ds_mod.Dataset("train.txt", cfg, tc, sort=True, drop_last=True))
+        concat = ds_mod.ConcatDataset(cfg_dir, dsets)
+        order = np.random.default_rng(1).permutation(len(concat))
+        res["order"] = order
+        draws = [order[:16], order[16:]]  # a loader batch of batch_size * 4, then the rest
+        cfg = dict(corpora[1])
+        cfg["preprocessing"] = dict(pp, text=corpora[1]["text"], accent=corpora[1]["accent"])
+        plain = ds_mod.Dataset("train.txt", cfg, tc, sort=False, drop_last=False)
+        runs = [("c0", concat, draws[0]), ("c1", concat, draws[1]),
+                ("p0", plain, np.arange(len(plain)))]
+        for tag, ds, idx in runs:
+            batches = ds.collate_fn([ds[int(i)] for i in idx])
+            res[f"{tag}.n"] = np.int64(len(batches))
+            for j, b in enumerate(batches):
+                for name, v in zip(BATCH_FIELDS, b):
+                    res[f"{tag}.{j}.{name}"] = np.asarray(v)
+    np.savez_compressed(os.path.join(OUT, "g8_data.npz"), **res)
+    print("g8:", {k: v for k, v in res.items() if k.endswith(".n")})
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
+    if "--only-g8" in sys.argv:
+        sys.path.insert(0, REF)
+        sys.dont_write_bytecode = True
+        for n in ("unidecode", "inflect"):
+            sys.modules.setdefault(n, types.ModuleType(n))
+        sys.modules["unidecode"].unidecode = lambda s: s
+        sys.modules["inflect"].engine = lambda: None
+        g8()
+        return
     fs2, loss_mod, mods, layers = import_reference()
     no_dropout()
     torch.set_num_threads(8)
@@ -376,6 +427,7 @@ def main():
     g4(fs2, loss_mod, mods, layers)
     g6(fs2, loss_mod)
     g7(fs2)
+    g8()
     sizes = [(3, 16), (8, 32)] + ([(48, 128)] if "--full" in sys.argv else [])
     for B, Ts in sizes:
         g5(fs2, loss_mod, B, Ts)

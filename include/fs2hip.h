@@ -39,7 +39,11 @@ enum {
   FS2_EPI_ADD_AUX = 4,       /* y += aux[m, n]   (residual-gradient fusion)    */
   FS2_EPI_RELU_MASK_AUX = 8, /* y *= (aux[m, n] > 0)   (ReLU backward fusion)  */
   FS2_EPI_OUT_BF16 = 16,     /* bf16 path: store y as bf16 (default fp32)       */
-  FS2_EPI_AUX_BF16 = 32      /* bf16 path: aux is bf16 (default fp32)           */
+  FS2_EPI_AUX_BF16 = 32,     /* bf16 path: aux is bf16 (default fp32)           */
+  /* fs2_conv_gemm_ex only (vocoder, hifigan/models.py), applied after BIAS / ADD_AUX:  */
+  FS2_EPI_LRELU = 64,        /* y = y >= 0 ? y : alpha * y                      */
+  FS2_EPI_ACC_Y = 128,       /* y = (y + y_old[m, n]) * scale  (y read, then written) */
+  FS2_EPI_Y2 = 256           /* y2[m, n] = y >= 0 ? y : alpha2 * y  (compute dtype) */
 };
 
 const char* fs2_last_error(void);
@@ -65,6 +69,37 @@ int fs2_conv_gemm(int dtype, const void* x, int64_t ldx, const void* wk, void* y
                   int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out, int taps, int pad,
                   const int64_t* lens, const float* bias, int flags, const void* aux,
                   int64_t ld_aux, void* stream);
+
+/* Dilated Conv1d with the vocoder epilogue (HiFi-GAN generator, hifigan/models.py:19-178):
+ *   v[r, o] = sum_{j, c} wk[o, j*c_in + c] * x[r + j*dilation - pad, c]   (zero outside the
+ *   utterance of seq_len rows), then BIAS, ADD_AUX, ACC_Y, LRELU in that order; y stored
+ *   (skipped when y is NULL) and, with FS2_EPI_Y2, a second output y2 = leaky_relu(v, alpha2)
+ *   in the compute dtype (bf16 for FS2_BF16, fp32 for FS2_F32; ld = c_out): the input copy
+ *   of the next convolution (models.py:95-97,157,167).  pad <= (taps-1)*dilation.
+ *   ConvTranspose1d(k = 2s, stride s, pad s/2) runs as taps=3, pad=1 over s*c_out phase
+ *   columns (see fs2_convT_weight_prep).  fs2_conv_gemm(...) == fs2_conv_gemm_ex(...,
+ *   dilation 1, alpha 0, scale 1, y2 NULL, alpha2 0).                                   */
+int fs2_conv_gemm_ex(int dtype, const void* x, int64_t ldx, const void* wk, void* y, int64_t ldy,
+                     int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out, int taps, int pad,
+                     int dilation, const float* bias, int flags, const void* aux, int64_t ld_aux,
+                     float alpha, float scale, void* y2, float alpha2, void* stream);
+
+/* ConvTranspose1d(c_in -> c_out, k = 2*stride, stride, padding = stride/2) weight
+ * w (c_in, c_out, k) (hifigan/models.py:127-137) as the equivalent 3-tap Conv1d weight
+ * wc (stride*c_out, c_in, 3) over input frames q-1, q, q+1 producing output samples
+ * stride*q + ph (column ph*c_out + o):
+ *   wc[ph*c_out + o, c, d+1] = w[c, o, ph + stride/2 - stride*d]  if that tap is in [0, k)
+ * (else 0), and bias_c[ph*c_out + o] = bias[o].  Feed wc to fs2_conv_weight_prep.        */
+int fs2_convT_weight_prep(const float* w, const float* bias, int64_t c_in, int64_t c_out,
+                          int stride, float* wc, float* bias_c, void* stream);
+
+/* HiFi-GAN output head (hifigan/models.py:167-169, utils/model.py:74-90):
+ *   wav[r] = tanh(bias + sum_{j<7, c} w[0, c, j] * x[r + j - 3, c])   (zero outside the
+ *   utterance), x (rows, c_in) in the compute dtype; wav fp32 and, when pcm is not NULL,
+ *   pcm[r] = (int16) (wav[r] * max_wav_value) truncated toward zero as numpy's astype.      */
+int fs2_vocoder_post(int dtype, const void* x, int64_t rows, int64_t seq_len, int64_t c_in,
+                     const float* w, const float* bias, float max_wav_value, float* wav,
+                     int16_t* pcm, void* stream);
 
 /* Weight re-layout (and cast for bf16) of a (c_out, c_in, taps) fp32 master weight:
  *   w_fwd[o, j*c_in + c]        = w[o, c, j]

@@ -51,15 +51,24 @@ int colsum_final_multi_launch(const ColsumJobs& jobs, hipStream_t st);
 int colsum_launch(const float* x, int64_t ldx, int64_t rows, int64_t cols, float* out, int acc,
                   float* ws, hipStream_t st);
 
+// vocoder extension of the conv epilogue (fs2_conv_gemm_ex): tap dilation, leaky-ReLU slope,
+// ACC_Y scale, second output y2 (compute dtype, ld = c_out) with its own slope
+struct VocEpi {
+  int dil = 1;
+  float alpha = 0.f, scale = 1.f;
+  void* y2 = nullptr;
+  float alpha2 = 0.f;
+};
+
 // bf16 launchers (gemm_bf16.hip)
 int conv_gemm_bf16_launch(const void* x, int64_t ldx, const void* wk, void* y, int64_t ldy,
                           int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out, int taps,
                           int pad, const int64_t* lens, const float* bias, int flags,
-                          const void* aux, int64_t ld_aux, hipStream_t st);
+                          const void* aux, int64_t ld_aux, const VocEpi& ve, hipStream_t st);
 int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, int64_t ldy,
                           int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out, int taps,
                           int pad, const int64_t* lens, const float* bias, int flags,
-                          const void* aux, int64_t ld_aux, hipStream_t st);
+                          const void* aux, int64_t ld_aux, const VocEpi& ve, hipStream_t st);
 int conv_wgrad_glds_launch(const void* dy, int64_t ldy, const void* x, int64_t ldx, float* dw,
                            float* db, int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out,
                            int taps, int pad, const int64_t* lens, int splits, int tile, float* ws,

@@ -28,6 +28,10 @@ struct ConvArgs {
   int flags;
   const float* aux;
   int64_t ld_aux;
+  int dil;                 // tap dilation (vocoder); 1 elsewhere
+  float alpha, scale;      // FS2_EPI_LRELU slope, FS2_EPI_ACC_Y scale
+  float* y2;               // FS2_EPI_Y2 output (ld = N)
+  float alpha2;
 };
 
 // A-operand loader of the NT kernel: 4 consecutive k of row m with the tap shift applied.
@@ -37,7 +41,7 @@ FS2_DEV f32x4 load_conv_a(const ConvArgs& a, int64_t m, int k) {
   int j = k / a.Cin;
   int c = k - j * a.Cin;
   int64_t s = m / a.T;
-  int64_t t = m - s * a.T + j - a.pad;
+  int64_t t = m - s * a.T + (int64_t)j * a.dil - a.pad;
   if (t < 0 || t >= a.T) return z;
   return ld4(a.x + (s * a.T + t) * a.ldx + c);
 }
@@ -135,9 +139,12 @@ __global__ __launch_bounds__(256) void conv_gemm_nt_f32(ConvArgs a) {
         if (m >= a.M) continue;
         float v = acc[i][j][r] + bv;
         if (a.flags & FS2_EPI_ADD_AUX) v += a.aux[m * a.ld_aux + n];
+        if (a.flags & FS2_EPI_ACC_Y) v = (v + a.y[m * a.ldy + n]) * a.scale;
         if (a.flags & FS2_EPI_RELU) v = fmaxf(v, 0.f);
+        if (a.flags & FS2_EPI_LRELU) v = v >= 0.f ? v : a.alpha * v;
         if (a.flags & FS2_EPI_RELU_MASK_AUX) v = a.aux[m * a.ld_aux + n] > 0.f ? v : 0.f;
-        a.y[m * a.ldy + n] = v;
+        if (a.y) a.y[m * a.ldy + n] = v;
+        if (a.flags & FS2_EPI_Y2) a.y2[m * a.N + n] = v >= 0.f ? v : a.alpha2 * v;
       }
     }
 }
@@ -406,19 +413,24 @@ using namespace fs2;
 
 extern "C" {
 
-int fs2_conv_gemm(int dtype, const void* x, int64_t ldx, const void* wk, void* y, int64_t ldy,
-                  int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out, int taps, int pad,
-                  const int64_t* lens, const float* bias, int flags, const void* aux,
-                  int64_t ld_aux, void* stream) {
-  FS2_CHECK_ARG(rows >= 0 && seq_len > 0 && taps >= 1 && pad >= 0 && pad < taps,
-                "fs2_conv_gemm: bad geometry");
+int fs2_conv_gemm_ex(int dtype, const void* x, int64_t ldx, const void* wk, void* y, int64_t ldy,
+                     int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out, int taps, int pad,
+                     int dilation, const float* bias, int flags, const void* aux, int64_t ld_aux,
+                     float alpha, float scale, void* y2, float alpha2, void* stream) {
+  FS2_CHECK_ARG(rows >= 0 && seq_len > 0 && taps >= 1 && dilation >= 1 && pad >= 0 &&
+                    pad <= (taps - 1) * dilation,
+                "fs2_conv_gemm: bad geometry (taps %d, pad %d, dilation %d)", taps, pad, dilation);
   FS2_CHECK_ARG(!(flags & FS2_EPI_BIAS) || bias, "fs2_conv_gemm: bias flag without bias");
   FS2_CHECK_ARG(!(flags & (FS2_EPI_ADD_AUX | FS2_EPI_RELU_MASK_AUX)) || aux,
                 "fs2_conv_gemm: aux flag without aux");
+  FS2_CHECK_ARG(!(flags & FS2_EPI_Y2) || y2, "fs2_conv_gemm: Y2 flag without y2");
+  FS2_CHECK_ARG(!(flags & FS2_EPI_ACC_Y) || y, "fs2_conv_gemm: ACC_Y needs y");
+  FS2_CHECK_ARG(y || (flags & FS2_EPI_Y2), "fs2_conv_gemm: no output");
   if (rows == 0) return FS2_OK;
+  const VocEpi ve{dilation, alpha, scale, y2, alpha2};
   if (dtype == FS2_BF16)
-    return conv_gemm_bf16_launch(x, ldx, wk, y, ldy, rows, seq_len, c_in, c_out, taps, pad, lens,
-                                 bias, flags, aux, ld_aux, as_stream(stream));
+    return conv_gemm_bf16_launch(x, ldx, wk, y, ldy, rows, seq_len, c_in, c_out, taps, pad, nullptr,
+                                 bias, flags, aux, ld_aux, ve, as_stream(stream));
   if (dtype != FS2_F32) {
     set_error("fs2_conv_gemm: dtype %d not built", dtype);
     return FS2_ERR_DTYPE;
@@ -426,7 +438,8 @@ int fs2_conv_gemm(int dtype, const void* x, int64_t ldx, const void* wk, void* y
   FS2_CHECK_ARG(!(flags & (FS2_EPI_OUT_BF16 | FS2_EPI_AUX_BF16)), "fs2_conv_gemm: bf16 flags on the fp32 path");
   FS2_CHECK_ARG(c_in % 4 == 0 && ldx % 4 == 0, "fs2_conv_gemm: c_in/ldx must be multiples of 4");
   ConvArgs a{(const float*)x, ldx, (const float*)wk, (float*)y, ldy, rows, seq_len, (int)c_in,
-             (int)c_out, taps, pad, (int)(taps * c_in), bias, flags, (const float*)aux, ld_aux};
+             (int)c_out, taps, pad, (int)(taps * c_in), bias, flags, (const float*)aux, ld_aux,
+             dilation, alpha, scale, (float*)y2, alpha2};
   hipStream_t st = as_stream(stream);
   const int64_t big = ((rows + 127) / 128) * ((c_out + 127) / 128);
   if (big >= 256) {
@@ -437,6 +450,25 @@ int fs2_conv_gemm(int dtype, const void* x, int64_t ldx, const void* wk, void* y
     conv_gemm_nt_f32<64, 64><<<grid, 256, 0, st>>>(a);
   }
   return launch_status("fs2_conv_gemm");
+}
+
+int fs2_conv_gemm(int dtype, const void* x, int64_t ldx, const void* wk, void* y, int64_t ldy,
+                  int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out, int taps, int pad,
+                  const int64_t* lens, const float* bias, int flags, const void* aux,
+                  int64_t ld_aux, void* stream) {
+  FS2_CHECK_ARG(rows >= 0 && seq_len > 0 && taps >= 1 && pad >= 0 && pad < taps,
+                "fs2_conv_gemm: bad geometry");
+  FS2_CHECK_ARG(!(flags & (FS2_EPI_LRELU | FS2_EPI_ACC_Y | FS2_EPI_Y2)),
+                "fs2_conv_gemm: vocoder epilogue flags need fs2_conv_gemm_ex");
+  FS2_CHECK_ARG(!(flags & FS2_EPI_BIAS) || bias, "fs2_conv_gemm: bias flag without bias");
+  FS2_CHECK_ARG(!(flags & (FS2_EPI_ADD_AUX | FS2_EPI_RELU_MASK_AUX)) || aux,
+                "fs2_conv_gemm: aux flag without aux");
+  if (rows == 0) return FS2_OK;
+  if (dtype == FS2_BF16)
+    return conv_gemm_bf16_launch(x, ldx, wk, y, ldy, rows, seq_len, c_in, c_out, taps, pad, lens,
+                                 bias, flags, aux, ld_aux, VocEpi{}, as_stream(stream));
+  return fs2_conv_gemm_ex(dtype, x, ldx, wk, y, ldy, rows, seq_len, c_in, c_out, taps, pad, 1,
+                          bias, flags, aux, ld_aux, 0.f, 1.f, nullptr, 0.f, stream);
 }
 
 int fs2_conv_weight_prep(int dtype, const float* w, int64_t c_out, int64_t c_in, int taps,

@@ -376,10 +376,11 @@ __global__ void colsum_partial_bf16(const u16* x, int64_t ldx, int64_t rows, int
 int conv_gemm_bf16_launch(const void* x, int64_t ldx, const void* wk, void* y, int64_t ldy,
                           int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out, int taps,
                           int pad, const int64_t* lens, const float* bias, int flags,
-                          const void* aux, int64_t ld_aux, hipStream_t st) {
-  if (!g_tune[FS2_TUNE_LEGACY_GEMM])
+                          const void* aux, int64_t ld_aux, const VocEpi& ve, hipStream_t st) {
+  const bool voc = ve.dil != 1 || (flags & (FS2_EPI_LRELU | FS2_EPI_ACC_Y | FS2_EPI_Y2)) || !y;
+  if (!g_tune[FS2_TUNE_LEGACY_GEMM] || voc)  // the round-1 kernels have no vocoder epilogue
     return conv_gemm_glds_launch(x, ldx, wk, y, ldy, rows, seq_len, c_in, c_out, taps, pad, lens,
-                                 bias, flags, aux, ld_aux, st);
+                                 bias, flags, aux, ld_aux, ve, st);
   FS2_CHECK_ARG(c_in % 8 == 0 && ldx % 8 == 0, "fs2_conv_gemm(bf16): c_in/ldx must be multiples of 8");
   ConvArgsB a{(const u16*)x, ldx, (const u16*)wk, y, ldy, rows, seq_len, (int)c_in, (int)c_out,
               taps, pad, (int)(taps * c_in), bias, flags, aux, ld_aux};

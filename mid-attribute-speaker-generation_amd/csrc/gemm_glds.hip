@@ -48,6 +48,10 @@ struct GldsArgs {
   int vec;    // 8-wide epilogue legal (N, ldy, ld_aux multiples of 8; aligned pointers)
   int group;  // n-tiles per tile group (see the block order below)
   const int64_t* lens;  // optional utterance lengths: all-padding row tiles are not computed
+  int dil;              // tap dilation (vocoder convs; 1 elsewhere)
+  float alpha, scale;   // FS2_EPI_LRELU slope, FS2_EPI_ACC_Y scale
+  u16* y2;              // FS2_EPI_Y2 bf16 output (ld = N)
+  float alpha2;
 };
 
 // Are rows [r0, r1) all padding (t >= lens[b] for r = b*T + t)?  Scalar, block-uniform.
@@ -114,7 +118,7 @@ FS2_DEV void kloop(int nk, Issue&& issue, Compute&& compute) {
 
 // Epilogue through LDS, one half (wm) at a time: bias, aux add, ReLU / ReLU-mask, bf16 cast
 // on 8-element row vectors (16-B / 32-B coalesced stores).  Shared by both NT kernels.
-template <int BM, int BN>
+template <int BM, int BN, bool VOC>
 FS2_DEV void nt_epilogue(const GldsArgs& a, f32x4 (&acc)[BM / 32][BN / 32], u16* smem, int64_t m0,
                          int n0, bool skip, int tid, int wm, int wn, int g, int r16) {
   constexpr int MI = BM / 32, NI = BN / 32;
@@ -181,12 +185,47 @@ FS2_DEV void nt_epilogue(const GldsArgs& a, f32x4 (&acc)[BM / 32][BN / 32], u16*
             }
           }
         }
+        float yo[8];
+        if (VOC && (a.flags & FS2_EPI_ACC_Y)) {
+          if (out_bf16) {
+            const uint4 raw = *reinterpret_cast<const uint4*>((const u16*)a.y + m * a.ldy + n);
+            const uint32_t wv[4] = {raw.x, raw.y, raw.z, raw.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              yo[2 * e] = __uint_as_float(wv[e] << 16);
+              yo[2 * e + 1] = __uint_as_float(wv[e] & 0xffff0000u);
+            }
+          } else {
+            const float* yp = (const float*)a.y + m * a.ldy + n;
+            const f32x4 y0 = *reinterpret_cast<const f32x4*>(yp);
+            const f32x4 y1 = *reinterpret_cast<const f32x4*>(yp + 4);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              yo[e] = y0[e];
+              yo[e + 4] = y1[e];
+            }
+          }
+        }
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           if (a.flags & FS2_EPI_ADD_AUX) v[e] += av[e];
+          if (VOC && (a.flags & FS2_EPI_ACC_Y)) v[e] = (v[e] + yo[e]) * a.scale;
           if (a.flags & FS2_EPI_RELU) v[e] = fmaxf(v[e], 0.f);
+          if (VOC && (a.flags & FS2_EPI_LRELU)) v[e] = v[e] >= 0.f ? v[e] : a.alpha * v[e];
           if (a.flags & FS2_EPI_RELU_MASK_AUX) v[e] = av[e] > 0.f ? v[e] : 0.f;
         }
+        if (VOC && (a.flags & FS2_EPI_Y2)) {
+          float w2[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) w2[e] = v[e] >= 0.f ? v[e] : a.alpha2 * v[e];
+          uint4 o;
+          o.x = (uint32_t)fbv(w2[0]) | ((uint32_t)fbv(w2[1]) << 16);
+          o.y = (uint32_t)fbv(w2[2]) | ((uint32_t)fbv(w2[3]) << 16);
+          o.z = (uint32_t)fbv(w2[4]) | ((uint32_t)fbv(w2[5]) << 16);
+          o.w = (uint32_t)fbv(w2[6]) | ((uint32_t)fbv(w2[7]) << 16);
+          *reinterpret_cast<uint4*>(a.y2 + m * a.N + n) = o;
+        }
+        if (VOC && !a.y) continue;
         if (out_bf16) {
           uint4 o;
           o.x = (uint32_t)fbv(v[0]) | ((uint32_t)fbv(v[1]) << 16);
@@ -210,8 +249,14 @@ FS2_DEV void nt_epilogue(const GldsArgs& a, f32x4 (&acc)[BM / 32][BN / 32], u16*
             av = aux_bf16 ? bfv(((const u16*)a.aux)[m * a.ld_aux + n + e])
                           : ((const float*)a.aux)[m * a.ld_aux + n + e];
           if (a.flags & FS2_EPI_ADD_AUX) x += av;
+          if (VOC && (a.flags & FS2_EPI_ACC_Y))
+            x = (x + (out_bf16 ? bfv(((const u16*)a.y)[m * a.ldy + n + e])
+                               : ((const float*)a.y)[m * a.ldy + n + e])) * a.scale;
           if (a.flags & FS2_EPI_RELU) x = fmaxf(x, 0.f);
+          if (VOC && (a.flags & FS2_EPI_LRELU)) x = x >= 0.f ? x : a.alpha * x;
           if (a.flags & FS2_EPI_RELU_MASK_AUX) x = av > 0.f ? x : 0.f;
+          if (VOC && (a.flags & FS2_EPI_Y2)) a.y2[m * a.N + n + e] = fbv(x >= 0.f ? x : a.alpha2 * x);
+          if (VOC && !a.y) continue;
           if (out_bf16) ((u16*)a.y)[m * a.ldy + n + e] = fbv(x);
           else ((float*)a.y)[m * a.ldy + n + e] = x;
         }
@@ -221,8 +266,9 @@ FS2_DEV void nt_epilogue(const GldsArgs& a, f32x4 (&acc)[BM / 32][BN / 32], u16*
   }
 }
 
-template <int BM, int BN, int STAGES, bool TAPALIGNED>
+template <int BM, int BN, int STAGES, bool TAPALIGNED, bool VOC>
 __global__ __launch_bounds__(256) void conv_gemm_nt_glds(GldsArgs a) {
+  const int dil = VOC ? a.dil : 1;
   constexpr int BK = 64;
   constexpr int AW = BM / 32, BW = BN / 32;  // glds per wave per tile (8 rows each)
   constexpr int MI = BM / 32, NI = BN / 32;  // 16x16 fragments per wave (2x2 waves)
@@ -302,7 +348,7 @@ __global__ __launch_bounds__(256) void conv_gemm_nt_glds(GldsArgs a) {
         j = k / a.Cin;
         c = k - j * a.Cin;
       }
-      const int tt = a_t[i] + j - a.pad;
+      const int tt = a_t[i] + j * dil - a.pad;
       if (kok && a_base[i] >= 0 && tt >= 0 && tt < a.T)
         src = a.x + (a_base[i] + tt) * a.ldx + c;
       glds16(src, As + (wave * AW + i) * 8 * BK);
@@ -348,7 +394,7 @@ __global__ __launch_bounds__(256) void conv_gemm_nt_glds(GldsArgs a) {
 
   if (!skip) kloop<STAGES, AW + BW>(nk, issue, compute);
 
-  nt_epilogue<BM, BN>(a, acc, smem, m0, n0, skip, tid, wm, wn, g, r16);
+  nt_epilogue<BM, BN, VOC>(a, acc, smem, m0, n0, skip, tid, wm, wn, g, r16);
 }
 
 // ------------------------------------------------------------------------ halo variant
@@ -361,11 +407,12 @@ __global__ __launch_bounds__(256) void conv_gemm_nt_glds(GldsArgs a) {
 // of a 128 x 128 tile, and that traffic, not the MFMA, bounds the tap-major kernel
 // (per-CU vector-memory rate; profiles/).  LDS rows are swizzled chunk c -> c ^ (row & 7),
 // which keeps the 16-row fragment reads conflict-free at every row offset.
-template <int BM, int BN, int BST>
-__global__ __launch_bounds__(256, BST == 1 ? 4 : 3) void conv_gemm_halo(GldsArgs a) {
+template <int BM, int BN, int BST, int HX, bool VOC>
+__global__ __launch_bounds__(256, BST == 1 ? 4 : HX > 16 ? 2 : 3) void conv_gemm_halo(GldsArgs a) {
+  const int dil = VOC ? a.dil : 1;
   constexpr int BK = 64;
   constexpr int MI = BM / 32, NI = BN / 32;
-  constexpr int HMAX = BM + 16;                     // halo rows allocated (taps <= 17)
+  constexpr int HMAX = BM + HX;                     // halo rows allocated ((taps-1)*dil <= HX)
   constexpr int QMAX = (HMAX / 8 + 3) / 4;          // 8-row halo pieces per wave
   constexpr int BW = BN / 32;                       // weight pieces per wave
   constexpr int A_E = HMAX * BK, B_E = BN * BK;
@@ -393,7 +440,7 @@ __global__ __launch_bounds__(256, BST == 1 ? 4 : 3) void conv_gemm_halo(GldsArgs
 
   const int lrow = lane >> 3;
   const u16* zero = reinterpret_cast<const u16*>(g_zero_line);
-  const int HR = BM + a.taps - 1, HP = (HR + 7) / 8;
+  const int HR = BM + (a.taps - 1) * dil, HP = (HR + 7) / 8;
   const int64_t u0 = (m0 / a.T) * a.T, u1 = u0 + a.T < a.M ? u0 + a.T : a.M;
   // halo piece p = wave + 4 q: rows h = 8 p + lrow, global row m0 - pad + h
   const u16* h_src[QMAX];
@@ -438,7 +485,7 @@ __global__ __launch_bounds__(256, BST == 1 ? 4 : 3) void conv_gemm_halo(GldsArgs
   };
   auto compute = [&](int j, int slot) {
     // fragment rows differ by multiples of 16, so one swizzle serves all of them
-    const int ha = a_row + j, sa = ha & 7;
+    const int ha = a_row + j * dil, sa = ha & 7;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       bf16x8g fa[MI], fb[NI];
@@ -495,7 +542,7 @@ __global__ __launch_bounds__(256, BST == 1 ? 4 : 3) void conv_gemm_halo(GldsArgs
       __builtin_amdgcn_s_barrier();
     }
   }
-  nt_epilogue<BM, BN>(a, acc, smem, m0, n0, skip, tid, wm, wn, g, r16);
+  nt_epilogue<BM, BN, VOC>(a, acc, smem, m0, n0, skip, tid, wm, wn, g, r16);
 }
 
 // ------------------------------------------------------------------------ weight gradient
@@ -837,20 +884,26 @@ int conv_wgrad_glds_launch(const void* dy, int64_t ldy, const void* x, int64_t l
 
 
 template <int BM, int BN, int S>
-static void launch_nt(GldsArgs a, bool tapaligned, hipStream_t st) {
+static void launch_nt(GldsArgs a, bool tapaligned, bool voc, hipStream_t st) {
   // n-tiles per group: all of them by default (measured: smaller weight-slice groups did not
   // pay on the step's shapes and multiplied the A re-reads of the long-K data gradient)
   const int g = g_tune[FS2_TUNE_NT_GROUP] > 0 ? g_tune[FS2_TUNE_NT_GROUP] : a.tiles_n;
   a.group = g > a.tiles_n ? a.tiles_n : g;
   const unsigned grid = (unsigned)(a.tiles_m * a.tiles_n);
-  if (tapaligned) conv_gemm_nt_glds<BM, BN, S, true><<<grid, 256, 0, st>>>(a);
-  else conv_gemm_nt_glds<BM, BN, S, false><<<grid, 256, 0, st>>>(a);
+  if (voc) {  // vocoder convs: one pipeline depth, dilation + the extended epilogue
+    if (tapaligned) conv_gemm_nt_glds<BM, BN, 2, true, true><<<grid, 256, 0, st>>>(a);
+    else conv_gemm_nt_glds<BM, BN, 2, false, true><<<grid, 256, 0, st>>>(a);
+  } else if (tapaligned) {
+    conv_gemm_nt_glds<BM, BN, S, true, false><<<grid, 256, 0, st>>>(a);
+  } else {
+    conv_gemm_nt_glds<BM, BN, S, false, false><<<grid, 256, 0, st>>>(a);
+  }
 }
 
 int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, int64_t ldy,
                           int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out, int taps,
                           int pad, const int64_t* lens, const float* bias, int flags,
-                          const void* aux, int64_t ld_aux, hipStream_t st) {
+                          const void* aux, int64_t ld_aux, const VocEpi& ve, hipStream_t st) {
   FS2_CHECK_ARG(c_in % 8 == 0 && ldx % 8 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)wk & 15) == 0,
                 "fs2_conv_gemm(bf16): c_in/ldx must be multiples of 8 and operands 16-B aligned");
   const int K = (int)(taps * c_in);
@@ -861,37 +914,48 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
   const bool uses_aux = flags & (FS2_EPI_ADD_AUX | FS2_EPI_RELU_MASK_AUX);
   const int vec = c_out % 8 == 0 && ldy % 8 == 0 && ((uintptr_t)y % 16) == 0 &&
                   (!(flags & FS2_EPI_BIAS) || ((uintptr_t)bias % 16) == 0) &&
-                  (!uses_aux || (ld_aux % 8 == 0 && ((uintptr_t)aux % 16) == 0));
+                  (!uses_aux || (ld_aux % 8 == 0 && ((uintptr_t)aux % 16) == 0)) &&
+                  (!(flags & FS2_EPI_Y2) || ((uintptr_t)ve.y2 % 16) == 0);
   GldsArgs a{(const u16*)x, ldx, (const u16*)wk, y, ldy, rows, seq_len, (int)c_in, (int)c_out,
-             taps, pad, K, bias, flags, aux, ld_aux, 0, 0, vec, 1, lens};
+             taps, pad, K, bias, flags, aux, ld_aux, 0, 0, vec, 1, lens,
+             ve.dil, ve.alpha, ve.scale, (u16*)ve.y2, ve.alpha2};
   const bool tapaligned = c_in % 64 == 0;
+  const bool voc = ve.dil != 1 || (flags & (FS2_EPI_LRELU | FS2_EPI_ACC_Y | FS2_EPI_Y2)) || !y;
   const int64_t big = ((rows + 127) / 128) * ((c_out + 127) / 128);
 #define FS2_NT(BM_, BN_)                                                  \
   switch (stages) {                                                       \
-    case 2: launch_nt<BM_, BN_, 2>(a, tapaligned, st); break;             \
-    case 3: launch_nt<BM_, BN_, 3>(a, tapaligned, st); break;             \
-    case 4: launch_nt<BM_, BN_, 4>(a, tapaligned, st); break;             \
-    default: launch_nt<BM_, BN_, 1>(a, tapaligned, st);                   \
+    case 2: launch_nt<BM_, BN_, 2>(a, tapaligned, voc, st); break;        \
+    case 3: launch_nt<BM_, BN_, 3>(a, tapaligned, voc, st); break;        \
+    case 4: launch_nt<BM_, BN_, 4>(a, tapaligned, voc, st); break;        \
+    default: launch_nt<BM_, BN_, 1>(a, tapaligned, voc, st);              \
   }
   // halo kernel (tile sizes as the tap-major choice below: 128x128 / 128x64 / 64x64 by grid;
   // FS2_TUNE_NT_HALO = 2 forces 128 x 128).  Every row tile must lie inside one utterance.
   const bool halo_wide = big >= 512 || g_tune[FS2_TUNE_NT_HALO] == 2;
   const int halo_bm = halo_wide || big >= 128 ? 128 : 64;
-  if (taps > 1 && taps <= 17 && tapaligned && seq_len % halo_bm == 0 &&
+  if (taps > 1 && (taps - 1) * ve.dil <= 64 && tapaligned && seq_len % halo_bm == 0 &&
       g_tune[FS2_TUNE_NT_HALO] >= 0) {
     a.tiles_m = (int)((rows + halo_bm - 1) / halo_bm);
     a.tiles_n = (int)((c_out + (halo_wide ? 127 : 63)) / (halo_wide ? 128 : 64));
     a.group = a.tiles_n;
     const unsigned grid = (unsigned)(a.tiles_m * a.tiles_n);
+    // HX: halo rows beyond the tile, 16 (taps <= 17 undilated: the FFT/PostNet/VP convs) or
+    // 64 (dilated vocoder convs; the larger A image leaves 2 blocks per CU)
+    const bool hx64 = (taps - 1) * ve.dil > 16;
+#define FS2_HALO(BM_, BN_, BST_)                                                    \
+  if (hx64) conv_gemm_halo<BM_, BN_, 2, 64, true><<<grid, 256, 0, st>>>(a);        \
+  else if (voc) conv_gemm_halo<BM_, BN_, 2, 16, true><<<grid, 256, 0, st>>>(a);    \
+  else conv_gemm_halo<BM_, BN_, BST_, 16, false><<<grid, 256, 0, st>>>(a);
     if (g_tune[FS2_TUNE_NT_HALO] == 3) {  // single-buffered weight tile (A/B experiments)
-      if (halo_wide) conv_gemm_halo<128, 128, 1><<<grid, 256, 0, st>>>(a);
-      else if (halo_bm == 128) conv_gemm_halo<128, 64, 1><<<grid, 256, 0, st>>>(a);
-      else conv_gemm_halo<64, 64, 1><<<grid, 256, 0, st>>>(a);
+      if (halo_wide) { FS2_HALO(128, 128, 1) }
+      else if (halo_bm == 128) { FS2_HALO(128, 64, 1) }
+      else { FS2_HALO(64, 64, 1) }
     } else {
-      if (halo_wide) conv_gemm_halo<128, 128, 2><<<grid, 256, 0, st>>>(a);
-      else if (halo_bm == 128) conv_gemm_halo<128, 64, 2><<<grid, 256, 0, st>>>(a);
-      else conv_gemm_halo<64, 64, 2><<<grid, 256, 0, st>>>(a);
+      if (halo_wide) { FS2_HALO(128, 128, 2) }
+      else if (halo_bm == 128) { FS2_HALO(128, 64, 2) }
+      else { FS2_HALO(64, 64, 2) }
     }
+#undef FS2_HALO
   } else if (big >= 512) {
     a.tiles_m = (int)((rows + 127) / 128);
     a.tiles_n = (int)((c_out + 127) / 128);

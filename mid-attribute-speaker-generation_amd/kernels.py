@@ -18,6 +18,7 @@ F32 = 0
 BF16 = 1
 F64 = 2
 EPI_BIAS, EPI_RELU, EPI_ADD_AUX, EPI_RELU_MASK_AUX, EPI_OUT_BF16, EPI_AUX_BF16 = 1, 2, 4, 8, 16, 32
+EPI_LRELU, EPI_ACC_Y, EPI_Y2 = 64, 128, 256
 _CODE = {torch.float32: F32, torch.bfloat16: BF16}
 
 
@@ -89,6 +90,53 @@ def conv_gemm(x, wk, rows, seq_len, c_in, c_out, taps, pad, bias=None, flags=0, 
                       c_in, c_out, taps, pad, ptr(lens), ptr(bias), flags, ptr(aux), c_out,
                       stream())
     return out
+
+
+def conv_gemm_ex(x, wk, rows, seq_len, c_in, c_out, taps, pad, dilation=1, bias=None, flags=0,
+                 aux=None, out=None, y2=None, alpha=0.1, scale=1.0, alpha2=0.1):
+    """Dilated conv with the vocoder epilogue (fs2_conv_gemm_ex): out and/or y2 (the
+    leaky-ReLU'd compute copy, dtype of x) must be given; ACC_Y reads ``out`` first."""
+    _dev(x, wk, bias, aux, out, y2)
+    if x.dtype != wk.dtype:
+        raise RuntimeError(f"conv_gemm_ex operand dtypes differ: {x.dtype} vs {wk.dtype}")
+    if out is None and y2 is None:
+        raise RuntimeError("conv_gemm_ex: give out and/or y2")
+    if y2 is not None:
+        if y2.dtype != x.dtype or y2.shape != (rows, c_out):
+            raise RuntimeError("conv_gemm_ex: y2 must be (rows, c_out) in the compute dtype")
+        flags |= EPI_Y2
+    if bias is not None:
+        flags |= EPI_BIAS
+    if out is not None and out.dtype == torch.bfloat16:
+        flags |= EPI_OUT_BF16
+    if aux is not None and aux.dtype == torch.bfloat16:
+        flags |= EPI_AUX_BF16
+    lib.fs2_conv_gemm_ex(code(x.dtype), ptr(x), c_in, ptr(wk), ptr(out), c_out, rows, seq_len,
+                         c_in, c_out, taps, pad, dilation, ptr(bias), flags, ptr(aux), c_out,
+                         alpha, scale, ptr(y2), alpha2, stream())
+    return out, y2
+
+
+def convT_weight_prep(w, bias, stride):
+    """ConvTranspose1d (c_in, c_out, 2*stride) weight -> (stride*c_out, c_in, 3) conv weight
+    and the phase-tiled bias (fs2_convT_weight_prep)."""
+    _dev(w, bias)
+    c_in, c_out, k = w.shape
+    if k != 2 * stride:
+        raise RuntimeError(f"convT_weight_prep: kernel {k} != 2 * stride {stride}")
+    wc = torch.empty(stride * c_out, c_in, 3, dtype=torch.float32, device=w.device)
+    bc = torch.empty(stride * c_out, dtype=torch.float32, device=w.device)
+    lib.fs2_convT_weight_prep(ptr(w), ptr(bias), c_in, c_out, stride, ptr(wc), ptr(bc), stream())
+    return wc, bc
+
+
+def vocoder_post(x, rows, seq_len, c_in, w, bias, max_wav_value=32768.0, pcm=True):
+    _dev(x, w, bias)
+    wav = torch.empty(rows, dtype=torch.float32, device=x.device)
+    p = torch.empty(rows, dtype=torch.int16, device=x.device) if pcm else None
+    lib.fs2_vocoder_post(code(x.dtype), ptr(x), rows, seq_len, c_in, ptr(w), ptr(bias),
+                         max_wav_value, ptr(wav), ptr(p), stream())
+    return wav, p
 
 
 def weight_prep(w, c_out, c_in, taps, w_fwd=None, w_bwd=None):

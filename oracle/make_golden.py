@@ -26,6 +26,9 @@ Fixtures:
                    tests/synth_corpus.py (one corpus with accent files, one without): two
                    sorted/drop-last draws through the concatenation (14-tuples) and the
                    accent-free corpus alone unsorted with its tail kept (13-tuples)
+  g9_hifigan.npz   HiFi-GAN generator (hifigan/models.py, config.json V1) after
+                   remove_weight_norm with name-seeded weights: waveform and the int16 PCM of
+                   vocoder_infer for a seeded (2, 80, 24) mel, and one utterance of 37 frames
 """
 import importlib
 import os
@@ -403,8 +406,38 @@ def g8():
     print("g8:", {k: v for k, v in res.items() if k.endswith(".n")})
 
 
+def g9():
+    import json
+    hf = importlib.import_module("hifigan")
+    with open(os.path.join(REF, "hifigan", "config.json")) as f:
+        h = hf.AttrDict(json.load(f))
+    gen = hf.Generator(h)
+    gen.eval()
+    gen.remove_weight_norm()
+    seeded(gen)
+    sd = gen.state_dict()
+    res = {"keys": np.array(list(sd.keys())),
+           "shapes": np.array([",".join(map(str, v.shape)) for v in sd.values()])}
+    rng = np.random.default_rng(9)
+    for tag, (B, T) in (("a", (2, 24)), ("b", (1, 37))):
+        mel = torch.from_numpy((rng.standard_normal((B, 80, T)) * 2 - 5).astype(np.float32))
+        with torch.no_grad():
+            wav = gen(mel).squeeze(1)
+        res[f"{tag}.mel"] = mel.numpy()
+        res[f"{tag}.wav"] = wav.numpy()
+        res[f"{tag}.pcm"] = (wav.numpy() * 32768.0).astype("int16")  # utils/model.py:84-88
+    np.savez_compressed(os.path.join(OUT, "g9_hifigan.npz"), **res)
+    print("g9:", {k: v.shape for k, v in res.items()})
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
+    if "--only-g9" in sys.argv:
+        sys.path.insert(0, REF)
+        sys.dont_write_bytecode = True
+        torch.set_num_threads(8)
+        g9()
+        return
     if "--only-g8" in sys.argv:
         sys.path.insert(0, REF)
         sys.dont_write_bytecode = True
@@ -428,6 +461,7 @@ def main():
     g6(fs2, loss_mod)
     g7(fs2)
     g8()
+    g9()
     sizes = [(3, 16), (8, 32)] + ([(48, 128)] if "--full" in sys.argv else [])
     for B, Ts in sizes:
         g5(fs2, loss_mod, B, Ts)

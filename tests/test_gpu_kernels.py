@@ -562,3 +562,54 @@ def test_batchnorm_dropout(c, act):
     close(dz, zr.grad)
     close(dg, gr.grad)
     close(db, br.grad)
+
+
+@pytest.mark.parametrize("B,T,C,k,d", [(2, 192, 256, 3, 5), (2, 192, 256, 7, 3),
+                                       (1, 300, 256, 11, 5), (2, 128, 64, 11, 5),
+                                       (3, 100, 32, 7, 5)])
+def test_conv_gemm_ex_dilated_epilogues(B, T, C, k, d):
+    """fs2_conv_gemm_ex (vocoder convs): dilated taps on the halo and tap-major kernels (bf16)
+    and the fp32 kernel, with the LRELU / ADD_AUX / ACC_Y / Y2 epilogue, against torch."""
+    pad = d * (k - 1) // 2
+    xs = rnd(B * T, C, seed=51)
+    w = bf(rnd(C, C, k, scale=1 / math.sqrt(C * k), seed=52)).float()
+    b = rnd(C, seed=53) * 0.1
+    aux, y_old = rnd(B * T, C, seed=54), rnd(B * T, C, seed=55)
+    conv = F.conv1d(bf(xs).float().view(B, T, C).transpose(1, 2), w, b, padding=pad,
+                    dilation=d).transpose(1, 2).reshape(B * T, C)
+    v = (conv + aux + y_old) * (1 / 3)
+    want_y = torch.where(v >= 0, v, 0.1 * v)
+    want_y2 = torch.where(want_y >= 0, want_y, 0.01 * want_y)
+    flags = K.EPI_LRELU | K.EPI_ADD_AUX | K.EPI_ACC_Y
+    for dt, tol in ((torch.bfloat16, 1e-5), (torch.float32, 1e-5)):
+        x = bf(xs) if dt == torch.bfloat16 else bf(xs).float()
+        wf = torch.empty(C * C * k, dtype=dt, device=DEV)
+        K.weight_prep(w, C, C, k, w_fwd=wf)
+        for mode in ((0, -1) if dt == torch.bfloat16 else (0,)):
+            K.lib.fs2_set_tuning(6, mode)
+            try:
+                y = y_old.clone()
+                y2 = torch.empty(B * T, C, dtype=dt, device=DEV)
+                K.conv_gemm_ex(x, wf, B * T, T, C, C, k, pad, dilation=d, bias=b, flags=flags,
+                               aux=aux, out=y, y2=y2, alpha=0.1, scale=1 / 3, alpha2=0.01)
+            finally:
+                K.lib.fs2_set_tuning(6, 0)
+            close(y, want_y, tol)
+            close(y2.float(), want_y2, 8e-3 if dt == torch.bfloat16 else tol)
+
+
+def test_convT_as_phase_conv():
+    """ConvTranspose1d(k = 2s, stride s, pad s/2) == the 3-tap phase conv of
+    fs2_convT_weight_prep, whose (rows, s*c_out) output is the (rows*s, c_out) signal."""
+    for s, cin, cout, B, T in ((8, 128, 64, 2, 20), (2, 64, 32, 3, 33)):
+        w = rnd(cin, cout, 2 * s, scale=0.1, seed=61)
+        b = rnd(cout, seed=62)
+        x = rnd(B * T, cin, seed=63)
+        want = F.conv_transpose1d(x.view(B, T, cin).transpose(1, 2), w, b, stride=s,
+                                  padding=s // 2).transpose(1, 2).reshape(B * T * s, cout)
+        wc, bc = K.convT_weight_prep(w, b, s)
+        wf = torch.empty(s * cout * cin * 3, dtype=torch.float32, device=DEV)
+        K.weight_prep(wc, s * cout, cin, 3, w_fwd=wf)
+        y = torch.empty(B * T * s, cout, device=DEV)
+        K.conv_gemm_ex(x, wf, B * T, T, cin, s * cout, 3, 1, bias=bc, out=y.view(B * T, s * cout))
+        close(y, want, 1e-5)

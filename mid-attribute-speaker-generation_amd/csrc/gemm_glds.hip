@@ -929,6 +929,24 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
     case 4: launch_nt<BM_, BN_, 4>(a, tapaligned, voc, st); break;        \
     default: launch_nt<BM_, BN_, 1>(a, tapaligned, voc, st);              \
   }
+  // narrow vocoder convs (HiFi-GAN's 64- and 32-channel stages, millions of rows): the
+  // n-tile matches c_out instead of wasting 1/2-3/4 of a 128-wide tile's MFMAs
+  if (voc && c_out <= 64 && big >= 128) {
+    a.tiles_m = (int)((rows + 127) / 128);
+    a.tiles_n = 1;
+    a.group = 1;
+    const unsigned grid = (unsigned)a.tiles_m;
+    if (c_out <= 32) {
+      launch_nt<128, 32, 2>(a, tapaligned, true, st);
+    } else if (taps > 1 && (taps - 1) * ve.dil <= 64 && tapaligned && seq_len % 128 == 0 &&
+               g_tune[FS2_TUNE_NT_HALO] >= 0) {
+      if ((taps - 1) * ve.dil > 16) conv_gemm_halo<128, 64, 2, 64, true><<<grid, 256, 0, st>>>(a);
+      else conv_gemm_halo<128, 64, 2, 16, true><<<grid, 256, 0, st>>>(a);
+    } else {
+      launch_nt<128, 64, 2>(a, tapaligned, true, st);
+    }
+    return launch_status("fs2_conv_gemm(bf16)");
+  }
   // halo kernel (tile sizes as the tap-major choice below: 128x128 / 128x64 / 64x64 by grid;
   // FS2_TUNE_NT_HALO = 2 forces 128 x 128).  Every row tile must lie inside one utterance.
   const bool halo_wide = big >= 512 || g_tune[FS2_TUNE_NT_HALO] == 2;

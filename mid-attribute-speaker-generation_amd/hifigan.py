@@ -235,8 +235,7 @@ def vocoder_infer(mels, vocoder, model_config, preprocess_config, lengths=None):
     each cropped to ``lengths[i]`` samples when given."""
     B, C, T = mels.shape
     rows = mels.transpose(1, 2).contiguous().reshape(B * T, C)
-    max_wav = preprocess_config["preprocessing"]["audio"]["max_wav_value"] \
-        if "preprocessing" in preprocess_config else preprocess_config["audio"]["max_wav_value"]
+    max_wav = preprocess_config["audio"]["max_wav_value"]  # utils/model.py:84-86
     _, pcm = vocoder.forward_rows(rows, B, T, pcm=True, max_wav_value=float(max_wav))
     wavs = list(pcm.view(B, -1).cpu().numpy())
     if lengths is not None:

@@ -105,3 +105,32 @@ def test_vocoder_lengths_crop_and_batch_independence():
     assert np.abs(full[1].astype(np.int32) - one.astype(np.int32)).max() <= 1
     cropped = HG.vocoder_infer(mel, gen, None, pp, lengths=[1000, 2500])
     assert [len(w) for w in cropped] == [1000, 2500]
+
+
+@pytest.mark.gpu
+def test_synthesize_end_to_end():
+    """synthesize.py flow: text batch -> eval-mode FastSpeech2 (predicted durations) ->
+    HiFi-GAN on the PostNet rows -> int16 PCM cropped to mel_len * hop_length; equal to
+    vocoder_infer on the (B, 80, T) transpose, as utils/tools.py:264-270 calls it."""
+    M = importlib.import_module("mid-attribute-speaker-generation_amd.model")
+    SY = importlib.import_module("mid-attribute-speaker-generation_amd.synthesize")
+    DS = importlib.import_module("mid-attribute-speaker-generation_amd.dataset")
+    pp, mc, tc, path = PKG.config.load_configs("JVS-VCTK")
+    model = M.FastSpeech2(pp, mc, path, device="cuda", compute_dtype=torch.float32)
+    PKG.seeded.load_seeded_(model)
+    with torch.no_grad():
+        model.state_dict()["variance_adaptor.duration_predictor.linear_layer.bias"].fill_(1.0)
+    model.eval()
+    voc, _ = _gpu_gen(torch.float32)
+    b = PKG.data.syn_batch(3, 16, seed=4)
+    text = (b[0], b[1], b[2], b[3], b[4], b[5], b[12], b[13])
+    (ids, wavs), = SY.synthesize(model, (pp, mc, tc), voc, [text], (1.0, 1.0, 1.0))
+    assert list(ids) == list(b[0])
+    with torch.no_grad():
+        dev_b = DS.to_device(text, "cuda")
+        out = model(*dev_b[2:6], accents=dev_b[7], speaker_meta=dev_b[6])
+    lengths = (out[9] * 256).tolist()
+    assert [len(w) for w in wavs] == lengths and min(lengths) > 0
+    ref = HG.vocoder_infer(out[1].transpose(1, 2), voc, mc, pp, lengths=lengths)
+    for w, r in zip(wavs, ref):
+        assert np.abs(w.astype(np.int32) - r.astype(np.int32)).max() <= 1

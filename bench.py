@@ -194,6 +194,9 @@ def main():
     ap.add_argument("--graph", action="store_true",
                     help="N=1: capture the step once into a HIP graph and replay it (measured "
                          "slower than eager here: replay serialises the weight-gradient stream)")
+    ap.add_argument("--use-clf", action="store_true",
+                    help="BASELINE config 3: the --use_clf step (second forward with shuffled "
+                         "speakers + GE2E language discriminator on 150-frame chunks)")
     ap.add_argument("--probe-conv", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.probe_conv:
@@ -214,7 +217,21 @@ def main():
     model.train()
     model.seed(1234 + rank)
     use_graph = world == 1 and args.graph
-    trainer = TR.Trainer(model, pp, mc, tc, graph=use_graph)
+    trainer = TR.Trainer(model, pp, mc, tc, graph=use_graph and not args.use_clf)
+    if args.use_clf:
+        import random
+        G = importlib.import_module("mid-attribute-speaker-generation_amd.ge2e")
+        disc = G.SpeechEmbedder(device=dev)
+        PKG.seeded.load_seeded_(disc)
+        clf = (disc, G.GE2ELoss(dev))
+        rnd = random.Random(1234 + rank)
+        counter = [0]
+
+        def clf_kw():  # train.py:171 draws the shuffle with random.sample each step
+            counter[0] += 1
+            return {"clf": clf, "clf_args": (rnd.sample(range(args.batch), args.batch),
+                                             counter[0], tc["step"]["total_step"],
+                                             float(tc.get("lambda", 1)))}
     batch_np = PKG.data.syn_batch(args.batch, args.src_len, seed=rank)
     batch = PKG.data.to_device(batch_np, dev)
     frames_local = int(np.sum(batch_np[7]))
@@ -227,14 +244,14 @@ def main():
         timer.install()
         timer.capture = use_graph
     for _ in range(max(args.warmup, 2 if use_graph else 0)):  # graph: step 1 captures
-        trainer.step(batch)
+        trainer.step(batch, **(clf_kw() if args.use_clf else {}))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     timer.on = not use_graph
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        losses, eloss, gnorm, _ = trainer.step(batch)
+        losses, eloss, gnorm = trainer.step(batch, **(clf_kw() if args.use_clf else {}))[:3]
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -292,6 +309,7 @@ def main():
                           "valid_frames_per_rank_step": frames_local,
                           "padded_frames_per_rank_step": padded_local,
                           "parallelism": f"dp{world}",
+                          "use_clf": bool(args.use_clf),
                           "execution": "hip-graph replay" if use_graph else "eager"},
                "roofline": roof, "cpu_baseline": cpu, "final_loss": round(loss_now, 5)}
         print(json.dumps(out), flush=True)

@@ -101,6 +101,46 @@ int fs2_vocoder_post(int dtype, const void* x, int64_t rows, int64_t seq_len, in
                      const float* w, const float* bias, float max_wav_value, float* wav,
                      int16_t* pcm, void* stream);
 
+/* ---------------------------------------------------------------- language discriminator
+ * The --use_clf branch (train.py:168-197): GE2E SpeechEmbedder (speech_embedder_net.py:65-162)
+ * and GE2ELoss's BCE term (165-186), fp32.
+ * One LSTM layer (nn.LSTM, batch_first, gates i,f,g,o, h0 = c0 = 0) over n_seq sequences of
+ * `steps` rows (row n*steps + t): gx = x W_ih^T + bias (bias = b_ih + b_hh; one GEMM), then
+ * the recurrence, one launch per step issued from C.  w_ih (4H, c_in) natural, w_hh_t
+ * (H, 4H) = W_hh^T.  Saves h_all, c_all (rows, H) and the activated gates act (rows, 4H).   */
+int fs2_lstm_layer_fwd(const float* x, int64_t n_seq, int64_t steps, int64_t c_in, int64_t hidden,
+                       const float* w_ih, const float* bias, const float* w_hh_t, float* gx,
+                       float* h_all, float* c_all, float* act, void* stream);
+/* Backward through time: dh_out (rows, H; NULL = 0) is the gradient of the layer's outputs;
+ * writes dgates (rows, 4H; pre-activation gate gradients) and, when dx is given,
+ * dx = dgates W_ih (rows, c_in; w_ih_t = W_ih^T (c_in, 4H)).  dc_ws: 2*n_seq*H floats.
+ * Weight gradients are not formed (train.py never steps the discriminator).            */
+int fs2_lstm_layer_bwd(const float* dh_out, int64_t n_seq, int64_t steps, int64_t c_in,
+                       int64_t hidden, const float* w_ih_t, const float* w_hh, const float* act,
+                       const float* c_all, float* dgates, float* dc_ws, float* dx, void* stream);
+/* Embedding + domain-classifier head on the last LSTM frame (x row n at x + n*ldx, 256 wide):
+ * projection 256->64, L2 norm (emb), Linear 64->64, dropout, ReLU, Linear 64->64, dropout,
+ * ReLU, Linear 64->1 (logit).  w*t are the transposed weights (forward), w* the natural
+ * ones (backward).  With dx: dx = d(head)/dx for the given demb / dlogit (NULL = 0), the
+ * dropout masks regenerated from (seed, site).                                           */
+int fs2_clf_head(const float* x, int64_t ldx, int64_t n, const float* wp, const float* wpt,
+                 const float* bp, const float* w0, const float* w0t, const float* b0,
+                 const float* w1, const float* w1t, const float* b1, const float* w2,
+                 const float* b2, float p_drop, const uint64_t* seed, uint64_t site, float* emb,
+                 float* logit, const float* demb, const float* dlogit, float* dx, int64_t lddx,
+                 void* stream);
+/* BCEWithLogits per row (loss_rows, nullable) and dlogit = g[0] * scale * (sigmoid - y)
+ * (g nullable = 1).                                                                      */
+int fs2_bce_logits(const float* logit, const float* y, int64_t n, float* loss_rows,
+                   const float* g, float scale, float* dlogit, void* stream);
+/* (batch, t_src, c) rows -> (batch, t_dst, c): copy the first min(t_src, t_dst) frames,
+ * zero the rest (the 150-frame chunking of train.py:178-183 and its gradient).          */
+int fs2_rows_repad(const float* src, int64_t batch, int64_t t_src, int64_t t_dst, int64_t c,
+                   float* dst, void* stream);
+/* y[b*rep + k] = meta[b*ld + col] (per-chunk language labels, train.py:184).             */
+int fs2_repeat_col(const float* meta, int64_t batch, int64_t ld, int col, int rep, float* y,
+                   void* stream);
+
 /* Weight re-layout (and cast for bf16) of a (c_out, c_in, taps) fp32 master weight:
  *   w_fwd[o, j*c_in + c]        = w[o, c, j]
  *   w_bwd[c, j*c_out + o]       = w[o, c, taps-1-j]      (either output may be NULL)     */

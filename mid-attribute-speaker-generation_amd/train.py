@@ -1,5 +1,5 @@
-"""The training step of ``train.py:134-206`` (``use_clf`` off, ``grad_acc_step`` 1) and its
-data-parallel form.
+"""The training step of ``train.py:134-206`` (``grad_acc_step`` 1; ``use_clf`` optional) and
+its data-parallel form.
 
 Single process: ``train_step`` is line-for-line the reference's step semantics
 (forward, FastSpeech2Loss backward, negated speaker-prior log-likelihood backward,
@@ -23,17 +23,49 @@ from .loss import FastSpeech2Loss, SpeakerMetaEncLoss
 from .optimizer import ScheduledOptim
 
 
-def train_step(model, optimizer, Loss, eLoss, batch, grad_clip_thresh=1.0, grad_sync=None):
+def clf_backward(model, batch, clf, perm, step, total_step, lambd=1.0):
+    """The ``--use_clf`` branch of ``train.py:168-197``: a second forward with the speakers
+    (and their metadata) shuffled by ``perm`` (the reference draws it with
+    ``random.sample``), the predicted mel cut into 150-frame chunks, the language
+    discriminator on every chunk, and ``dloss * coef(step / total_step) / len(langs) *
+    lambd`` back-propagated into the model.  ``clf = (SpeechEmbedder, GE2ELoss)``.  Returns
+    ``(dloss, cross-lingual chunk count, chunk count)``."""
+    from . import ge2e
+    disc, dLoss = clf
+    idx = torch.as_tensor(perm, device=batch[2].device)
+    speakers = batch[2].index_select(0, idx)  # (B,) ids: the gather of train.py:172
+    meta = batch[12].index_select(0, idx)
+    output = model(speakers, *batch[3:12], accents=batch[13], speaker_meta=meta)
+    chunks, rep = ge2e.chunk_mels(output[0])
+    langs = ge2e.chunk_langs(meta, rep)
+    langs_original = ge2e.chunk_langs(batch[12], rep)
+    out_r = disc(chunks)
+    _, _, dloss = dLoss(out_r["embeddings"].view(chunks.shape[0], 1, -1),
+                        out_r["da_lang_logits"], langs, reduction="sum")
+    scale = ge2e.da_coefficient(step, total_step) / langs.shape[0] * lambd
+    (dloss * scale).backward()
+    return dloss, (langs != langs_original).sum(), langs.shape[0]
+
+
+def train_step(model, optimizer, Loss, eLoss, batch, grad_clip_thresh=1.0, grad_sync=None,
+               clf=None, clf_args=None):
+    """One optimiser step -> (losses, eloss, grad norm, output); with ``clf`` (and
+    ``clf_args = (perm, step, total_step, lambd)``) the ``--use_clf`` branch runs between the
+    losses' backward and the clip, and its ``(dloss, cross-lingual chunks, chunks)`` is
+    appended."""
     output = model(*(batch[2:12]), accents=batch[13], speaker_meta=batch[12])
     losses = Loss(batch[:12], output[:-2])
     losses[0].backward()
     eloss = eLoss(output[-1], output[-2])
     (-eloss).backward()
+    clf_out = clf_backward(model, batch, clf, *clf_args) if clf is not None else None
     if grad_sync is not None:
         grad_sync()
     gnorm = optimizer.clip_grad_norm_(grad_clip_thresh)
     optimizer.step_and_update_lr()
     optimizer.zero_grad()
+    if clf_out is not None:
+        return losses, eloss, gnorm, output, clf_out
     return losses, eloss, gnorm, output
 
 
@@ -158,7 +190,14 @@ class Trainer:
         self._graph, self._graph_key = g, key
         return out
 
-    def step(self, batch):
+    def step(self, batch, clf=None, clf_args=None):
+        """One step; ``clf=(SpeechEmbedder, GE2ELoss)`` with ``clf_args=(perm, step,
+        total_step, lambd)`` adds the ``--use_clf`` branch (eager, single process)."""
+        if clf is not None:
+            if self.world > 1:
+                raise NotImplementedError("use_clf with data parallelism")
+            return train_step(self.model, self.opt, self.Loss, self.eLoss, batch, self.clip,
+                              clf=clf, clf_args=clf_args)
         if self.graph_mode and self.world == 1:
             return self._graph_step(batch)
         if self.world > 1:

@@ -29,6 +29,13 @@ Fixtures:
   g9_hifigan.npz   HiFi-GAN generator (hifigan/models.py, config.json V1) after
                    remove_weight_norm with name-seeded weights: waveform and the int16 PCM of
                    vocoder_infer for a seeded (2, 80, 24) mel, and one utterance of 37 frames
+  g10_clf.npz      the --use_clf language discriminator (train.py:168-197): the GE2E
+                   SpeechEmbedder (3-layer LSTM 80->256, projection 64, DA classifier) and
+                   GE2ELoss's BCE term on seeded weights -- embeddings, logits, da_loss and the
+                   input gradient of a weighted da_loss -- and 2 training steps of the full
+                   use_clf step at SYN-3x48 (the hparam file path and librosa are stubbed: the
+                   module reads /path/to/.../config.yaml at import, values from its own
+                   config/config.yaml)
 """
 import importlib
 import os
@@ -430,8 +437,111 @@ def g9():
     print("g9:", {k: v.shape for k, v in res.items()})
 
 
+def import_discriminator():
+    """The reference's SpeechEmbedder / GE2ELoss package, with its import-time hparam file
+    (an absolute placeholder path) read from the package's own config/config.yaml and
+    librosa (absent, used only by data utilities) stubbed."""
+    pkg_dir = os.path.join(REF, "Multilingual-Speaker-Encoder-with-Domain-Adaptation")
+    name = "Multilingual-Speaker-Encoder-with-Domain-Adaptation"
+    sys.modules.setdefault("librosa", types.ModuleType("librosa"))
+    pkg = types.ModuleType(name)
+    pkg.__path__ = [pkg_dir]
+    sys.modules[name] = pkg
+    hmod = types.ModuleType(name + ".hparam")
+    src = open(os.path.join(pkg_dir, "hparam.py")).read()
+    src = src.replace("hparam = Hparam()", "")
+    exec(compile(src, os.path.join(pkg_dir, "hparam.py"), "exec"), hmod.__dict__)
+    hmod.hparam = hmod.Hparam(os.path.join(pkg_dir, "config", "config.yaml"))
+    sys.modules[name + ".hparam"] = hmod
+    return importlib.import_module(name + ".speech_embedder_net")
+
+
+CLF_PERM = {"B3": [2, 0, 1]}
+
+
+def g10(fs2, loss_mod):
+    import math
+    sen = import_discriminator()
+    torch.manual_seed(0)
+    disc = sen.SpeechEmbedder()
+    seeded(disc)
+    dl = sen.GE2ELoss("cpu")
+    res = {"disc.keys": np.array(list(disc.state_dict().keys())),
+           "disc.shapes": np.array([",".join(map(str, v.shape)) for v in disc.state_dict().values()])}
+    rng = np.random.default_rng(10)
+    x = torch.from_numpy((rng.standard_normal((6, 150, 80)) * 2 - 3).astype(np.float32))
+    x[4:, 100:] = 0.0  # zero-padded tail, as the chunked mel has
+    langs = torch.tensor([1., 0., 1., 1., 0., 0.])
+    xr = x.clone().requires_grad_()
+    out = disc(xr)
+    _, _, da = dl(out["embeddings"].view(6, 1, -1), out["da_lang_logits"], langs, reduction="sum")
+    (da * 0.37).backward()
+    res.update({"d.x": x.numpy(), "d.langs": langs.numpy(),
+                "d.emb": out["embeddings"].detach().numpy(),
+                "d.logits": out["da_lang_logits"].detach().numpy(),
+                "d.da": np.float64(da.item()), "d.dx": xr.grad.numpy()})
+    # full use_clf steps (train.py:142-206) at SYN-3x48, dropout off, fixed speaker shuffle
+    cfg = "/root/reference/config/JVS-VCTK_langemb_configs/JVS-VCTK_1"
+    import yaml
+    pp = yaml.safe_load(open(cfg + "/preprocess.yaml"))
+    mc = yaml.safe_load(open(cfg + "/model.yaml"))
+    tc = yaml.safe_load(open(cfg + "/train.yaml"))
+    model = fs2.FastSpeech2(pp, mc, cfg)
+    seeded(model)
+    model.train()
+    opt_mod = importlib.import_module("model.optimizer")
+    optim = opt_mod.ScheduledOptim(model, tc, mc, 0)
+    Loss = loss_mod.FastSpeech2Loss(pp, mc)
+    eLoss = loss_mod.SpeakerMetaEncLoss(pp, mc)
+    b = PKG.data.syn_batch(3, 48, seed=3)
+    batch = PKG.data.to_device(b, "cpu")
+    perm = CLF_PERM["B3"]
+    step_of, total = 4, 10  # the DA coefficient 2/(1+e^{-10 p})-1 at p = 0.4 (0.96)
+    for it in range(2):
+        accents, speaker_meta = batch[13], batch[12]
+        bb = batch[:12]
+        output = model(*(bb[2:]), accents=accents, speaker_meta=speaker_meta)
+        losses = Loss(bb, output[:-2])
+        losses[0].backward()
+        eloss = eLoss(output[-1], output[-2])
+        (-eloss).backward()
+        speakers = torch.stack([bb[2][perm[i]] for i in range(3)])
+        sm = torch.stack([speaker_meta[perm[i]] for i in range(3)])
+        bb2 = bb[:2] + (speakers,) + bb[3:]
+        output = model(*(bb2[2:]), accents=accents, speaker_meta=sm)
+        max_len = output[0].shape[1]
+        max_len_r = max_len // 150 + 1
+        n_mels = output[0].shape[2]
+        batch_r_m = torch.cat([output[0], torch.zeros(3, max_len_r * 150 - max_len, n_mels)],
+                              dim=1).view(3 * max_len_r, 150, n_mels)
+        langs = sm[:, 2].view(-1, 1).repeat(1, max_len_r).view(-1)
+        output_r = disc(batch_r_m)
+        _, _, dloss = dl(output_r.get("embeddings").view(3 * max_len_r, 1, -1),
+                         output_r.get("da_lang_logits"), langs, reduction="sum")
+        coef = 2 / (1 + math.exp(-10 * (step_of / total))) - 1
+        (dloss * coef / len(langs) * 1.0).backward()
+        gn = torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+        optim.step_and_update_lr()
+        optim.zero_grad()
+        res[f"s{it}.losses"] = np.array([l.item() for l in losses])
+        res[f"s{it}.eloss"] = np.float64(eloss.item())
+        res[f"s{it}.dloss"] = np.float64(dloss.item())
+        res[f"s{it}.gnorm"] = np.float64(gn.item())
+        res[f"s{it}.max_len_r"] = np.int64(max_len_r)
+        step_of += 1
+    res["perm"] = np.array(perm)
+    np.savez_compressed(os.path.join(OUT, "g10_clf.npz"), **res)
+    print("g10:", {k: v for k, v in res.items() if k.startswith(("s0", "s1", "d.da"))})
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
+    if "--only-g10" in sys.argv:
+        fs2, loss_mod, mods, layers = import_reference()
+        no_dropout()
+        torch.set_num_threads(8)
+        g10(fs2, loss_mod)
+        return
     if "--only-g9" in sys.argv:
         sys.path.insert(0, REF)
         sys.dont_write_bytecode = True
@@ -462,6 +572,7 @@ def main():
     g7(fs2)
     g8()
     g9()
+    g10(fs2, loss_mod)
     sizes = [(3, 16), (8, 32)] + ([(48, 128)] if "--full" in sys.argv else [])
     for B, Ts in sizes:
         g5(fs2, loss_mod, B, Ts)

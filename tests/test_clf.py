@@ -1,0 +1,99 @@
+"""The --use_clf language discriminator against the reference's own
+outputs (g10): the GE2E SpeechEmbedder + GE2ELoss BCE on seeded weights, and two full
+use_clf training steps at SYN-3x48 (fp32, dropout off, fixed speaker shuffle)."""
+import importlib
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_golden
+
+PKG = importlib.import_module("mid-attribute-speaker-generation_amd")
+G = importlib.import_module("mid-attribute-speaker-generation_amd.ge2e")
+
+
+def _keys(g):
+    return {k: tuple(int(x) for x in s.split(",")) for k, s in zip(g["disc.keys"], g["disc.shapes"])}
+
+
+def test_discriminator_state_dict_matches_reference():
+    g = load_golden("g10_clf.npz")
+    d = G.SpeechEmbedder(device="meta")
+    assert {k: tuple(v.shape) for k, v in d.state_dict().items()} == _keys(g)
+
+
+def test_da_coefficient_and_chunk_count():
+    assert G.da_coefficient(0, 10) == 0.0
+    assert abs(G.da_coefficient(4, 10) - (2 / (1 + np.exp(-4.0)) - 1)) < 1e-12
+    # train.py:180: T // 150 + 1 chunks (a full zero chunk when T is a multiple of 150)
+    assert [t // 150 + 1 for t in (149, 150, 151, 300)] == [1, 2, 2, 3]
+
+
+def _disc(dev="cuda"):
+    d = G.SpeechEmbedder(device=dev)
+    PKG.seeded.load_seeded_(d)
+    d.da_dropout = 0.0  # the fixtures ran with dropout patched off
+    return d
+
+
+@pytest.mark.gpu
+def test_discriminator_matches_reference():
+    g = load_golden("g10_clf.npz")
+    d, dl = _disc(), G.GE2ELoss("cuda")
+    x = torch.from_numpy(g["d.x"]).cuda().requires_grad_()
+    langs = torch.from_numpy(g["d.langs"]).cuda()
+    out = d(x)
+    tot, ge2e, da = dl(out["embeddings"].view(6, 1, -1), out["da_lang_logits"], langs,
+                       reduction="sum")
+    assert torch.isnan(ge2e) and torch.isnan(tot)  # M = 1: exclude-self centroid / 0
+    np.testing.assert_allclose(out["embeddings"].detach().cpu().numpy(), g["d.emb"], atol=2e-5)
+    np.testing.assert_allclose(out["da_lang_logits"].detach().cpu().numpy(), g["d.logits"],
+                               rtol=1e-4, atol=1e-5)
+    assert abs(da.item() - float(g["d.da"])) <= 1e-4 * abs(float(g["d.da"]))
+    (da * 0.37).backward()
+    dx, ref = x.grad.cpu().numpy(), g["d.dx"]
+    assert np.abs(dx - ref).max() <= 1e-4 * np.abs(ref).max()
+    # only the last frame of each sequence reaches the classifier: a zero-padded tail still
+    # back-propagates through the recurrence
+    assert np.abs(dx[4:, 100:]).max() > 0
+
+
+@pytest.mark.gpu
+def test_discriminator_dropout_keeps_forward_backward_consistent():
+    """Classifier dropout (p = 0.2, train mode): the backward regenerates the forward's
+    masks -- the input gradient matches a finite difference of the same call's key."""
+    d = G.SpeechEmbedder(device="cuda")
+    PKG.seeded.load_seeded_(d)
+    g = load_golden("g10_clf.npz")
+    x = torch.from_numpy(g["d.x"]).cuda().requires_grad_()
+    out = d(x)
+    assert d.da_dropout == 0.2
+    out["da_lang_logits"].sum().backward()
+    assert torch.isfinite(x.grad).all() and x.grad.abs().max() > 0
+
+
+@pytest.mark.gpu
+def test_use_clf_training_steps_match_reference():
+    g = load_golden("g10_clf.npz")
+    M = importlib.import_module("mid-attribute-speaker-generation_amd.model")
+    TR = importlib.import_module("mid-attribute-speaker-generation_amd.train")
+    pp, mc, tc, path = PKG.config.load_configs("JVS-VCTK")
+    model = M.FastSpeech2(pp, mc, path, device="cuda", compute_dtype=torch.float32)
+    PKG.seeded.load_seeded_(model)
+    model.dropout = False
+    model.train()
+    tr = TR.Trainer(model, pp, mc, tc)
+    clf = (_disc(), G.GE2ELoss("cuda"))
+    batch = PKG.data.to_device(PKG.data.syn_batch(3, 48, seed=3), "cuda")
+    perm = [int(i) for i in g["perm"]]
+    for it, step in enumerate((4, 5)):
+        out = TR.train_step(model, tr.opt, tr.Loss, tr.eLoss, batch, tr.clip, clf=clf,
+                            clf_args=(perm, step, 10, 1.0))
+        losses, eloss, gnorm, _, (dloss, cross, n_chunks) = out
+        assert n_chunks == 3 * int(g[f"s{it}.max_len_r"])
+        got = np.array([float(l) for l in losses] + [float(eloss), float(dloss), float(gnorm)])
+        want = np.concatenate([g[f"s{it}.losses"],
+                               [g[f"s{it}.eloss"], g[f"s{it}.dloss"], g[f"s{it}.gnorm"]]])
+        err = np.abs(got - want) / np.maximum(np.abs(want), 1e-6)
+        assert err.max() < 1e-4, (it, got, want)

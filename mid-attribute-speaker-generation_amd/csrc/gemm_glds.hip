@@ -408,7 +408,7 @@ __global__ __launch_bounds__(256) void conv_gemm_nt_glds(GldsArgs a) {
 // (per-CU vector-memory rate; profiles/).  LDS rows are swizzled chunk c -> c ^ (row & 7),
 // which keeps the 16-row fragment reads conflict-free at every row offset.
 template <int BM, int BN, int BST, int HX, bool VOC>
-__global__ __launch_bounds__(256, BST == 1 ? 4 : HX > 16 ? 2 : 3) void conv_gemm_halo(GldsArgs a) {
+__global__ __launch_bounds__(256, BST == 1 ? 4 : (HX > 16 || BST > 2) ? 2 : 3) void conv_gemm_halo(GldsArgs a) {
   const int dil = VOC ? a.dil : 1;
   constexpr int BK = 64;
   constexpr int MI = BM / 32, NI = BN / 32;
@@ -517,25 +517,36 @@ __global__ __launch_bounds__(256, BST == 1 ? 4 : HX > 16 ? 2 : 3) void conv_gemm
         }
       }
     } else {
-      // the next tap's weight tile is in flight during this tap's MFMAs; at a channel-block
-      // boundary the halo (single buffer) and the first weight tile are loaded after a barrier
+      // weight-tile ring of BST slots, BST-1 tiles ahead: step s = (cb, j) reads slot s % BST
+      // while tiles s+1 .. s+BST-1 are in flight.  At a channel-block boundary the single
+      // halo buffer is reloaded after a barrier (everyone finished the previous block).
+      const int S = ncb * a.taps;
       issue_a(0);
-      issue_b(0, 0, 0);
-      int slot = 0;
-      for (int cb = 0; cb < ncb; ++cb) {
-        for (int j = 0; j < a.taps; ++j) {
+      for (int d = 0; d < BST - 1 && d < S; ++d) issue_b(d / a.taps, d % a.taps, d);
+      int cb = 0, j = 0, slot = 0;
+      for (int s = 0; s < S; ++s) {
+        if (j == 0 && s > 0) {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_s_barrier();
+          issue_a(cb);
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          __builtin_amdgcn_s_barrier();
-          if (j + 1 < a.taps) issue_b(cb, j + 1, slot ^ 1);
-          compute(j, slot);
-          slot ^= 1;
+        } else if (BST == 3 && s + 1 < S) {
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(BW) : "memory");  // tile s+1 may fly
+        } else {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
-        if (cb + 1 < ncb) {
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          __builtin_amdgcn_s_barrier();
-          issue_a(cb + 1);
-          issue_b(cb + 1, 0, slot);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        const int sn = s + BST - 1;
+        if (sn < S) {
+          const int cbn = sn / a.taps;
+          issue_b(cbn, sn - cbn * a.taps, sn % BST);
+        }
+        compute(j, slot);
+        slot = slot + 1 == BST ? 0 : slot + 1;
+        if (++j == a.taps) {
+          j = 0;
+          ++cb;
         }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -968,6 +979,15 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
       if (halo_wide) { FS2_HALO(128, 128, 1) }
       else if (halo_bm == 128) { FS2_HALO(128, 64, 1) }
       else { FS2_HALO(64, 64, 1) }
+    } else if (g_tune[FS2_TUNE_NT_HALO] == 4) {  // 3-slot weight ring, 2 tiles ahead
+      if (halo_wide) { FS2_HALO(128, 128, 3) }
+      else if (halo_bm == 128) { FS2_HALO(128, 64, 3) }
+      else { FS2_HALO(64, 64, 3) }
+    } else if (!halo_wide && c_in >= 1024) {
+      // long channel reductions on the narrower tiles (the FFN k=9 data gradients): a third
+      // ring slot keeps two weight tiles in flight (scripts/halo_check.py: encoder 71 -> 65 us)
+      if (halo_bm == 128) { FS2_HALO(128, 64, 3) }
+      else { FS2_HALO(64, 64, 3) }
     } else {
       if (halo_wide) { FS2_HALO(128, 128, 2) }
       else if (halo_bm == 128) { FS2_HALO(128, 64, 2) }

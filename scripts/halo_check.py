@@ -40,14 +40,14 @@ for name, M, T, cin, cout, k, lens in SHAPES:
     w = (torch.randn(cout * cin * k, device=dev) * 0.05).to(torch.bfloat16)
     b = torch.randn(cout, device=dev)
     res = {}
-    for mode in (-1, 3, 0):
+    for mode in (-1, 3, 0, 4):
         K.lib.fs2_set_tuning(6, mode)
         run = lambda: K.conv_gemm(x, w, M, T, cin, cout, k, (k - 1) // 2, bias=b, lens=lens)
         y = run()
         res[mode] = (y.clone(), timeit(run))
     K.lib.fs2_set_tuning(6, 0)
-    (y0, t0), (y1, t1), (y3, t3) = res[-1], res[0], res[3]
-    assert torch.equal(y1, y3), name  # same reduction order: bitwise equal
+    (y0, t0), (y1, t1), (y3, t3), (y4, t4) = res[-1], res[0], res[3], res[4]
+    assert torch.equal(y1, y3) and torch.equal(y1, y4), name  # same order: bitwise equal
     # torch fp32 reference on the same bf16 operands (per-utterance zero padding)
     W = w.float().view(cout, k, cin).permute(0, 2, 1)
     B_ = M // T
@@ -66,6 +66,6 @@ for name, M, T, cin, cout, k, lens in SHAPES:
     err = ((y1 - y0).abs().max() / y0.abs().max()).item()
     fl = 2 * M * cout * cin * k
     print(f"{name:22s} tap-major {t0:7.1f}us {fl / t0 / 1e6:5.0f}TF | halo-1 {t3:7.1f}us "
-          f"{fl / t3 / 1e6:5.0f}TF | halo {t1:7.1f}us "
+          f"{fl / t3 / 1e6:5.0f}TF | halo-3 {t4:7.1f}us {fl / t4 / 1e6:5.0f}TF | halo {t1:7.1f}us "
           f"{fl / t1 / 1e6:5.0f}TF | rel err {err:.1e}", flush=True)
     assert e1 < 1e-5, name

@@ -37,7 +37,7 @@ TR = importlib.import_module("mid-attribute-speaker-generation_amd.train")
 PEAK = {"f32": (157.3, "TFLOP/s"), "bf16": (2500.0, "TFLOP/s")}
 # the dominant kernel as rocprofv3 names it (bf16 path: the channel-block-major halo kernel,
 # 1,536 workgroups of 128 x 128 at SYN-48; scripts/kshape.py isolates the same launches)
-ROOF_KERNEL = "conv_gemm_halo<128, 128, 2, 16, false>"
+ROOF_KERNEL = "conv_gemm_halo<256, 128, 2, 16, false, 8>"
 _SYN = PKG.data.syn_batch(48, 128, seed=0)
 _N, _VALID = 48 * int(_SYN[8]), int(np.sum(_SYN[7]))
 # compulsory bytes of one decoder FFN Conv1d(256 -> 1024, k=9) forward launch at SYN-48 (rank

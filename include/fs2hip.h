@@ -161,8 +161,10 @@ int fs2_weight_prep_batch(int dtype, const int64_t* jobs, int n_jobs, int64_t n_
  *   FS2_TUNE_WGRAD_SPLITS  weight-gradient row splits (1..64)
  *   FS2_TUNE_LEGACY_GEMM   1 = the register-staged bf16 kernels of round 1
  *   FS2_TUNE_NT_GROUP      fwd/dX n-tiles per L2 tile group
- *   FS2_TUNE_NT_HALO       fwd/dX Conv1d (taps > 1) halo kernel: 0 = where it applies
- *                          (default), -1 = off (tap-major kernel), 2 = force 128-wide tiles
+ *   FS2_TUNE_NT_HALO       fwd/dX Conv1d (taps > 1) halo kernel: 0 = automatic (default),
+ *                          -1 = off (tap-major kernel), 1 = 4-wave tiles only, 2 = force
+ *                          128-wide tiles, 3 = single-buffered weight tile, 4 = 3-slot ring,
+ *                          5 / 6 / 7 = 8-wave 256x128 3-slot / 128x128 3-slot / 256x128 2-slot
  * Process-wide; query workspace sizes after setting.                                 */
 enum { FS2_TUNE_GEMM_STAGES = 0, FS2_TUNE_WGRAD_STAGES = 1, FS2_TUNE_WGRAD_TILE = 2,
        FS2_TUNE_WGRAD_SPLITS = 3, FS2_TUNE_LEGACY_GEMM = 4, FS2_TUNE_NT_GROUP = 5,

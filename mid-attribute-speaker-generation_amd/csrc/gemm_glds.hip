@@ -118,10 +118,10 @@ FS2_DEV void kloop(int nk, Issue&& issue, Compute&& compute) {
 
 // Epilogue through LDS, one half (wm) at a time: bias, aux add, ReLU / ReLU-mask, bf16 cast
 // on 8-element row vectors (16-B / 32-B coalesced stores).  Shared by both NT kernels.
-template <int BM, int BN, bool VOC>
-FS2_DEV void nt_epilogue(const GldsArgs& a, f32x4 (&acc)[BM / 32][BN / 32], u16* smem, int64_t m0,
-                         int n0, bool skip, int tid, int wm, int wn, int g, int r16) {
-  constexpr int MI = BM / 32, NI = BN / 32;
+template <int BM, int BN, bool VOC, int NWAVE = 4, int WN = 2>
+FS2_DEV void nt_epilogue(const GldsArgs& a, f32x4 (&acc)[BM / 32][BN / WN / 16], u16* smem,
+                         int64_t m0, int n0, bool skip, int tid, int wm, int wn, int g, int r16) {
+  constexpr int MI = BM / 32, NI = BN / WN / 16;
   constexpr int EPI_LD = BN + 4;
   float* Cs = reinterpret_cast<float*>(smem);
   const bool out_bf16 = a.flags & FS2_EPI_OUT_BF16, aux_bf16 = a.flags & FS2_EPI_AUX_BF16;
@@ -134,11 +134,11 @@ FS2_DEV void nt_epilogue(const GldsArgs& a, f32x4 (&acc)[BM / 32][BN / 32], u16*
         for (int j = 0; j < NI; ++j)
 #pragma unroll
           for (int r = 0; r < 4; ++r)
-            Cs[(i * 16 + 4 * g + r) * EPI_LD + wn * (BN / 2) + j * 16 + r16] = acc[i][j][r];
+            Cs[(i * 16 + 4 * g + r) * EPI_LD + wn * (BN / WN) + j * 16 + r16] = acc[i][j][r];
     }
     __syncthreads();
     constexpr int TPR = BN / 8;           // threads per row
-    constexpr int RPP = 256 / TPR;        // rows per pass
+    constexpr int RPP = NWAVE * 64 / TPR; // rows per pass
     const int cc = (tid % TPR) * 8;
     const int n = n0 + cc;
 #pragma unroll
@@ -407,14 +407,17 @@ __global__ __launch_bounds__(256) void conv_gemm_nt_glds(GldsArgs a) {
 // of a 128 x 128 tile, and that traffic, not the MFMA, bounds the tap-major kernel
 // (per-CU vector-memory rate; profiles/).  LDS rows are swizzled chunk c -> c ^ (row & 7),
 // which keeps the 16-row fragment reads conflict-free at every row offset.
-template <int BM, int BN, int BST, int HX, bool VOC>
-__global__ __launch_bounds__(256, BST == 1 ? 4 : (HX > 16 || BST > 2) ? 2 : 3) void conv_gemm_halo(GldsArgs a) {
+template <int BM, int BN, int BST, int HX, bool VOC, int NWAVE = 4>
+__global__ __launch_bounds__(NWAVE * 64, NWAVE == 8 ? 1 : BST == 1 ? 4 : (HX > 16 || BST > 2) ? 2 : 3)
+void conv_gemm_halo(GldsArgs a) {
+  // NWAVE = 4: 2 x 2 waves; NWAVE = 8: 2 (rows) x 4 (columns) waves, one block per CU
   const int dil = VOC ? a.dil : 1;
   constexpr int BK = 64;
-  constexpr int MI = BM / 32, NI = BN / 32;
+  constexpr int WN = NWAVE / 2;
+  constexpr int MI = BM / 32, NI = BN / WN / 16;
   constexpr int HMAX = BM + HX;                     // halo rows allocated ((taps-1)*dil <= HX)
-  constexpr int QMAX = (HMAX / 8 + 3) / 4;          // 8-row halo pieces per wave
-  constexpr int BW = BN / 32;                       // weight pieces per wave
+  constexpr int QMAX = (HMAX / 8 + NWAVE - 1) / NWAVE;  // 8-row halo pieces per wave
+  constexpr int BW = BN / 8 / NWAVE;                // weight pieces per wave
   constexpr int A_E = HMAX * BK, B_E = BN * BK;
   constexpr int EPI_E = (BM / 2) * (BN + 4) * 2;
   constexpr int SMEM_E = A_E + BST * B_E > EPI_E ? A_E + BST * B_E : EPI_E;
@@ -424,7 +427,7 @@ __global__ __launch_bounds__(256, BST == 1 ? 4 : (HX > 16 || BST > 2) ? 2 : 3) v
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WN, wn = wave % WN;
   const int g = lane >> 4, r16 = lane & 15;
 
   const int nwg = a.tiles_m * a.tiles_n;
@@ -442,11 +445,11 @@ __global__ __launch_bounds__(256, BST == 1 ? 4 : (HX > 16 || BST > 2) ? 2 : 3) v
   const u16* zero = reinterpret_cast<const u16*>(g_zero_line);
   const int HR = BM + (a.taps - 1) * dil, HP = (HR + 7) / 8;
   const int64_t u0 = (m0 / a.T) * a.T, u1 = u0 + a.T < a.M ? u0 + a.T : a.M;
-  // halo piece p = wave + 4 q: rows h = 8 p + lrow, global row m0 - pad + h
+  // halo piece p = wave + NWAVE q: rows h = 8 p + lrow, global row m0 - pad + h
   const u16* h_src[QMAX];
 #pragma unroll
   for (int q = 0; q < QMAX; ++q) {
-    const int h = (wave + 4 * q) * 8 + lrow;
+    const int h = (wave + NWAVE * q) * 8 + lrow;
     const int64_t gr = m0 - a.pad + h;
     const int lc = (lane & 7) ^ (h & 7);
     h_src[q] = (gr >= u0 && gr < u1) ? a.x + gr * a.ldx + lc * 8 : nullptr;
@@ -466,14 +469,14 @@ __global__ __launch_bounds__(256, BST == 1 ? 4 : (HX > 16 || BST > 2) ? 2 : 3) v
     for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int a_row = wm * (BM / 2) + r16;
-  const int b_row = wn * (BN / 2) + r16;
+  const int b_row = wn * (BN / WN) + r16;
   const int b_off[2] = {b_row * BK + ((0 + g) ^ (b_row & 7)) * 8, b_row * BK + ((4 + g) ^ (b_row & 7)) * 8};
   // step s = cb * taps + j: weight tile (tap j, channel block cb) into ring slot s % BST; the
   // halo of channel block cb is staged at j == 0
   auto issue_a = [&](int cb) {
 #pragma unroll
     for (int q = 0; q < QMAX; ++q) {
-      const int pc = wave + 4 * q;
+      const int pc = wave + NWAVE * q;
       if (pc < HP) glds16(h_src[q] ? h_src[q] + cb * BK : zero, As + pc * 8 * BK);
     }
   };
@@ -484,23 +487,27 @@ __global__ __launch_bounds__(256, BST == 1 ? 4 : (HX > 16 || BST > 2) ? 2 : 3) v
       glds16(b_src[i] ? b_src[i] + k0 : zero, Bs + slot * B_E + (wave * BW + i) * 8 * BK);
   };
   auto compute = [&](int j, int slot) {
-    // fragment rows differ by multiples of 16, so one swizzle serves all of them
+    // fragment rows differ by multiples of 16, so one swizzle serves all of them.  All 16
+    // fragment reads of the step are issued before the first MFMA: the waits before the
+    // MFMAs are then counted (the second k-half's reads land under the first half's MFMAs)
     const int ha = a_row + j * dil, sa = ha & 7;
+    bf16x8g fa[2][MI], fb[2][NI];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      bf16x8g fa[MI], fb[NI];
       const u16* pa = As + ha * BK + ((ks * 4 + g) ^ sa) * 8;
       const u16* pb = Bs + slot * B_E + b_off[ks];
 #pragma unroll
-      for (int i = 0; i < MI; ++i) fa[i] = *reinterpret_cast<const bf16x8g*>(pa + i * 16 * BK);
+      for (int i = 0; i < MI; ++i) fa[ks][i] = *reinterpret_cast<const bf16x8g*>(pa + i * 16 * BK);
 #pragma unroll
-      for (int jj = 0; jj < NI; ++jj) fb[jj] = *reinterpret_cast<const bf16x8g*>(pb + jj * 16 * BK);
+      for (int jj = 0; jj < NI; ++jj) fb[ks][jj] = *reinterpret_cast<const bf16x8g*>(pb + jj * 16 * BK);
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int jj = 0; jj < NI; ++jj)
-          acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[jj], acc[i][jj], 0, 0, 0);
-    }
+          acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[ks][i], fb[ks][jj], acc[i][jj], 0, 0, 0);
   };
   if (!skip) {
     const int ncb = a.Cin / BK;
@@ -553,7 +560,7 @@ __global__ __launch_bounds__(256, BST == 1 ? 4 : (HX > 16 || BST > 2) ? 2 : 3) v
       __builtin_amdgcn_s_barrier();
     }
   }
-  nt_epilogue<BM, BN, VOC>(a, acc, smem, m0, n0, skip, tid, wm, wn, g, r16);
+  nt_epilogue<BM, BN, VOC, NWAVE, WN>(a, acc, smem, m0, n0, skip, tid, wm, wn, g, r16);
 }
 
 // ------------------------------------------------------------------------ weight gradient
@@ -962,6 +969,25 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
   // FS2_TUNE_NT_HALO = 2 forces 128 x 128).  Every row tile must lie inside one utterance.
   const bool halo_wide = big >= 512 || g_tune[FS2_TUNE_NT_HALO] == 2;
   const int halo_bm = halo_wide || big >= 128 ? 128 : 64;
+  // 8-wave variants (FS2_TUNE_NT_HALO 5 / 6 / 7: 256x128 3-slot / 128x128 3-slot / 256x128
+  // 2-slot), one block per CU with the weight prefetch in flight across the barrier
+  // Default for the wide forward shapes (c_in <= 512, >= 512 128x128 tiles, T % 256 == 0: the
+  // decoder FFN k=9 and PostNet 512 convs): 256 x 128 two-slot, 8 waves (k=9 decoder forward
+  // 114 -> 102 us alone, scripts/halo_check.py).  FS2_TUNE_NT_HALO 1 disables it.
+  int h8 = g_tune[FS2_TUNE_NT_HALO];
+  if (h8 == 0 && big >= 512 && c_in <= 512) h8 = 7;
+  if ((h8 == 5 || h8 == 6 || h8 == 7) && taps > 1 && (taps - 1) * ve.dil <= 16 && tapaligned &&
+      !voc && seq_len % (h8 == 6 ? 128 : 256) == 0) {
+    const int bm = h8 == 6 ? 128 : 256;
+    a.tiles_m = (int)((rows + bm - 1) / bm);
+    a.tiles_n = (int)((c_out + 127) / 128);
+    a.group = a.tiles_n;
+    const unsigned grid = (unsigned)(a.tiles_m * a.tiles_n);
+    if (h8 == 5) conv_gemm_halo<256, 128, 3, 16, false, 8><<<grid, 512, 0, st>>>(a);
+    else if (h8 == 6) conv_gemm_halo<128, 128, 3, 16, false, 8><<<grid, 512, 0, st>>>(a);
+    else conv_gemm_halo<256, 128, 2, 16, false, 8><<<grid, 512, 0, st>>>(a);
+    return launch_status("fs2_conv_gemm(bf16)");
+  }
   if (taps > 1 && (taps - 1) * ve.dil <= 64 && tapaligned && seq_len % halo_bm == 0 &&
       g_tune[FS2_TUNE_NT_HALO] >= 0) {
     a.tiles_m = (int)((rows + halo_bm - 1) / halo_bm);

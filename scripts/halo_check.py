@@ -40,13 +40,16 @@ for name, M, T, cin, cout, k, lens in SHAPES:
     w = (torch.randn(cout * cin * k, device=dev) * 0.05).to(torch.bfloat16)
     b = torch.randn(cout, device=dev)
     res = {}
-    for mode in (-1, 3, 0, 4):
+    for mode in (-1, 3, 0, 4, 5, 6, 7):
         K.lib.fs2_set_tuning(6, mode)
         run = lambda: K.conv_gemm(x, w, M, T, cin, cout, k, (k - 1) // 2, bias=b, lens=lens)
         y = run()
         res[mode] = (y.clone(), timeit(run))
     K.lib.fs2_set_tuning(6, 0)
     (y0, t0), (y1, t1), (y3, t3), (y4, t4) = res[-1], res[0], res[3], res[4]
+    errs = {md: ((res[md][0] - y1).abs().max() / y1.abs().max()).item() for md in (5, 6, 7)}
+    print(f"    8-wave: 256x128/3 {res[5][1]:7.1f}us  128x128/3 {res[6][1]:7.1f}us  "
+          f"256x128/2 {res[7][1]:7.1f}us  max rel diff vs 4-wave {errs}")
     assert torch.equal(y1, y3) and torch.equal(y1, y4), name  # same order: bitwise equal
     # torch fp32 reference on the same bf16 operands (per-utterance zero padding)
     W = w.float().view(cout, k, cin).permute(0, 2, 1)

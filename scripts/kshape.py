@@ -14,7 +14,7 @@ import csv
 import sys
 from collections import defaultdict
 
-ROOF_NAME, ROOF_WGS = "conv_gemm_halo<128, 128, 2, 16, false>", 1536
+ROOF_NAME, ROOF_WGS = "conv_gemm_halo<256, 128, 2, 16, false, 8>", 768
 
 
 def main():

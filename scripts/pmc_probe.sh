@@ -14,7 +14,7 @@ import csv, glob, collections
 for f in sorted(glob.glob("gpurun_out/pmc/p*/**/*counter_collection.csv", recursive=True)):
     acc = collections.defaultdict(list)
     for r in csv.DictReader(open(f)):
-        if "conv_gemm_halo<128, 128, 2, 16, false>" in r["Kernel_Name"]:
+        if "conv_gemm_halo<256, 128, 2, 16, false, 8>" in r["Kernel_Name"]:
             acc[r["Counter_Name"]].append(float(r["Counter_Value"]))
     for k, v in acc.items():
         print(f"{k:32s} n={len(v):3d} mean={sum(v)/len(v):.4g}")

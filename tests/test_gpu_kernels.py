@@ -517,7 +517,7 @@ def test_conv_gemm_bf16_halo(B, T, cin, cout, k):
     try:
         K.lib.fs2_set_tuning(6, -1)  # FS2_TUNE_NT_HALO off: tap-major kernel
         y_tm = K.conv_gemm(x, wf, B * T, T, cin, cout, k, pad, bias=b)
-        for mode in (0, 2):
+        for mode in (0, 2, 5, 6, 7):  # 5-7: the 8-wave (one block per CU) variants
             K.lib.fs2_set_tuning(6, mode)
             y = K.conv_gemm(x, wf, B * T, T, cin, cout, k, pad, bias=b)
             close(y, ref, 1e-5)

@@ -165,10 +165,12 @@ int fs2_weight_prep_batch(int dtype, const int64_t* jobs, int n_jobs, int64_t n_
  *                          -1 = off (tap-major kernel), 1 = 4-wave tiles only, 2 = force
  *                          128-wide tiles, 3 = single-buffered weight tile, 4 = 3-slot ring,
  *                          5 / 6 / 7 = 8-wave 256x128 3-slot / 128x128 3-slot / 256x128 2-slot
+ *   FS2_TUNE_WGRAD_HALO    weight gradient of Conv1d taps 3/5/9: 0 = halo kernel (default),
+ *                          -1 = tap-major kernel
  * Process-wide; query workspace sizes after setting.                                 */
 enum { FS2_TUNE_GEMM_STAGES = 0, FS2_TUNE_WGRAD_STAGES = 1, FS2_TUNE_WGRAD_TILE = 2,
        FS2_TUNE_WGRAD_SPLITS = 3, FS2_TUNE_LEGACY_GEMM = 4, FS2_TUNE_NT_GROUP = 5,
-       FS2_TUNE_NT_HALO = 6, FS2_TUNE_COUNT = 7 };
+       FS2_TUNE_NT_HALO = 6, FS2_TUNE_WGRAD_HALO = 7, FS2_TUNE_COUNT = 8 };
 int fs2_set_tuning(int knob, int value);
 
 /* Weight (and optionally bias) gradient, accumulated into the fp32 master-gradient layout:

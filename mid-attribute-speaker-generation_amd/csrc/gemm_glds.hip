@@ -791,6 +791,178 @@ __global__ __launch_bounds__(256) void conv_wgrad_tn_glds(WgradGlds a) {
   }
 }
 
+// Halo weight gradient for Conv1d with 2 <= taps <= 9 (C_in, C_out multiples of 64, T a
+// multiple of 64): a block owns a 64 (o) x 64 (c) tile for ALL taps.  Per 64-row k-tile it
+// stages the dy tile (64 x 64) and the x rows of the tile plus the tap halo
+// (64 + taps - 1 rows, zero outside the utterance) ONCE, and tap j reads the x image at row
+// offset j: the tap-major kernel above re-stages both operands for every (tap, channel)
+// column tile, i.e. taps x more staging per FLOP.  dy fragments are read once per k-step
+// and reused by every tap.  Both images are [rows][64] bf16 (128-B rows) filled by LDS-DMA
+// with the chunk swizzle ((R >> 1) & 3) << 1 and read with ds_read_b64_tr_b16 (rows
+// {4g+q} u {16+4g+q} of a 32-row step; a row offset j keeps the pair in one swizzle class).
+// Output: the same split-K slab layout (and bias slab) as conv_wgrad_tn_glds.
+template <int TAPS>
+__global__ __launch_bounds__(256, 2) void conv_wgrad_halo(WgradGlds a) {
+  constexpr int BO = 64, BC = 64, BK = 64, STAGES = 2;
+  constexpr int HX = 8;                      // halo rows allocated (taps <= 9)
+  constexpr int A_E = BK * BO;               // dy image
+  constexpr int X_E = (BK + HX) * BC;        // x halo image
+  constexpr int STAGE_E = A_E + X_E;
+  constexpr int MAXKT = 1024;
+  __shared__ __attribute__((aligned(1024))) u16 smem[STAGES * STAGE_E + MAXKT + 64];
+  short* ktl = reinterpret_cast<short*>(smem + STAGES * STAGE_E);
+  int* wcnt = reinterpret_cast<int*>(smem + STAGES * STAGE_E + MAXKT);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3, r16 = lane & 15;
+
+  const int per_split = a.tiles_o * a.tiles_k;  // tiles_k = C_in / 64 here
+  const int nwg = per_split * a.splits;
+  const int orig = blockIdx.x, xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int z = wg / per_split, rem = wg - z * per_split;
+  const int tc = rem % a.tiles_k, to = rem / a.tiles_k;
+  const int o0 = to * BO, c0 = tc * BC;
+  const int64_t r_begin = (int64_t)z * a.rows_per_split;
+  int64_t r_end = r_begin + a.rows_per_split;
+  if (r_end > a.M) r_end = a.M;
+  const int nk_all = r_end > r_begin ? (int)((r_end - r_begin + BK - 1) / BK) : 0;
+  const bool use_list = a.lens != nullptr && nk_all <= MAXKT;
+  int nk = nk_all;
+  if (use_list) {  // ordered list of k-tiles holding a real row (as conv_wgrad_tn_glds)
+    int total = 0;
+    for (int cc0 = 0; cc0 < nk_all; cc0 += 256) {
+      const int kt = cc0 + tid;
+      bool v = false;
+      if (kt < nk_all) {
+        const int64_t k0 = r_begin + (int64_t)kt * BK;
+        v = !rows_all_padding(a.lens, a.T, k0, k0 + BK < r_end ? k0 + BK : r_end);
+      }
+      const uint64_t mask = __ballot(v);
+      if (lane == 0) wcnt[wave] = __popcll(mask);
+      __syncthreads();
+      int before = total;
+      for (int w = 0; w < wave; ++w) before += wcnt[w];
+      const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
+      if (v) ktl[before + below] = (short)kt;
+      for (int w = 0; w < 4; ++w) total += wcnt[w];
+      __syncthreads();
+    }
+    nk = total;
+  }
+
+  auto swz = [](int R) { return ((R >> 1) & 3) << 1; };
+  const u16* zero = reinterpret_cast<const u16*>(g_zero_line);
+  const int lrow = lane >> 3, lch = lane & 7;
+  const int HR = BK + a.taps - 1, HP = (HR + 7) / 8;  // x halo rows / 8-row pieces
+  auto issue = [&](int kt, int stage) {
+    u16* As = smem + stage * STAGE_E;
+    u16* Xs = As + A_E;
+    const int tile = use_list ? (int)ktl[kt] : kt;
+    const int64_t k0 = r_begin + (int64_t)tile * BK;
+    // the 64 rows of a k-tile lie in one utterance (T % 64 == 0, splits are 64-row aligned)
+    const int64_t u0 = (k0 / a.T) * a.T, u1 = u0 + a.T < a.M ? u0 + a.T : a.M;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {  // dy: 8 pieces of 8 rows, 2 per wave
+      const int R = (wave * 2 + i) * 8 + lrow;
+      const int64_t m = k0 + R;
+      const u16* src = m < r_end ? a.dy + m * a.ldy + o0 + ((lch ^ swz(R)) << 3) : zero;
+      glds16(src, As + (wave * 2 + i) * 8 * BO);
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {  // x halo: up to 9 pieces, wave + 4 i
+      const int pc = wave + 4 * i;
+      if (pc < HP) {
+        const int h = pc * 8 + lrow;
+        const int64_t gr = k0 - a.pad + h;
+        // rows past the split's end only meet zero dy rows; only the utterance matters
+        const u16* src = (gr >= u0 && gr < u1) ? a.x + gr * a.ldx + c0 + ((lch ^ swz(h)) << 3)
+                                               : zero;
+        glds16(src, Xs + pc * 8 * BC);
+      }
+    }
+  };
+
+  f32x4 acc[TAPS][2][2], accb[2];
+#pragma unroll
+  for (int j = 0; j < TAPS; ++j)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      acc[j][i][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+      acc[j][i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  accb[0] = accb[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool do_bias = a.bslab != nullptr && tc == 0 && wn == 0;  // wave-uniform
+  bf16x8g ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = (__bf16)1.0f;
+
+  // transposed fragment: 16 columns at col0, rows rb + {4g+q} and rb + {16+4g+q}
+  auto tr_frag = [&](const u16* img, int rb, int col0) -> bf16x8g {
+    const int R = rb + 4 * g + q;
+    const int lc = (col0 >> 3) + (p >> 1);
+    const int off = R * 64 + ((lc ^ swz(R)) << 3) + ((p & 1) << 2);
+    const s16x4g lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4g*)(img + off));
+    const s16x4g hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4g*)(img + off + 16 * 64));
+    return __builtin_bit_cast(bf16x8g, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+  };
+  auto compute = [&](int stage) {
+    const u16* As = smem + stage * STAGE_E;
+    const u16* Xs = As + A_E;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8g fa[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) fa[i] = tr_frag(As, ks * 32, wm * 32 + i * 16);
+      if (do_bias) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], ones, accb[i], 0, 0, 0);
+      }
+#pragma unroll
+      for (int j = 0; j < TAPS; ++j) {
+        bf16x8g fb[2];
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) fb[jj] = tr_frag(Xs, ks * 32 + j, wn * 32 + jj * 16);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj)
+            acc[j][i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[jj], acc[j][i][jj], 0, 0, 0);
+      }
+    }
+  };
+
+  kloop<STAGES, 5>(nk, issue, compute);  // per-wave DMA count varies (<= 5): kloop waits vmcnt(0)-style
+
+  if (do_bias && r16 == 0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int o = o0 + wm * 32 + i * 16 + 4 * g + r;
+        a.bslab[(int64_t)z * a.Cout + o] = accb[i][r];
+      }
+  }
+  // slab[z][o][j*Cin + c]: 16 consecutive c per row group (64-B runs)
+  float* slab = a.slab + (int64_t)z * a.Cout * a.Kp;
+#pragma unroll
+  for (int j = 0; j < TAPS; ++j)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int o = o0 + wm * 32 + i * 16 + 4 * g + r;
+          const int c = c0 + wn * 32 + jj * 16 + r16;
+          slab[(int64_t)o * a.Kp + (int64_t)j * a.Cin + c] = acc[j][i][jj][r];
+        }
+}
+
 // dw[o][c][j] (+)= sum_z slab[z][o][j*Cin + c]; db[o] += sum_z bslab[z][o].  Split order is
 // fixed (bitwise reproducible).  taps == 1: the layouts coincide, 4 consecutive elements per
 // thread.  taps > 1: one block per (o, 64-channel chunk); slab rows are read as 256-B runs
@@ -869,11 +1041,23 @@ int conv_wgrad_glds_launch(const void* dy, int64_t ldy, const void* x, int64_t l
   WgradGlds a{(const u16*)dy, ldy, (const u16*)x, ldx, ws, bslab, rows, seq_len, (int)c_in,
               (int)c_out, taps, pad, (int)Kp, rps, (int)((c_out + tile - 1) / tile),
               (int)((Kp + tile - 1) / tile), splits, lens};
+  const bool halo = taps >= 2 && taps <= 9 && (taps == 3 || taps == 5 || taps == 9) &&
+                    c_in % 64 == 0 && c_out % 64 == 0 && seq_len % 64 == 0 &&
+                    g_tune[FS2_TUNE_WGRAD_HALO] >= 0;
+  if (halo) {
+    a.tiles_o = (int)(c_out / 64);
+    a.tiles_k = (int)(c_in / 64);
+    const unsigned hgrid = (unsigned)(a.tiles_o * a.tiles_k * splits);
+    if (taps == 9) conv_wgrad_halo<9><<<hgrid, 256, 0, st>>>(a);
+    else if (taps == 5) conv_wgrad_halo<5><<<hgrid, 256, 0, st>>>(a);
+    else conv_wgrad_halo<3><<<hgrid, 256, 0, st>>>(a);
+  }
   const unsigned grid = (unsigned)(a.tiles_o * a.tiles_k * splits);
   const int stages = g_tune[FS2_TUNE_WGRAD_STAGES] >= 1 && g_tune[FS2_TUNE_WGRAD_STAGES] <= 4
                          ? g_tune[FS2_TUNE_WGRAD_STAGES] : (tile == 128 ? 1 : 2);
 #define FS2_WG(BT, S) conv_wgrad_tn_glds<BT, S><<<grid, 256, 0, st>>>(a)
-  if (tile == 128) {
+  if (halo) {
+  } else if (tile == 128) {
     switch (stages) {
       case 2: FS2_WG(128, 2); break;
       case 3: FS2_WG(128, 3); break;
@@ -1009,12 +1193,10 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
       if (halo_wide) { FS2_HALO(128, 128, 3) }
       else if (halo_bm == 128) { FS2_HALO(128, 64, 3) }
       else { FS2_HALO(64, 64, 3) }
-    } else if (!halo_wide && c_in >= 1024) {
-      // long channel reductions on the narrower tiles (the FFN k=9 data gradients): a third
-      // ring slot keeps two weight tiles in flight (scripts/halo_check.py: encoder 71 -> 65 us)
-      if (halo_bm == 128) { FS2_HALO(128, 64, 3) }
-      else { FS2_HALO(64, 64, 3) }
     } else {
+      // (a third ring slot measured faster alone for the k=9 data gradients, 71 -> 65 us, but
+      // 1.7-2x slower inside the step, where the weight-gradient stream shares the CUs and
+      // the lower occupancy (2 blocks/CU) cannot absorb it: knob 4 keeps it for experiments)
       if (halo_wide) { FS2_HALO(128, 128, 2) }
       else if (halo_bm == 128) { FS2_HALO(128, 64, 2) }
       else { FS2_HALO(64, 64, 2) }

@@ -12,6 +12,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 K = importlib.import_module("mid-attribute-speaker-generation_amd.kernels")
 
 dev = "cuda:0"
+K.lib.fs2_set_tuning(7, int(os.environ.get("WGRAD_HALO", "0")))  # -1: tap-major weight gradient
 # --lens: pass the SYN-48 utterance lengths, as the step does (all-padding row tiles skipped)
 LENS = "--lens" in sys.argv
 PKG = importlib.import_module("mid-attribute-speaker-generation_amd")

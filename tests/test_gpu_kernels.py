@@ -613,3 +613,39 @@ def test_convT_as_phase_conv():
         y = torch.empty(B * T * s, cout, device=DEV)
         K.conv_gemm_ex(x, wf, B * T, T, cin, s * cout, 3, 1, bias=bc, out=y.view(B * T, s * cout))
         close(y, want, 1e-5)
+
+
+@pytest.mark.parametrize("B,T,cin,cout,k", [(6, 512, 256, 1024, 9), (4, 128, 256, 256, 3),
+                                            (3, 256, 512, 512, 5), (48, 128, 256, 1024, 9),
+                                            (2, 64, 1024, 256, 9)])
+def test_conv_wgrad_halo(B, T, cin, cout, k):
+    """The all-taps halo weight gradient (taps 3/5/9, T % 64 == 0) against fp32 autograd on
+    the same bf16 data and against the tap-major kernel, with the fused bias gradient and
+    the padding k-tile skip."""
+    pad = (k - 1) // 2
+    x = bf(rnd(B * T, cin, seed=71))
+    dy = bf(rnd(B * T, cout, seed=72))
+    w = rnd(cout, cin, k, scale=1 / math.sqrt(cin * k), seed=73)
+    xr, wr = x.float().clone().requires_grad_(), w.clone().requires_grad_()
+    ref_conv(xr, wr, None, B, T, pad).backward(dy.float())
+    out = {}
+    try:
+        for mode in (0, -1):
+            K.lib.fs2_set_tuning(7, mode)  # FS2_TUNE_WGRAD_HALO
+            dw, db = torch.zeros_like(w), torch.zeros(cout, device=DEV)
+            K.conv_wgrad(dy, x, dw, B * T, T, cin, cout, k, pad, db=db)
+            out[mode] = (dw, db)
+    finally:
+        K.lib.fs2_set_tuning(7, 0)
+    close(out[0][0], wr.grad, 1e-5)
+    close(out[0][1], dy.float().sum(0), 1e-5)
+    close(out[0][0], out[-1][0], 1e-5)
+    # lens: zero dy rows past each length, skipped k-tiles change nothing (bitwise)
+    lens = torch.tensor([T - (13 * u) % T for u in range(B)], device=DEV)
+    padr = (torch.arange(T, device=DEV)[None] >= lens[:, None]).reshape(-1)
+    dyz = dy * (~padr)[:, None]
+    dw0, db0 = torch.zeros_like(w), torch.zeros(cout, device=DEV)
+    dw1, db1 = torch.zeros_like(w), torch.zeros(cout, device=DEV)
+    K.conv_wgrad(dyz, x, dw0, B * T, T, cin, cout, k, pad, db=db0)
+    K.conv_wgrad(dyz, x, dw1, B * T, T, cin, cout, k, pad, db=db1, lens=lens)
+    assert torch.equal(dw0, dw1) and torch.equal(db0, db1)

@@ -106,17 +106,19 @@ int fs2_vocoder_post(int dtype, const void* x, int64_t rows, int64_t seq_len, in
  * and GE2ELoss's BCE term (165-186), fp32.
  * One LSTM layer (nn.LSTM, batch_first, gates i,f,g,o, h0 = c0 = 0) over n_seq sequences of
  * `steps` rows (row n*steps + t): gx = x W_ih^T + bias (bias = b_ih + b_hh; one GEMM), then
- * the recurrence, one launch per step issued from C.  w_ih (4H, c_in) natural, w_hh_t
- * (H, 4H) = W_hh^T.  Saves h_all, c_all (rows, H) and the activated gates act (rows, 4H).   */
+ * the recurrence, one launch per step issued from C.  w_ih (4H, c_in) and w_hh (4H, H)
+ * natural; hidden a multiple of 256.  Saves h_all, c_all (rows, H) and the activated gates
+ * act (rows, 4H).                                                                         */
 int fs2_lstm_layer_fwd(const float* x, int64_t n_seq, int64_t steps, int64_t c_in, int64_t hidden,
-                       const float* w_ih, const float* bias, const float* w_hh_t, float* gx,
+                       const float* w_ih, const float* bias, const float* w_hh, float* gx,
                        float* h_all, float* c_all, float* act, void* stream);
 /* Backward through time: dh_out (rows, H; NULL = 0) is the gradient of the layer's outputs;
  * writes dgates (rows, 4H; pre-activation gate gradients) and, when dx is given,
- * dx = dgates W_ih (rows, c_in; w_ih_t = W_ih^T (c_in, 4H)).  dc_ws: 2*n_seq*H floats.
+ * dx = dgates W_ih (rows, c_in; w_ih_t = W_ih^T (c_in, 4H)); w_hh_t = W_hh^T (H, 4H).
+ * dc_ws: 2*n_seq*H floats.
  * Weight gradients are not formed (train.py never steps the discriminator).            */
 int fs2_lstm_layer_bwd(const float* dh_out, int64_t n_seq, int64_t steps, int64_t c_in,
-                       int64_t hidden, const float* w_ih_t, const float* w_hh, const float* act,
+                       int64_t hidden, const float* w_ih_t, const float* w_hh_t, const float* act,
                        const float* c_all, float* dgates, float* dc_ws, float* dx, void* stream);
 /* Embedding + domain-classifier head on the last LSTM frame (x row n at x + n*ldx, 256 wide):
  * projection 256->64, L2 norm (emb), Linear 64->64, dropout, ReLU, Linear 64->64, dropout,

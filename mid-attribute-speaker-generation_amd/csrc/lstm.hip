@@ -7,11 +7,11 @@
 //   * the input projection of all T steps is ONE implicit GEMM (fs2_conv_gemm, taps = 1):
 //     gx = x W_ih^T + b_ih + b_hh, (N*T, 4H);
 //   * the recurrence runs one launch per step from the C entry point (no host round trip
-//     per step): lstm_fwd_step fuses h_{t-1} W_hh^T (h rows staged in LDS, W_hh^T read
-//     coalesced along the hidden unit) with the gate nonlinearities and the cell update, and
-//     saves the activated gates and cell for the backward;
+//     per step): lstm_fwd_step fuses h_{t-1} W_hh^T (f32 MFMA, split-K over the block's
+//     waves) with the gate nonlinearities and the cell update, and saves the activated gates
+//     and cell for the backward;
 //   * the backward runs the same T steps in reverse; lstm_bwd_step fuses the recurrent
-//     gradient dh_{t} += dgates_{t+1} W_hh (dgates row in LDS) with the gate derivatives, and
+//     gradient dh_{t} += dgates_{t+1} W_hh (same MFMA scheme) with the gate derivatives, and
 //     the input gradient of all steps is again one GEMM: dx = dgates W_ih.
 // PyTorch gate order i, f, g, o; h0 = c0 = 0 (nn.LSTM defaults).
 #include <math.h>
@@ -20,128 +20,167 @@
 
 namespace fs2 {
 
-constexpr int LSTM_RPT = 1;   // rows per thread
-constexpr int LSTM_RB = 4 * LSTM_RPT;  // rows (sequences) per block
-constexpr int LSTM_JB = 64;   // hidden units per block
-constexpr int LSTM_HMAX = 256;
-
 FS2_DEV float sigm(float x) { return 1.f / (1.f + expf(-x)); }
 
-__global__ __launch_bounds__(256) void lstm_fwd_step(const float* __restrict__ gx,
-                                                     const float* __restrict__ wt, float* h_all,
-                                                     float* c_all, float* act, int N, int T, int H,
-                                                     int t) {
-  // 4 waves x LSTM_RPT rows each: every W_hh^T element a thread loads serves LSTM_RPT rows
-  __shared__ float hs[LSTM_RB][LSTM_HMAX];
-  const int tid = threadIdx.x, r0 = tid / LSTM_JB, jj = tid % LSTM_JB;
-  const int n0 = blockIdx.x * LSTM_RB;
-  for (int e = tid; e < LSTM_RB * H; e += 256) {
-    const int rr = e / H, k = e - rr * H, nn = n0 + rr;
-    hs[rr][k] = (t > 0 && nn < N) ? h_all[((int64_t)nn * T + t - 1) * H + k] : 0.f;
-  }
-  __syncthreads();
-  const int j = blockIdx.y * LSTM_JB + jj;
-  if (j >= H) return;
-  float a[LSTM_RPT][4];
+// The recurrent products run on the f32-input MFMA (v_mfma_f32_16x16x4_f32: f32 operands,
+// f32 accumulation, the fp32 arithmetic of the reference's cuDNN/ATen LSTM).  A step is a
+// (N x 4H x H) product, ~50 MFLOP: latency, not throughput, bounds it, so each output tile is
+// split over the K dimension across the waves of a block (all loads of a wave issued up
+// front) and the partials meet in LDS.  K order inside a 16-wide k group: operand register c
+// of lane quarter kq is k = 16 g + 4 kq + c, so every lane fetches a float4 of A and of B.
+using f32x4m = __attribute__((__vector_size__(4 * sizeof(float)))) float;
+
+FS2_DEV f32x4m mfma4(float a, float b, f32x4m c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+FS2_DEV void mfma_k16(const float4& a, const float4& b, f32x4m& c0, f32x4m& c1) {
+  c0 = mfma4(a.x, b.x, c0);
+  c1 = mfma4(a.y, b.y, c1);
+  c0 = mfma4(a.z, b.z, c0);
+  c1 = mfma4(a.w, b.w, c1);
+}
+
+// one wave's share of a split-K tile: kper / (16 GT) trips, each issuing GT float4 loads of
+// A and of B before its 4 GT MFMAs
+template <int GT>
+FS2_DEV void lstm_mfma_share(const float* ap, const float* bp, bool bvalid, int kb, int kper,
+                             f32x4m& c0, f32x4m& c1) {
+  for (int k = kb; k < kb + kper; k += 16 * GT) {
+    float4 av[GT], bv[GT];
 #pragma unroll
-  for (int q = 0; q < LSTM_RPT; ++q) {
-    const int n = n0 + r0 + 4 * q;
-    const float* g = gx + ((int64_t)(n < N ? n : 0) * T + t) * 4 * H;
-#pragma unroll
-    for (int gi = 0; gi < 4; ++gi) a[q][gi] = g[gi * H + j];
-  }
-  if (t > 0) {
-    for (int k = 0; k < H; ++k) {
-      const float* w = wt + (int64_t)k * 4 * H + j;
-      const float w0 = w[0], w1 = w[H], w2 = w[2 * H], w3 = w[3 * H];
-#pragma unroll
-      for (int q = 0; q < LSTM_RPT; ++q) {
-        const float hk = hs[r0 + 4 * q][k];
-        a[q][0] = fmaf(hk, w0, a[q][0]);
-        a[q][1] = fmaf(hk, w1, a[q][1]);
-        a[q][2] = fmaf(hk, w2, a[q][2]);
-        a[q][3] = fmaf(hk, w3, a[q][3]);
-      }
+    for (int g = 0; g < GT; ++g) {
+      av[g] = *reinterpret_cast<const float4*>(ap + k + 16 * g);
+      bv[g] = *reinterpret_cast<const float4*>(bp + k + 16 * g);
     }
-  }
 #pragma unroll
-  for (int q = 0; q < LSTM_RPT; ++q) {
-    const int n = n0 + r0 + 4 * q;
-    if (n >= N) continue;
-    const int64_t row = (int64_t)n * T + t;
-    const float i = sigm(a[q][0]), f = sigm(a[q][1]), gg = tanhf(a[q][2]), o = sigm(a[q][3]);
-    const float cp = t > 0 ? c_all[(row - 1) * H + j] : 0.f;
-    const float c = f * cp + i * gg;
-    c_all[row * H + j] = c;
-    h_all[row * H + j] = o * tanhf(c);
-    float* ap = act + row * 4 * H;
-    ap[j] = i;
-    ap[H + j] = f;
-    ap[2 * H + j] = gg;
-    ap[3 * H + j] = o;
+    for (int g = 0; g < GT; ++g) {
+      if (!bvalid) bv[g] = make_float4(0.f, 0.f, 0.f, 0.f);
+      mfma_k16(av[g], bv[g], c0, c1);
+    }
   }
 }
 
-// reverse step t: dh = dh_out[t] + dgates_{t+1} W_hh ; gate derivatives ; dc ping-pong
-__global__ __launch_bounds__(256) void lstm_bwd_step(const float* __restrict__ dh_out,
-                                                     const float* __restrict__ w_hh,
+constexpr int LSTM_FWD_WAVES = 8;  // split-K ways of the forward tile (K = H)
+constexpr int LSTM_FWD_GT = 2;     // 16-k groups per trip (H / 8 = 32 k per wave at H = 256)
+constexpr int LSTM_BWD_WAVES = 8;  // split-K ways of the backward tile (K = 4H)
+
+// Forward step t.  Block tile: 4 hidden units (16 gate rows m = 4 uu + gate, so a lane's 4
+// accumulators are the i, f, g, o of one (unit, sequence)) x 16 sequences:
+//   gates^T[m][n] = sum_k W_hh[gate * H + u][k] h_{t-1}[n][k]  (+ gx, which holds x W_ih^T + b)
+// then the cell update; saves h, c and the activated gates for the backward.
+__global__ __launch_bounds__(64 * LSTM_FWD_WAVES) void lstm_fwd_step(const float* __restrict__ gx,
+                                                     const float* __restrict__ w_hh, float* h_all,
+                                                     float* c_all, float* act, int N, int T, int H,
+                                                     int t) {
+  __shared__ float red[LSTM_FWD_WAVES][4][64];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int u0 = blockIdx.x * 4, n0 = blockIdx.y * 16;
+  // epilogue thread (wave 0) -> (sequence nn, unit uu), units fastest; its accumulators sit at
+  // lane uu*16 + nn.  Its gx and c_{t-1} loads are issued before the product.
+  const int uu = threadIdx.x & 3, nn = (threadIdx.x >> 2) & 15, ne = n0 + nn, u = u0 + uu;
+  const bool epi = wave == 0 && ne < N;
+  const int64_t row = (int64_t)(epi ? ne : 0) * T + t;
+  float z[4], cp = 0.f;
+  if (epi) {
+    const float* g = gx + row * 4 * H;
+#pragma unroll
+    for (int gi = 0; gi < 4; ++gi) z[gi] = g[gi * H + u];
+    if (t > 0) cp = c_all[(row - 1) * H + u];
+  }
+  if (t > 0) {
+    const int kq = lane >> 4, r = lane & 15;
+    const int m_unit = u0 + (r >> 2), m_gate = r & 3;   // A row of this lane
+    const int n = n0 + r;                              // B column of this lane
+    const float* ap = w_hh + ((int64_t)m_gate * H + m_unit) * H + 4 * kq;
+    const bool nv = n < N;
+    const float* bp = h_all + ((int64_t)(nv ? n : 0) * T + t - 1) * H + 4 * kq;
+    const int kper = H / LSTM_FWD_WAVES;
+    f32x4m c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0;
+    lstm_mfma_share<LSTM_FWD_GT>(ap, bp, nv, wave * kper, kper, c0, c1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) red[wave][i][lane] = c0[i] + c1[i];
+  }
+  __syncthreads();
+  if (!epi) return;
+  if (t > 0) {
+#pragma unroll
+    for (int gi = 0; gi < 4; ++gi) {
+      float r = 0.f;
+#pragma unroll
+      for (int w = 0; w < LSTM_FWD_WAVES; ++w) r += red[w][gi][uu * 16 + nn];
+      z[gi] += r;
+    }
+  }
+  // D rows m = 4 * (lane >> 4) + i: lane quarter = unit, register i = gate
+  const float i = sigm(z[0]), f = sigm(z[1]), gg = tanhf(z[2]), o = sigm(z[3]);
+  const float c = f * cp + i * gg;
+  c_all[row * H + u] = c;
+  h_all[row * H + u] = o * tanhf(c);
+  float* ap = act + row * 4 * H;
+  ap[u] = i;
+  ap[H + u] = f;
+  ap[2 * H + u] = gg;
+  ap[3 * H + u] = o;
+}
+
+// Reverse step t.  Block tile: 16 hidden units x 16 sequences,
+//   dh^T[u][n] = sum_q W_hh^T[u][q] dgates_{t+1}[n][q]  (+ dh_out[t]),
+// split over K = 4H across 8 waves, then the gate derivatives and the dc ping-pong, one
+// (sequence, unit) per thread (units fastest: coalesced dgates / dc stores).
+__global__ __launch_bounds__(512) void lstm_bwd_step(const float* __restrict__ dh_out,
+                                                     const float* __restrict__ w_hh_t,
                                                      const float* __restrict__ act,
                                                      const float* __restrict__ c_all,
                                                      float* dgates, const float* dc_in,
                                                      float* dc_out, int N, int T, int H, int t) {
-  __shared__ float ds[LSTM_RB][4 * LSTM_HMAX];
-  const int tid = threadIdx.x, r0 = tid / LSTM_JB, jj = tid % LSTM_JB;
-  const int n0 = blockIdx.x * LSTM_RB;
+  __shared__ float red[LSTM_BWD_WAVES][4][64];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int u0 = blockIdx.x * 16, n0 = blockIdx.y * 16;
   const bool has_next = t + 1 < T;
+  // epilogue thread (waves 0-3) -> (sequence nn, unit uu), units fastest; its operands are
+  // loaded before the product
+  const int uu = threadIdx.x & 15, nn = (threadIdx.x >> 4) & 15, ne = n0 + nn, u = u0 + uu;
+  const bool epi = threadIdx.x < 256 && ne < N;
+  const int64_t row = (int64_t)(epi ? ne : 0) * T + t;
+  float dh = 0.f, i = 0.f, f = 0.f, gg = 0.f, o = 0.f, c = 0.f, cp = 0.f, dcn = 0.f;
+  if (epi) {
+    if (dh_out) dh = dh_out[row * H + u];
+    const float* ap = act + row * 4 * H;
+    i = ap[u], f = ap[H + u], gg = ap[2 * H + u], o = ap[3 * H + u];
+    c = c_all[row * H + u];
+    if (t > 0) cp = c_all[(row - 1) * H + u];
+    if (has_next) dcn = dc_in[(int64_t)ne * H + u];
+  }
   if (has_next) {
-    for (int e = tid; e < LSTM_RB * 4 * H; e += 256) {
-      const int rr = e / (4 * H), q = e - rr * 4 * H, nn = n0 + rr;
-      ds[rr][q] = nn < N ? dgates[((int64_t)nn * T + t + 1) * 4 * H + q] : 0.f;
-    }
+    const int kq = lane >> 4, r = lane & 15, n = n0 + r;
+    const bool nv = n < N;
+    const float* ap = w_hh_t + (int64_t)(u0 + r) * 4 * H + 4 * kq;
+    const float* bp = dgates + ((int64_t)(nv ? n : 0) * T + t + 1) * 4 * H + 4 * kq;
+    const int kper = 4 * H / LSTM_BWD_WAVES;
+    f32x4m c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0;
+    lstm_mfma_share<4>(ap, bp, nv, wave * kper, kper, c0, c1);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) red[wave][q][lane] = c0[q] + c1[q];
   }
   __syncthreads();
-  const int j = blockIdx.y * LSTM_JB + jj;
-  if (j >= H) return;
-  // recurrent gradient, 4 independent partial sums per row (one per gate block of W_hh)
-  float acc[LSTM_RPT][4];
-#pragma unroll
-  for (int q = 0; q < LSTM_RPT; ++q)
-#pragma unroll
-    for (int gi = 0; gi < 4; ++gi) acc[q][gi] = 0.f;
+  if (!epi) return;
   if (has_next) {
-    for (int u = 0; u < H; ++u) {
-      const float w0 = w_hh[(int64_t)u * H + j], w1 = w_hh[(int64_t)(H + u) * H + j];
-      const float w2 = w_hh[(int64_t)(2 * H + u) * H + j], w3 = w_hh[(int64_t)(3 * H + u) * H + j];
+    // D row m = unit uu = 4 * (lane >> 4) + q, column = sequence nn = lane & 15
+    const int ln = (uu >> 2) * 16 + nn, q = uu & 3;
+    float r = 0.f;
 #pragma unroll
-      for (int q = 0; q < LSTM_RPT; ++q) {
-        const float* d = ds[r0 + 4 * q];
-        acc[q][0] = fmaf(d[u], w0, acc[q][0]);
-        acc[q][1] = fmaf(d[H + u], w1, acc[q][1]);
-        acc[q][2] = fmaf(d[2 * H + u], w2, acc[q][2]);
-        acc[q][3] = fmaf(d[3 * H + u], w3, acc[q][3]);
-      }
-    }
+    for (int w = 0; w < LSTM_BWD_WAVES; ++w) r += red[w][q][ln];
+    dh += r;
   }
-#pragma unroll
-  for (int q = 0; q < LSTM_RPT; ++q) {
-    const int n = n0 + r0 + 4 * q;
-    if (n >= N) continue;
-    const int64_t row = (int64_t)n * T + t;
-    float dh = (acc[q][0] + acc[q][1]) + (acc[q][2] + acc[q][3]);
-    if (dh_out) dh += dh_out[row * H + j];
-    const float* ap = act + row * 4 * H;
-    const float i = ap[j], f = ap[H + j], gg = ap[2 * H + j], o = ap[3 * H + j];
-    const float c = c_all[row * H + j];
-    const float cp = t > 0 ? c_all[(row - 1) * H + j] : 0.f;
-    const float tc = tanhf(c);
-    const float dc = (has_next ? dc_in[(int64_t)n * H + j] : 0.f) + dh * o * (1.f - tc * tc);
-    float* dg = dgates + row * 4 * H;
-    dg[j] = dc * gg * i * (1.f - i);
-    dg[H + j] = dc * cp * f * (1.f - f);
-    dg[2 * H + j] = dc * i * (1.f - gg * gg);
-    dg[3 * H + j] = dh * tc * o * (1.f - o);
-    dc_out[(int64_t)n * H + j] = dc * f;
-  }
+  const float tc = tanhf(c);
+  const float dc = dcn + dh * o * (1.f - tc * tc);
+  float* dg = dgates + row * 4 * H;
+  dg[u] = dc * gg * i * (1.f - i);
+  dg[H + u] = dc * cp * f * (1.f - f);
+  dg[2 * H + u] = dc * i * (1.f - gg * gg);
+  dg[3 * H + u] = dh * tc * o * (1.f - o);
+  dc_out[(int64_t)ne * H + u] = dc * f;
 }
 
 // ---------------------------------------------------------------- discriminator head
@@ -274,10 +313,10 @@ using namespace fs2;
 extern "C" {
 
 int fs2_lstm_layer_fwd(const float* x, int64_t n_seq, int64_t steps, int64_t c_in, int64_t hidden,
-                       const float* w_ih, const float* bias, const float* w_hh_t, float* gx,
+                       const float* w_ih, const float* bias, const float* w_hh, float* gx,
                        float* h_all, float* c_all, float* act, void* stream) {
-  FS2_CHECK_ARG(hidden > 0 && hidden <= LSTM_HMAX && hidden % LSTM_JB == 0 && c_in % 4 == 0,
-                "fs2_lstm_layer_fwd: hidden %lld (<= 256, multiple of 64), c_in %% 4",
+  FS2_CHECK_ARG(hidden > 0 && hidden % 256 == 0 && c_in % 4 == 0,
+                "fs2_lstm_layer_fwd: hidden %lld (multiple of 256), c_in %% 4",
                 (long long)hidden);
   if (n_seq == 0 || steps == 0) return FS2_OK;
   const int64_t rows = n_seq * steps, G = 4 * hidden;
@@ -286,25 +325,25 @@ int fs2_lstm_layer_fwd(const float* x, int64_t n_seq, int64_t steps, int64_t c_i
                          FS2_EPI_BIAS, nullptr, 0, stream);
   if (rc) return rc;
   hipStream_t st = as_stream(stream);
-  const dim3 grid((unsigned)((n_seq + LSTM_RB - 1) / LSTM_RB), (unsigned)(hidden / LSTM_JB));
+  const dim3 grid((unsigned)(hidden / 4), (unsigned)((n_seq + 15) / 16));
   for (int t = 0; t < (int)steps; ++t)
-    lstm_fwd_step<<<grid, 256, 0, st>>>(gx, w_hh_t, h_all, c_all, act, (int)n_seq, (int)steps,
+    lstm_fwd_step<<<grid, 64 * LSTM_FWD_WAVES, 0, st>>>(gx, w_hh, h_all, c_all, act, (int)n_seq, (int)steps,
                                         (int)hidden, t);
   return launch_status("fs2_lstm_layer_fwd");
 }
 
 int fs2_lstm_layer_bwd(const float* dh_out, int64_t n_seq, int64_t steps, int64_t c_in,
-                       int64_t hidden, const float* w_ih_t, const float* w_hh, const float* act,
+                       int64_t hidden, const float* w_ih_t, const float* w_hh_t, const float* act,
                        const float* c_all, float* dgates, float* dc_ws, float* dx, void* stream) {
-  FS2_CHECK_ARG(hidden > 0 && hidden <= LSTM_HMAX && hidden % LSTM_JB == 0,
-                "fs2_lstm_layer_bwd: hidden %lld (<= 256, multiple of 64)", (long long)hidden);
+  FS2_CHECK_ARG(hidden > 0 && hidden % 256 == 0,
+                "fs2_lstm_layer_bwd: hidden %lld (multiple of 256)", (long long)hidden);
   if (n_seq == 0 || steps == 0) return FS2_OK;
   hipStream_t st = as_stream(stream);
-  const dim3 grid((unsigned)((n_seq + LSTM_RB - 1) / LSTM_RB), (unsigned)(hidden / LSTM_JB));
+  const dim3 grid((unsigned)(hidden / 16), (unsigned)((n_seq + 15) / 16));
   float* dc_a = dc_ws;                 // (n_seq, hidden) ping-pong
   float* dc_b = dc_ws + n_seq * hidden;
   for (int t = (int)steps - 1; t >= 0; --t) {
-    lstm_bwd_step<<<grid, 256, 0, st>>>(dh_out, w_hh, act, c_all, dgates, dc_a, dc_b, (int)n_seq,
+    lstm_bwd_step<<<grid, 512, 0, st>>>(dh_out, w_hh_t, act, c_all, dgates, dc_a, dc_b, (int)n_seq,
                                         (int)steps, (int)hidden, t);
     float* tmp = dc_a;
     dc_a = dc_b;

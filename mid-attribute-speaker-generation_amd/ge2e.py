@@ -54,7 +54,7 @@ class _EmbedderFn(torch.autograd.Function):
             act = torch.empty(N * T, 4 * HIDDEN, device=dev)
             wl = w["lstm"][l]
             lib.fs2_lstm_layer_fwd(_p(inp), N, T, c_in, HIDDEN, _p(wl["w_ih"]), _p(wl["bias"]),
-                                   _p(wl["w_hh_t"]), _p(gx), _p(h), _p(c), _p(act), K.stream())
+                                   _p(wl["w_hh"]), _p(gx), _p(h), _p(c), _p(act), K.stream())
             del gx
             saved.append((c_in, c, act))
             inp = h
@@ -90,7 +90,7 @@ class _EmbedderFn(torch.autograd.Function):
             c_in, c, act = fctx.saved[l]
             dx = torch.empty(N * T, c_in, device=dev)
             wl = w["lstm"][l]
-            lib.fs2_lstm_layer_bwd(_p(dh), N, T, c_in, HIDDEN, _p(wl["w_ih_t"]), _p(wl["w_hh"]),
+            lib.fs2_lstm_layer_bwd(_p(dh), N, T, c_in, HIDDEN, _p(wl["w_ih_t"]), _p(wl["w_hh_t"]),
                                    _p(act), _p(c), _p(dgates), _p(dc), _p(dx), K.stream())
             dh = dx
         return dh.view(N, T, D), None, None

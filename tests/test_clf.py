@@ -97,3 +97,40 @@ def test_use_clf_training_steps_match_reference():
                                [g[f"s{it}.eloss"], g[f"s{it}.dloss"], g[f"s{it}.gnorm"]]])
         err = np.abs(got - want) / np.maximum(np.abs(want), 1e-6)
         assert err.max() < 1e-4, (it, got, want)
+
+
+@pytest.mark.gpu
+def test_lstm_layer_matches_torch_lstm():
+    """One LSTM layer through the C-ABI (f32 MFMA recurrence, split-K step kernels) against
+    torch.nn.LSTM in fp32: ragged sequence count (37: partial 16-sequence tiles), c_in 80,
+    outputs h within 2e-5 and the input gradient within 1e-4 of its peak."""
+    K = importlib.import_module("mid-attribute-speaker-generation_amd.kernels")
+    lib = importlib.import_module("mid-attribute-speaker-generation_amd._lib").lib
+    N, T, H, D = 37, 23, 256, 80
+    gen = torch.Generator().manual_seed(11)
+    x = torch.randn(N * T, D, generator=gen).cuda()
+    w_ih = (torch.randn(4 * H, D, generator=gen) * 0.1).cuda()
+    w_hh = (torch.randn(4 * H, H, generator=gen) * 0.1).cuda()
+    b = (torch.randn(4 * H, generator=gen) * 0.1).cuda()
+    dh = (torch.randn(N * T, H, generator=gen) * 0.1).cuda()
+    gx, act, dg = (torch.empty(N * T, 4 * H, device="cuda") for _ in range(3))
+    h, c = torch.empty(N * T, H, device="cuda"), torch.empty(N * T, H, device="cuda")
+    dc, dx = torch.empty(2 * N * H, device="cuda"), torch.empty(N * T, D, device="cuda")
+    P = lambda t: t.data_ptr()
+    assert lib.fs2_lstm_layer_fwd(P(x), N, T, D, H, P(w_ih), P(b), P(w_hh), P(gx), P(h), P(c),
+                                  P(act), K.stream()) == 0
+    w_ih_t, w_hh_t = w_ih.t().contiguous(), w_hh.t().contiguous()
+    assert lib.fs2_lstm_layer_bwd(P(dh), N, T, D, H, P(w_ih_t), P(w_hh_t), P(act), P(c), P(dg),
+                                  P(dc), P(dx), K.stream()) == 0
+    torch.cuda.synchronize()
+    ref = torch.nn.LSTM(D, H, batch_first=True).cuda()
+    with torch.no_grad():
+        ref.weight_ih_l0.copy_(w_ih)
+        ref.weight_hh_l0.copy_(w_hh)
+        ref.bias_ih_l0.copy_(b)
+        ref.bias_hh_l0.zero_()
+    xr = x.view(N, T, D).clone().requires_grad_()
+    out, _ = ref(xr)
+    out.backward(dh.view(N, T, H))
+    assert (h.view(N, T, H) - out.detach()).abs().max().item() < 2e-5
+    assert (dx.view(N, T, D) - xr.grad).abs().max().item() < 1e-4 * xr.grad.abs().max().item()

@@ -120,6 +120,24 @@ int fs2_lstm_layer_fwd(const float* x, int64_t n_seq, int64_t steps, int64_t c_i
 int fs2_lstm_layer_bwd(const float* dh_out, int64_t n_seq, int64_t steps, int64_t c_in,
                        int64_t hidden, const float* w_ih_t, const float* w_hh_t, const float* act,
                        const float* c_all, float* dgates, float* dc_ws, float* dx, void* stream);
+/* The whole L-layer stack (the GE2E LSTM_stack, nn.LSTM(num_layers = L)) as a wavefront:
+ * launch s runs layer l at step s - l, so the stack takes steps + L - 1 launches; the inputs
+ * of layers >= 1 are folded into their step kernels.  Layer-major buffers: h_all, c_all
+ * (L, rows, H), act (L, rows, 4H); weights w_ih0 (4H, c_in), w_ih_up (L-1, 4H, H) = W_ih of
+ * layers 1.., w_hh (L, 4H, H), bias (L, 4H) = b_ih + b_hh; gx (rows, 4H) workspace.  Same
+ * results as fs2_lstm_layer_fwd layer by layer, within fp32 summation order.              */
+int fs2_lstm_stack_fwd(const float* x, int64_t n_seq, int64_t steps, int64_t c_in,
+                       int64_t hidden, int layers, const float* w_ih0, const float* w_ih_up,
+                       const float* w_hh, const float* bias, float* gx, float* h_all,
+                       float* c_all, float* act, void* stream);
+/* Backward of the stack: dh_out (rows, H; NULL = 0) is the top layer's output gradient;
+ * writes dgates (L, rows, 4H) and, with dx, dx = dgates_0 W_ih0 (rows, c_in).  Transposed
+ * weights: w_ih0_t (c_in, 4H), w_ih_up_t (L-1, H, 4H), w_hh_t (L, H, 4H).
+ * dc_ws: L * 2 * n_seq * H floats.                                                      */
+int fs2_lstm_stack_bwd(const float* dh_out, int64_t n_seq, int64_t steps, int64_t c_in,
+                       int64_t hidden, int layers, const float* w_ih0_t, const float* w_ih_up_t,
+                       const float* w_hh_t, const float* act, const float* c_all, float* dgates,
+                       float* dc_ws, float* dx, void* stream);
 /* Embedding + domain-classifier head on the last LSTM frame (x row n at x + n*ldx, 256 wide):
  * projection 256->64, L2 norm (emb), Linear 64->64, dropout, ReLU, Linear 64->64, dropout,
  * ReLU, Linear 64->1 (logit).  w*t are the transposed weights (forward), w* the natural

@@ -61,6 +61,27 @@ FS2_DEV void lstm_mfma_share(const float* ap, const float* bp, bool bvalid, int 
   }
 }
 
+// the same with two A tiles (rows ap0 / ap1) sharing every B load
+template <int GT>
+FS2_DEV void lstm_mfma_share2(const float* ap0, const float* ap1, const float* bp, bool bvalid,
+                              int kb, int kper, f32x4m (&c)[2][2]) {
+  for (int k = kb; k < kb + kper; k += 16 * GT) {
+    float4 a0[GT], a1[GT], bv[GT];
+#pragma unroll
+    for (int g = 0; g < GT; ++g) {
+      a0[g] = *reinterpret_cast<const float4*>(ap0 + k + 16 * g);
+      a1[g] = *reinterpret_cast<const float4*>(ap1 + k + 16 * g);
+      bv[g] = *reinterpret_cast<const float4*>(bp + k + 16 * g);
+    }
+#pragma unroll
+    for (int g = 0; g < GT; ++g) {
+      if (!bvalid) bv[g] = make_float4(0.f, 0.f, 0.f, 0.f);
+      mfma_k16(a0[g], bv[g], c[0][0], c[0][1]);
+      mfma_k16(a1[g], bv[g], c[1][0], c[1][1]);
+    }
+  }
+}
+
 constexpr int LSTM_FWD_WAVES = 8;  // split-K ways of the forward tile (K = H)
 constexpr int LSTM_FWD_GT = 2;     // 16-k groups per trip (H / 8 = 32 k per wave at H = 256)
 constexpr int LSTM_BWD_WAVES = 8;  // split-K ways of the backward tile (K = 4H)
@@ -180,6 +201,184 @@ __global__ __launch_bounds__(512) void lstm_bwd_step(const float* __restrict__ d
   dg[H + u] = dc * cp * f * (1.f - f);
   dg[2 * H + u] = dc * i * (1.f - gg * gg);
   dg[3 * H + u] = dh * tc * o * (1.f - o);
+  dc_out[(int64_t)ne * H + u] = dc * f;
+}
+
+// ---------------------------------------------------------------- stacked layers
+// The whole L-layer stack as a wavefront: launch s runs layer l at step t = s - l (forward)
+// or t = T - 1 - s + (L - 1 - l) (backward), so the stack takes T + L - 1 launches instead
+// of L * T, and the inter-layer products move into the step kernels:
+//   forward, l >= 1:  gates = b_l + W_ih^l h^{l-1}_t + W_hh^l h^l_{t-1}   (K = 2H)
+//   backward, l < L-1: dh^l_t = dgates^{l+1}_t W_ih^{l+1} + dgates^l_{t+1} W_hh^l  (K = 8H)
+// (layer l-1's h_t / layer l+1's dgates_t were written by the previous launch).  Layer 0's
+// input projection and input gradient stay one GEMM each (c_in = 80 mel channels).
+// Buffers are layer-major: h, c (L, rows, H), act, dgates (L, rows, 4H), weights
+// w_hh (L, 4H, H), w_ih of layers 1.. (L-1, 4H, H) and their transposes, bias (L, 4H).
+struct LstmStackFwd {
+  const float* gx0;     // layer 0: x W_ih^T + b (rows, 4H)
+  const float* w_ih_up;
+  const float* w_hh;
+  const float* bias;
+  float* h;
+  float* c;
+  float* act;
+  int N, T, H, L, s;
+};
+
+// 4 waves, 8 hidden units (two 16-gate-row A tiles sharing the h loads) x 16 sequences:
+// layer 0 splits the recurrent K = H 4 ways; layers >= 1 give the input product (K = H) to
+// waves 0-1 and the recurrent one to waves 2-3
+__global__ __launch_bounds__(256) void lstm_stack_fwd_step(LstmStackFwd a) {
+  __shared__ float red[4][2][4][64];
+  const int l = blockIdx.z, t = a.s - l;
+  if (t < 0 || t >= a.T) return;  // block-uniform
+  const int N = a.N, T = a.T, H = a.H;
+  const int64_t rows = (int64_t)N * T;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int u0 = blockIdx.x * 8, n0 = blockIdx.y * 16;
+  float* h_l = a.h + l * rows * H;
+  float* c_l = a.c + l * rows * H;
+  // epilogue thread (waves 0-1) -> (tile ut, sequence nn, unit uu)
+  const int ut = (threadIdx.x >> 6) & 1, uu = threadIdx.x & 3, nn = (threadIdx.x >> 2) & 15;
+  const int ne = n0 + nn, u = u0 + ut * 4 + uu;
+  const bool epi = threadIdx.x < 128 && ne < N;
+  const int64_t row = (int64_t)(epi ? ne : 0) * T + t;
+  float z[4], cp = 0.f;
+  if (epi) {
+    const float* g = l == 0 ? a.gx0 + row * 4 * H : a.bias + (int64_t)l * 4 * H;
+#pragma unroll
+    for (int gi = 0; gi < 4; ++gi) z[gi] = g[gi * H + u];
+    if (t > 0) cp = c_l[(row - 1) * H + u];
+  }
+  const int kq = lane >> 4, r = lane & 15;
+  const int m_row = (r & 3) * H + u0 + (r >> 2);  // gate row of tile 0 (tile 1: + 4)
+  const int n = n0 + r;
+  const bool nv = n < N;
+  const int64_t nrow = (int64_t)(nv ? n : 0) * T;
+  f32x4m c[2][2] = {{{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}},
+                    {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}}};
+  const float* w = nullptr;
+  const float* bp = nullptr;
+  int kb = 0, kper = 0;
+  if (l == 0) {
+    if (t > 0) {
+      w = a.w_hh;
+      bp = h_l + (nrow + t - 1) * H;
+      kb = wave * (H / 4), kper = H / 4;
+    }
+  } else if (wave < 2) {
+    w = a.w_ih_up + (int64_t)(l - 1) * 4 * H * H;
+    bp = a.h + (l - 1) * rows * H + (nrow + t) * H;
+    kb = wave * (H / 2), kper = H / 2;
+  } else if (t > 0) {
+    w = a.w_hh + (int64_t)l * 4 * H * H;
+    bp = h_l + (nrow + t - 1) * H;
+    kb = (wave - 2) * (H / 2), kper = H / 2;
+  }
+  if (w) {
+    const float* ap0 = w + (int64_t)m_row * H + 4 * kq;
+    lstm_mfma_share2<4>(ap0, ap0 + 4 * H, bp + 4 * kq, nv, kb, kper, c);
+  }
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) red[wave][x][i][lane] = c[x][0][i] + c[x][1][i];
+  __syncthreads();
+  if (!epi) return;
+#pragma unroll
+  for (int gi = 0; gi < 4; ++gi) {
+    float acc = 0.f;
+#pragma unroll
+    for (int wv = 0; wv < 4; ++wv) acc += red[wv][ut][gi][uu * 16 + nn];
+    z[gi] += acc;
+  }
+  const float i = sigm(z[0]), f = sigm(z[1]), gg = tanhf(z[2]), o = sigm(z[3]);
+  const float cc = f * cp + i * gg;
+  c_l[row * H + u] = cc;
+  h_l[row * H + u] = o * tanhf(cc);
+  float* ap = a.act + (l * rows + row) * 4 * H;
+  ap[u] = i;
+  ap[H + u] = f;
+  ap[2 * H + u] = gg;
+  ap[3 * H + u] = o;
+}
+
+struct LstmStackBwd {
+  const float* dh_out;     // top layer's output gradient (rows, H) or NULL
+  const float* w_ih_up_t;  // (L-1, H, 4H): W_ih^T of layers 1..
+  const float* w_hh_t;     // (L, H, 4H)
+  const float* act;
+  const float* c;
+  float* dg;               // (L, rows, 4H)
+  float* dc;               // (L, 2, N, H) ping-pong by launch parity
+  int N, T, H, L, s;
+};
+
+// 8 waves, 16 hidden units x 16 sequences: the top layer splits K = 4H (recurrent) 8 ways;
+// lower layers give the gradient from the layer above (K = 4H) to waves 0-3 and the
+// recurrent one to waves 4-7
+__global__ __launch_bounds__(512) void lstm_stack_bwd_step(LstmStackBwd a) {
+  __shared__ float red[8][4][64];
+  const int l = blockIdx.z, L = a.L, t = a.T - 1 - a.s + (L - 1 - l);
+  if (t < 0 || t >= a.T) return;  // block-uniform
+  const int N = a.N, T = a.T, H = a.H;
+  const int64_t rows = (int64_t)N * T;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int u0 = blockIdx.x * 16, n0 = blockIdx.y * 16;
+  const bool has_next = t + 1 < T, top = l == L - 1;
+  float* dg_l = a.dg + l * rows * 4 * H;
+  const float* dc_in = a.dc + ((int64_t)l * 2 + (a.s & 1)) * N * H;
+  float* dc_out = a.dc + ((int64_t)l * 2 + ((a.s + 1) & 1)) * N * H;
+  const int uu = threadIdx.x & 15, nn = (threadIdx.x >> 4) & 15, ne = n0 + nn, u = u0 + uu;
+  const bool epi = threadIdx.x < 256 && ne < N;
+  const int64_t row = (int64_t)(epi ? ne : 0) * T + t;
+  float dh = 0.f, i = 0.f, f = 0.f, gg = 0.f, o = 0.f, c = 0.f, cp = 0.f, dcn = 0.f;
+  if (epi) {
+    if (top && a.dh_out) dh = a.dh_out[row * H + u];
+    const float* ap = a.act + (l * rows + row) * 4 * H;
+    i = ap[u], f = ap[H + u], gg = ap[2 * H + u], o = ap[3 * H + u];
+    const float* c_l = a.c + l * rows * H;
+    c = c_l[row * H + u];
+    if (t > 0) cp = c_l[(row - 1) * H + u];
+    if (has_next) dcn = dc_in[(int64_t)ne * H + u];
+  }
+  const int kq = lane >> 4, r = lane & 15, n = n0 + r;
+  const bool nv = n < N;
+  const int64_t nrow = (int64_t)(nv ? n : 0) * T;
+  f32x4m c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0;
+  if (top) {
+    if (has_next) {
+      const float* ap = a.w_hh_t + ((int64_t)l * H + u0 + r) * 4 * H + 4 * kq;
+      const float* bp = dg_l + (nrow + t + 1) * 4 * H + 4 * kq;
+      lstm_mfma_share<8>(ap, bp, nv, wave * (H / 2), H / 2, c0, c1);
+    }
+  } else if (wave < 4) {
+    const float* ap = a.w_ih_up_t + ((int64_t)l * H + u0 + r) * 4 * H + 4 * kq;  // layer l+1
+    const float* bp = a.dg + (l + 1) * rows * 4 * H + (nrow + t) * 4 * H + 4 * kq;
+    lstm_mfma_share<8>(ap, bp, nv, wave * H, H, c0, c1);
+  } else if (has_next) {
+    const float* ap = a.w_hh_t + ((int64_t)l * H + u0 + r) * 4 * H + 4 * kq;
+    const float* bp = dg_l + (nrow + t + 1) * 4 * H + 4 * kq;
+    lstm_mfma_share<8>(ap, bp, nv, (wave - 4) * H, H, c0, c1);
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) red[wave][q][lane] = c0[q] + c1[q];
+  __syncthreads();
+  if (!epi) return;
+  {
+    const int ln = (uu >> 2) * 16 + nn, q = uu & 3;
+    float acc = 0.f;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) acc += red[w][q][ln];
+    dh += acc;
+  }
+  const float tc = tanhf(c);
+  const float dc = dcn + dh * o * (1.f - tc * tc);
+  float* dgp = dg_l + row * 4 * H;
+  dgp[u] = dc * gg * i * (1.f - i);
+  dgp[H + u] = dc * cp * f * (1.f - f);
+  dgp[2 * H + u] = dc * i * (1.f - gg * gg);
+  dgp[3 * H + u] = dh * tc * o * (1.f - o);
   dc_out[(int64_t)ne * H + u] = dc * f;
 }
 
@@ -355,6 +554,54 @@ int fs2_lstm_layer_bwd(const float* dh_out, int64_t n_seq, int64_t steps, int64_
   const int64_t rows = n_seq * steps;
   return fs2_conv_gemm(FS2_F32, dgates, 4 * hidden, w_ih_t, dx, c_in, rows, rows, 4 * hidden, c_in,
                        1, 0, nullptr, nullptr, 0, nullptr, 0, stream);
+}
+
+int fs2_lstm_stack_fwd(const float* x, int64_t n_seq, int64_t steps, int64_t c_in,
+                       int64_t hidden, int layers, const float* w_ih0, const float* w_ih_up,
+                       const float* w_hh, const float* bias, float* gx, float* h_all,
+                       float* c_all, float* act, void* stream) {
+  FS2_CHECK_ARG(hidden > 0 && hidden % 256 == 0 && c_in % 4 == 0 && layers >= 1,
+                "fs2_lstm_stack_fwd: hidden %lld (multiple of 256), c_in %% 4, layers >= 1",
+                (long long)hidden);
+  FS2_CHECK_ARG(layers == 1 || w_ih_up, "fs2_lstm_stack_fwd: w_ih_up needed for layers > 1");
+  if (n_seq == 0 || steps == 0) return FS2_OK;
+  const int64_t rows = n_seq * steps, G = 4 * hidden;
+  int rc = fs2_conv_gemm(FS2_F32, x, c_in, w_ih0, gx, G, rows, rows, c_in, G, 1, 0, nullptr, bias,
+                         FS2_EPI_BIAS, nullptr, 0, stream);
+  if (rc) return rc;
+  hipStream_t st = as_stream(stream);
+  const dim3 grid((unsigned)(hidden / 8), (unsigned)((n_seq + 15) / 16), (unsigned)layers);
+  LstmStackFwd a{gx, w_ih_up, w_hh, bias, h_all, c_all, act, (int)n_seq, (int)steps,
+                 (int)hidden, layers, 0};
+  for (int s = 0; s < (int)steps + layers - 1; ++s) {
+    a.s = s;
+    lstm_stack_fwd_step<<<grid, 256, 0, st>>>(a);
+  }
+  return launch_status("fs2_lstm_stack_fwd");
+}
+
+int fs2_lstm_stack_bwd(const float* dh_out, int64_t n_seq, int64_t steps, int64_t c_in,
+                       int64_t hidden, int layers, const float* w_ih0_t, const float* w_ih_up_t,
+                       const float* w_hh_t, const float* act, const float* c_all, float* dgates,
+                       float* dc_ws, float* dx, void* stream) {
+  FS2_CHECK_ARG(hidden > 0 && hidden % 256 == 0 && layers >= 1,
+                "fs2_lstm_stack_bwd: hidden %lld (multiple of 256), layers >= 1",
+                (long long)hidden);
+  FS2_CHECK_ARG(layers == 1 || w_ih_up_t, "fs2_lstm_stack_bwd: w_ih_up_t needed for layers > 1");
+  if (n_seq == 0 || steps == 0) return FS2_OK;
+  hipStream_t st = as_stream(stream);
+  const dim3 grid((unsigned)(hidden / 16), (unsigned)((n_seq + 15) / 16), (unsigned)layers);
+  LstmStackBwd a{dh_out, w_ih_up_t, w_hh_t, act, c_all, dgates, dc_ws, (int)n_seq, (int)steps,
+                 (int)hidden, layers, 0};
+  for (int s = 0; s < (int)steps + layers - 1; ++s) {
+    a.s = s;
+    lstm_stack_bwd_step<<<grid, 512, 0, st>>>(a);
+  }
+  int rc = launch_status("fs2_lstm_stack_bwd");
+  if (rc || !dx) return rc;
+  const int64_t rows = n_seq * steps;
+  return fs2_conv_gemm(FS2_F32, dgates, 4 * hidden, w_ih0_t, dx, c_in, rows, rows, 4 * hidden,
+                       c_in, 1, 0, nullptr, nullptr, 0, nullptr, 0, stream);
 }
 
 int fs2_clf_head(const float* x, int64_t ldx, int64_t n, const float* wp, const float* wpt,

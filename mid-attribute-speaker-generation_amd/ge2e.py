@@ -16,9 +16,10 @@ Mirrors ``Multilingual-Speaker-Encoder-with-Domain-Adaptation/speech_embedder_ne
   returned as NaN here as well (M > 1, the speaker-encoder pre-training loss, is outside
   the hot path and raises).
 
-Kernels (``csrc/lstm.hip``): each LSTM layer is one GEMM for the input projection of all
-steps plus one fused recurrent launch per step issued from C; the backward is the same in
-reverse plus one GEMM for the input gradient.  The head (projection .. logit) is one kernel,
+Kernels (``csrc/lstm.hip``): the 3-layer stack runs as a wavefront -- launch s computes
+layer l at step s - l, all layers in one launch (T + 2 launches instead of 3T), with the
+inputs of layers 1-2 folded into their step kernels; layer 0's input projection is one GEMM.
+The backward is the same in reverse plus one GEMM for the input gradient.  The head (projection .. logit) is one kernel,
 one wave per sequence, forward and backward.  The discriminator's own weight gradients are
 not formed: ``train.py`` never steps it (its parameters are set ``requires_grad`` but no
 optimiser holds them), so only the gradient into FastSpeech2's mel output is computed.
@@ -45,19 +46,17 @@ class _EmbedderFn(torch.autograd.Function):
         N, T, D = x.shape
         dev = x.device
         w = emb_mod._prep()
-        inp, saved = x.contiguous().view(N * T, D), []
-        for l in range(LAYERS):
-            c_in = inp.shape[1]
-            gx = torch.empty(N * T, 4 * HIDDEN, device=dev)
-            h = torch.empty(N * T, HIDDEN, device=dev)
-            c = torch.empty(N * T, HIDDEN, device=dev)
-            act = torch.empty(N * T, 4 * HIDDEN, device=dev)
-            wl = w["lstm"][l]
-            lib.fs2_lstm_layer_fwd(_p(inp), N, T, c_in, HIDDEN, _p(wl["w_ih"]), _p(wl["bias"]),
-                                   _p(wl["w_hh"]), _p(gx), _p(h), _p(c), _p(act), K.stream())
-            del gx
-            saved.append((c_in, c, act))
-            inp = h
+        st, rows = w["stack"], N * T
+        gx = torch.empty(rows, 4 * HIDDEN, device=dev)
+        h = torch.empty(LAYERS, rows, HIDDEN, device=dev)
+        c = torch.empty(LAYERS, rows, HIDDEN, device=dev)
+        act = torch.empty(LAYERS, rows, 4 * HIDDEN, device=dev)
+        xc = x.contiguous()
+        lib.fs2_lstm_stack_fwd(_p(xc), N, T, D, HIDDEN, LAYERS, _p(st["w_ih0"]),
+                               _p(st["w_ih_up"]), _p(st["w_hh"]), _p(st["bias"]), _p(gx), _p(h),
+                               _p(c), _p(act), K.stream())
+        del gx
+        saved, inp = (c, act), h[LAYERS - 1]
         emb = torch.empty(N, PROJ, device=dev)
         logit = torch.empty(N, device=dev)
         hd = w["head"]
@@ -84,15 +83,15 @@ class _EmbedderFn(torch.autograd.Function):
                          _p(demb) if demb is not None else None,
                          _p(dlogit) if dlogit is not None else None, last_out, T * HIDDEN,
                          K.stream())
-        dgates = torch.empty(N * T, 4 * HIDDEN, device=dev)
-        dc = torch.empty(2 * N * HIDDEN, device=dev)
-        for l in reversed(range(LAYERS)):
-            c_in, c, act = fctx.saved[l]
-            dx = torch.empty(N * T, c_in, device=dev)
-            wl = w["lstm"][l]
-            lib.fs2_lstm_layer_bwd(_p(dh), N, T, c_in, HIDDEN, _p(wl["w_ih_t"]), _p(wl["w_hh_t"]),
-                                   _p(act), _p(c), _p(dgates), _p(dc), _p(dx), K.stream())
-            dh = dx
+        c, act = fctx.saved
+        st = w["stack"]
+        dgates = torch.empty(LAYERS, N * T, 4 * HIDDEN, device=dev)
+        dc = torch.empty(LAYERS * 2 * N * HIDDEN, device=dev)
+        dx = torch.empty(N * T, D, device=dev)
+        lib.fs2_lstm_stack_bwd(_p(dh), N, T, D, HIDDEN, LAYERS, _p(st["w_ih0_t"]),
+                               _p(st["w_ih_up_t"]), _p(st["w_hh_t"]), _p(act), _p(c), _p(dgates),
+                               _p(dc), _p(dx), K.stream())
+        dh = dx
         return dh.view(N, T, D), None, None
 
 
@@ -152,6 +151,14 @@ class SpeechEmbedder(nn.Module):
                          getattr(self.LSTM_stack, f"bias_hh_l{l}").detach().contiguous())
             lstm.append({"w_ih": w_ih, "w_ih_t": t(w_ih), "w_hh": w_hh, "w_hh_t": t(w_hh),
                          "bias": bias})
+        stack = {
+            "w_ih0": lstm[0]["w_ih"], "w_ih0_t": lstm[0]["w_ih_t"],
+            "w_ih_up": torch.stack([lstm[l]["w_ih"] for l in range(1, LAYERS)]),
+            "w_ih_up_t": torch.stack([lstm[l]["w_ih_t"] for l in range(1, LAYERS)]),
+            "w_hh": torch.stack([lstm[l]["w_hh"] for l in range(LAYERS)]),
+            "w_hh_t": torch.stack([lstm[l]["w_hh_t"] for l in range(LAYERS)]),
+            "bias": torch.stack([lstm[l]["bias"] for l in range(LAYERS)]),
+        }
         L = [self.projection.linear_layer] + [
             getattr(self.da_classifier.classifier.layer, f"linear_{i}").linear_layer
             for i in range(3)]
@@ -160,7 +167,7 @@ class SpeechEmbedder(nn.Module):
         keep = (wts[0], t(wts[0]), bs[0], wts[1], t(wts[1]), bs[1], wts[2], t(wts[2]), bs[2],
                 wts[3], bs[3])
         head = tuple(_p(a) for a in keep)
-        self._cache = {"lstm": lstm, "head": head, "keep": keep}
+        self._cache = {"lstm": lstm, "stack": stack, "head": head, "keep": keep}
         self._key = key
         return self._cache
 

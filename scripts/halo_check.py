@@ -49,23 +49,22 @@ for name, M, T, cin, cout, k, lens in SHAPES:
     (y0, t0), (y1, t1), (y3, t3), (y4, t4) = res[-1], res[0], res[3], res[4]
     errs = {md: ((res[md][0] - y1).abs().max() / y1.abs().max()).item() for md in (5, 6, 7)}
     print(f"    8-wave: 256x128/3 {res[5][1]:7.1f}us  128x128/3 {res[6][1]:7.1f}us  "
-          f"256x128/2 {res[7][1]:7.1f}us  max rel diff vs 4-wave {errs}")
-    assert torch.equal(y1, y3) and torch.equal(y1, y4), name  # same order: bitwise equal
+          f"256x128/2 {res[7][1]:7.1f}us  max rel diff vs default {errs}")
+    # same tiles, same order: bitwise equal (128-row and 256-row tilings differ only in the
+    # padded rows of partially valid tiles, which the 256-row kernels compute)
+    assert torch.equal(y3, y4), name
+    assert torch.equal(res[5][0], res[7][0]), name
     # torch fp32 reference on the same bf16 operands (per-utterance zero padding)
     W = w.float().view(cout, k, cin).permute(0, 2, 1)
     B_ = M // T
     yr = torch.nn.functional.conv1d(x.float().view(B_, T, cin).transpose(1, 2), W, b,
                                     padding=(k - 1) // 2).transpose(1, 2).reshape(M, cout)
-    if lens is not None:  # all-padding row tiles are skipped (zeros, no bias)
-        for u in range(B_):
-            bm = 128 if ((M + 127) // 128) * ((cout + 127) // 128) >= 128 else 64
-            t0_ = (int(lens[u]) + bm - 1) // bm * bm
-            yr[u * T + t0_:(u + 1) * T] = 0
+    if lens is not None:  # compare valid rows (padded rows: skipped tiles or computed)
+        keep = torch.cat([torch.arange(T, device=dev) < int(lens[u]) for u in range(B_)])
+        y0, y1, yr = y0[keep], y1[keep], yr[keep]
     e0 = ((y0 - yr).abs().max() / yr.abs().max()).item()
     e1 = ((y1 - yr).abs().max() / yr.abs().max()).item()
     print(f"    vs torch: tap-major {e0:.1e} halo {e1:.1e}")
-    if lens is not None:
-        e1 = 0.0 if e1 < 1e-5 else e1
     err = ((y1 - y0).abs().max() / y0.abs().max()).item()
     fl = 2 * M * cout * cin * k
     print(f"{name:22s} tap-major {t0:7.1f}us {fl / t0 / 1e6:5.0f}TF | halo-1 {t3:7.1f}us "

@@ -43,6 +43,22 @@ def timeit(run, n=5):
     return s.elapsed_time(e) / n
 
 
+if os.environ.get("LSTM_PROBE"):  # PMC probe: only the stacked kernels, a few launches
+    L = 3
+    w_ih_up = torch.randn(L - 1, 4 * H, H, device=dev) * 0.05
+    w_hh3 = torch.randn(L, 4 * H, H, device=dev) * 0.05
+    bias3 = torch.randn(L, 4 * H, device=dev) * 0.05
+    w_ih_up_t, w_hh3_t = w_ih_up.transpose(1, 2).contiguous(), w_hh3.transpose(1, 2).contiguous()
+    h3, c3 = torch.empty(L, N * T, H, device=dev), torch.empty(L, N * T, H, device=dev)
+    act3, dg3 = torch.empty(L, N * T, 4 * H, device=dev), torch.empty(L, N * T, 4 * H, device=dev)
+    dc3 = torch.empty(L * 2 * N * H, device=dev)
+    lib.fs2_lstm_stack_fwd(P(x), N, T, D, H, L, P(w_ih), P(w_ih_up), P(w_hh3), P(bias3), P(gx),
+                           P(h3), P(c3), P(act3), K.stream())
+    lib.fs2_lstm_stack_bwd(P(dh), N, T, D, H, L, P(w_ih_t), P(w_ih_up_t), P(w_hh3_t), P(act3),
+                           P(c3), P(dg3), P(dc3), P(dx), K.stream())
+    torch.cuda.synchronize()
+    sys.exit(0)
+
 # reference: torch LSTM cell recurrence (fp32) on the same weights, for a correctness check
 fwd()
 torch.cuda.synchronize()
@@ -59,3 +75,29 @@ torch.cuda.synchronize()
 print("bwd dx max abs err vs torch", (dx.view(N, T, D) - xr.grad).abs().max().item(),
       "ref max", xr.grad.abs().max().item(), flush=True)
 print(f"layer fwd {timeit(fwd):.3f} ms, bwd {timeit(bwd):.3f} ms", flush=True)
+
+
+# the 3-layer stack: per-layer path vs the wavefront entry points
+L = 3
+w_ih_up = torch.randn(L - 1, 4 * H, H, device=dev) * 0.05
+w_hh3 = torch.randn(L, 4 * H, H, device=dev) * 0.05
+bias3 = torch.randn(L, 4 * H, device=dev) * 0.05
+w_ih_up_t, w_hh3_t = w_ih_up.transpose(1, 2).contiguous(), w_hh3.transpose(1, 2).contiguous()
+h3, c3 = torch.empty(L, N * T, H, device=dev), torch.empty(L, N * T, H, device=dev)
+act3, dg3 = torch.empty(L, N * T, 4 * H, device=dev), torch.empty(L, N * T, 4 * H, device=dev)
+dc3 = torch.empty(L * 2 * N * H, device=dev)
+dh3 = torch.randn(N * T, H, device=dev) * 0.01
+
+
+def sfwd():
+    lib.fs2_lstm_stack_fwd(P(x), N, T, D, H, L, P(w_ih), P(w_ih_up), P(w_hh3), P(bias3), P(gx),
+                           P(h3), P(c3), P(act3), K.stream())
+
+
+def sbwd():
+    lib.fs2_lstm_stack_bwd(P(dh3), N, T, D, H, L, P(w_ih_t), P(w_ih_up_t), P(w_hh3_t), P(act3),
+                           P(c3), P(dg3), P(dc3), P(dx), K.stream())
+
+
+print(f"3-layer stack (wavefront): fwd {timeit(sfwd):.3f} ms, bwd {timeit(sbwd):.3f} ms "
+      f"(per-layer path: about 3x the layer times above plus 4 GEMMs)", flush=True)

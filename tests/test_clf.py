@@ -134,3 +134,46 @@ def test_lstm_layer_matches_torch_lstm():
     out.backward(dh.view(N, T, H))
     assert (h.view(N, T, H) - out.detach()).abs().max().item() < 2e-5
     assert (dx.view(N, T, D) - xr.grad).abs().max().item() < 1e-4 * xr.grad.abs().max().item()
+
+
+@pytest.mark.gpu
+def test_lstm_stack_wavefront_matches_torch_lstm():
+    """The 3-layer stack as one wavefront (fs2_lstm_stack_fwd/bwd: launch s runs layer l at
+    step s - l, inter-layer products inside the step kernels) against torch.nn.LSTM(
+    num_layers=3) in fp32 on a ragged sequence count: every layer's h within 2e-5, the input
+    gradient within 1e-4 of its peak."""
+    K = importlib.import_module("mid-attribute-speaker-generation_amd.kernels")
+    lib = importlib.import_module("mid-attribute-speaker-generation_amd._lib").lib
+    N, T, H, D, L = 21, 17, 256, 80, 3
+    ref = torch.nn.LSTM(D, H, num_layers=L, batch_first=True).cuda()
+    gen = torch.Generator().manual_seed(5)
+    with torch.no_grad():
+        for prm in ref.parameters():
+            prm.copy_(torch.randn(prm.shape, generator=gen) * 0.1)
+    W = lambda n: getattr(ref, n).detach().contiguous()
+    w_ih = [W(f"weight_ih_l{l}") for l in range(L)]
+    w_hh = torch.stack([W(f"weight_hh_l{l}") for l in range(L)])
+    bias = torch.stack([W(f"bias_ih_l{l}") + W(f"bias_hh_l{l}") for l in range(L)])
+    w_ih_up = torch.stack(w_ih[1:])
+    x = torch.randn(N * T, D, generator=gen).cuda()
+    dh = (torch.randn(N * T, H, generator=gen) * 0.1).cuda()
+    rows = N * T
+    gx = torch.empty(rows, 4 * H, device="cuda")
+    h, c = (torch.empty(L, rows, H, device="cuda") for _ in range(2))
+    act, dg = (torch.empty(L, rows, 4 * H, device="cuda") for _ in range(2))
+    dc, dx = torch.empty(L * 2 * N * H, device="cuda"), torch.empty(rows, D, device="cuda")
+    P = lambda t: t.data_ptr()
+    assert lib.fs2_lstm_stack_fwd(P(x), N, T, D, H, L, P(w_ih[0]), P(w_ih_up), P(w_hh), P(bias),
+                                  P(gx), P(h), P(c), P(act), K.stream()) == 0
+    tr = lambda t: t.transpose(-1, -2).contiguous()
+    w_ih0_t, w_ih_up_t, w_hh_t = tr(w_ih[0]), tr(w_ih_up), tr(w_hh)
+    assert lib.fs2_lstm_stack_bwd(P(dh), N, T, D, H, L, P(w_ih0_t), P(w_ih_up_t), P(w_hh_t),
+                                  P(act), P(c), P(dg), P(dc), P(dx), K.stream()) == 0
+    torch.cuda.synchronize()
+    xr = x.view(N, T, D).clone().requires_grad_()
+    out, (hn, _) = ref(xr)
+    out.backward(dh.view(N, T, H))
+    assert (h[L - 1].view(N, T, H) - out.detach()).abs().max().item() < 2e-5
+    for l in range(L):  # last step of every layer
+        assert (h[l].view(N, T, H)[:, -1] - hn[l].detach()).abs().max().item() < 2e-5
+    assert (dx.view(N, T, D) - xr.grad).abs().max().item() < 1e-4 * xr.grad.abs().max().item()

@@ -70,7 +70,7 @@ def main():
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     for _ in range(args.iters):
-        voc.forward_rows(rows, B, T)
+        voc.forward_rows(rows, B, T, lengths=out[9])
     torch.cuda.synchronize()
     t_voc = (time.perf_counter() - t1) / args.iters
     audio_s = frames * hop / sr

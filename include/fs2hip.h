@@ -43,7 +43,9 @@ enum {
   /* fs2_conv_gemm_ex only (vocoder, hifigan/models.py), applied after BIAS / ADD_AUX:  */
   FS2_EPI_LRELU = 64,        /* y = y >= 0 ? y : alpha * y                      */
   FS2_EPI_ACC_Y = 128,       /* y = (y + y_old[m, n]) * scale  (y read, then written) */
-  FS2_EPI_Y2 = 256           /* y2[m, n] = y >= 0 ? y : alpha2 * y  (compute dtype) */
+  FS2_EPI_Y2 = 256,          /* y2[m, n] = y >= 0 ? y : alpha2 * y  (compute dtype) */
+  FS2_EPI_SKIP_NOSTORE = 512 /* with lens: skipped row tiles store nothing (y, y2 keep their
+                                contents there) -- for consumers that never read those rows */
 };
 
 const char* fs2_last_error(void);
@@ -77,12 +79,17 @@ int fs2_conv_gemm(int dtype, const void* x, int64_t ldx, const void* wk, void* y
  *   in the compute dtype (bf16 for FS2_BF16, fp32 for FS2_F32; ld = c_out): the input copy
  *   of the next convolution (models.py:95-97,157,167).  pad <= (taps-1)*dilation.
  *   ConvTranspose1d(k = 2s, stride s, pad s/2) runs as taps=3, pad=1 over s*c_out phase
- *   columns (see fs2_convT_weight_prep).  fs2_conv_gemm(...) == fs2_conv_gemm_ex(...,
- *   dilation 1, alpha 0, scale 1, y2 NULL, alpha2 0).                                   */
+ *   columns (see fs2_convT_weight_prep).  lens (optional, device, one per utterance): as
+ *   fs2_conv_gemm -- bf16 row tiles made only of rows t >= lens[b] skip the product (their
+ *   outputs are the epilogue of a zero accumulator); rows t < lens[b] are exact.  The
+ *   vocoder passes its valid length plus the network's receptive radius, so the kept samples
+ *   equal the padded-batch result bitwise.  fs2_conv_gemm(...) == fs2_conv_gemm_ex(...,
+ *   dilation 1, lens, alpha 0, scale 1, y2 NULL, alpha2 0).                              */
 int fs2_conv_gemm_ex(int dtype, const void* x, int64_t ldx, const void* wk, void* y, int64_t ldy,
                      int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out, int taps, int pad,
-                     int dilation, const float* bias, int flags, const void* aux, int64_t ld_aux,
-                     float alpha, float scale, void* y2, float alpha2, void* stream);
+                     int dilation, const int64_t* lens, const float* bias, int flags,
+                     const void* aux, int64_t ld_aux, float alpha, float scale, void* y2,
+                     float alpha2, void* stream);
 
 /* ConvTranspose1d(c_in -> c_out, k = 2*stride, stride, padding = stride/2) weight
  * w (c_in, c_out, k) (hifigan/models.py:127-137) as the equivalent 3-tap Conv1d weight
@@ -96,10 +103,11 @@ int fs2_convT_weight_prep(const float* w, const float* bias, int64_t c_in, int64
 /* HiFi-GAN output head (hifigan/models.py:167-169, utils/model.py:74-90):
  *   wav[r] = tanh(bias + sum_{j<7, c} w[0, c, j] * x[r + j - 3, c])   (zero outside the
  *   utterance), x (rows, c_in) in the compute dtype; wav fp32 and, when pcm is not NULL,
- *   pcm[r] = (int16) (wav[r] * max_wav_value) truncated toward zero as numpy's astype.      */
+ *   pcm[r] = (int16) (wav[r] * max_wav_value) truncated toward zero as numpy's astype.
+ *   lens (optional, device, samples per utterance): rows t >= lens[b] are written as 0.     */
 int fs2_vocoder_post(int dtype, const void* x, int64_t rows, int64_t seq_len, int64_t c_in,
-                     const float* w, const float* bias, float max_wav_value, float* wav,
-                     int16_t* pcm, void* stream);
+                     const int64_t* lens, const float* w, const float* bias, float max_wav_value,
+                     float* wav, int16_t* pcm, void* stream);
 
 /* ---------------------------------------------------------------- language discriminator
  * The --use_clf branch (train.py:168-197): GE2E SpeechEmbedder (speech_embedder_net.py:65-162)

@@ -415,8 +415,9 @@ extern "C" {
 
 int fs2_conv_gemm_ex(int dtype, const void* x, int64_t ldx, const void* wk, void* y, int64_t ldy,
                      int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out, int taps, int pad,
-                     int dilation, const float* bias, int flags, const void* aux, int64_t ld_aux,
-                     float alpha, float scale, void* y2, float alpha2, void* stream) {
+                     int dilation, const int64_t* lens, const float* bias, int flags,
+                     const void* aux, int64_t ld_aux, float alpha, float scale, void* y2,
+                     float alpha2, void* stream) {
   FS2_CHECK_ARG(rows >= 0 && seq_len > 0 && taps >= 1 && dilation >= 1 && pad >= 0 &&
                     pad <= (taps - 1) * dilation,
                 "fs2_conv_gemm: bad geometry (taps %d, pad %d, dilation %d)", taps, pad, dilation);
@@ -429,7 +430,7 @@ int fs2_conv_gemm_ex(int dtype, const void* x, int64_t ldx, const void* wk, void
   if (rows == 0) return FS2_OK;
   const VocEpi ve{dilation, alpha, scale, y2, alpha2};
   if (dtype == FS2_BF16)
-    return conv_gemm_bf16_launch(x, ldx, wk, y, ldy, rows, seq_len, c_in, c_out, taps, pad, nullptr,
+    return conv_gemm_bf16_launch(x, ldx, wk, y, ldy, rows, seq_len, c_in, c_out, taps, pad, lens,
                                  bias, flags, aux, ld_aux, ve, as_stream(stream));
   if (dtype != FS2_F32) {
     set_error("fs2_conv_gemm: dtype %d not built", dtype);
@@ -468,7 +469,7 @@ int fs2_conv_gemm(int dtype, const void* x, int64_t ldx, const void* wk, void* y
     return conv_gemm_bf16_launch(x, ldx, wk, y, ldy, rows, seq_len, c_in, c_out, taps, pad, lens,
                                  bias, flags, aux, ld_aux, VocEpi{}, as_stream(stream));
   return fs2_conv_gemm_ex(dtype, x, ldx, wk, y, ldy, rows, seq_len, c_in, c_out, taps, pad, 1,
-                          bias, flags, aux, ld_aux, 0.f, 1.f, nullptr, 0.f, stream);
+                          lens, bias, flags, aux, ld_aux, 0.f, 1.f, nullptr, 0.f, stream);
 }
 
 int fs2_conv_weight_prep(int dtype, const float* w, int64_t c_out, int64_t c_in, int taps,

@@ -63,6 +63,27 @@ FS2_DEV bool rows_all_padding(const int64_t* lens, int64_t T, int64_t r0, int64_
   return true;
 }
 
+// With lens (all-padding row tiles skipped) the XCD-contiguous tile order would give each XCD
+// a contiguous run of utterances, and the XCD holding the longest ones would set the launch
+// time.  m-tiles are therefore visited in a stride permutation (tm' -> tm' * s mod tiles_m,
+// s ~ tiles_m / 8 coprime with tiles_m): each XCD's contiguous run of tm' lands on m-tiles
+// spread over the whole batch.  Every n-tile of an m-tile stays on one XCD (A-row reuse).
+FS2_DEV int igcd(int a, int b) {
+  while (b) {
+    const int t = a % b;
+    a = b;
+    b = t;
+  }
+  return a;
+}
+
+FS2_DEV int m_interleave(int tm, int tiles_m, bool on) {
+  if (!on || tiles_m < 16) return tm;
+  int s = tiles_m / 8 + 1;
+  while (igcd(s, tiles_m) != 1) ++s;
+  return (int)(((int64_t)tm * s) % tiles_m);
+}
+
 FS2_DEV void glds16(const void* src, u16* lds_wave_base) {
   __builtin_amdgcn_global_load_lds(
       (const __attribute__((address_space(1))) void*)src,
@@ -123,6 +144,7 @@ FS2_DEV void nt_epilogue(const GldsArgs& a, f32x4 (&acc)[BM / 32][BN / WN / 16],
                          int64_t m0, int n0, bool skip, int tid, int wm, int wn, int g, int r16) {
   constexpr int MI = BM / 32, NI = BN / WN / 16;
   constexpr int EPI_LD = BN + 4;
+  if (skip && (a.flags & FS2_EPI_SKIP_NOSTORE)) return;  // block-uniform
   float* Cs = reinterpret_cast<float*>(smem);
   const bool out_bf16 = a.flags & FS2_EPI_OUT_BF16, aux_bf16 = a.flags & FS2_EPI_AUX_BF16;
 #pragma unroll
@@ -292,7 +314,8 @@ __global__ __launch_bounds__(256) void conv_gemm_nt_glds(GldsArgs a) {
   const int gfull = a.tiles_m * a.group;
   const int ng = wg / gfull, rem = wg - ng * gfull;
   const int gsz = a.tiles_n - ng * a.group < a.group ? a.tiles_n - ng * a.group : a.group;
-  const int tm = rem / gsz, tn = ng * a.group + (rem - (rem / gsz) * gsz);
+  const int tm = m_interleave(rem / gsz, a.tiles_m, a.lens != nullptr);
+  const int tn = ng * a.group + (rem - (rem / gsz) * gsz);
   const int64_t m0 = (int64_t)tm * BM;
   const int n0 = tn * BN;
   const bool skip = a.lens && rows_all_padding(a.lens, a.T, m0, m0 + BM < a.M ? m0 + BM : a.M);
@@ -436,7 +459,8 @@ void conv_gemm_halo(GldsArgs a) {
   const int gfull = a.tiles_m * a.group;
   const int ng = wg / gfull, rem = wg - ng * gfull;
   const int gsz = a.tiles_n - ng * a.group < a.group ? a.tiles_n - ng * a.group : a.group;
-  const int tm = rem / gsz, tn = ng * a.group + (rem - (rem / gsz) * gsz);
+  const int tm = m_interleave(rem / gsz, a.tiles_m, a.lens != nullptr);
+  const int tn = ng * a.group + (rem - (rem / gsz) * gsz);
   const int64_t m0 = (int64_t)tm * BM;
   const int n0 = tn * BN;
   const bool skip = a.lens && rows_all_padding(a.lens, a.T, m0, m0 + BM < a.M ? m0 + BM : a.M);

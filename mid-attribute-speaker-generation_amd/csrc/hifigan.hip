@@ -48,13 +48,33 @@ constexpr int POST_ROWS = 256, POST_TAPS = 7, POST_PAD = 3;
 
 template <typename T>
 __global__ __launch_bounds__(256) void vocoder_post_kernel(const T* x, int64_t rows, int64_t T_,
-                                                           int c_in, const float* w,
+                                                           int c_in, const int64_t* lens,
+                                                           const float* w,
                                                            const float* bias, float max_wav,
                                                            float* wav, int16_t* pcm) {
   extern __shared__ float sm[];  // [(POST_ROWS + 6) * c_in] rows, then [7 * c_in] weights
   float* xs = sm;
   float* ws = sm + (POST_ROWS + POST_TAPS - 1) * c_in;
   const int64_t r0 = (int64_t)blockIdx.x * POST_ROWS;
+  if (lens) {  // a block of rows past their utterances' valid lengths writes zeros only
+    const int64_t r1 = r0 + POST_ROWS < rows ? r0 + POST_ROWS : rows;
+    bool all_pad = true;
+    for (int64_t b = r0 / T_; b <= (r1 - 1) / T_; ++b) {
+      const int64_t lo = b * T_ > r0 ? b * T_ : r0;
+      if (lo - b * T_ < lens[b]) {
+        all_pad = false;
+        break;
+      }
+    }
+    if (all_pad) {
+      const int64_t r = r0 + threadIdx.x;
+      if (r < rows) {
+        wav[r] = 0.f;
+        if (pcm) pcm[r] = 0;
+      }
+      return;
+    }
+  }
   const int HR = POST_ROWS + POST_TAPS - 1;
   for (int i = threadIdx.x; i < POST_TAPS * c_in; i += blockDim.x) {
     const int j = i / c_in, c = i - j * c_in;
@@ -71,6 +91,11 @@ __global__ __launch_bounds__(256) void vocoder_post_kernel(const T* x, int64_t r
   const int64_t r = r0 + threadIdx.x;
   if (r >= rows) return;
   const int64_t t = r % T_;  // frame within the utterance
+  if (lens && t >= lens[r / T_]) {
+    wav[r] = 0.f;
+    if (pcm) pcm[r] = 0;
+    return;
+  }
   float acc = bias[0];
   for (int j = 0; j < POST_TAPS; ++j) {
     const int64_t tt = t + j - POST_PAD;
@@ -106,8 +131,8 @@ int fs2_convT_weight_prep(const float* w, const float* bias, int64_t c_in, int64
 }
 
 int fs2_vocoder_post(int dtype, const void* x, int64_t rows, int64_t seq_len, int64_t c_in,
-                     const float* w, const float* bias, float max_wav_value, float* wav,
-                     int16_t* pcm, void* stream) {
+                     const int64_t* lens, const float* w, const float* bias, float max_wav_value,
+                     float* wav, int16_t* pcm, void* stream) {
   FS2_CHECK_ARG(x && w && bias && wav && rows >= 0 && seq_len > 0 && c_in > 0 && c_in <= 64,
                 "fs2_vocoder_post: bad arguments (c_in %lld <= 64)", (long long)c_in);
   if (rows == 0) return FS2_OK;
@@ -116,10 +141,11 @@ int fs2_vocoder_post(int dtype, const void* x, int64_t rows, int64_t seq_len, in
   hipStream_t st = as_stream(stream);
   if (dtype == FS2_BF16)
     vocoder_post_kernel<unsigned short><<<grid, 256, smem, st>>>(
-        (const unsigned short*)x, rows, seq_len, (int)c_in, w, bias, max_wav_value, wav, pcm);
+        (const unsigned short*)x, rows, seq_len, (int)c_in, lens, w, bias, max_wav_value, wav,
+        pcm);
   else if (dtype == FS2_F32)
     vocoder_post_kernel<float><<<grid, 256, smem, st>>>((const float*)x, rows, seq_len, (int)c_in,
-                                                        w, bias, max_wav_value, wav, pcm);
+                                                        lens, w, bias, max_wav_value, wav, pcm);
   else {
     set_error("fs2_vocoder_post: dtype %d not built", dtype);
     return FS2_ERR_DTYPE;

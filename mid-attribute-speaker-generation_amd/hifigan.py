@@ -26,6 +26,7 @@ parity) with the surrounding elementwise work fused into its epilogue:
 * ``conv_post`` + ``tanh`` (+ the int16 PCM of ``vocoder_infer``) is ``fs2_vocoder_post``.
 """
 import json
+import math
 import os
 
 import numpy as np
@@ -151,12 +152,61 @@ class Generator(nn.Module):
         wav, _ = self.forward_rows(rows, B, T, pcm=False)
         return wav.view(B, 1, -1)
 
+    def receptive_frames(self):
+        """Receptive radius of one output sample, in mel frames (rounded up): conv_pre, each
+        upsample's 3-tap phase conv, each stage's widest resblock chain and conv_post, every
+        radius divided by the rows per frame at its resolution."""
+        h, res = self.h, 1
+        r = 3.0  # conv_pre k=7
+        for i, s in enumerate(h.upsample_rates):
+            r += 1.0 / res  # phase conv (taps 3, pad 1) at the input resolution
+            res *= s
+            r += max(sum((k - 1) // 2 * d + (k - 1) // 2 for d in dil)
+                     for k, dil in zip(h.resblock_kernel_sizes, h.resblock_dilation_sizes)) / res
+        r += 3.0 / res  # conv_post k=7
+        return int(math.ceil(r))
+
+    def _stage_lens(self, lengths, B, T, dev):
+        """Per-resolution row limits for length-aware launches: min(T, len + R) frames times
+        the rows per frame (R = receptive_frames), so every kept sample is computed from
+        exactly the rows the padded-batch pass uses; the last entry (samples) is len * up."""
+        R = self.receptive_frames()
+        if torch.is_tensor(lengths):  # device lengths (the model's mel_len): no host sync
+            if lengths.numel() != B:
+                raise ValueError(f"lengths must hold {B} frame counts")
+            l = lengths.to(device=dev, dtype=torch.int64).reshape(B)
+            ext = torch.clamp(l + R, max=T)
+            res, out = 1, []
+            for s in [1] + list(self.h.upsample_rates):
+                res *= s
+                out.append((ext * res).contiguous())
+            out.append((torch.clamp(l, 0, T) * res).contiguous())
+            return out
+        lens = [int(l) for l in lengths]
+        if len(lens) != B or min(lens) < 0 or max(lens) > T:
+            raise ValueError(f"lengths must be {B} frame counts in [0, {T}]")
+        res, table = 1, []
+        for s in [1] + list(self.h.upsample_rates):
+            res *= s
+            table.append([min(T, l + R) * res for l in lens])
+        table.append([l * res for l in lens])
+        t = torch.tensor(table, dtype=torch.int64).to(dev, non_blocking=True)
+        return [t[i] for i in range(len(table))]
+
     @torch.no_grad()
-    def forward_rows(self, mel_rows, B, T, pcm=True, max_wav_value=32768.0):
+    def forward_rows(self, mel_rows, B, T, pcm=True, max_wav_value=32768.0, lengths=None):
         """mel_rows (B*T, 80) fp32 (the FastSpeech2 row layout) -> (wav (B*T*up,) fp32,
-        pcm int16 or None)."""
+        pcm int16 or None).  ``lengths`` (mel frames per utterance, optional; a list or a
+        device tensor such as the model's mel_len): row tiles past
+        length + receptive radius are not computed and samples past length * up are 0; the
+        samples before it are bitwise those of the full padded pass."""
         prep = self._prep()
         cdt, dev = self.compute_dtype, mel_rows.device
+        sl = self._stage_lens(lengths, B, T, dev) if lengths is not None else None
+        L = (lambda i: sl[i]) if sl is not None else (lambda i: None)
+        # skipped tiles store nothing: rows past length + radius are never read for a kept
+        # sample (a GEMM output row depends only on the input rows within its taps)
+        NS = K.EPI_SKIP_NOSTORE if sl is not None else 0
         x_c = mel_rows.contiguous()
         if x_c.dtype != cdt:
             x_c = K.cast_bf16(x_c.float()) if cdt == torch.bfloat16 else x_c.float()
@@ -165,7 +215,7 @@ class Generator(nn.Module):
         # conv_pre: only its leaky-ReLU'd copy is consumed (models.py:156-157)
         h_c = torch.empty(rows, ch, dtype=cdt, device=dev)
         K.conv_gemm_ex(x_c, prep["pre"], rows, seq, x_c.shape[1], ch, 7, 3,
-                       bias=self.conv_pre.bias, y2=h_c, alpha2=LRELU_SLOPE)
+                       bias=self.conv_pre.bias, y2=h_c, alpha2=LRELU_SLOPE, lens=L(0), flags=NS)
         nk = self.num_kernels
         for i in range(self.num_upsamples):
             s = self.h.upsample_rates[i]
@@ -176,7 +226,7 @@ class Generator(nn.Module):
             # ConvTranspose1d as the 3-tap phase conv: (rows, s*c_out) == (rows*s, c_out)
             K.conv_gemm_ex(h_c, wk, rows, seq, c_in, s * c_out, 3, 1, bias=bc,
                            out=x.view(rows, s * c_out), y2=xl.view(rows, s * c_out),
-                           alpha2=LRELU_SLOPE)
+                           alpha2=LRELU_SLOPE, lens=L(i), flags=NS)
             rows, seq = rows * s, seq * s
             xs = torch.empty(rows, c_out, dtype=torch.float32, device=dev)
             last_stage = i == self.num_upsamples - 1
@@ -189,29 +239,30 @@ class Generator(nn.Module):
                 for m, d in enumerate(rb.dilation):
                     t_c = torch.empty(rows, c_out, dtype=cdt, device=dev)
                     K.conv_gemm_ex(cur_l, w1[m], rows, seq, c_out, c_out, k, get_padding(k, d),
-                                   dilation=d, bias=rb.convs1[m].bias, flags=K.EPI_LRELU,
-                                   alpha=LRELU_SLOPE, out=t_c)
+                                   dilation=d, bias=rb.convs1[m].bias, flags=K.EPI_LRELU | NS,
+                                   alpha=LRELU_SLOPE, out=t_c, lens=L(i + 1))
                     if m < 2:
                         nxt = torch.empty(rows, c_out, dtype=torch.float32, device=dev)
                         nxt_l = torch.empty(rows, c_out, dtype=cdt, device=dev)
                         K.conv_gemm_ex(t_c, w2[m], rows, seq, c_out, c_out, k, get_padding(k, 1),
-                                       bias=rb.convs2[m].bias, flags=K.EPI_ADD_AUX, aux=cur,
-                                       out=nxt, y2=nxt_l, alpha2=LRELU_SLOPE)
+                                       bias=rb.convs2[m].bias, flags=K.EPI_ADD_AUX | NS, aux=cur,
+                                       out=nxt, y2=nxt_l, alpha2=LRELU_SLOPE, lens=L(i + 1))
                         cur, cur_l = nxt, nxt_l
                     else:
                         # xs (+)= this resblock's output; the third also averages and emits the
                         # leaky-ReLU'd input of the next upsample / of conv_post (slope 0.01,
                         # F.leaky_relu's default, models.py:167)
-                        flags = K.EPI_ADD_AUX | (K.EPI_ACC_Y if j > 0 else 0)
+                        flags = K.EPI_ADD_AUX | (K.EPI_ACC_Y if j > 0 else 0) | NS
                         fin = j == nk - 1
                         K.conv_gemm_ex(t_c, w2[m], rows, seq, c_out, c_out, k, get_padding(k, 1),
                                        bias=rb.convs2[m].bias, flags=flags, aux=cur, out=xs,
                                        y2=h_c if fin else None,
                                        scale=1.0 / nk if fin else 1.0,
-                                       alpha2=0.01 if last_stage else LRELU_SLOPE)
+                                       alpha2=0.01 if last_stage else LRELU_SLOPE,
+                                       lens=L(i + 1))
         c_last = ch // 2 ** self.num_upsamples
         return K.vocoder_post(h_c, rows, seq, c_last, prep["post_w"], self.conv_post.bias,
-                              max_wav_value, pcm=pcm)
+                              max_wav_value, pcm=pcm, lens=L(self.num_upsamples + 1))
 
 
 def get_vocoder(config=None, device="cuda", ckpt=None, compute_dtype=torch.bfloat16):
@@ -236,7 +287,12 @@ def vocoder_infer(mels, vocoder, model_config, preprocess_config, lengths=None):
     B, C, T = mels.shape
     rows = mels.transpose(1, 2).contiguous().reshape(B * T, C)
     max_wav = preprocess_config["audio"]["max_wav_value"]  # utils/model.py:84-86
-    _, pcm = vocoder.forward_rows(rows, B, T, pcm=True, max_wav_value=float(max_wav))
+    # with lengths, only the frames that reach a kept sample are computed (length-aware
+    # launches; the kept samples are identical to the padded pass)
+    up = math.prod(vocoder.h.upsample_rates)
+    frames = None if lengths is None else [min(T, -(-int(l) // up)) for l in lengths]
+    _, pcm = vocoder.forward_rows(rows, B, T, pcm=True, max_wav_value=float(max_wav),
+                                  lengths=frames)
     wavs = list(pcm.view(B, -1).cpu().numpy())
     if lengths is not None:
         wavs = [w[: lengths[i]] for i, w in enumerate(wavs)]

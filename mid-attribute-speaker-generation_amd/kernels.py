@@ -18,7 +18,7 @@ F32 = 0
 BF16 = 1
 F64 = 2
 EPI_BIAS, EPI_RELU, EPI_ADD_AUX, EPI_RELU_MASK_AUX, EPI_OUT_BF16, EPI_AUX_BF16 = 1, 2, 4, 8, 16, 32
-EPI_LRELU, EPI_ACC_Y, EPI_Y2 = 64, 128, 256
+EPI_LRELU, EPI_ACC_Y, EPI_Y2, EPI_SKIP_NOSTORE = 64, 128, 256, 512
 _CODE = {torch.float32: F32, torch.bfloat16: BF16}
 
 
@@ -93,10 +93,11 @@ def conv_gemm(x, wk, rows, seq_len, c_in, c_out, taps, pad, bias=None, flags=0, 
 
 
 def conv_gemm_ex(x, wk, rows, seq_len, c_in, c_out, taps, pad, dilation=1, bias=None, flags=0,
-                 aux=None, out=None, y2=None, alpha=0.1, scale=1.0, alpha2=0.1):
+                 aux=None, out=None, y2=None, alpha=0.1, scale=1.0, alpha2=0.1, lens=None):
     """Dilated conv with the vocoder epilogue (fs2_conv_gemm_ex): out and/or y2 (the
-    leaky-ReLU'd compute copy, dtype of x) must be given; ACC_Y reads ``out`` first."""
-    _dev(x, wk, bias, aux, out, y2)
+    leaky-ReLU'd compute copy, dtype of x) must be given; ACC_Y reads ``out`` first.
+    ``lens`` (int64 per utterance, rows of this resolution): tiles past it may be skipped."""
+    _dev(x, wk, bias, aux, out, y2, lens)
     if x.dtype != wk.dtype:
         raise RuntimeError(f"conv_gemm_ex operand dtypes differ: {x.dtype} vs {wk.dtype}")
     if out is None and y2 is None:
@@ -112,8 +113,8 @@ def conv_gemm_ex(x, wk, rows, seq_len, c_in, c_out, taps, pad, dilation=1, bias=
     if aux is not None and aux.dtype == torch.bfloat16:
         flags |= EPI_AUX_BF16
     lib.fs2_conv_gemm_ex(code(x.dtype), ptr(x), c_in, ptr(wk), ptr(out), c_out, rows, seq_len,
-                         c_in, c_out, taps, pad, dilation, ptr(bias), flags, ptr(aux), c_out,
-                         alpha, scale, ptr(y2), alpha2, stream())
+                         c_in, c_out, taps, pad, dilation, ptr(lens), ptr(bias), flags, ptr(aux),
+                         c_out, alpha, scale, ptr(y2), alpha2, stream())
     return out, y2
 
 
@@ -130,11 +131,11 @@ def convT_weight_prep(w, bias, stride):
     return wc, bc
 
 
-def vocoder_post(x, rows, seq_len, c_in, w, bias, max_wav_value=32768.0, pcm=True):
-    _dev(x, w, bias)
+def vocoder_post(x, rows, seq_len, c_in, w, bias, max_wav_value=32768.0, pcm=True, lens=None):
+    _dev(x, w, bias, lens)
     wav = torch.empty(rows, dtype=torch.float32, device=x.device)
     p = torch.empty(rows, dtype=torch.int16, device=x.device) if pcm else None
-    lib.fs2_vocoder_post(code(x.dtype), ptr(x), rows, seq_len, c_in, ptr(w), ptr(bias),
+    lib.fs2_vocoder_post(code(x.dtype), ptr(x), rows, seq_len, c_in, ptr(lens), ptr(w), ptr(bias),
                          max_wav_value, ptr(wav), ptr(p), stream())
     return wav, p
 

@@ -28,8 +28,10 @@ def synth_batch(model, vocoder, batch, control_values=(1.0, 1.0, 1.0), hop_lengt
                 speaker_meta=speaker_meta)
     post, mel_len = out[1], out[9]
     B, T, C = post.shape
+    # length-aware vocoder launches (frames past mel_len + the receptive radius are not
+    # computed); the kept samples equal the padded pass of utils/tools.py:264-270
     _, pcm = vocoder.forward_rows(post.reshape(B * T, C), B, T, pcm=True,
-                                  max_wav_value=max_wav_value)
+                                  max_wav_value=max_wav_value, lengths=mel_len)
     lengths = (mel_len * hop_length).tolist()
     pcm = pcm.view(B, -1)
     wavs = [pcm[i, : lengths[i]].cpu().numpy() for i in range(B)]

@@ -134,3 +134,23 @@ def test_synthesize_end_to_end():
     ref = HG.vocoder_infer(out[1].transpose(1, 2), voc, mc, pp, lengths=lengths)
     for w, r in zip(wavs, ref):
         assert np.abs(w.astype(np.int32) - r.astype(np.int32)).max() <= 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_vocoder_length_aware_equals_padded_pass(dtype):
+    """vocoder_infer with lengths launches length-aware convs (row tiles past each
+    utterance's length + the receptive radius are skipped): the kept samples are bitwise
+    those of the full padded-batch pass, as the reference computes them."""
+    gen, _ = _gpu_gen(dtype)
+    g = torch.Generator().manual_seed(3)
+    B, T = 4, 160
+    mel = (torch.randn(B, 80, T, generator=g) * 2.0 - 4.0).cuda()
+    pp = {"audio": {"max_wav_value": 32768.0}}
+    full = HG.vocoder_infer(mel, gen, None, pp)
+    lengths = [160 * 256, 17 * 256 - 100, 96 * 256, 1]
+    short = HG.vocoder_infer(mel, gen, None, pp, lengths=lengths)
+    for f, s_, n in zip(full, short, lengths):
+        assert len(s_) == n
+        assert np.array_equal(f[:n], s_), n
+    assert gen.receptive_frames() == 14  # V1: 3 + 1 + 60/8 + ... + 3/256 -> 14

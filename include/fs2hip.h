@@ -100,6 +100,23 @@ int fs2_conv_gemm_ex(int dtype, const void* x, int64_t ldx, const void* wk, void
 int fs2_convT_weight_prep(const float* w, const float* bias, int64_t c_in, int64_t c_out,
                           int stride, float* wc, float* bias_c, void* stream);
 
+/* Fused HiFi-GAN ResBlock1 (hifigan/models.py:21-53) for the narrow stages: one launch runs
+ * the block's three (leaky_relu 0.1, dilated conv k, leaky_relu 0.1, conv k, residual add)
+ * pairs on an LDS-resident row tile (R = 256 rows at 32 channels, 128 at 64) and folds the
+ * stage's running average: v = acc ? (xs + out) * scale : out * scale; xs = v when store_xs;
+ * hc = bf16(leaky_relu(v, alpha2)) when hc is given.  x (rows, C) fp32; w1 / w2: HOST arrays
+ * of 3 device pointers to fs2_conv_weight_prep bf16 weights (C, k*C); b1 / b2: host arrays
+ * of 3 fp32 bias pointers; dil: host array of 3 dilations.  seq_len % R == 0 (tiles inside
+ * one utterance; zero padding at its edges as each Conv1d).  lens (optional): tiles made
+ * only of rows t >= lens[b] store nothing.  fs2_resblock1_supported() returns 1 when a shape
+ * qualifies (channels 32 / 64, receptive radius <= 64 rows), else 0 (not an error code). */
+int fs2_resblock1_supported(int64_t channels, int64_t seq_len, int kernel_size, const int* dil);
+int fs2_resblock1_fused(const void* x, int64_t rows, int64_t seq_len, int64_t channels,
+                        int kernel_size, const int* dil, const void* const* w1,
+                        const void* const* w2, const float* const* b1, const float* const* b2,
+                        float* xs, int acc, float scale, int store_xs, void* hc, float alpha2,
+                        const int64_t* lens, void* stream);
+
 /* HiFi-GAN output head (hifigan/models.py:167-169, utils/model.py:74-90):
  *   wav[r] = tanh(bias + sum_{j<7, c} w[0, c, j] * x[r + j - 3, c])   (zero outside the
  *   utterance), x (rows, c_in) in the compute dtype; wav fp32 and, when pcm is not NULL,

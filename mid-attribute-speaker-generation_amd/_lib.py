@@ -79,7 +79,8 @@ class _Lib:
             raise AttributeError(name)
         dll = self.load()
         fn = getattr(dll, name)
-        if fn.restype is ctypes.c_int and name not in ("fs2_abi_version", "fs2_weight_prep_tile_channels"):
+        if fn.restype is ctypes.c_int and name not in ("fs2_abi_version", "fs2_weight_prep_tile_channels",
+                                                        "fs2_resblock1_supported"):
             def call(*args, _fn=fn, _name=name):
                 rc = _fn(*args)
                 if rc != 0:

@@ -1176,7 +1176,10 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
   // halo kernel (tile sizes as the tap-major choice below: 128x128 / 128x64 / 64x64 by grid;
   // FS2_TUNE_NT_HALO = 2 forces 128 x 128).  Every row tile must lie inside one utterance.
   const bool halo_wide = big >= 512 || g_tune[FS2_TUNE_NT_HALO] == 2;
-  const int halo_bm = halo_wide || big >= 128 ? 128 : 64;
+  int halo_bm = halo_wide || big >= 128 ? 128 : 64;
+  // utterances a multiple of 64 rows only (the vocoder's 64-rows-per-frame stage over an odd
+  // frame count): 64-row tiles keep the halo kernel (the tap-major one re-stages A per tap)
+  if (halo_bm == 128 && seq_len % 128 != 0 && seq_len % 64 == 0) halo_bm = 64;
   // 8-wave variants (FS2_TUNE_NT_HALO 5 / 6 / 7: 256x128 3-slot / 128x128 3-slot / 256x128
   // 2-slot), one block per CU with the weight prefetch in flight across the barrier
   // Default for the wide forward shapes (c_in <= 512, >= 512 128x128 tiles, T % 256 == 0: the
@@ -1210,18 +1213,21 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
   else if (voc) conv_gemm_halo<BM_, BN_, 2, 16, true><<<grid, 256, 0, st>>>(a);    \
   else conv_gemm_halo<BM_, BN_, BST_, 16, false><<<grid, 256, 0, st>>>(a);
     if (g_tune[FS2_TUNE_NT_HALO] == 3) {  // single-buffered weight tile (A/B experiments)
-      if (halo_wide) { FS2_HALO(128, 128, 1) }
+      if (halo_wide && halo_bm == 128) { FS2_HALO(128, 128, 1) }
+      else if (halo_wide) { FS2_HALO(64, 128, 1) }
       else if (halo_bm == 128) { FS2_HALO(128, 64, 1) }
       else { FS2_HALO(64, 64, 1) }
     } else if (g_tune[FS2_TUNE_NT_HALO] == 4) {  // 3-slot weight ring, 2 tiles ahead
-      if (halo_wide) { FS2_HALO(128, 128, 3) }
+      if (halo_wide && halo_bm == 128) { FS2_HALO(128, 128, 3) }
+      else if (halo_wide) { FS2_HALO(64, 128, 3) }
       else if (halo_bm == 128) { FS2_HALO(128, 64, 3) }
       else { FS2_HALO(64, 64, 3) }
     } else {
       // (a third ring slot measured faster alone for the k=9 data gradients, 71 -> 65 us, but
       // 1.7-2x slower inside the step, where the weight-gradient stream shares the CUs and
       // the lower occupancy (2 blocks/CU) cannot absorb it: knob 4 keeps it for experiments)
-      if (halo_wide) { FS2_HALO(128, 128, 2) }
+      if (halo_wide && halo_bm == 128) { FS2_HALO(128, 128, 2) }
+      else if (halo_wide) { FS2_HALO(64, 128, 2) }
       else if (halo_bm == 128) { FS2_HALO(128, 64, 2) }
       else { FS2_HALO(64, 64, 2) }
     }

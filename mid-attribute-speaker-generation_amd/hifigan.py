@@ -79,6 +79,7 @@ class Generator(nn.Module):
         self.num_kernels = len(h.resblock_kernel_sizes)
         self.num_upsamples = len(h.upsample_rates)
         self.compute_dtype = compute_dtype
+        self.fused_resblocks = True  # bf16: narrow-stage resblocks as one fused launch each
         dev = torch.device(device)
         P = lambda *shape: nn.Parameter(torch.zeros(*shape, device=dev), requires_grad=False)
         ch0 = h.upsample_initial_channel
@@ -221,16 +222,34 @@ class Generator(nn.Module):
             s = self.h.upsample_rates[i]
             c_in, c_out = ch // 2 ** i, ch // 2 ** (i + 1)
             wk, bc = prep["ups"][i]
+            # narrow stages (32 / 64 channels, bf16): each resblock is one fused launch on an
+            # LDS-resident tile (fs2_resblock1_fused), which takes x and applies its own
+            # leaky ReLU -- no bf16 copy of x needed
+            fused = (self.fused_resblocks and cdt == torch.bfloat16 and all(
+                K.resblock1_supported(c_out, seq * s, rb.kernel_size, rb.dilation)
+                for rb in self.resblocks[i * nk:(i + 1) * nk]))
             x = torch.empty(rows * s, c_out, dtype=torch.float32, device=dev)
-            xl = torch.empty(rows * s, c_out, dtype=cdt, device=dev)
+            xl = None if fused else torch.empty(rows * s, c_out, dtype=cdt, device=dev)
             # ConvTranspose1d as the 3-tap phase conv: (rows, s*c_out) == (rows*s, c_out)
             K.conv_gemm_ex(h_c, wk, rows, seq, c_in, s * c_out, 3, 1, bias=bc,
-                           out=x.view(rows, s * c_out), y2=xl.view(rows, s * c_out),
+                           out=x.view(rows, s * c_out),
+                           y2=None if fused else xl.view(rows, s * c_out),
                            alpha2=LRELU_SLOPE, lens=L(i), flags=NS)
             rows, seq = rows * s, seq * s
             xs = torch.empty(rows, c_out, dtype=torch.float32, device=dev)
             last_stage = i == self.num_upsamples - 1
             h_c = torch.empty(rows, c_out, dtype=cdt, device=dev)
+            if fused:
+                for j in range(nk):
+                    rb = self.resblocks[i * nk + j]
+                    w1, w2 = prep["rb"][i * nk + j]
+                    fin = j == nk - 1
+                    K.resblock1_fused(x, rows, seq, c_out, rb.kernel_size, rb.dilation, w1, w2,
+                                      [c.bias for c in rb.convs1], [c.bias for c in rb.convs2],
+                                      xs, acc=j > 0, scale=1.0 / nk if fin else 1.0,
+                                      store_xs=not fin, hc=h_c if fin else None,
+                                      alpha2=0.01 if last_stage else LRELU_SLOPE, lens=L(i + 1))
+                continue
             for j in range(nk):
                 rb = self.resblocks[i * nk + j]
                 w1, w2 = prep["rb"][i * nk + j]

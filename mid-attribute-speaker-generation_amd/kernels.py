@@ -131,6 +131,31 @@ def convT_weight_prep(w, bias, stride):
     return wc, bc
 
 
+def resblock1_supported(channels, seq_len, kernel_size, dilations):
+    d = (ctypes.c_int * 3)(*dilations)
+    return bool(lib.fs2_resblock1_supported(channels, seq_len, kernel_size, ctypes.addressof(d)))
+
+
+def resblock1_fused(x, rows, seq_len, channels, kernel_size, dilations, w1, w2, b1, b2, xs,
+                    acc, scale, store_xs=True, hc=None, alpha2=0.1, lens=None):
+    """One HiFi-GAN ResBlock1 in one launch (fs2_resblock1_fused): x (rows, C) fp32 ->
+    xs (= (xs + out) * scale when acc, else out * scale) and / or hc (bf16 leaky ReLU)."""
+    _dev(x, xs, hc, lens, *w1, *w2, *b1, *b2)
+    if x.dtype != torch.float32 or xs.dtype != torch.float32:
+        raise RuntimeError("resblock1_fused: x and xs are fp32")
+    if any(w.dtype != torch.bfloat16 for w in (*w1, *w2)):
+        raise RuntimeError("resblock1_fused: bf16 weights (fs2_conv_weight_prep)")
+    P = lambda ts: (ctypes.c_void_p * 3)(*[t.data_ptr() for t in ts])
+    d = (ctypes.c_int * 3)(*dilations)
+    pw1, pw2, pb1, pb2 = P(w1), P(w2), P(b1), P(b2)
+    rc = lib.fs2_resblock1_fused(ptr(x), rows, seq_len, channels, kernel_size,
+                                 ctypes.addressof(d), ctypes.addressof(pw1), ctypes.addressof(pw2),
+                                 ctypes.addressof(pb1), ctypes.addressof(pb2), ptr(xs), int(acc),
+                                 float(scale), int(store_xs), ptr(hc), float(alpha2), ptr(lens),
+                                 stream())
+    return rc
+
+
 def vocoder_post(x, rows, seq_len, c_in, w, bias, max_wav_value=32768.0, pcm=True, lens=None):
     _dev(x, w, bias, lens)
     wav = torch.empty(rows, dtype=torch.float32, device=x.device)

@@ -566,7 +566,10 @@ def test_batchnorm_dropout(c, act):
 
 @pytest.mark.parametrize("B,T,C,k,d", [(2, 192, 256, 3, 5), (2, 192, 256, 7, 3),
                                        (1, 300, 256, 11, 5), (2, 128, 64, 11, 5),
-                                       (3, 100, 32, 7, 5)])
+                                       (3, 100, 32, 7, 5),
+                                       # 64 x odd rows per utterance (the vocoder's 64-rows-
+                                       # per-frame stage): 64-row halo tiles, wide grid
+                                       (2, 64 * 513, 128, 11, 5), (3, 64 * 91, 128, 7, 3)])
 def test_conv_gemm_ex_dilated_epilogues(B, T, C, k, d):
     """fs2_conv_gemm_ex (vocoder convs): dilated taps on the halo and tap-major kernels (bf16)
     and the fp32 kernel, with the LRELU / ADD_AUX / ACC_Y / Y2 epilogue, against torch."""

@@ -69,45 +69,59 @@ struct ResBlockArgs {
 // k loop is straight-line code the compiler can schedule reads ahead in.
 constexpr int RB_FG = 4;  // row fragments per pass (independent accumulators)
 
+// the wave's weight slice for one conv: every k-step's A fragment, loaded once
+template <int C, int KT>
+FS2_DEV void rb_load_w(const u16* __restrict__ w, int wave, int lane, bf16x8r (&wr)[KT * (C / 32)]) {
+  constexpr int NB = C / 16, CH = C / 32;
+  const int n = wave % NB;
+  const u16* wl = w + (int64_t)(n * 16 + (lane & 15)) * (KT * C) + (lane >> 4) * 8;
+#pragma unroll
+  for (int st = 0; st < KT * CH; ++st)
+    wr[st] = *reinterpret_cast<const bf16x8r*>(wl + (st / CH) * C + (st % CH) * 32);
+}
+
 template <int C, int R, int KT, typename Epi>
-FS2_DEV void rb_conv(const u16* in, const u16* __restrict__ w, int dil, int pad, int E, int wave,
-                     int lane, Epi epi) {
+FS2_DEV void rb_conv(const u16* in, bf16x8r (&wr)[KT * (C / 32)], const u16* w_next, int dil,
+                     int pad, int E, int wave, int lane, Epi epi) {
   constexpr int NB = C / 16;            // output-channel slices
   constexpr int WPS = RB_WAVES / NB;    // waves per slice
   constexpr int CH = C / 32;            // 32-channel chunks per tap
   constexpr int STEPS = KT * CH;        // k-steps
+  constexpr int NFMAX = (R + 2 * RB_RAD + 15) / 16;
+  constexpr int FW = ((NFMAX + WPS - 1) / WPS + RB_FG - 1) / RB_FG * RB_FG;  // frags per wave
   const int NF = (R + 2 * E + 15) / 16;
   const int col = lane & 15, kq = lane >> 4;
-  const int n = wave % NB, part = wave / NB;
-  bf16x8r wr[STEPS];
-  const u16* wl = w + (int64_t)(n * 16 + col) * (KT * C) + kq * 8;
+  const int part = wave / NB;
+  f32x4 acc[FW];
 #pragma unroll
-  for (int st = 0; st < STEPS; ++st)
-    wr[st] = *reinterpret_cast<const bf16x8r*>(wl + (st / CH) * C + (st % CH) * 32);
-  for (int f0 = part; f0 < NF; f0 += RB_FG * WPS) {
-    // fragments f0 + g * WPS; one past NF reads a valid row range and is not stored
-    f32x4 acc[RB_FG];
-    int base[RB_FG];
-#pragma unroll
-    for (int g = 0; g < RB_FG; ++g) {
-      acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
-      const int f = f0 + g * WPS < NF ? f0 + g * WPS : f0;
-      base[g] = RB_RAD - E - pad + 16 * f + col;
-    }
-#pragma unroll
-    for (int st = 0; st < STEPS; ++st) {
-      const int j = st / CH, ch = (st % CH) * 32 + kq * 8;
+  for (int g0 = 0; g0 < FW; g0 += RB_FG) {
+    if (part + g0 * WPS < NF) {  // wave-uniform
+      int base[RB_FG];
 #pragma unroll
       for (int g = 0; g < RB_FG; ++g) {
-        const bf16x8r x = *reinterpret_cast<const bf16x8r*>(in + op_index(base[g] + j * dil, ch));
-        acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[st], x, acc[g], 0, 0, 0);
+        acc[g0 + g] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const int f = part + (g0 + g) * WPS;
+        base[g] = RB_RAD - E - pad + 16 * (f < NF ? f : part) + col;  // past NF: not stored
+      }
+#pragma unroll
+      for (int st = 0; st < STEPS; ++st) {
+        const int j = st / CH, ch = (st % CH) * 32 + kq * 8;
+#pragma unroll
+        for (int g = 0; g < RB_FG; ++g) {
+          const bf16x8r x = *reinterpret_cast<const bf16x8r*>(in + op_index(base[g] + j * dil, ch));
+          acc[g0 + g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[st], x, acc[g0 + g], 0, 0, 0);
+        }
       }
     }
-    // D: column = row (lane & 15), rows = output channels 4 * (lane >> 4) + i: each lane
-    // holds 4 consecutive channels of one row -> 16-B / 8-B LDS accesses in the epilogue
+  }
+  // the next conv's weights fly during this conv's epilogue and the barrier after it
+  if (w_next) rb_load_w<C, KT>(w_next, wave, lane, wr);
+  // D: column = row (lane & 15), rows = output channels 4 * (lane >> 4) + i: each lane
+  // holds 4 consecutive channels of one row -> 16-B / 8-B LDS accesses in the epilogue
 #pragma unroll
-    for (int g = 0; g < RB_FG; ++g)
-      if (f0 + g * WPS < NF) epi(-E + 16 * (f0 + g * WPS) + col, n * 16 + 4 * kq, acc[g]);
+  for (int g = 0; g < FW; ++g) {
+    const int f = part + g * WPS;
+    if (f < NF) epi(-E + 16 * f + col, (wave % NB) * 16 + 4 * kq, acc[g]);
   }
 }
 
@@ -131,6 +145,8 @@ __global__ __launch_bounds__(RB_WAVES * 64, 1) void resblock1_fused(ResBlockArgs
     if (m0 - u * a.T >= a.lens[u]) continue;
   }
   const int64_t u0 = (m0 / a.T) * a.T, u1 = u0 + a.T < a.rows ? u0 + a.T : a.rows;
+  bf16x8r wr[KT * (C / 32)];
+  rb_load_w<C, KT>(a.w1[0], wave, lane, wr);  // in flight under the tile load
   auto pack4 = [](float x0, float x1, float x2, float x3) {
     uint2 p;
     p.x = (uint32_t)to_bf16(x0) | ((uint32_t)to_bf16(x1) << 16);
@@ -156,7 +172,7 @@ __global__ __launch_bounds__(RB_WAVES * 64, 1) void resblock1_fused(ResBlockArgs
     const int p1 = (a.k - 1) / 2 * a.dil[m];
     used += p1;
     const float* b1 = a.b1[m];
-    rb_conv<C, R, KT>(curl, a.w1[m], a.dil[m], p1, rad - used, wave, lane,
+    rb_conv<C, R, KT>(curl, wr, a.w2[m], a.dil[m], p1, rad - used, wave, lane,
                   [&](int rel, int o, f32x4 v) {
                     const int64_t g = m0 + rel;
                     const bool in = g >= u0 && g < u1;
@@ -171,7 +187,7 @@ __global__ __launch_bounds__(RB_WAVES * 64, 1) void resblock1_fused(ResBlockArgs
     used += p2;
     const float* b2 = a.b2[m];
     const bool next = m < 2;
-    rb_conv<C, R, KT>(tb, a.w2[m], 1, p2, rad - used, wave, lane,
+    rb_conv<C, R, KT>(tb, wr, next ? a.w1[m + 1] : nullptr, 1, p2, rad - used, wave, lane,
                   [&](int rel, int o, f32x4 v) {
                     const int64_t g = m0 + rel;
                     const int b = rel + RB_RAD;

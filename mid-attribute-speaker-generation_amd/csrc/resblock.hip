@@ -129,7 +129,9 @@ template <int C, int R, int KT>
 __global__ __launch_bounds__(RB_WAVES * 64, 1) void resblock1_fused(ResBlockArgs a) {
   constexpr int WR = R + 2 * RB_RAD + 16;
   constexpr int LDC = C + 4;  // fp32 row stride: +16 B per row spreads a fragment's rows over the banks
-  extern __shared__ __attribute__((aligned(16))) unsigned char rb_smem[];
+  // static LDS: with the same size as dynamic LDS (hipFuncSetAttribute opt-in) an EMPTY launch
+  // of this kernel measured 0.5-2.3 ms; declared statically it dispatches in ~5 us
+  __shared__ __attribute__((aligned(16))) unsigned char rb_smem[WR * LDC * 4 + 2 * WR * RB_LD * 2];
   float* cur = reinterpret_cast<float*>(rb_smem);              // [WR][LDC]
   u16* curl = reinterpret_cast<u16*>(cur + WR * LDC);          // [WR][64] swizzled
   u16* tb = curl + WR * RB_LD;                                 // [WR][64] swizzled
@@ -154,15 +156,29 @@ __global__ __launch_bounds__(RB_WAVES * 64, 1) void resblock1_fused(ResBlockArgs
     return p;
   };
   // ---- load x rows [m0 - RB_RAD, m0 + R + RB_RAD + 16): CUR and CURL = lrelu(x, 0.1)
-  constexpr int V4 = C / 4;
-  for (int e = tid; e < WR * V4; e += RB_WAVES * 64) {
+  // every global load of the tile is issued before the first LDS store (a rolled loop would
+  // wait one HBM round trip per iteration)
+  constexpr int V4 = C / 4, NT = RB_WAVES * 64;
+  constexpr int LIT = (WR * V4 + NT - 1) / NT;
+  float4 xv[LIT];
+#pragma unroll
+  for (int it = 0; it < LIT; ++it) {
+    const int e = tid + it * NT;
     const int b = e / V4, c4 = (e - b * V4) * 4;
     const int64_t g = m0 - RB_RAD + b;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (g >= u0 && g < u1) v = *reinterpret_cast<const float4*>(a.x + g * C + c4);
-    *reinterpret_cast<float4*>(cur + b * LDC + c4) = v;
-    *reinterpret_cast<uint2*>(curl + op_index(b, c4)) =
-        pack4(lrelu(v.x, 0.1f), lrelu(v.y, 0.1f), lrelu(v.z, 0.1f), lrelu(v.w, 0.1f));
+    xv[it] = (e < WR * V4 && g >= u0 && g < u1) ? *reinterpret_cast<const float4*>(a.x + g * C + c4)
+                                               : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+#pragma unroll
+  for (int it = 0; it < LIT; ++it) {
+    const int e = tid + it * NT;
+    if (e < WR * V4) {
+      const int b = e / V4, c4 = (e - b * V4) * 4;
+      const float4 v = xv[it];
+      *reinterpret_cast<float4*>(cur + b * LDC + c4) = v;
+      *reinterpret_cast<uint2*>(curl + op_index(b, c4)) =
+          pack4(lrelu(v.x, 0.1f), lrelu(v.y, 0.1f), lrelu(v.z, 0.1f), lrelu(v.w, 0.1f));
+    }
   }
   __syncthreads();
   int rad = 0;
@@ -207,16 +223,26 @@ __global__ __launch_bounds__(RB_WAVES * 64, 1) void resblock1_fused(ResBlockArgs
     __syncthreads();
   }
   // ---- store rows [m0, m0 + R): the stage's running sum and / or its leaky-ReLU'd copy
-  for (int e = tid; e < R * V4; e += RB_WAVES * 64) {
-    const int r = e / V4, c4 = (e - r * V4) * 4;
+  // (the xs reads of the running sum are all issued first, as in the loader)
+  constexpr int SIT = R * V4 / NT;
+  static_assert(R * V4 % NT == 0, "store loop");
+  float4 ov[SIT];
+#pragma unroll
+  for (int it = 0; it < SIT; ++it) {
+    const int e = tid + it * NT, r = e / V4, c4 = (e - r * V4) * 4;
+    const int64_t g = m0 + r;
+    ov[it] = (a.acc && g < a.rows) ? *reinterpret_cast<const float4*>(a.xs + g * C + c4)
+                                   : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+#pragma unroll
+  for (int it = 0; it < SIT; ++it) {
+    const int e = tid + it * NT, r = e / V4, c4 = (e - r * V4) * 4;
     const int64_t g = m0 + r;
     if (g >= a.rows) continue;
     float4 v = *reinterpret_cast<const float4*>(cur + (r + RB_RAD) * LDC + c4);
-    if (a.acc) {
-      const float4 o = *reinterpret_cast<const float4*>(a.xs + g * C + c4);
-      v = make_float4(v.x + o.x, v.y + o.y, v.z + o.z, v.w + o.w);
-    }
-    v = make_float4(v.x * a.scale, v.y * a.scale, v.z * a.scale, v.w * a.scale);
+    const float4 o = ov[it];
+    v = make_float4((v.x + o.x) * a.scale, (v.y + o.y) * a.scale, (v.z + o.z) * a.scale,
+                    (v.w + o.w) * a.scale);
     if (a.store_xs) *reinterpret_cast<float4*>(a.xs + g * C + c4) = v;
     if (a.hc) {
       uint2 p;
@@ -231,17 +257,6 @@ __global__ __launch_bounds__(RB_WAVES * 64, 1) void resblock1_fused(ResBlockArgs
 
 template <int C, int R, int KT>
 int launch_rb(const ResBlockArgs& a, hipStream_t st) {
-  constexpr int WR = R + 2 * RB_RAD + 16;
-  const size_t smem = (size_t)WR * (C + 4) * 4 + 2 * (size_t)WR * RB_LD * 2;
-  static bool attr = false;
-  if (!attr) {  // > 64 KiB of dynamic LDS must be opted into once per kernel
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&resblock1_fused<C, R, KT>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem) != hipSuccess) {
-      set_error("fs2_resblock1_fused: cannot reserve %zu B of LDS", smem);
-      return FS2_ERR_LAUNCH;
-    }
-    attr = true;
-  }
   static int n_cu = 0;
   if (!n_cu) {
     int dev = 0;
@@ -252,7 +267,7 @@ int launch_rb(const ResBlockArgs& a, hipStream_t st) {
   }
   const int64_t ntiles = a.rows / R;
   const unsigned grid = (unsigned)(ntiles < n_cu ? ntiles : n_cu);
-  resblock1_fused<C, R, KT><<<grid, RB_WAVES * 64, smem, st>>>(a);
+  resblock1_fused<C, R, KT><<<grid, RB_WAVES * 64, 0, st>>>(a);
   return launch_status("fs2_resblock1_fused");
 }
 

@@ -23,6 +23,8 @@
 // Epilogue: accumulators go through LDS (fp32, 132-float rows, conflict-free writes) and
 // leave as 8-element row vectors: bias, residual/aux add, ReLU, ReLU-mask and the bf16 cast
 // are applied on 16-B (bf16) / 32-B (fp32) coalesced stores.
+#include <mutex>
+
 #include "common.hpp"
 
 namespace fs2 {
@@ -52,6 +54,8 @@ struct GldsArgs {
   float alpha, scale;   // FS2_EPI_LRELU slope, FS2_EPI_ACC_Y scale
   u16* y2;              // FS2_EPI_Y2 bf16 output (ld = N)
   float alpha2;
+  int kz;               // halo kernel: channel-block splits (0/1 = none; see halo_splitk_reduce)
+  float* slab;          // kz > 1: [kz][M][N] fp32 partial products
 };
 
 // Are rows [r0, r1) all padding (t >= lens[b] for r = b*T + t)?  Scalar, block-uniform.
@@ -453,9 +457,13 @@ void conv_gemm_halo(GldsArgs a) {
   const int wm = wave / WN, wn = wave % WN;
   const int g = lane >> 4, r16 = lane & 15;
 
-  const int nwg = a.tiles_m * a.tiles_n;
-  const int orig = blockIdx.x, xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  // kz > 1 (split-K over channel blocks): split z owns channel blocks [cb0, cb1) of every
+  // tile; the splits are the outer index of the XCD-contiguous order
+  const int kz = a.kz > 1 ? a.kz : 1;
+  const int nwg = a.tiles_m * a.tiles_n, nall = nwg * kz;
+  const int orig = blockIdx.x, xcd = orig & 7, q8 = nall >> 3, r8 = nall & 7;
+  const int wga = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int z = wga / nwg, wg = wga - z * nwg;
   const int gfull = a.tiles_m * a.group;
   const int ng = wg / gfull, rem = wg - ng * gfull;
   const int gsz = a.tiles_n - ng * a.group < a.group ? a.tiles_n - ng * a.group : a.group;
@@ -464,6 +472,7 @@ void conv_gemm_halo(GldsArgs a) {
   const int64_t m0 = (int64_t)tm * BM;
   const int n0 = tn * BN;
   const bool skip = a.lens && rows_all_padding(a.lens, a.T, m0, m0 + BM < a.M ? m0 + BM : a.M);
+  const int ncb_all = a.Cin / 64, cb0 = z * ncb_all / kz, cb1 = (z + 1) * ncb_all / kz;
 
   const int lrow = lane >> 3;
   const u16* zero = reinterpret_cast<const u16*>(g_zero_line);
@@ -476,14 +485,14 @@ void conv_gemm_halo(GldsArgs a) {
     const int h = (wave + NWAVE * q) * 8 + lrow;
     const int64_t gr = m0 - a.pad + h;
     const int lc = (lane & 7) ^ (h & 7);
-    h_src[q] = (gr >= u0 && gr < u1) ? a.x + gr * a.ldx + lc * 8 : nullptr;
+    h_src[q] = (gr >= u0 && gr < u1) ? a.x + gr * a.ldx + lc * 8 + cb0 * BK : nullptr;
   }
   const u16* b_src[BW];
 #pragma unroll
   for (int i = 0; i < BW; ++i) {
     const int R = (wave * BW + i) * 8 + lrow;
     const int n = n0 + R;
-    b_src[i] = n < a.N ? a.w + (int64_t)n * a.K + ((lane & 7) ^ (R & 7)) * 8 : nullptr;
+    b_src[i] = n < a.N ? a.w + (int64_t)n * a.K + ((lane & 7) ^ (R & 7)) * 8 + cb0 * BK : nullptr;
   }
 
   f32x4 acc[MI][NI];
@@ -534,7 +543,7 @@ void conv_gemm_halo(GldsArgs a) {
           acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[ks][i], fb[ks][jj], acc[i][jj], 0, 0, 0);
   };
   if (!skip) {
-    const int ncb = a.Cin / BK;
+    const int ncb = cb1 - cb0;
     if constexpr (BST == 1) {
       for (int cb = 0; cb < ncb; ++cb) {
         for (int j = 0; j < a.taps; ++j) {
@@ -584,7 +593,86 @@ void conv_gemm_halo(GldsArgs a) {
       __builtin_amdgcn_s_barrier();
     }
   }
+  if (kz > 1) {  // raw fp32 partial product into slab z (halo_splitk_reduce applies the epilogue)
+    GldsArgs e = a;
+    e.flags = 0;
+    e.y = a.slab + (int64_t)z * a.M * a.N;
+    e.ldy = a.N;
+    e.vec = 1;
+    nt_epilogue<BM, BN, VOC, NWAVE, WN>(e, acc, smem, m0, n0, skip, tid, wm, wn, g, r16);
+    return;
+  }
   nt_epilogue<BM, BN, VOC, NWAVE, WN>(a, acc, smem, m0, n0, skip, tid, wm, wn, g, r16);
+}
+
+// Split-K epilogue of the halo kernel: y = epilogue(sum_z slab[z]) in split order, 8 columns
+// per thread, with nt_epilogue's non-vocoder semantics (bias, aux add, ReLU / ReLU mask, bf16
+// cast; tiles of BM rows that are all padding get no bias, as in the unsplit kernel).
+template <int BM>
+__global__ __launch_bounds__(256) void halo_splitk_reduce(GldsArgs a) {
+  const int64_t n8 = a.N / 8, total = a.M * n8;
+  const bool out_bf16 = a.flags & FS2_EPI_OUT_BF16, aux_bf16 = a.flags & FS2_EPI_AUX_BF16;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * 256) {
+    const int64_t m = e / n8;
+    const int n = (int)(e - m * n8) * 8;
+    const float* sp = a.slab + m * a.N + n;
+    f32x4 lo = ld4(sp), hi = ld4(sp + 4);
+    for (int z = 1; z < a.kz; ++z) {
+      const float* q = sp + (int64_t)z * a.M * a.N;
+      lo += ld4(q);
+      hi += ld4(q + 4);
+    }
+    float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    const int64_t t0 = m / BM * BM;
+    const bool skip = a.lens && rows_all_padding(a.lens, a.T, t0, t0 + BM < a.M ? t0 + BM : a.M);
+    if ((a.flags & FS2_EPI_BIAS) && !skip) {
+      const f32x4 b0 = ld4(a.bias + n), b1 = ld4(a.bias + n + 4);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        v[i] += b0[i];
+        v[i + 4] += b1[i];
+      }
+    }
+    float av[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (a.flags & (FS2_EPI_ADD_AUX | FS2_EPI_RELU_MASK_AUX)) {
+      if (aux_bf16) {
+        const uint4 raw = *reinterpret_cast<const uint4*>((const u16*)a.aux + m * a.ld_aux + n);
+        const uint32_t wv[4] = {raw.x, raw.y, raw.z, raw.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          av[2 * i] = __uint_as_float(wv[i] << 16);
+          av[2 * i + 1] = __uint_as_float(wv[i] & 0xffff0000u);
+        }
+      } else {
+        const float* ap = (const float*)a.aux + m * a.ld_aux + n;
+        const f32x4 a0 = ld4(ap), a1 = ld4(ap + 4);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          av[i] = a0[i];
+          av[i + 4] = a1[i];
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if (a.flags & FS2_EPI_ADD_AUX) v[i] += av[i];
+      if (a.flags & FS2_EPI_RELU) v[i] = fmaxf(v[i], 0.f);
+      if (a.flags & FS2_EPI_RELU_MASK_AUX) v[i] = av[i] > 0.f ? v[i] : 0.f;
+    }
+    if (out_bf16) {
+      uint4 o;
+      o.x = (uint32_t)fbv(v[0]) | ((uint32_t)fbv(v[1]) << 16);
+      o.y = (uint32_t)fbv(v[2]) | ((uint32_t)fbv(v[3]) << 16);
+      o.z = (uint32_t)fbv(v[4]) | ((uint32_t)fbv(v[5]) << 16);
+      o.w = (uint32_t)fbv(v[6]) | ((uint32_t)fbv(v[7]) << 16);
+      *reinterpret_cast<uint4*>((u16*)a.y + m * a.ldy + n) = o;
+    } else {
+      float* yp = (float*)a.y + m * a.ldy + n;
+      st4(yp, f32x4{v[0], v[1], v[2], v[3]});
+      st4(yp + 4, f32x4{v[4], v[5], v[6], v[7]});
+    }
+  }
 }
 
 // ------------------------------------------------------------------------ weight gradient
@@ -1031,8 +1119,19 @@ __global__ __launch_bounds__(256) void wgrad_reduce_taps(const float* __restrict
       const int jj = e >> 6, c = e & 63;
       if (c < nc) {
         const int64_t off = (int64_t)o * Kp + (int64_t)(jb + jj) * Cin + c0 + c;
+        // split slabs loaded four at a time (independent loads in flight), summed in split
+        // order so the result does not depend on the unrolling
         float s = slab[off];
-        for (int zz = 1; zz < splits; ++zz) s += slab[zz * total + off];
+        int zz = 1;
+        for (; zz + 3 < splits; zz += 4) {
+          const float v0 = slab[zz * total + off], v1 = slab[(zz + 1) * total + off];
+          const float v2 = slab[(zz + 2) * total + off], v3 = slab[(zz + 3) * total + off];
+          s += v0;
+          s += v1;
+          s += v2;
+          s += v3;
+        }
+        for (; zz < splits; ++zz) s += slab[zz * total + off];
         tile[c * 33 + jj] = s;
       }
     }
@@ -1124,6 +1223,52 @@ static void launch_nt(GldsArgs a, bool tapaligned, bool voc, hipStream_t st) {
   } else {
     conv_gemm_nt_glds<BM, BN, S, false, false><<<grid, 256, 0, st>>>(a);
   }
+}
+
+// Split-K choice + workspace for the 64x64 halo kernel.  A grid below ~3 blocks per CU with a
+// long channel loop (the encoder's k=9 data gradient: 384 tiles, 16 channel blocks x 9 taps
+// each) leaves CUs with one block and the rest with two; splitting the channel blocks kz ways
+// fills the chip and halves each block's serial loop, at the cost of kz fp32 partial products
+// summed by halo_splitk_reduce.  The partials live in one process-wide buffer, grown outside
+// graph capture only (a too-small buffer during capture falls back to the unsplit launch), so
+// an eager step and its captured replay take the same decomposition (bitwise-equal results).
+// A launch from a different stream than the previous user first drains that stream; the
+// launches of one captured graph all come from its capture stream.
+static int halo_splitk(GldsArgs& a, unsigned grid, bool voc, bool hx64, hipStream_t st) {
+  const int knob = g_tune[FS2_TUNE_HALO_SPLITK];
+  const int ncb = a.Cin / 64;
+  const int keep = FS2_EPI_BIAS | FS2_EPI_RELU | FS2_EPI_ADD_AUX | FS2_EPI_RELU_MASK_AUX |
+                   FS2_EPI_OUT_BF16 | FS2_EPI_AUX_BF16;
+  if (knob == -1 || voc || hx64 || !a.vec || (a.flags & ~keep) || a.N % 8) return 1;
+  int kz = knob > 0 ? knob : (grid < 512 && ncb >= 8 ? (int)((768 + grid - 1) / grid) : 1);
+  if (kz > ncb / 4) kz = ncb / 4;
+  if (kz < 2) return 1;
+  static std::mutex mu;
+  static float* buf = nullptr;
+  static size_t cap = 0;
+  static hipStream_t last = nullptr;
+  const size_t need = (size_t)kz * (size_t)a.M * (size_t)a.N * sizeof(float);
+  std::lock_guard<std::mutex> lock(mu);
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess) return 1;
+  const bool capturing = cs != hipStreamCaptureStatusNone;
+  if (!capturing && last && last != st && hipStreamSynchronize(last) != hipSuccess) return 1;
+  if (cap < need) {
+    if (capturing) return 1;
+    if (buf) {
+      if (hipDeviceSynchronize() != hipSuccess) return 1;
+      (void)hipFree(buf);
+      buf = nullptr;
+      cap = 0;
+    }
+    void* p = nullptr;
+    if (hipMalloc(&p, need) != hipSuccess) return 1;
+    buf = static_cast<float*>(p);
+    cap = need;
+  }
+  if (!capturing) last = st;
+  a.slab = buf;
+  return kz;
 }
 
 int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, int64_t ldy,
@@ -1229,7 +1374,31 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
       if (halo_wide && halo_bm == 128) { FS2_HALO(128, 128, 2) }
       else if (halo_wide) { FS2_HALO(64, 128, 2) }
       else if (halo_bm == 128) { FS2_HALO(128, 64, 2) }
-      else { FS2_HALO(64, 64, 2) }
+      else {
+        // under-filled 64x64 grid: with 128-row utterance multiples, 128x64 tiles split kz ways
+        // (half the weight-tile re-staging per output row of 64x64 tiles); else 64x64 split
+        GldsArgs a2 = a;
+        a2.tiles_m = (int)((rows + 127) / 128);
+        const unsigned grid2 = (unsigned)(a2.tiles_m * a2.tiles_n);
+        const int kz2 = seq_len % 128 == 0 && g_tune[FS2_TUNE_HALO_SPLITK] != -2
+                            ? halo_splitk(a2, grid2, voc, hx64, st) : 1;
+        const int kz = kz2 > 1 ? 1 : halo_splitk(a, grid, voc, hx64, st);
+        if (kz2 > 1) {
+          a2.kz = kz2;
+          conv_gemm_halo<128, 64, 2, 16, false><<<grid2 * kz2, 256, 0, st>>>(a2);
+          const int64_t n8 = rows * (c_out / 8);
+          halo_splitk_reduce<128><<<(unsigned)((n8 + 255) / 256 < 2048 ? (n8 + 255) / 256 : 2048),
+                                    256, 0, st>>>(a2);
+        } else if (kz > 1) {
+          a.kz = kz;
+          conv_gemm_halo<64, 64, 2, 16, false><<<grid * kz, 256, 0, st>>>(a);
+          const int64_t n8 = rows * (c_out / 8);
+          halo_splitk_reduce<64><<<(unsigned)((n8 + 255) / 256 < 2048 ? (n8 + 255) / 256 : 2048),
+                                   256, 0, st>>>(a);
+        } else {
+          FS2_HALO(64, 64, 2)
+        }
+      }
     }
 #undef FS2_HALO
   } else if (big >= 512) {

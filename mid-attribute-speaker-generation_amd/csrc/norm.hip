@@ -147,12 +147,38 @@ __global__ __launch_bounds__(256) void ln_bwd_f32(LnBwd a) {
   float pdb = 0.f;
   const uint64_t seed = a.seed ? *a.seed : 0ull;
   const int64_t rbeg = (int64_t)blockIdx.x * LN_ROWS;
-#pragma unroll 1
-  for (int i = wave; i < LN_ROWS / 2; i += 4) {
-    const int64_t r = rbeg + 2 * i + half;
+  // Every row pair of the wave is loaded before the first is reduced: the grid is only a
+  // few blocks per CU, so the loads of all LN_ROWS / 8 iterations must be in flight together
+  // (one pair at a time left the kernel latency-bound at ~1 TB/s).
+  constexpr int IT = LN_ROWS / 8;
+  f32x4 XH[IT][2], DU[IT][2];
+  float RS[IT], RD[IT];
+  bool LIVE[IT];
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int64_t r = rbeg + 2 * (wave + 4 * it) + half;
+    LIVE[it] = r < a.rows && !row_padded(a.lens, a.T, r);
+    XH[it][0] = XH[it][1] = DU[it][0] = DU[it][1] = zz;
+    RS[it] = RD[it] = 0.f;
+    if (LIVE[it]) {
+      const int64_t e0 = r * LN_D + c8;
+      RD[it] = a.rstd[r];
+      XH[it][0] = ld4(a.xhat + e0);
+      XH[it][1] = ld4(a.xhat + e0 + 4);
+      if constexpr (DDOT) {
+        RS[it] = a.ddot[r];  // the dot gradient rides in RS until the row is reduced
+      } else {
+        DU[it][0] = ld4(a.dout + e0);
+        DU[it][1] = ld4(a.dout + e0 + 4);
+      }
+    }
+  }
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int64_t r = rbeg + 2 * (wave + 4 * it) + half;
     if (r >= a.rows) break;
     const int64_t e0 = r * LN_D + c8;
-    if (row_padded(a.lens, a.T, r)) {  // masked row: zero upstream gradient, nothing to add
+    if (!LIVE[it]) {  // masked row: zero upstream gradient, nothing to add
       if (a.dres && !a.dres_add) {
         st4(a.dres + e0, zz);
         st4(a.dres + e0 + 4, zz);
@@ -164,20 +190,20 @@ __global__ __launch_bounds__(256) void ln_bwd_f32(LnBwd a) {
       if (a.dy_t) st8_bf16(a.dy_t + e0, zz, zz);
       continue;
     }
-    const f32x4 xh0 = ld4(a.xhat + e0), xh1 = ld4(a.xhat + e0 + 4);
+    const f32x4 xh0 = XH[it][0], xh1 = XH[it][1];
     f32x4 mo0 = {1.f, 1.f, 1.f, 1.f}, mo1 = mo0;
     if (a.p_out > 0.f) dropout8(seed, a.site_out, (uint64_t)e0, a.p_out, mo0, mo1);
     f32x4 du0, du1;
     if constexpr (DDOT) {
-      const float gr = a.ddot[r];
+      const float gr = RS[it];
       du0 = gr * w0;
       du1 = gr * w1;
       pw0 += gr * ((xh0 * gam0 + bet0) * mo0);
       pw1 += gr * ((xh1 * gam1 + bet1) * mo1);
       pdb += gr;
     } else {
-      du0 = ld4(a.dout + e0);
-      du1 = ld4(a.dout + e0 + 4);
+      du0 = DU[it][0];
+      du1 = DU[it][1];
     }
     du0 *= mo0;
     du1 *= mo1;
@@ -191,7 +217,7 @@ __global__ __launch_bounds__(256) void ln_bwd_f32(LnBwd a) {
     const float m2 = half_sum((dxh0.x * xh0.x + dxh0.y * xh0.y + dxh0.z * xh0.z + dxh0.w * xh0.w) +
                               (dxh1.x * xh1.x + dxh1.y * xh1.y + dxh1.z * xh1.z + dxh1.w * xh1.w)) *
                      (1.f / LN_D);
-    const float rs = a.rstd[r];
+    const float rs = RD[it];
     const f32x4 dz0 = rs * (dxh0 - m1 - xh0 * m2), dz1 = rs * (dxh1 - m1 - xh1 * m2);
     if (a.dres) {
       st4(a.dres + e0, a.dres_add ? ld4(a.dres + e0) + dz0 : dz0);

@@ -538,6 +538,51 @@ def test_conv_gemm_bf16_halo(B, T, cin, cout, k):
         K.lib.fs2_set_tuning(6, 0)
 
 
+@pytest.mark.parametrize("B,T,cin,cout,k,flags", [
+    (48, 128, 1024, 256, 9, "add_aux"), (48, 128, 1024, 256, 9, "bias_relu_bf16"),
+    (8, 64, 512, 256, 5, "relu_mask_bf16")])
+def test_conv_gemm_bf16_halo_splitk(B, T, cin, cout, k, flags):
+    """Split-K 64x64 halo launch (channel blocks split over the grid, fp32 partials summed by
+    halo_splitk_reduce) against the unsplit launch (FS2_TUNE_HALO_SPLITK = -1) on the encoder
+    data-gradient shape, with lens: the epilogue (bias only on computed tiles, aux add, ReLU /
+    ReLU mask, bf16 cast) must match on the valid rows; sums differ only by the split's
+    rounding.  Padded rows are compared only when the tiling is the same: a 128-row tile that
+    holds a valid frame computes padded rows a skipped 64-row tile leaves at the epilogue of 0."""
+    pad = (k - 1) // 2
+    x = bf(rnd(B * T, cin, seed=51))
+    w = bf(rnd(cout, cin, k, scale=1 / math.sqrt(cin * k), seed=52)).float()
+    b = rnd(cout, seed=53)
+    wf = torch.empty(cout * cin * k, device=DEV, dtype=torch.bfloat16)
+    wb = torch.empty(cout * cin * k, device=DEV, dtype=torch.bfloat16)
+    K.weight_prep(w, cout, cin, k, wf, wb)
+    lens = torch.tensor([T - (5 * u) % T for u in range(B)], device=DEV)
+    lens[-1] = 1
+    aux = rnd(B * T, cout, seed=54)
+
+    def run():
+        if flags == "add_aux":
+            return K.conv_gemm(x, wf, B * T, T, cin, cout, k, pad, flags=K.EPI_ADD_AUX, aux=aux,
+                               lens=lens)
+        if flags == "bias_relu_bf16":
+            return K.conv_gemm(x, wf, B * T, T, cin, cout, k, pad, bias=b, flags=K.EPI_RELU,
+                               out_dtype=torch.bfloat16, lens=lens)
+        return K.conv_gemm(x, wf, B * T, T, cin, cout, k, pad, flags=K.EPI_RELU_MASK_AUX,
+                           aux=bf(aux), out_dtype=torch.bfloat16, lens=lens)
+    valid = (torch.arange(T, device=DEV)[None] < lens[:, None]).reshape(-1)
+    try:
+        K.lib.fs2_set_tuning(8, -1)
+        want = run().float()
+        for kz in (0, 2, 4, -2):  # -2: 64x64 tiles only
+            K.lib.fs2_set_tuning(8, kz)
+            got = run().float()
+            tol = 1e-5 if flags == "add_aux" else 8e-3
+            close(got[valid], want[valid], tol)
+            if kz == -2:  # same 64-row tiling as the unsplit launch: padded rows too
+                close(got, want, tol)
+    finally:
+        K.lib.fs2_set_tuning(8, 0)
+
+
 @pytest.mark.parametrize("c,act", [(512, True), (80, False)])
 def test_batchnorm_dropout(c, act):
     """PostNet BatchNorm with dropout (p = 0.5): keep-rate of the 16-bit Philox draws, and the

@@ -1371,8 +1371,18 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
       // (a third ring slot measured faster alone for the k=9 data gradients, 71 -> 65 us, but
       // 1.7-2x slower inside the step, where the weight-gradient stream shares the CUs and
       // the lower occupancy (2 blocks/CU) cannot absorb it: knob 4 keeps it for experiments)
-      if (halo_wide && halo_bm == 128) { FS2_HALO(128, 128, 2) }
-      else if (halo_wide) { FS2_HALO(64, 128, 2) }
+      if (halo_wide && halo_bm == 128) {
+        const int kz = g_tune[FS2_TUNE_HALO_SPLITK] > 0 ? halo_splitk(a, grid, voc, hx64, st) : 1;
+        if (kz > 1) {  // forced split of 128x128 tiles (experiments)
+          a.kz = kz;
+          conv_gemm_halo<128, 128, 2, 16, false><<<grid * kz, 256, 0, st>>>(a);
+          const int64_t n8 = rows * (c_out / 8);
+          halo_splitk_reduce<128><<<(unsigned)((n8 + 255) / 256 < 2048 ? (n8 + 255) / 256 : 2048),
+                                    256, 0, st>>>(a);
+        } else {
+          FS2_HALO(128, 128, 2)
+        }
+      } else if (halo_wide) { FS2_HALO(64, 128, 2) }
       else if (halo_bm == 128) {
         // a forced split count (FS2_TUNE_HALO_SPLITK > 0) also applies to full 128x64 grids
         const int kz = g_tune[FS2_TUNE_HALO_SPLITK] > 0 ? halo_splitk(a, grid, voc, hx64, st) : 1;

@@ -1,5 +1,7 @@
 """Decoder FFN k=9 data gradient (Conv1d 1024 -> 256 over 48 x 512 frames, ADD_AUX, mel lens)
-under the halo variants (FS2_TUNE_NT_HALO) and forced channel-block splits."""
+under the halo variants (FS2_TUNE_NT_HALO) and forced channel-block splits.
+``--fwd``: the forward instead (Conv1d 256 -> 1024, bias + ReLU, bf16 out), the bench's
+roofline launch."""
 import importlib
 import math
 import os
@@ -13,7 +15,8 @@ PKG = importlib.import_module("mid-attribute-speaker-generation_amd")
 dev = "cuda:0"
 _b = PKG.data.syn_batch(48, 128, seed=0)
 lens = torch.tensor(_b[7], device=dev)
-B, T, cin, cout, k = 48, 512, 1024, 256, 9
+FWD = "--fwd" in sys.argv
+B, T, cin, cout, k = (48, 512, 256, 1024, 9) if FWD else (48, 512, 1024, 256, 9)
 M = B * T
 x = torch.randn(M, cin, device=dev).to(torch.bfloat16)
 w = torch.randn(cout, cin, k, device=dev) / math.sqrt(cin * k)
@@ -21,15 +24,25 @@ wf = torch.empty(cout * cin * k, device=dev, dtype=torch.bfloat16)
 wb = torch.empty_like(wf)
 K.weight_prep(w, cout, cin, k, wf, wb)
 aux = torch.randn(M, cout, device=dev)
-out = torch.empty(M, cout, device=dev)
-run = lambda: K.conv_gemm(x, wf, M, T, cin, cout, k, 4, flags=K.EPI_ADD_AUX, aux=aux, out=out,
-                          lens=lens)
+out = torch.empty(M, cout, device=dev, dtype=torch.bfloat16 if FWD else torch.float32)
+bias = torch.randn(cout, device=dev)
+if FWD:
+    run = lambda: K.conv_gemm(x, wf, M, T, cin, cout, k, 4, bias=bias, flags=K.EPI_RELU, out=out,
+                              lens=lens)
+else:
+    run = lambda: K.conv_gemm(x, wf, M, T, cin, cout, k, 4, flags=K.EPI_ADD_AUX, aux=aux, out=out,
+                              lens=lens)
 valid = int(lens.sum())
+for _ in range(400):  # clocks settle (the first ~0.3 s of launches run slow)
+    run()
+torch.cuda.synchronize()
 ref = None
-for nt, sk, name in ((0, 0, "auto"), (4, 0, "3-slot"), (5, 0, "8w 256x128 3s"),
-                     (6, 0, "8w 128x128 3s"), (7, 0, "8w 256x128 2s"), (2, 0, "128x128"),
-                     (0, 2, "128x64 kz2"), (0, 3, "128x64 kz3"), (0, 4, "128x64 kz4"),
-                     (0, 0, "auto")):
+CONFIGS = ((0, 0, "auto"), (1, 0, "4-wave"), (4, 0, "3-slot"), (5, 0, "8w 256x128 3s"),
+           (6, 0, "8w 128x128 3s"), (7, 0, "8w 256x128 2s"), (2, 0, "128x128"))
+if not FWD:
+    CONFIGS += ((0, 2, "128x64 kz2"), (0, 4, "128x64 kz4"), (2, 2, "128x128 kz2"),
+                (2, 3, "128x128 kz3"), (2, 4, "128x128 kz4"))
+for nt, sk, name in CONFIGS + CONFIGS:
     K.lib.fs2_set_tuning(6, nt)
     K.lib.fs2_set_tuning(8, sk)
     for _ in range(3):
@@ -44,7 +57,7 @@ for nt, sk, name in ((0, 0, "auto"), (4, 0, "3-slot"), (5, 0, "8w 256x128 3s"),
     keep = (torch.arange(T, device=dev)[None] < lens[:, None]).reshape(-1)
     if ref is None:
         ref = out[keep].clone()
-    err = (out[keep] - ref).abs().max().item()
+    err = (out[keep].float() - ref.float()).abs().max().item()
     print(f"{name:16s} {us:7.1f} us  {2 * valid * cin * cout * k / us / 1e6:6.0f} TFLOP/s (valid)"
           f"  max|diff| {err:.2e}", flush=True)
 K.lib.fs2_set_tuning(6, 0)

@@ -1096,12 +1096,22 @@ __global__ __launch_bounds__(256) void wgrad_reduce_k1(const float* __restrict__
   __syncthreads();
   if (ty == 0 && i4 < total)
     st4(dw + i4, ld4(dw + i4) + (((red[0][tx] + red[1][tx]) + red[2][tx]) + red[3][tx]));
-  if (db && blockIdx.x == 0) {
-    for (int o = threadIdx.x; o < Cout; o += 256) {
-      float b = 0.f;
-      for (int zz = 0; zz < splits; ++zz) b += bslab[(int64_t)zz * Cout + o];
-      db[o] += b;
+  // bias: one output per thread over the first blocks (block 0 looping over every output
+  // made the launch's tail), split loads four at a time, summed in split order
+  const int ob = blockIdx.x * 256 + threadIdx.x;
+  if (db && ob < Cout) {
+    float b = 0.f;
+    int zz = 0;
+    for (; zz + 3 < splits; zz += 4) {
+      const float v0 = bslab[(int64_t)zz * Cout + ob], v1 = bslab[(int64_t)(zz + 1) * Cout + ob];
+      const float v2 = bslab[(int64_t)(zz + 2) * Cout + ob], v3 = bslab[(int64_t)(zz + 3) * Cout + ob];
+      b += v0;
+      b += v1;
+      b += v2;
+      b += v3;
     }
+    for (; zz < splits; ++zz) b += bslab[(int64_t)zz * Cout + ob];
+    db[ob] += b;
   }
 }
 

@@ -334,32 +334,35 @@ __global__ __launch_bounds__(1024) void colsum_final(const float* part, int64_t 
 }
 
 // Several independent finals in one launch (blockIdx.y = job), each as colsum_final.
+// 16 columns x 64 row groups per block: each thread sums every 64th partial row of its column
+// (a dozen loads for the LN backward's 768 partial rows, four in flight), then a fixed-order
+// LDS tree over the 64 groups.  Deterministic; the blocks of all jobs run in one launch.
 __global__ __launch_bounds__(1024) void colsum_final_multi(ColsumJobs jobs) {
-  __shared__ float red[16][65];
+  __shared__ float red[64][17];
   const ColsumJob& jb = jobs.job[blockIdx.y];
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  const int64_t c = (int64_t)blockIdx.x * 64 + tx;
-  if ((int64_t)blockIdx.x * 64 >= jb.cols) return;  // block-uniform
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const int64_t c = (int64_t)blockIdx.x * 16 + tx;
+  if ((int64_t)blockIdx.x * 16 >= jb.cols) return;  // block-uniform
   float s = 0.f;
   if (c < jb.cols) {
 #pragma unroll 4
-    for (int64_t p = ty; p < jb.nparts; p += 16) s += jb.part[p * jb.cols + c];
+    for (int64_t p = ty; p < jb.nparts; p += 64) s += jb.part[p * jb.cols + c];
   }
   red[ty][tx] = s;
   __syncthreads();
-  if (ty == 0 && c < jb.cols) {
-    float t = 0.f;
 #pragma unroll
-    for (int y = 0; y < 16; ++y) t += red[y][tx];
-    jb.out[c] = jobs.acc ? jb.out[c] + t : t;
+  for (int h = 32; h > 0; h >>= 1) {
+    if (ty < h) red[ty][tx] += red[ty + h][tx];
+    __syncthreads();
   }
+  if (ty == 0 && c < jb.cols) jb.out[c] = jobs.acc ? jb.out[c] + red[0][tx] : red[0][tx];
 }
 
 int colsum_final_multi_launch(const ColsumJobs& jobs, hipStream_t st) {
   if (jobs.n == 0) return FS2_OK;
   int64_t maxc = 0;
   for (int i = 0; i < jobs.n; ++i) maxc = jobs.job[i].cols > maxc ? jobs.job[i].cols : maxc;
-  dim3 grid((unsigned)((maxc + 63) / 64), (unsigned)jobs.n);
+  dim3 grid((unsigned)((maxc + 15) / 16), (unsigned)jobs.n);
   colsum_final_multi<<<grid, 1024, 0, st>>>(jobs);
   return launch_status("colsum_final_multi");
 }

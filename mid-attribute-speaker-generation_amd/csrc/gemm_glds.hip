@@ -1125,24 +1125,27 @@ __global__ __launch_bounds__(256) void wgrad_reduce_taps(const float* __restrict
   const int nc = Cin - c0 < 64 ? Cin - c0 : 64;
   for (int jb = 0; jb < taps; jb += 32) {
     const int nj = taps - jb < 32 ? taps - jb : 32;
-    for (int e = threadIdx.x; e < 64 * nj; e += 256) {
-      const int jj = e >> 6, c = e & 63;
+    // 16-B loads: thread e owns 4 consecutive channels of one tap row (nc and every offset
+    // are multiples of 4); split slabs four at a time, summed in split order
+    for (int e = threadIdx.x; e < 16 * nj; e += 256) {
+      const int jj = e >> 4, c = (e & 15) * 4;
       if (c < nc) {
         const int64_t off = (int64_t)o * Kp + (int64_t)(jb + jj) * Cin + c0 + c;
-        // split slabs loaded four at a time (independent loads in flight), summed in split
-        // order so the result does not depend on the unrolling
-        float s = slab[off];
+        f32x4 s = ld4(slab + off);
         int zz = 1;
         for (; zz + 3 < splits; zz += 4) {
-          const float v0 = slab[zz * total + off], v1 = slab[(zz + 1) * total + off];
-          const float v2 = slab[(zz + 2) * total + off], v3 = slab[(zz + 3) * total + off];
+          const f32x4 v0 = ld4(slab + zz * total + off), v1 = ld4(slab + (zz + 1) * total + off);
+          const f32x4 v2 = ld4(slab + (zz + 2) * total + off), v3 = ld4(slab + (zz + 3) * total + off);
           s += v0;
           s += v1;
           s += v2;
           s += v3;
         }
-        for (; zz < splits; ++zz) s += slab[zz * total + off];
-        tile[c * 33 + jj] = s;
+        for (; zz < splits; ++zz) s += ld4(slab + zz * total + off);
+        tile[(c + 0) * 33 + jj] = s.x;
+        tile[(c + 1) * 33 + jj] = s.y;
+        tile[(c + 2) * 33 + jj] = s.z;
+        tile[(c + 3) * 33 + jj] = s.w;
       }
     }
     __syncthreads();

@@ -404,7 +404,9 @@ FS2_DEV void bn_g8(const float* dout, const float* z, const float* mean, const f
 
 // column partials of g and g*xhat: block (x, y) covers channels [512x, 512x+512) (8 per
 // lane) of rows [BN_ROWS*y, BN_ROWS*(y+1)), four row lanes summed in lane order
-__global__ __launch_bounds__(256) void bn_bwd_partial(const float* dout, const float* z,
+// 8 waves per block (one row group each): the PostNet shape gives only 1.5 blocks per CU,
+// so the row groups are what keeps enough loads in flight
+__global__ __launch_bounds__(512) void bn_bwd_partial(const float* dout, const float* z,
                                                       const float* mean, const float* rstd,
                                                       const float* gamma, const float* beta,
                                                       int64_t rows, int64_t c, int act_tanh,
@@ -414,11 +416,11 @@ __global__ __launch_bounds__(256) void bn_bwd_partial(const float* dout, const f
   const int tx = threadIdx.x & 63, ry = threadIdx.x >> 6;
   const int64_t col = ((int64_t)blockIdx.x * 64 + tx) * 8;
   const int64_t r0 = (int64_t)blockIdx.y * BN_ROWS;
-  __shared__ f32x4 red[2][4][128];
+  __shared__ f32x4 red[2][8][128];
   f32x4 sg[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}}, sgx[2] = {sg[0], sg[0]};
   if (col < c) {
     const int64_t r1 = r0 + BN_ROWS < rows ? r0 + BN_ROWS : rows;
-    for (int64_t r = r0 + ry; r < r1; r += 4) {
+    for (int64_t r = r0 + ry; r < r1; r += 8) {
       f32x4 g[2], xh[2];
       bn_g8(dout, z, mean, rstd, gamma, beta, (int)col, act_tanh, p, seed, site, r * c + col, g, xh);
 #pragma unroll
@@ -439,9 +441,11 @@ __global__ __launch_bounds__(256) void bn_bwd_partial(const float* dout, const f
     for (int h = 0; h < 2; ++h) {
       const int q = 2 * tx + h;
       st4(part_g + (int64_t)blockIdx.y * c + col + 4 * h,
-          ((red[0][0][q] + red[0][1][q]) + red[0][2][q]) + red[0][3][q]);
+          ((((((red[0][0][q] + red[0][1][q]) + red[0][2][q]) + red[0][3][q]) + red[0][4][q]) +
+            red[0][5][q]) + red[0][6][q]) + red[0][7][q]);
       st4(part_gx + (int64_t)blockIdx.y * c + col + 4 * h,
-          ((red[1][0][q] + red[1][1][q]) + red[1][2][q]) + red[1][3][q]);
+          ((((((red[1][0][q] + red[1][1][q]) + red[1][2][q]) + red[1][3][q]) + red[1][4][q]) +
+            red[1][5][q]) + red[1][6][q]) + red[1][7][q]);
     }
   }
 }
@@ -641,7 +645,7 @@ int fs2_bn_bwd(int dtype, const float* dout, const float* z, const float* mean, 
   unsigned short* zt = dtype == FS2_BF16 ? (unsigned short*)dz_t : nullptr;
   FS2_CHECK_ARG(dz || zt, "fs2_bn_bwd: no output requested");
   dim3 grid((unsigned)((c + 511) / 512), (unsigned)nparts);
-  bn_bwd_partial<<<grid, 256, 0, st>>>(dout, z, mean, rstd, gamma, beta, rows, c, act_tanh, p,
+  bn_bwd_partial<<<grid, 512, 0, st>>>(dout, z, mean, rstd, gamma, beta, rows, c, act_tanh, p,
                                        seed, site, part_g, part_gx);
   bn_bwd_final<<<(unsigned)((c + 63) / 64), 1024, 0, st>>>(part_g, part_gx, nparts, c, sums,
                                                              dgamma, dbeta);

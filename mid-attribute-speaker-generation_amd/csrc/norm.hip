@@ -19,7 +19,7 @@
 namespace fs2 {
 
 constexpr int LN_D = 256;
-constexpr int LN_ROWS = 32;  // rows per block in the backward (4 row pairs per wave)
+constexpr int LN_ROWS = 32;  // rows per block in the backward (2 row pairs per wave of 8)
 
 struct LnFwd {
   const float* y;
@@ -128,10 +128,13 @@ struct LnBwd {
 
 // Row pairs: half-wave h of a wave takes row 2i + h, 8 channels per lane.  Column partials
 // (8 per lane) are combined over the 8 half-waves of the block through LDS in a fixed order.
+constexpr int LN_BWD_WAVES = 8;  // 8 waves: 3 blocks per CU keep 24 waves' loads in flight
+
 template <bool DDOT>
-__global__ __launch_bounds__(256) void ln_bwd_f32(LnBwd a) {
-  __shared__ f32x4 red[8][64];
-  __shared__ float redb[8];
+__global__ __launch_bounds__(LN_BWD_WAVES * 64) void ln_bwd_f32(LnBwd a) {
+  constexpr int NSLOT = 2 * LN_BWD_WAVES;
+  __shared__ f32x4 red[NSLOT][64];
+  __shared__ float redb[NSLOT];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int half = lane >> 5, hl = lane & 31, slot = wave * 2 + half;
   const int c8 = 8 * hl;
@@ -150,13 +153,13 @@ __global__ __launch_bounds__(256) void ln_bwd_f32(LnBwd a) {
   // Every row pair of the wave is loaded before the first is reduced: the grid is only a
   // few blocks per CU, so the loads of all LN_ROWS / 8 iterations must be in flight together
   // (one pair at a time left the kernel latency-bound at ~1 TB/s).
-  constexpr int IT = LN_ROWS / 8;
+  constexpr int IT = LN_ROWS / NSLOT;
   f32x4 XH[IT][2], DU[IT][2];
   float RS[IT], RD[IT];
   bool LIVE[IT];
 #pragma unroll
   for (int it = 0; it < IT; ++it) {
-    const int64_t r = rbeg + 2 * (wave + 4 * it) + half;
+    const int64_t r = rbeg + 2 * (wave + LN_BWD_WAVES * it) + half;
     LIVE[it] = r < a.rows && !row_padded(a.lens, a.T, r);
     XH[it][0] = XH[it][1] = DU[it][0] = DU[it][1] = zz;
     RS[it] = RD[it] = 0.f;
@@ -175,7 +178,7 @@ __global__ __launch_bounds__(256) void ln_bwd_f32(LnBwd a) {
   }
 #pragma unroll
   for (int it = 0; it < IT; ++it) {
-    const int64_t r = rbeg + 2 * (wave + 4 * it) + half;
+    const int64_t r = rbeg + 2 * (wave + LN_BWD_WAVES * it) + half;
     if (r >= a.rows) break;
     const int64_t e0 = r * LN_D + c8;
     if (!LIVE[it]) {  // masked row: zero upstream gradient, nothing to add
@@ -254,7 +257,7 @@ __global__ __launch_bounds__(256) void ln_bwd_f32(LnBwd a) {
     if (wave == 0) {
       f32x4 sum = red[0][lane];
 #pragma unroll
-      for (int q = 1; q < 8; ++q) sum += red[q][lane];
+      for (int q = 1; q < NSLOT; ++q) sum += red[q][lane];
       st4(a.part + ((int64_t)kind * a.nblk + blockIdx.x) * LN_D + 4 * lane, sum);
     }
     __syncthreads();
@@ -268,7 +271,7 @@ __global__ __launch_bounds__(256) void ln_bwd_f32(LnBwd a) {
   if (threadIdx.x == 0) {
     float b = redb[0];
 #pragma unroll
-    for (int q = 1; q < 8; ++q) b += redb[q];
+    for (int q = 1; q < NSLOT; ++q) b += redb[q];
     a.part[4 * a.nblk * LN_D + blockIdx.x] = b;
   }
 }
@@ -557,8 +560,8 @@ int fs2_ln_bwd(int dtype, const float* dout, const float* ddot, const float* dot
   LnBwd a{dout, ddot, dot_w, xhat, rstd, gamma, beta, lens, seq_len, rows, p_in, p_out, seed,
           site_in, site_out, relu_y, dy, dres, dres_add, ws, nblk,
           dtype == FS2_BF16 ? (unsigned short*)dy_t : nullptr};
-  if (ddot) ln_bwd_f32<true><<<(unsigned)nblk, 256, 0, st>>>(a);
-  else ln_bwd_f32<false><<<(unsigned)nblk, 256, 0, st>>>(a);
+  if (ddot) ln_bwd_f32<true><<<(unsigned)nblk, LN_BWD_WAVES * 64, 0, st>>>(a);
+  else ln_bwd_f32<false><<<(unsigned)nblk, LN_BWD_WAVES * 64, 0, st>>>(a);
   int rc = launch_status("fs2_ln_bwd");
   if (rc) return rc;
   ColsumJobs jobs{};

@@ -1,7 +1,11 @@
 """Throughput of the FastSpeech2 + TacoSpawn training step on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--dtype bf16|f32]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (N > 1)
+
+``--gpus N`` without a launcher (no WORLD_SIZE in the environment) starts N fresh child
+processes itself, one per GPU (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1),
+before anything touches the GPU; under a launcher WORLD_SIZE must equal ``--gpus``.
 
 A step is one full optimiser step of train.py:138-206 (forward, FastSpeech2Loss + GMM
 backward, clip_grad_norm_, Adam + LR schedule, zero_grad) on a synthetic SYN-48 batch per
@@ -9,17 +13,27 @@ rank (B = 48, 128 phonemes x 512 frames padded) with inputs resi
 value = valid mel frames of all ranks per second (max-over-ranks time, weak scaling).
 
 The JSON line also carries
-  roofline     the decoder FFN Conv1d(256->1024, k=9) forward implicit GEMM (the dominant
-               kernel: the k=9 convs are 75% of the FFT-block FLOPs), achieved FLOP/s from HIP
-               events around its launches inside the timed region, against the dense MFMA
-               peak of the compute dtype;
-  cpu_baseline the CPU oracle (oracle/fs2_cpu.py, a restatement of the reference step) timed
-               on this host's cores on a bounded sample (rank 0, N = 1 only).
+  roofline      the DOMINANT launch set of the step by in-step time: HIP events (on the
+                stream each launch runs on, the weight-gradient side stream included) around
+                every GEMM / conv / attention launch of the timed steps, grouped by op class;
+                achieved = the class's algorithmic FLOP (valid frames) per step / its
+                launches' summed duration per step; ``classes`` lists every class;
+                ``traffic``: PMC bytes per launch of the class's decoder-shaped launches;
+  fft_block     one decoder FFT block fwd+bwd (north_star's target): HIP events around the
+                decoder's forward and backward (its weight-gradient stream joined) in extra
+                steps after the timed region, / 6 layers, against SURVEY §8d's 463.9 GFLOP
+                (padded shapes) and the valid-frame FLOP;
+  step_roofline the whole step: 3,904.7 GFLOP (§8d, padded) / ms_per_step;
+  f32           (bf16 runs, N = 1) the same step at the reference's precision (fp32);
+  cpu_baseline  the CPU oracle (oracle/fs2_cpu.py, a restatement of the reference step) timed
+                on this host's cores: median of 3 steps after 1 warm-up (rank 0, N = 1 only).
 """
 import argparse
 import importlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -30,108 +44,221 @@ import torch.distributed as dist
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 PKG = importlib.import_module("mid-attribute-speaker-generation_amd")
-M = importlib.import_module("mid-attribute-speaker-generation_amd.model")
-K = importlib.import_module("mid-attribute-speaker-generation_amd.kernels")
-TR = importlib.import_module("mid-attribute-speaker-generation_amd.train")
 
 PEAK = {"f32": (157.3, "TFLOP/s"), "bf16": (2500.0, "TFLOP/s")}
-# the dominant kernel as rocprofv3 names it (bf16 path: the channel-block-major halo kernel,
-# 1,536 workgroups of 128 x 128 at SYN-48; scripts/kshape.py isolates the same launches)
-ROOF_KERNEL = "conv_gemm_halo<256, 128, 2, 16, false, 8>"
-_SYN = PKG.data.syn_batch(48, 128, seed=0)
-_N, _VALID = 48 * int(_SYN[8]), int(np.sum(_SYN[7]))
-# compulsory bytes of one decoder FFN Conv1d(256 -> 1024, k=9) forward launch at SYN-48 (rank
-# 0's batch), bf16 operands: read the valid rows of x (V x 256) and the re-laid-out weight
-# (1024 x 9*256) once, write every row of h (N x 1024; padded rows are written as zeros)
-ALG_BYTES = _VALID * 256 * 2 + 1024 * 2304 * 2 + _N * 1024 * 2
+METRIC = "mel-frames/sec (node) FastSpeech2 train step, JVS-VCTK bs=48, 1/2/4/8 MI355X"
+STEP_GFLOP_PADDED = 3904.7  # SURVEY.md §8d, SYN-48 fwd+bwd at padded shapes
+DEC_BLOCK_GFLOP_PADDED = 463.9  # SURVEY.md §8d, one decoder FFT block fwd+bwd at 48 x 512
+D, F, KW = 256, 1024, 9
 
 
-class ConvTimer:
-    """HIP events around every decoder FFN Conv1d(256 -> 1024, k=9) forward launch (the
-    dominant kernel; 6 launches per step at SYN-48, each a 24,576 x 1,024 x 2,304 implicit
-    GEMM, grid 1,536 tiles of 128 x 128 -- the only launch of that grid in the step, so the
-    rocprofv3 trace isolates the same launches: scripts/kshape.py).
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
 
-    Eager steps: events are recorded around the launches of the timed steps.  Graph replay:
-    the event records are captured into the step graph next to the kernels (``capture``
-    mode), so every replay re-records them and the durations read after the timed loop are
-    those of the last timed replay."""
 
-    def __init__(self):
+def launch_ranks(n, argv):
+    """Start ``n`` ranks of this script (one process per GPU) and wait for them.  Called
+    before anything initialises the GPU; returns the first non-zero exit code (and stops the
+    remaining ranks, by PID) or 0."""
+    env = dict(os.environ, WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(_free_port()), LOCAL_WORLD_SIZE=str(n))
+    procs = []
+    for r in range(n):
+        e = dict(env, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=e))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c != 0 and rc == 0:
+                rc = c
+                for q in live:  # a failed rank leaves the others waiting in a collective
+                    q.kill()
+        time.sleep(0.05)
+    return rc
+
+
+# ----------------------------------------------------------------------------- timing
+class ClassTimer:
+    """HIP events around every GEMM / conv / attention launch, on the stream it runs on.
+
+    Launch classes (the k=9 class is the FFN Conv1d of all 10 FFT blocks, forward and data
+    gradient, encoder and decoder):
+      conv_k9 / conv_k5 / conv_k3 / linear_k1   fwd + data-gradient implicit GEMMs
+      wgrad_k9 / wgrad_k5 / wgrad_k3 / wgrad_k1 weight(+bias)-gradient GEMMs incl. reduce
+      attention_fwd / attention_bwd             flash attention
+    FLOP per launch = 2 * algorithmic rows * C_out * C_in * taps (attention: 4 * d * sum L^2
+    forward, 2.5x that backward), algorithmic rows = valid frames of launches given the
+    utterance lengths (the kernels skip all-padding tiles), all rows otherwise."""
+
+    def __init__(self, K, valid_by_T, sq_by_T):
+        self.K = K
+        self.valid_by_T = valid_by_T  # seq_len -> valid rows of the batch
+        self.sq_by_T = sq_by_T        # seq_len -> sum of squared lengths (attention)
         self.on = False
-        self.capture = False
-        self.events, self.flops = [], []
-        self.rows = 0  # padded mel frames of the batch (the decoder's rows)
-        self.valid = 0  # valid mel frames of the batch (algorithmic rows)
-        self._orig = K.conv_gemm
+        self.rec = []                  # (class, start, end, flop)
+        self._streams = {}
+        self._orig = {n: getattr(K, n) for n in ("conv_gemm", "conv_wgrad", "attn_fwd", "attn_bwd")}
+
+    def _stream(self, handle):
+        if handle is None:
+            return torch.cuda.current_stream()
+        s = self._streams.get(handle)
+        if s is None:
+            s = self._streams[handle] = torch.cuda.ExternalStream(handle)
+        return s
+
+    def _timed(self, cls, flop, stream_handle, fn, *a, **kw):
+        if not self.on:
+            return fn(*a, **kw)
+        st = self._stream(stream_handle)
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record(st)
+        y = fn(*a, **kw)
+        e.record(st)
+        self.rec.append((cls, s, e, flop))
+        return y
+
+    def _rows(self, rows, seq_len, lens):
+        return self.valid_by_T.get(seq_len, rows) if lens is not None else rows
 
     def install(self):
-        orig = self._orig
+        o = self._orig
+        T = self
 
-        def timed(x, wk, rows, seq_len, c_in, c_out, taps, pad, **kw):
-            rec = (taps == 9 and c_out > c_in and rows == self.rows and
-                   (self.on or (self.capture and torch.cuda.is_current_stream_capturing())))
-            if not rec:
-                return orig(x, wk, rows, seq_len, c_in, c_out, taps, pad, **kw)
+        def conv_gemm(x, wk, rows, seq_len, c_in, c_out, taps, pad, **kw):
+            r = T._rows(rows, seq_len, kw.get("lens"))
+            cls = f"conv_k{taps}" if taps > 1 else "linear_k1"
+            return T._timed(cls, 2.0 * r * c_out * c_in * taps, None, o["conv_gemm"],
+                            x, wk, rows, seq_len, c_in, c_out, taps, pad, **kw)
+
+        def conv_wgrad(dy, x, dw, rows, seq_len, c_in, c_out, taps, pad, **kw):
+            r = T._rows(rows, seq_len, kw.get("lens"))
+            return T._timed(f"wgrad_k{taps}", 2.0 * r * c_out * c_in * taps, kw.get("on_stream"),
+                            o["conv_wgrad"], dy, x, dw, rows, seq_len, c_in, c_out, taps, pad, **kw)
+
+        def attn_fwd(qkv, lens, batch, seq_len, heads, d_head, scale):
+            fl = 4.0 * heads * d_head * T.sq_by_T.get(seq_len, batch * seq_len * seq_len)
+            return T._timed("attention_fwd", fl, None, o["attn_fwd"], qkv, lens, batch, seq_len,
+                            heads, d_head, scale)
+
+        def attn_bwd(qkv, o_, d_o, lse, lens, batch, seq_len, heads, d_head, scale):
+            fl = 10.0 * heads * d_head * T.sq_by_T.get(seq_len, batch * seq_len * seq_len)
+            return T._timed("attention_bwd", fl, None, o["attn_bwd"], qkv, o_, d_o, lse, lens,
+                            batch, seq_len, heads, d_head, scale)
+
+        self.K.conv_gemm, self.K.conv_wgrad = conv_gemm, conv_wgrad
+        self.K.attn_fwd, self.K.attn_bwd = attn_fwd, attn_bwd
+
+    def table(self, steps, peak):
+        torch.cuda.synchronize()
+        agg = {}
+        for cls, s, e, fl in self.rec:
+            ms = s.elapsed_time(e)
+            a = agg.setdefault(cls, [0.0, 0.0, 0])
+            a[0] += ms
+            a[1] += fl
+            a[2] += 1
+        out = {}
+        for cls, (ms, fl, n) in agg.items():
+            tf = fl / (ms / 1e3) / 1e12 if ms > 0 else 0.0
+            out[cls] = {"ms_per_step": round(ms / steps, 4), "launches_per_step": round(n / steps, 2),
+                        "avg_launch_ms": round(ms / n, 4), "gflop_per_step": round(fl / steps / 1e9, 2),
+                        "tflops": round(tf, 1), "frac": round(tf / peak, 4)}
+        return out
+
+
+class BlockTimer:
+    """Decoder forward / backward timing with the side stream joined at the decoder's end."""
+
+    def __init__(self, M, model):
+        self.M, self.model = M, model
+        self.on = False
+        self.ev = []
+        Fn = M.DecoderFn
+        self._f, self._b = Fn.forward, Fn.backward
+        me = self
+
+        def fwd(fctx, *a):
+            if not me.on:
+                return me._f(fctx, *a)
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
-            y = orig(x, wk, rows, seq_len, c_in, c_out, taps, pad, **kw)
+            r = me._f(fctx, *a)
             e.record()
-            self.events.append((s, e))
-            # algorithmic FLOP: valid frames only (the kernel also computes the padded rows
-            # of tiles that hold a valid frame, and skips all-padding tiles)
-            self.flops.append(2.0 * self.valid * c_out * c_in * taps)
-            return y
+            me.ev.append(("fwd", s, e))
+            return r
 
-        K.conv_gemm = timed
+        def bwd(fctx, *a):
+            if not me.on:
+                return me._b(fctx, *a)
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            r = me._b(fctx, *a)
+            me.model.join_side()  # the decoder's weight gradients belong to its backward
+            e.record()
+            me.ev.append(("bwd", s, e))
+            return r
+
+        Fn.forward, Fn.backward = staticmethod(fwd), staticmethod(bwd)
 
     def result(self):
-        if not self.events:
-            return None, None, 0
         torch.cuda.synchronize()
-        try:
-            ms = [s.elapsed_time(e) for s, e in self.events]
-        except RuntimeError:
-            return None, None, 0
-        if not all(np.isfinite(ms)) or min(ms) <= 0:
-            return None, None, 0
-        return float(np.sum(self.flops)), float(np.sum(ms)) / 1e3, len(ms)
+        f = [s.elapsed_time(e) for k, s, e in self.ev if k == "fwd"]
+        b = [s.elapsed_time(e) for k, s, e in self.ev if k == "bwd"]
+        return (float(np.median(f)), float(np.median(b))) if f and b else (None, None)
 
 
-PROBE_SHAPES = [  # the decoder's FFN k=9 forward launch (h = relu(conv(x1) + b))
-    (24576, 512, 256, 1024, 9, "fwd")]
-
-
+# ----------------------------------------------------------------------------- PMC traffic
 def probe_conv(reps=10):
-    """The dominant kernel's launches alone (same shapes / epilogues as the step), for the
-    PMC passes of ``hbm_traffic``."""
+    """The decoder-shaped launches of the k=9 class alone (forward h = relu(conv(x1) + b) and
+    the data gradient dx1 += conv^T(dh), same shapes / epilogues / lens as the step), for
+    the PMC passes of ``hbm_traffic``."""
+    K = importlib.import_module("mid-attribute-speaker-generation_amd.kernels")
+    syn = PKG.data.syn_batch(48, 128, seed=0)
+    M_, T_ = 48 * int(syn[8]), int(syn[8])
     dev = torch.device("cuda", 0)
-    lens = torch.tensor(_SYN[7], device=dev)  # the step passes the mel lengths (tile skip)
-    for M_, T_, cin, cout, k, kind in PROBE_SHAPES:
-        x = torch.randn(M_, cin, device=dev).to(torch.bfloat16)
-        w = (torch.randn(cout * cin * k, device=dev) * 0.02).to(torch.bfloat16)
-        if kind == "fwd":
-            b = torch.randn(cout, device=dev)
-            run = lambda: K.conv_gemm(x, w, M_, T_, cin, cout, k, 4, bias=b, flags=K.EPI_RELU,
-                                      out_dtype=torch.bfloat16, lens=lens)
-        else:
-            aux = torch.randn(M_, cout, device=dev)
-            run = lambda: K.conv_gemm(x, w, M_, T_, cin, cout, k, 4, flags=K.EPI_ADD_AUX,
-                                      aux=aux, out=aux, lens=lens)
-        for _ in range(reps):
-            run()
+    lens = torch.tensor(syn[7], device=dev)
+    x = torch.randn(M_, D, device=dev).to(torch.bfloat16)
+    w = (torch.randn(F * D * KW, device=dev) * 0.02).to(torch.bfloat16)
+    b = torch.randn(F, device=dev)
+    dh = torch.randn(M_, F, device=dev).to(torch.bfloat16)
+    dx = torch.randn(M_, D, device=dev)
+    for _ in range(reps):
+        K.conv_gemm(x, w, M_, T_, D, F, KW, 4, bias=b, flags=K.EPI_RELU, out_dtype=torch.bfloat16,
+                    lens=lens)
+        K.conv_gemm(dh, w, M_, T_, F, D, KW, 4, flags=K.EPI_ADD_AUX, aux=dx, out=dx, lens=lens)
     torch.cuda.synchronize()
 
 
+def probe_alg_bytes(syn):
+    """Compulsory bytes of the probe's two launches (mean per launch): forward reads the
+    valid rows of x (V x 256 bf16) and the weight (1024 x 2304 bf16) once and writes every
+    row of h (N x 1024 bf16); the data gradient reads the valid rows of dh (V x 1024 bf16),
+    the weight, and reads + writes dx (N x 256 fp32)."""
+    V, N = int(np.sum(syn[7])), 48 * int(syn[8])
+    wb = F * D * KW * 2
+    fwd = V * D * 2 + wb + N * F * 2
+    dgr = V * F * 2 + wb + 2 * N * D * 4
+    return (fwd + dgr) // 2
+
+
 def hbm_traffic(timeout=300):
-    """Per-launch memory-side bytes of the k=9 conv GEMM from rocprofv3 PMC counters:
-    FETCH_SIZE and WRITE_SIZE (KiB) in separate passes (they do not fit one TCC pass),
-    FETCH_SIZE doubled (gfx950 reports half the bytes of 16-B-per-lane streaming reads;
-    MI355X_MICROARCH.md, HBM).  These count L2 misses, Infinity-Cache hits included."""
+    """Per-launch memory-side bytes of the probe's halo-conv launches from rocprofv3 PMC
+    counters: FETCH_SIZE and WRITE_SIZE (KiB) in separate passes (they do not fit one TCC
+    pass), FETCH_SIZE doubled (gfx950 reports half the bytes of 16-B-per-lane streaming
+    reads; MI355X_MICROARCH.md, HBM).  These count L2 misses, Infinity-Cache hits included."""
     import csv
     import glob
     import shutil
-    import subprocess
     import tempfile
     prof = shutil.which("rocprofv3")
     if prof is None:
@@ -140,10 +267,11 @@ def hbm_traffic(timeout=300):
     with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as tmp:
         for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
             d = os.path.join(tmp, ctr)
-            cmd = [prof, "--pmc", ctr, "-d", d, "-o", "probe", "--output-format", "csv", "--",
-                   sys.executable, os.path.abspath(__file__), "--probe-conv"]
+            cmd = ["timeout", "-s", "KILL", str(timeout), prof, "--pmc", ctr, "-d", d, "-o",
+                   "probe", "--output-format", "csv", "--", sys.executable,
+                   os.path.abspath(__file__), "--probe-conv"]
             try:
-                r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout)
+                r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout + 30)
             except subprocess.TimeoutExpired:
                 return None, f"{ctr} pass timed out"
             files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
@@ -151,16 +279,26 @@ def hbm_traffic(timeout=300):
                 return None, f"{ctr} pass failed (rc {r.returncode})"
             vals = []
             for row in csv.DictReader(open(files[0])):
-                if ROOF_KERNEL in row.get("Kernel_Name", "") and row.get("Counter_Name") == ctr:
+                if "conv_gemm_halo" in row.get("Kernel_Name", "") and row.get("Counter_Name") == ctr:
                     vals.append(float(row["Counter_Value"]))
             if not vals:
-                return None, f"{ctr}: no {ROOF_KERNEL} dispatches"
+                return None, f"{ctr}: no conv_gemm_halo dispatches"
             per[ctr] = float(np.mean(vals))
-    # both counters are in KiB
     return (per["FETCH_SIZE"] * 2.0 + per["WRITE_SIZE"]) * 1024.0, per
 
 
-def cpu_baseline(batch_np, steps=2):
+# ----------------------------------------------------------------------------- CPU baseline
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(batch_np, steps=3):
     from oracle import fs2_cpu
     n_thr = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
     torch.set_num_threads(n_thr)
@@ -169,15 +307,42 @@ def cpu_baseline(batch_np, steps=2):
     opt = fs2_cpu.make_opt(ref)
     b = PKG.data.to_device(batch_np, "cpu")
     fs2_cpu.train_step(ref, opt, b)  # warm-up
-    t0 = time.perf_counter()
+    ts = []
     for _ in range(steps):
+        t0 = time.perf_counter()
         fs2_cpu.train_step(ref, opt, b)
-    dt = time.perf_counter() - t0
+        ts.append(time.perf_counter() - t0)
+    med = float(np.median(ts))
     frames = int(np.sum(batch_np[7]))
-    return {"value": round(frames * steps / dt, 1), "unit": "mel-frames/s",
-            "cores": torch.get_num_threads(), "kind": "port",
-            "sample": f"oracle/fs2_cpu.py train step (dropout on), SYN-{len(batch_np[4])} "
-                      f"seed 0, {steps} timed steps after 1 warm-up, {dt:.1f} s"}
+    return {"value": round(frames / med, 1), "unit": "mel-frames/s",
+            "cores": torch.get_num_threads(), "kind": "port", "cpu_model": _cpu_model(),
+            "sample": f"oracle/fs2_cpu.py train step (dropout on), SYN-{len(batch_np[4])} seed 0: "
+                      f"median of {steps} timed steps after 1 warm-up "
+                      f"({', '.join(f'{t:.2f}' for t in ts)} s)"}
+
+
+# ----------------------------------------------------------------------------- main
+def build_trainer(M, TR, dtype, dev, rank, graph=False):
+    pp, mc, tc, path = PKG.config.load_configs("JVS-VCTK")
+    cdt = {"f32": torch.float32, "bf16": torch.bfloat16}[dtype]
+    model = M.FastSpeech2(pp, mc, path, device=dev, compute_dtype=cdt)
+    model.train()
+    model.seed(1234 + rank)
+    return model, TR.Trainer(model, pp, mc, tc, graph=graph), tc
+
+
+def launch_check(world, rank):
+    """--launch-check: the rank set the launcher produced (gloo, CPU only)."""
+    if world > 1:
+        dist.init_process_group("gloo")
+    t = torch.ones(1)
+    if world > 1:
+        dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"world": world, "ranks_seen": int(t.item()), "parallelism": f"dp{world}"}),
+              flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def main():
@@ -191,6 +356,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC passes")
+    ap.add_argument("--no-f32", action="store_true", help="skip the fp32 companion measurement")
     ap.add_argument("--graph", action="store_true",
                     help="N=1: capture the step once into a HIP graph and replay it (measured "
                          "slower than eager here: replay serialises the weight-gradient stream)")
@@ -198,26 +364,40 @@ def main():
                     help="BASELINE config 3: the --use_clf step (second forward with shuffled "
                          "speakers + GE2E language discriminator on 150-frame chunks)")
     ap.add_argument("--probe-conv", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.probe_conv:
         probe_conv()
-        return
+        return 0
 
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:  # no launcher: start one process per GPU (nothing touched the GPU yet)
+            return launch_ranks(args.gpus, sys.argv[1:])
+    elif int(os.environ["WORLD_SIZE"]) != args.gpus:
+        print(f"bench.py: WORLD_SIZE={os.environ['WORLD_SIZE']} but --gpus {args.gpus}",
+              file=sys.stderr)
+        return 2
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.launch_check:
+        launch_check(world, rank)
+        return 0
+
+    if torch.cuda.device_count() < world:
+        print(f"bench.py: {world} ranks but {torch.cuda.device_count()} GPUs", file=sys.stderr)
+        return 2
+    M = importlib.import_module("mid-attribute-speaker-generation_amd.model")
+    K = importlib.import_module("mid-attribute-speaker-generation_amd.kernels")
+    TR = importlib.import_module("mid-attribute-speaker-generation_amd.train")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    pp, mc, tc, path = PKG.config.load_configs("JVS-VCTK")
-    cdt = {"f32": torch.float32, "bf16": torch.bfloat16}[args.dtype]
-    model = M.FastSpeech2(pp, mc, path, device=dev, compute_dtype=cdt)
-    model.train()
-    model.seed(1234 + rank)
     use_graph = world == 1 and args.graph
-    trainer = TR.Trainer(model, pp, mc, tc, graph=use_graph and not args.use_clf)
+    model, trainer, tc = build_trainer(M, TR, args.dtype, dev, rank,
+                                       graph=use_graph and not args.use_clf)
     if args.use_clf:
         import random
         G = importlib.import_module("mid-attribute-speaker-generation_amd.ge2e")
@@ -235,23 +415,25 @@ def main():
     batch_np = PKG.data.syn_batch(args.batch, args.src_len, seed=rank)
     batch = PKG.data.to_device(batch_np, dev)
     frames_local = int(np.sum(batch_np[7]))
-    padded_local = int(args.batch * batch_np[8])
-
-    timer = ConvTimer()
-    timer.rows = padded_local
-    timer.valid = frames_local
-    if not args.no_roofline:
+    T_m, T_s = int(batch_np[8]), int(batch_np[5])
+    padded_local = int(args.batch * T_m)
+    mel = np.asarray(batch_np[7], np.float64)
+    src = np.asarray(batch_np[4], np.float64)
+    timer = ClassTimer(K, {T_m: frames_local, T_s: int(src.sum())},
+                       {T_m: float((mel ** 2).sum()), T_s: float((src ** 2).sum())})
+    if not args.no_roofline and not use_graph:
         timer.install()
-        timer.capture = use_graph
+
+    kw = (lambda: clf_kw()) if args.use_clf else (lambda: {})
     for _ in range(max(args.warmup, 2 if use_graph else 0)):  # graph: step 1 captures
-        trainer.step(batch, **(clf_kw() if args.use_clf else {}))
+        trainer.step(batch, **kw())
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    timer.on = not use_graph
+    timer.on = True
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        losses, eloss, gnorm = trainer.step(batch, **(clf_kw() if args.use_clf else {}))[:3]
+        losses = trainer.step(batch, **kw())[0]
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -263,59 +445,115 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dist.all_reduce(fr)
     dt, frames = float(t.item()), float(fr.item())
-    loss_now = float(losses[0])
+    loss_now = float(losses[0].detach())
+    ms_step = dt / args.steps * 1e3
+    peak, unit = PEAK[args.dtype]
 
+    out = None
     if rank == 0:
-        flops, secs, n = timer.result()
-        if not flops and use_graph and not args.no_roofline:
-            # event timing inside the graph unavailable: time the same launches in one
-            # eager step after the timed region (same kernels, same shapes)
-            timer.events, timer.flops, timer.capture, timer.on = [], [], False, True
-            trainer.graph_mode = False
-            trainer.step(batch)
-            timer.on = False
-            flops, secs, n = timer.result()
-        roof = None
-        if flops:
-            peak, unit = PEAK[args.dtype]
-            ach = flops / secs / 1e12
-            roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": unit,
-                    "frac": round(ach / peak, 4), "traffic": None,
-                    "kernel": (f"{ROOF_KERNEL if args.dtype == 'bf16' else 'conv_gemm_nt_f32'} "
-                               "(decoder FFN Conv1d 256->1024 k=9, forward)"),
-                    "flop_basis": "2 * valid frames * 1024 * 256 * 9 per launch",
-                    "per_launch_flop": round(flops / n), "avg_launch_ms": round(secs / n * 1e3, 4)}
-            if world == 1 and args.dtype == "bf16" and not args.no_traffic:
+        roof, classes = None, None
+        if timer.rec:
+            classes = timer.table(args.steps, peak)
+            dom = max(classes, key=lambda c: classes[c]["ms_per_step"])
+            c = classes[dom]
+            roof = {"bound": "mfma", "achieved": c["tflops"], "peak": peak, "unit": unit,
+                    "frac": c["frac"], "traffic": None,
+                    "kernel": f"{dom}: the step's dominant launch set by in-step time "
+                              f"({c['launches_per_step']} launches/step, {c['ms_per_step']} ms/step)",
+                    "flop_basis": "2 * valid frames * C_out * C_in * taps per launch (kernels "
+                                  "skip all-padding row tiles)",
+                    "per_launch_flop": round(c["gflop_per_step"] * 1e9 / c["launches_per_step"]),
+                    "avg_launch_ms": c["avg_launch_ms"]}
+            if dom == "conv_k9" and world == 1 and args.dtype == "bf16" and not args.no_traffic:
                 traffic, detail = hbm_traffic()
                 if traffic is not None:
                     roof["traffic"] = round(traffic)
-                    roof["traffic_unit"] = "bytes/launch (FETCH_SIZE x2 + WRITE_SIZE, PMC)"
-                    roof["traffic_algorithmic"] = ALG_BYTES
+                    roof["traffic_unit"] = ("bytes/launch (FETCH_SIZE x2 + WRITE_SIZE, PMC) of the "
+                                            "class's decoder-shaped fwd + data-gradient launches")
+                    roof["traffic_algorithmic"] = probe_alg_bytes(PKG.data.syn_batch(48, 128, seed=0))
                 else:
                     roof["traffic_note"] = detail
-        cpu = None
-        if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(batch_np)
-        out = {"metric": "mel-frames/sec (node) FastSpeech2 train step, JVS-VCTK bs=48, 1/2/4/8 MI355X",
-               "value": round(frames * args.steps / dt, 1), "unit": "mel-frames/s",
+            roof["classes"] = classes
+        step_roof = {"gflop_padded": STEP_GFLOP_PADDED, "achieved": None, "frac": None}
+        if args.batch == 48 and args.src_len == 128 and not args.use_clf:
+            ach = STEP_GFLOP_PADDED / (ms_step / 1e3) / 1e3
+            step_roof = {"gflop_padded": STEP_GFLOP_PADDED, "achieved": round(ach, 1),
+                         "unit": unit, "peak": peak, "frac": round(ach / peak, 4)}
+        out = {"metric": METRIC, "value": round(frames * args.steps / dt, 1), "unit": "mel-frames/s",
                "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-               "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
+               "ms_per_step": round(ms_step, 3), "higher_is_better": True,
                "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
                "data": "synthetic SYN-B (seeded, rank r uses seed r), random-init weights",
                "config": {"workload": f"SYN-{args.batch}: FastSpeech2+TacoSpawn train step, "
                                       f"B={args.batch}/GPU, {args.src_len} phonemes x "
-                                      f"{int(batch_np[8])} frames padded",
-                          "global_batch": args.batch * world, "seq_len": int(batch_np[8]),
+                                      f"{T_m} frames padded",
+                          "global_batch": args.batch * world, "seq_len": T_m,
                           "valid_frames_per_rank_step": frames_local,
                           "padded_frames_per_rank_step": padded_local,
                           "parallelism": f"dp{world}",
                           "use_clf": bool(args.use_clf),
                           "execution": "hip-graph replay" if use_graph else "eager"},
-               "roofline": roof, "cpu_baseline": cpu, "final_loss": round(loss_now, 5)}
+               "roofline": roof, "step_roofline": step_roof}
+
+    # decoder FFT block fwd + bwd, 3 extra steps (rank 0's figures; every rank runs them so
+    # collectives stay matched)
+    if not args.no_roofline and not use_graph and not args.use_clf:
+        bt = BlockTimer(M, model)
+        bt.on = True
+        for _ in range(3):
+            trainer.step(batch)
+        bt.on = False
+        f_ms, b_ms = bt.result()
+        if rank == 0 and f_ms is not None:
+            L = len(model.decoder.layer_stack)
+            blk_ms = (f_ms + b_ms) / L
+            per_block_fwd_valid = frames_local * (8 * D * D + 2 * KW * D * F + 2 * F * D) + \
+                4 * D * float((mel ** 2).sum())
+            gf_valid = 3 * per_block_fwd_valid / 1e9
+            gf_pad = DEC_BLOCK_GFLOP_PADDED if (args.batch == 48 and T_m == 512) else None
+            fb = {"fwd_ms_per_block": round(f_ms / L, 4), "bwd_ms_per_block": round(b_ms / L, 4),
+                  "gflop_valid": round(gf_valid, 1), "unit": unit, "peak": peak,
+                  "achieved_valid": round(gf_valid / blk_ms, 1),
+                  "frac_valid": round(gf_valid / blk_ms / peak, 4),
+                  "basis": "HIP events around DecoderFn forward / backward (+ its side-stream "
+                           "weight gradients joined) in 3 steps after the timed region, median, "
+                           "/ 6 layers"}
+            if gf_pad:
+                fb.update(gflop_padded=gf_pad, achieved_padded=round(gf_pad / blk_ms, 1),
+                          frac_padded=round(gf_pad / blk_ms / peak, 4))
+            out["fft_block"] = fb
+
+    # the reference's precision (fp32), N = 1, a short companion measurement
+    if world == 1 and args.dtype == "bf16" and not args.no_f32 and not args.use_clf:
+        timer.on = False
+        del trainer, model
+        torch.cuda.empty_cache()
+        m32, tr32, _ = build_trainer(M, TR, "f32", dev, rank)
+        for _ in range(2):
+            tr32.step(batch)
+        torch.cuda.synchronize()
+        n32 = 5
+        t0 = time.perf_counter()
+        for _ in range(n32):
+            tr32.step(batch)
+        torch.cuda.synchronize()
+        d32 = time.perf_counter() - t0
+        ach = STEP_GFLOP_PADDED / (d32 / n32) / 1e3
+        out["f32"] = {"value": round(frames_local * n32 / d32, 1), "unit": "mel-frames/s",
+                      "ms_per_step": round(d32 / n32 * 1e3, 3), "steps": n32, "warmup": 2,
+                      "step_frac_of_f32_peak": round(ach / PEAK["f32"][0], 4)}
+
+    if rank == 0:
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(batch_np)
+        else:
+            out["cpu_baseline"] = None
+        out["final_loss"] = round(loss_now, 5)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

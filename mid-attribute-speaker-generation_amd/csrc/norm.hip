@@ -127,7 +127,8 @@ struct LnBwd {
 };
 
 // Row pairs: half-wave h of a wave takes row 2i + h, 8 channels per lane.  Column partials
-// (8 per lane) are combined over the 8 half-waves of the block through LDS in a fixed order.
+// (8 per lane) are combined over the NSLOT = 16 half-waves (8 waves x 2) of the block through
+// LDS in a fixed slot order.
 constexpr int LN_BWD_WAVES = 8;  // 8 waves: 3 blocks per CU keep 24 waves' loads in flight
 
 template <bool DDOT>
@@ -151,7 +152,7 @@ __global__ __launch_bounds__(LN_BWD_WAVES * 64) void ln_bwd_f32(LnBwd a) {
   const uint64_t seed = a.seed ? *a.seed : 0ull;
   const int64_t rbeg = (int64_t)blockIdx.x * LN_ROWS;
   // Every row pair of the wave is loaded before the first is reduced: the grid is only a
-  // few blocks per CU, so the loads of all LN_ROWS / 8 iterations must be in flight together
+  // few blocks per CU, so the loads of all IT = LN_ROWS / NSLOT iterations must be in flight together
   // (one pair at a time left the kernel latency-bound at ~1 TB/s).
   constexpr int IT = LN_ROWS / NSLOT;
   f32x4 XH[IT][2], DU[IT][2];
@@ -249,7 +250,7 @@ __global__ __launch_bounds__(LN_BWD_WAVES * 64) void ln_bwd_f32(LnBwd a) {
     py1 += dy1;
   }
   // per kind: red[slot][q], f32x4 q covers channels 4q..4q+3 (lane hl owns q = 2hl, 2hl+1);
-  // wave 0 sums the 8 half-waves in slot order
+  // wave 0 sums the NSLOT = 16 half-waves in slot order
   auto flush = [&](f32x4 lo, f32x4 hi, int kind) {
     red[slot][2 * hl] = lo;
     red[slot][2 * hl + 1] = hi;
@@ -406,9 +407,9 @@ FS2_DEV void bn_g8(const float* dout, const float* z, const float* mean, const f
 }
 
 // column partials of g and g*xhat: block (x, y) covers channels [512x, 512x+512) (8 per
-// lane) of rows [BN_ROWS*y, BN_ROWS*(y+1)), four row lanes summed in lane order
-// 8 waves per block (one row group each): the PostNet shape gives only 1.5 blocks per CU,
-// so the row groups are what keeps enough loads in flight
+// lane) of rows [BN_ROWS*y, BN_ROWS*(y+1)); wave ry takes rows r0 + ry + 8i, and the eight
+// row-group (wave) partials are summed in wave order.  8 waves per block: the PostNet shape
+// gives only 1.5 blocks per CU, so the row groups are what keeps enough loads in flight
 __global__ __launch_bounds__(512) void bn_bwd_partial(const float* dout, const float* z,
                                                       const float* mean, const float* rstd,
                                                       const float* gamma, const float* beta,

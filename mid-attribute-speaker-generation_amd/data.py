@@ -56,6 +56,17 @@ def syn_batch(batch_size, max_src_len=128, seed=0, frames_per_phone=4, n_speaker
             Tm, pitches, energies, durations, meta, accents)
 
 
+def syn_batch_for(config_name, batch_size, max_src_len=128, seed=0, **kw):
+    """``syn_batch`` shaped for a bundled config: speaker ids on ``[0, len(speakers.json))``
+    and one one-hot per metadata attribute of ``preprocess.yaml`` (JVS-VCTK: gender +
+    language, width 4; JSUT: gender, width 2; ``model/fastspeech2.py:317``)."""
+    from . import config as cfg
+    pp, _, _, path = cfg.load_configs(config_name)
+    sizes = tuple(len(v) for v in pp["speaker_generation"]["metadata"].values())
+    return syn_batch(batch_size, max_src_len, seed=seed, n_speakers=cfg.n_speakers(path),
+                     meta_sizes=sizes, **kw)
+
+
 def to_device(batch, device):
     """Tensor conversion with the dtypes of ``utils/tools.py:to_device`` (14-tuple branch,
     61-105): ids long, pitches/mels/meta float, energies left in their array dtype."""

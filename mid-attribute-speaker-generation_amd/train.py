@@ -1,4 +1,4 @@
-"""The training step of ``train.py:134-206`` (``grad_acc_step`` 1; ``use_clf`` optional) and
+"""The training step of ``train.py:134-206`` (``grad_acc_step``, ``use_clf`` optional) and
 its data-parallel form.
 
 Single process: ``train_step`` is line-for-line the reference's step semantics
@@ -48,22 +48,28 @@ def clf_backward(model, batch, clf, perm, step, total_step, lambd=1.0):
 
 
 def train_step(model, optimizer, Loss, eLoss, batch, grad_clip_thresh=1.0, grad_sync=None,
-               clf=None, clf_args=None):
-    """One optimiser step -> (losses, eloss, grad norm, output); with ``clf`` (and
-    ``clf_args = (perm, step, total_step, lambd)``) the ``--use_clf`` branch runs between the
-    losses' backward and the clip, and its ``(dloss, cross-lingual chunks, chunks)`` is
-    appended."""
+               clf=None, clf_args=None, grad_acc_step=1, update=True):
+    """One batch of ``train.py:138-206`` -> (losses, eloss, grad norm, output).
+
+    Both losses are back-propagated divided by ``grad_acc_step`` (``train.py:159,165``);
+    with ``update`` (the reference's ``step % grad_acc_step == 0``, ``train.py:200``) the
+    accumulated gradients are clipped, Adam steps and the gradients are zeroed, otherwise
+    they stay accumulated and the grad norm is None.  With ``clf`` (and ``clf_args = (perm,
+    step, total_step, lambd)``) the ``--use_clf`` branch runs between the losses' backward
+    and the clip, and its ``(dloss, cross-lingual chunks, chunks)`` is appended."""
     output = model(*(batch[2:12]), accents=batch[13], speaker_meta=batch[12])
     losses = Loss(batch[:12], output[:-2])
-    losses[0].backward()
+    (losses[0] / grad_acc_step if grad_acc_step != 1 else losses[0]).backward()
     eloss = eLoss(output[-1], output[-2])
-    (-eloss).backward()
+    (-eloss / grad_acc_step if grad_acc_step != 1 else -eloss).backward()
     clf_out = clf_backward(model, batch, clf, *clf_args) if clf is not None else None
-    if grad_sync is not None:
-        grad_sync()
-    gnorm = optimizer.clip_grad_norm_(grad_clip_thresh)
-    optimizer.step_and_update_lr()
-    optimizer.zero_grad()
+    gnorm = None
+    if update:
+        if grad_sync is not None:
+            grad_sync()
+        gnorm = optimizer.clip_grad_norm_(grad_clip_thresh)
+        optimizer.step_and_update_lr()
+        optimizer.zero_grad()
     if clf_out is not None:
         return losses, eloss, gnorm, output, clf_out
     return losses, eloss, gnorm, output
@@ -143,6 +149,12 @@ class Trainer:
         self.eLoss = SpeakerMetaEncLoss(preprocess_config, model_config)
         self.opt = ScheduledOptim(model, train_config, model_config, current_step)
         self.clip = train_config["optimizer"]["grad_clip_thresh"]
+        # train.py:108,112: the batch counter starts at restore_step + 1; the optimiser steps
+        # on the batches where it is a multiple of grad_acc_step
+        self.grad_acc = int(train_config["optimizer"].get("grad_acc_step", 1))
+        if self.grad_acc < 1:
+            raise ValueError("grad_acc_step must be >= 1")
+        self.batch_step = int(current_step) + 1
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
         self.buckets = None
@@ -191,19 +203,28 @@ class Trainer:
         return out
 
     def step(self, batch, clf=None, clf_args=None):
-        """One step; ``clf=(SpeechEmbedder, GE2ELoss)`` with ``clf_args=(perm, step,
-        total_step, lambd)`` adds the ``--use_clf`` branch (eager, single process)."""
+        """One batch (``train.py:137-206``); the optimiser steps when the batch counter is a
+        multiple of ``grad_acc_step`` (the returned grad norm is None on the other batches).
+        ``clf=(SpeechEmbedder, GE2ELoss)`` with ``clf_args=(perm, step, total_step, lambd)``
+        adds the ``--use_clf`` branch (eager, single process)."""
+        update = self.batch_step % self.grad_acc == 0
+        self.batch_step += 1
+        acc = dict(grad_acc_step=self.grad_acc, update=update)
         if clf is not None:
             if self.world > 1:
                 raise NotImplementedError("use_clf with data parallelism")
             return train_step(self.model, self.opt, self.Loss, self.eLoss, batch, self.clip,
-                              clf=clf, clf_args=clf_args)
-        if self.graph_mode and self.world == 1:
+                              clf=clf, clf_args=clf_args, **acc)
+        if self.graph_mode and self.world == 1 and self.grad_acc == 1:
             return self._graph_step(batch)
         if self.world > 1:
             glob = self._global_denominators(batch)
             self.Loss.denoms = glob[0:2]
             self.eLoss.denom = glob[2:3]
+            # accumulated micro-batches are summed locally; the buckets all-reduce the
+            # accumulated buffer during the backward of the batch that steps (all-reduce is
+            # linear, so this equals all-reducing every micro-batch)
+            self.model._hooks["grad"] = self.buckets.ready if update else None
             return train_step(self.model, self.opt, self.Loss, self.eLoss, batch, self.clip,
-                              grad_sync=self.buckets.finish)
-        return train_step(self.model, self.opt, self.Loss, self.eLoss, batch, self.clip)
+                              grad_sync=self.buckets.finish, **acc)
+        return train_step(self.model, self.opt, self.Loss, self.eLoss, batch, self.clip, **acc)

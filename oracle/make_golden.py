@@ -208,9 +208,11 @@ def g4(fs2, loss_mod, mods, layers):
     np.savez_compressed(os.path.join(OUT, "g4_ops.npz"), **res)
 
 
-def g5(fs2, loss_mod, B, Ts, steps=3, seed=0):
+def g5(fs2, loss_mod, B, Ts, steps=3, seed=0, config="JVS-VCTK", name=None, curve_only=False):
+    """3-step trajectories (``g5_step_*``); with ``curve_only`` a long run that stores only
+    the per-step scalars (``g11_curve_*``: the loss curve the bf16 path is checked against)."""
     from model.optimizer import ScheduledOptim
-    pp, mc, tc, path = PKG.config.load_configs("JVS-VCTK")
+    pp, mc, tc, path = PKG.config.load_configs(config)
     torch.manual_seed(0)
     model = fs2.FastSpeech2(pp, mc, path)
     seeded(model)
@@ -218,9 +220,26 @@ def g5(fs2, loss_mod, B, Ts, steps=3, seed=0):
     opt = ScheduledOptim(model, tc, mc, 0)
     Loss = loss_mod.FastSpeech2Loss(pp, mc)
     eLoss = loss_mod.SpeakerMetaEncLoss(pp, mc)
-    res = {"B": np.array(B), "Ts": np.array(Ts), "seed": np.array(seed)}
-    batch = PKG.data.to_device(PKG.data.syn_batch(B, Ts, seed=seed), "cpu")
+    res = {"B": np.array(B), "Ts": np.array(Ts), "seed": np.array(seed),
+           "config": np.array(config)}
+    batch = PKG.data.to_device(PKG.data.syn_batch_for(config, B, Ts, seed=seed), "cpu")
     res["pos_enc_probe"] = model.encoder.position_enc.detach()[0, ::97, ::31].numpy()
+    if curve_only:
+        curve = []
+        for s in range(steps):
+            output = model(*(batch[2:12]), accents=batch[13], speaker_meta=batch[12])
+            losses = Loss(batch[:12], output[:-2])
+            losses[0].backward()
+            eloss = eLoss(output[-1], output[-2])
+            (-eloss).backward()
+            gn = torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+            opt.step_and_update_lr()
+            opt.zero_grad()
+            curve.append([float(l) for l in losses] + [float(eloss), float(gn)])
+        res["curve"] = np.array(curve)
+        np.savez_compressed(os.path.join(OUT, name), **res)
+        print(name, res["curve"][0], res["curve"][-1])
+        return
     for s in range(steps):
         output = model(*(batch[2:12]), accents=batch[13], speaker_meta=batch[12])
         losses = Loss(batch[:12], output[:-2])
@@ -242,8 +261,9 @@ def g5(fs2, loss_mod, B, Ts, steps=3, seed=0):
         res[f"s{s}.mel_lens"] = output[9].numpy()
     res["final_probe"] = torch.cat([p.detach().reshape(-1)[:64] for p in model.parameters()
                                     if p.requires_grad]).numpy()
-    np.savez_compressed(os.path.join(OUT, f"g5_step_b{B}_t{Ts}.npz"), **res)
-    print("g5", B, Ts, res["s0.losses"], res["s2.losses"])
+    name = name or f"g5_step_b{B}_t{Ts}.npz"
+    np.savez_compressed(os.path.join(OUT, name), **res)
+    print(name, res["s0.losses"], res["s2.losses"])
 
 
 def infer_overrides(model_prefix=""):
@@ -566,6 +586,9 @@ def main():
     if "--only-g7" in sys.argv:
         g7(fs2)
         return
+    if "--only-r2" in sys.argv:  # round-2 fixtures: JSUT (BASELINE config 1), loss curve
+        r2_fixtures(fs2, loss_mod)
+        return
     g1_g2_g3(mods)
     g4(fs2, loss_mod, mods, layers)
     g6(fs2, loss_mod)
@@ -576,6 +599,15 @@ def main():
     sizes = [(3, 16), (8, 32)] + ([(48, 128)] if "--full" in sys.argv else [])
     for B, Ts in sizes:
         g5(fs2, loss_mod, B, Ts)
+    r2_fixtures(fs2, loss_mod)
+
+
+def r2_fixtures(fs2, loss_mod):
+    """g5_step_jsut_b4_t128: BASELINE config 1 (config/JSUT/model.yaml: K = 1 GMM component,
+    1 speaker, gender-only metadata of width 2) at batch 4, 128 phonemes x 512 frames, 3 steps.
+    g11_curve_b8_t32: 100 steps at SYN-8x32 (per-step losses, eloss, grad norm)."""
+    g5(fs2, loss_mod, 4, 128, config="JSUT", name="g5_step_jsut_b4_t128.npz")
+    g5(fs2, loss_mod, 8, 32, steps=100, name="g11_curve_b8_t32.npz", curve_only=True)
 
 
 if __name__ == "__main__":

@@ -105,3 +105,47 @@ def test_optimizer_lr_schedule_matches_reference_formula():
         want = 256 ** -0.5 * min(s ** -0.5, 4000 ** -1.5 * s) * (0.3 if s > 300000 else 1.0)
         assert abs(lr - want) < 1e-15
     assert abs(fs2_cpu.lr_at(1) - 2.4705e-7) < 1e-10
+
+
+def _bench(*argv, env=None):
+    import json
+    import os
+    import subprocess
+    import sys
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    e.update(env or {})
+    r = subprocess.run([sys.executable, f"{REPO}/bench.py", *argv], capture_output=True,
+                       text=True, timeout=300, env=e)
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    return r.returncode, (json.loads(lines[-1]) if lines else None), r.stderr
+
+
+def test_bench_launcher_starts_n_ranks():
+    """bench.py --gpus 2 with no launcher spawns two rank processes (gloo probe on CPU)."""
+    rc, out, err = _bench("--gpus", "2", "--launch-check")
+    assert rc == 0, err
+    assert out == {"world": 2, "ranks_seen": 2, "parallelism": "dp2"}
+
+
+def test_bench_rejects_world_size_mismatch():
+    rc, out, err = _bench("--gpus", "4", "--launch-check",
+                          env={"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert rc == 2 and out is None and "WORLD_SIZE=2" in err
+
+
+def test_jsut_config_shapes():
+    """BASELINE config 1 (config/JSUT/model.yaml:42-43): one speaker, one GMM component,
+    gender-only metadata (width 2); the synthetic batch follows the config."""
+    pp, mc, tc, path = PKG.config.load_configs("JSUT")
+    ours = M.FastSpeech2(pp, mc, path, device="cpu")
+    sd = ours.state_dict()
+    assert sd["speaker_emb.weight"].shape == (1, 256)
+    assert sd["speaker_enc.pi_linear.0.weight"].shape == (1, 2)
+    assert sd["speaker_enc.sigma_linear.0.weight"].shape == (256, 2)
+    ref, _ = fs2_cpu.build("JSUT", seeded=False)
+    assert {k: tuple(v.shape) for k, v in ref.state_dict().items()} == \
+        {k: tuple(v.shape) for k, v in sd.items()}
+    b = PKG.data.syn_batch_for("JSUT", 4, 128, seed=0)
+    assert b[12].shape == (4, 2) and np.all(b[2] == 0) and np.all(b[12].sum(1) == 1)

@@ -144,16 +144,21 @@ def test_g4_gmm():
         np.testing.assert_allclose(p.grad.numpy(), g[f"gmm.{name}.grad"], rtol=1e-5, atol=1e-7)
 
 
-@pytest.mark.parametrize("B,Ts", [(3, 16), (8, 32)])
-def test_g5_train_trajectory(no_dropout, B, Ts):
-    g = load_golden(f"g5_step_b{B}_t{Ts}.npz")
+@pytest.mark.parametrize("B,Ts,config", [(3, 16, "JVS-VCTK"), (8, 32, "JVS-VCTK"),
+                                         (4, 128, "JSUT")])
+def test_g5_train_trajectory(no_dropout, B, Ts, config):
+    """3 reference training steps; JSUT is BASELINE config 1 (K = 1 GMM component, one
+    speaker, gender-only metadata)."""
+    name = f"g5_step_b{B}_t{Ts}.npz" if config == "JVS-VCTK" else f"g5_step_jsut_b{B}_t{Ts}.npz"
+    g = load_golden(name)
+    assert str(g["config"]) == config if "config" in g.files else config == "JVS-VCTK"
     torch.manual_seed(0)
-    m, _ = fs2_cpu.build("JVS-VCTK")
+    m, _ = fs2_cpu.build(config)
     m.train()
     np.testing.assert_array_equal(m.encoder.position_enc.detach()[0, ::97, ::31].numpy(),
                                   g["pos_enc_probe"])
     opt = fs2_cpu.make_opt(m)
-    batch = PKG.data.to_device(PKG.data.syn_batch(B, Ts, seed=int(g["seed"])), "cpu")
+    batch = PKG.data.to_device(PKG.data.syn_batch_for(config, B, Ts, seed=int(g["seed"])), "cpu")
     for s in range(3):
         losses, eloss, gn, out = fs2_cpu.train_step(m, opt, batch)
         np.testing.assert_allclose(losses, g[f"s{s}.losses"], rtol=1e-5)
@@ -164,6 +169,20 @@ def test_g5_train_trajectory(no_dropout, B, Ts):
         o, po = out[0].detach().double(), out[1].detach().double()
         np.testing.assert_allclose([o.sum(), o.abs().sum(), po.sum(), po.abs().sum()],
                                    g[f"s{s}.out_sum"], rtol=1e-4)
+
+
+def test_g11_loss_curve_oracle(no_dropout):
+    """The first 20 of the reference's 100 steps at SYN-8x32 (losses, eloss, grad norm)."""
+    g = load_golden("g11_curve_b8_t32.npz")
+    torch.manual_seed(0)
+    m, _ = fs2_cpu.build("JVS-VCTK")
+    m.train()
+    opt = fs2_cpu.make_opt(m)
+    batch = PKG.data.to_device(PKG.data.syn_batch(8, 32, seed=int(g["seed"])), "cpu")
+    for s in range(20):
+        losses, eloss, gn, _ = fs2_cpu.train_step(m, opt, batch)
+        np.testing.assert_allclose(losses + [eloss, gn], g["curve"][s], rtol=2e-4,
+                                   err_msg=f"step {s}")
 
 
 def _g6_model(g):

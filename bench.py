@@ -15,10 +15,11 @@ value = valid mel frames of all ranks per second (max-over-ranks time, weak scal
 The JSON line also carries
   roofline      the DOMINANT launch set of the step by in-step time: HIP events (on the
                 stream each launch runs on, the weight-gradient side stream included) around
-                every GEMM / conv / attention launch of the timed steps, grouped by op class;
-                achieved = the class's algorithmic FLOP (valid frames) per step / its
-                launches' summed duration per step; ``classes`` lists every class;
-                ``traffic``: PMC bytes per launch of the class's decoder-shaped launches;
+                every GEMM / conv / attention launch of the last 3 warm-up steps, grouped by
+                op class (``classes``); the class with the most time is then timed alone over
+                the timed steps: achieved = its algorithmic FLOP (valid frames) per step / its
+                launches' summed duration per step; ``traffic``: PMC bytes per launch of the
+                class's decoder-shaped launches;
   fft_block     one decoder FFT block fwd+bwd (north_star's target): HIP events around the
                 decoder's forward and backward (its weight-gradient stream joined) in extra
                 steps after the timed region, / 6 layers, against SURVEY §8d's 463.9 GFLOP
@@ -103,10 +104,16 @@ class ClassTimer:
         self.K = K
         self.valid_by_T = valid_by_T  # seq_len -> valid rows of the batch
         self.sq_by_T = sq_by_T        # seq_len -> sum of squared lengths (attention)
-        self.on = False
+        self.mode = None               # None: off; "all": every class; else one class name
         self.rec = []                  # (class, start, end, flop)
         self._streams = {}
+        self._pool, self._next = [], 0  # events created up front (creation is host-expensive)
         self._orig = {n: getattr(K, n) for n in ("conv_gemm", "conv_wgrad", "attn_fwd", "attn_bwd")}
+
+    def reset(self, mode, n_events):
+        self.mode, self.rec, self._next = mode, [], 0
+        while len(self._pool) < n_events:
+            self._pool.append(torch.cuda.Event(enable_timing=True))
 
     def _stream(self, handle):
         if handle is None:
@@ -117,10 +124,12 @@ class ClassTimer:
         return s
 
     def _timed(self, cls, flop, stream_handle, fn, *a, **kw):
-        if not self.on:
+        if self.mode is None or (self.mode != "all" and self.mode != cls) or \
+                self._next + 2 > len(self._pool):
             return fn(*a, **kw)
         st = self._stream(stream_handle)
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s, e = self._pool[self._next], self._pool[self._next + 1]
+        self._next += 2
         s.record(st)
         y = fn(*a, **kw)
         e.record(st)
@@ -425,12 +434,20 @@ def main():
         timer.install()
 
     kw = (lambda: clf_kw()) if args.use_clf else (lambda: {})
-    for _ in range(max(args.warmup, 2 if use_graph else 0)):  # graph: step 1 captures
+    n_warm = max(args.warmup, 2 if use_graph else 0)  # graph: step 1 captures
+    survey = 3 if (not args.no_roofline and not use_graph and n_warm >= 4) else 0
+    for i in range(n_warm):
+        if survey and i == n_warm - survey:
+            timer.reset("all", 600 * survey)  # class survey: the last warm-up steps
         trainer.step(batch, **kw())
     torch.cuda.synchronize()
+    classes, dom = None, None
+    if survey:
+        classes = timer.table(survey, PEAK[args.dtype][0])
+        dom = max(classes, key=lambda c: classes[c]["ms_per_step"])
+        timer.reset(dom, 200 * args.steps)  # timed region: the dominant class only
     if world > 1:
         dist.barrier()
-    timer.on = True
     t0 = time.perf_counter()
     for _ in range(args.steps):
         losses = trainer.step(batch, **kw())[0]
@@ -438,7 +455,8 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    timer.on = False
+    timed = timer.table(args.steps, PEAK[args.dtype][0]) if dom else None
+    timer.mode = None
     t = torch.tensor([dt], device=dev, dtype=torch.float64)
     fr = torch.tensor([frames_local], device=dev, dtype=torch.float64)
     if world > 1:
@@ -451,15 +469,14 @@ def main():
 
     out = None
     if rank == 0:
-        roof, classes = None, None
-        if timer.rec:
-            classes = timer.table(args.steps, peak)
-            dom = max(classes, key=lambda c: classes[c]["ms_per_step"])
-            c = classes[dom]
+        roof = None
+        if timed and dom in timed:
+            c = timed[dom]
             roof = {"bound": "mfma", "achieved": c["tflops"], "peak": peak, "unit": unit,
                     "frac": c["frac"], "traffic": None,
                     "kernel": f"{dom}: the step's dominant launch set by in-step time "
-                              f"({c['launches_per_step']} launches/step, {c['ms_per_step']} ms/step)",
+                              f"({c['launches_per_step']} launches/step, {c['ms_per_step']} ms/step "
+                              "in the timed steps)",
                     "flop_basis": "2 * valid frames * C_out * C_in * taps per launch (kernels "
                                   "skip all-padding row tiles)",
                     "per_launch_flop": round(c["gflop_per_step"] * 1e9 / c["launches_per_step"]),
@@ -474,6 +491,9 @@ def main():
                 else:
                     roof["traffic_note"] = detail
             roof["classes"] = classes
+            roof["classes_basis"] = ("every class timed in the last 3 warm-up steps (events on "
+                                     "~170 launches make those steps host-bound); the dominant "
+                                     "class alone is timed over the timed steps")
         step_roof = {"gflop_padded": STEP_GFLOP_PADDED, "achieved": None, "frac": None}
         if args.batch == 48 and args.src_len == 128 and not args.use_clf:
             ach = STEP_GFLOP_PADDED / (ms_step / 1e3) / 1e3
@@ -525,7 +545,6 @@ def main():
 
     # the reference's precision (fp32), N = 1, a short companion measurement
     if world == 1 and args.dtype == "bf16" and not args.no_f32 and not args.use_clf:
-        timer.on = False
         del trainer, model
         torch.cuda.empty_cache()
         m32, tr32, _ = build_trainer(M, TR, "f32", dev, rank)

@@ -126,7 +126,9 @@ class ScheduledOptim:
 
     def _update_learning_rate(self):
         self.current_step += 1
-        lr = self.init_lr * self._get_lr_scale()
+        # a Python float (the reference's is np.float64): checkpoints then load with
+        # torch.load(..., weights_only=True)
+        lr = float(self.init_lr * self._get_lr_scale())
         for g in self._optimizer.param_groups:
             g["lr"] = lr
 

@@ -605,9 +605,14 @@ def main():
 def r2_fixtures(fs2, loss_mod):
     """g5_step_jsut_b4_t128: BASELINE config 1 (config/JSUT/model.yaml: K = 1 GMM component,
     1 speaker, gender-only metadata of width 2) at batch 4, 128 phonemes x 512 frames, 3 steps.
-    g11_curve_b8_t32: 100 steps at SYN-8x32 (per-step losses, eloss, grad norm)."""
+    g11_curve_b8_t32: 100 steps at SYN-8x32 (per-step losses, eloss, grad norm).
+    g5_step_b2_t264_trunc: 3 steps with 1,056 mel frames (decoder truncation to 1,000)."""
     g5(fs2, loss_mod, 4, 128, config="JSUT", name="g5_step_jsut_b4_t128.npz")
     g5(fs2, loss_mod, 8, 32, steps=100, name="g11_curve_b8_t32.npz", curve_only=True)
+    # training-mode decoder truncation (transformer/Models.py:166-174): 4 x 264 = 1,056 frames
+    # > max_seq_len 1,000, so the decoder, its mask and the mel loss see 1,000 frames while
+    # mel_lens stay uncropped
+    g5(fs2, loss_mod, 2, 264, name="g5_step_b2_t264_trunc.npz")
 
 
 if __name__ == "__main__":

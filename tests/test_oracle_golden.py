@@ -144,12 +144,14 @@ def test_g4_gmm():
         np.testing.assert_allclose(p.grad.numpy(), g[f"gmm.{name}.grad"], rtol=1e-5, atol=1e-7)
 
 
-@pytest.mark.parametrize("B,Ts,config", [(3, 16, "JVS-VCTK"), (8, 32, "JVS-VCTK"),
-                                         (4, 128, "JSUT")])
-def test_g5_train_trajectory(no_dropout, B, Ts, config):
+@pytest.mark.parametrize("B,Ts,config,name", [
+    (3, 16, "JVS-VCTK", "g5_step_b3_t16.npz"), (8, 32, "JVS-VCTK", "g5_step_b8_t32.npz"),
+    (4, 128, "JSUT", "g5_step_jsut_b4_t128.npz"),
+    (2, 264, "JVS-VCTK", "g5_step_b2_t264_trunc.npz")])
+def test_g5_train_trajectory(no_dropout, B, Ts, config, name):
     """3 reference training steps; JSUT is BASELINE config 1 (K = 1 GMM component, one
-    speaker, gender-only metadata)."""
-    name = f"g5_step_b{B}_t{Ts}.npz" if config == "JVS-VCTK" else f"g5_step_jsut_b{B}_t{Ts}.npz"
+    speaker, gender-only metadata); t264 has 1,056 mel frames (decoder truncation to 1,000,
+    transformer/Models.py:166-174)."""
     g = load_golden(name)
     assert str(g["config"]) == config if "config" in g.files else config == "JVS-VCTK"
     torch.manual_seed(0)

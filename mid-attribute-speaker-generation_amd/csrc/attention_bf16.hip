@@ -1,7 +1,12 @@
 // bf16 fused attention (d_head = 128) on v_mfma_f32_16x16x32_bf16, fp32 softmax/accumulate.
 //
 // Same decomposition as attention.hip (transposed scores: each lane owns one query column
-// in the forward / dQ kernels, one key column in the dK/dV kernel).  The second product of
+// in the forward / dQ kernels, one key column in the dK/dV kernel), with every wave owning
+// TWO 16-row groups (32 queries, or 32 keys in dK/dV): each K/V/Q/dO fragment read from LDS
+// feeds two MFMAs, halving the LDS traffic per FLOP, and a workgroup of NW waves covers
+// 32 NW rows, so each K/V (Q/dO) tile is staged once per 32 NW rows.  The dQ kernel also
+// forms delta = rowsum(dO * O) for its queries (no separate launch) and publishes it for the
+// dK/dV kernel that follows on the stream.  The second product of
 // each kernel contracts over keys (or queries), which sit in the *rows* of the LDS tiles:
 // its A operand is read with ds_read_b64_tr_b16 (4 consecutive rows of one column per lane),
 // and its B operand is the fp32 score accumulator packed to bf16 in place — the MFMA
@@ -32,24 +37,42 @@ FS2_DEV u16 f2bf(float f) {
   return *reinterpret_cast<u16*>(&b);
 }
 
-// register-staged copy of a 64 x 128 tile: load into 4 x 16 B per thread (issued before the
-// MFMA work on the previous tile, so the global latency overlaps it), store after a barrier
-FS2_DEV void load_regs(uint4 (&r)[4], const u16* base, int64_t ld, int r0, int nrows, int tid) {
+// register-staged copy of a 64 x 128 tile by NT threads: 1024 16-B pieces, PER = 1024 / NT
+// per thread (issued before the MFMA work on the previous tile, so the global latency
+// overlaps it), stored to LDS after a barrier
+template <int NT>
+FS2_DEV void load_regs(uint4 (&r)[1024 / NT], const u16* base, int64_t ld, int r0, int nrows, int tid) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int c = tid + i * 256, row = c >> 4, col = (c & 15) * 8;
+  for (int i = 0; i < 1024 / NT; ++i) {
+    const int c = tid + i * NT, row = c >> 4, col = (c & 15) * 8;
     const int rr = r0 + row;
     r[i] = rr < nrows ? *reinterpret_cast<const uint4*>(base + (int64_t)rr * ld + col)
                       : make_uint4(0u, 0u, 0u, 0u);
   }
 }
-template <int LDS_LD>
-FS2_DEV void store_regs(u16* dst, const uint4 (&r)[4], int tid) {
+template <int LDS_LD, int NT>
+FS2_DEV void store_regs(u16* dst, const uint4 (&r)[1024 / NT], int tid) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int c = tid + i * 256, row = c >> 4, col = (c & 15) * 8;
+  for (int i = 0; i < 1024 / NT; ++i) {
+    const int c = tid + i * NT, row = c >> 4, col = (c & 15) * 8;
     *reinterpret_cast<uint4*>(&dst[row * LDS_LD + col]) = r[i];
   }
+}
+
+// the 4 x 16-B fragments of LDS row `row` (d = 32c + 8g .. +7)
+template <int LD>
+FS2_DEV void row_frags(bf16x8 (&f)[4], const u16* S, int row, int g) {
+  const u16* p = S + row * LD + 8 * g;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) f[c] = *reinterpret_cast<const bf16x8*>(p + 32 * c);
+}
+
+// sum over d = 128 of A-row fragments x B fragments (4 chained MFMAs)
+FS2_DEV f32x4 chain4(const bf16x8 (&a)[4], const bf16x8 (&b)[4]) {
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int c = 0; c < 4; ++c) acc = MFMA_BF16(a[c], b[c], acc);
+  return acc;
 }
 
 // per-lane row fragment: d = 32c + 8g .. +7 for c < 4
@@ -91,6 +114,19 @@ FS2_DEV void accum_t(f32x4 (&acc)[8], const u16* S, int rb, const bf16x8& w, int
   for (int ds = 0; ds < 8; ++ds) acc[ds] = MFMA_BF16(tr_frag<LD>(S, rb, 16 * ds, g, q, p), w, acc[ds]);
 }
 
+// acc[j][ds] += sum over 32 rows (rb..rb+31) of T^T[d][row] * w[j][row] for two B operands
+// (8 d-subtiles): each transposed fragment read from LDS feeds two MFMAs
+template <int LD>
+FS2_DEV void accum_t2(f32x4 (&acc)[2][8], const u16* S, int rb, const bf16x8& w0, const bf16x8& w1,
+                      int g, int q, int p) {
+#pragma unroll
+  for (int ds = 0; ds < 8; ++ds) {
+    const bf16x8 a = tr_frag<LD>(S, rb, 16 * ds, g, q, p);
+    acc[0][ds] = MFMA_BF16(a, w0, acc[0][ds]);
+    acc[1][ds] = MFMA_BF16(a, w1, acc[1][ds]);
+  }
+}
+
 FS2_DEV void store4_bf16(u16* p, const f32x4& v) {
   uint2 w;
   w.x = (uint32_t)f2bf(v.x) | ((uint32_t)f2bf(v.y) << 16);
@@ -99,7 +135,10 @@ FS2_DEV void store4_bf16(u16* p, const f32x4& v) {
 }
 }  // namespace
 
-__global__ __launch_bounds__(256) void attn_fwd_bf16(const u16* __restrict__ qkv, u16* __restrict__ o,
+
+// ---- one 16-row group per wave, 64 rows per 4-wave workgroup (the T = 128 encoder shapes:
+// twice the workgroups of the two-group kernels below, at 4 waves per SIMD)
+__global__ __launch_bounds__(256) void attn_fwd_bf16_g1(const u16* __restrict__ qkv, u16* __restrict__ o,
                                                      float* __restrict__ lse,
                                                      const int64_t* __restrict__ lens, int T, int H,
                                                      float scale) {
@@ -135,16 +174,16 @@ __global__ __launch_bounds__(256) void attn_fwd_bf16(const u16* __restrict__ qkv
   const u16* kbase = base + (int64_t)H * DH + h * DH;
   const u16* vbase = base + 2LL * H * DH + h * DH;
   uint4 kr[4], vr[4];
-  load_regs(kr, kbase, ld, 0, T, tid);
-  load_regs(vr, vbase, ld, 0, T, tid);
+  load_regs<256>(kr, kbase, ld, 0, T, tid);
+  load_regs<256>(vr, vbase, ld, 0, T, tid);
   for (int kt = 0; kt < nkt; ++kt) {
     __syncthreads();
-    store_regs<LDR>(Ks, kr, tid);
-    store_regs<LDT>(Vs, vr, tid);
+    store_regs<LDR, 256>(Ks, kr, tid);
+    store_regs<LDT, 256>(Vs, vr, tid);
     __syncthreads();
     if (kt + 1 < nkt) {  // next tile's loads in flight during this tile's MFMAs
-      load_regs(kr, kbase, ld, (kt + 1) * QB, T, tid);
-      load_regs(vr, vbase, ld, (kt + 1) * QB, T, tid);
+      load_regs<256>(kr, kbase, ld, (kt + 1) * QB, T, tid);
+      load_regs<256>(vr, vbase, ld, (kt + 1) * QB, T, tid);
     }
     f32x4 s[4];
     float mt = -INFINITY;
@@ -187,7 +226,7 @@ __global__ __launch_bounds__(256) void attn_fwd_bf16(const u16* __restrict__ qkv
   }
 }
 
-__global__ void attn_bwd_delta_bf16(const u16* __restrict__ o, const u16* __restrict__ d_o,
+__global__ void attn_bwd_delta_bf16_g1(const u16* __restrict__ o, const u16* __restrict__ d_o,
                                     float* __restrict__ delta, int64_t rows, int T, int H) {
   const int64_t w = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
@@ -203,7 +242,7 @@ __global__ void attn_bwd_delta_bf16(const u16* __restrict__ o, const u16* __rest
   }
 }
 
-__global__ __launch_bounds__(256) void attn_bwd_dq_bf16(const u16* __restrict__ qkv,
+__global__ __launch_bounds__(256) void attn_bwd_dq_bf16_g1(const u16* __restrict__ qkv,
                                                         const u16* __restrict__ d_o,
                                                         const float* __restrict__ lse,
                                                         const float* __restrict__ delta,
@@ -245,16 +284,16 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_bf16(const u16* __restrict__ 
   const u16* kbase = base + (int64_t)H * DH + h * DH;
   const u16* vbase = base + 2LL * H * DH + h * DH;
   uint4 kr[4], vr[4];
-  load_regs(kr, kbase, ld, 0, T, tid);
-  load_regs(vr, vbase, ld, 0, T, tid);
+  load_regs<256>(kr, kbase, ld, 0, T, tid);
+  load_regs<256>(vr, vbase, ld, 0, T, tid);
   for (int kt = 0; kt < nkt; ++kt) {
     __syncthreads();
-    store_regs<LDR>(Ks, kr, tid);
-    store_regs<LDR>(Vs, vr, tid);
+    store_regs<LDR, 256>(Ks, kr, tid);
+    store_regs<LDR, 256>(Vs, vr, tid);
     __syncthreads();
     if (kt + 1 < nkt) {
-      load_regs(kr, kbase, ld, (kt + 1) * QB, T, tid);
-      load_regs(vr, vbase, ld, (kt + 1) * QB, T, tid);
+      load_regs<256>(kr, kbase, ld, (kt + 1) * QB, T, tid);
+      load_regs<256>(vr, vbase, ld, (kt + 1) * QB, T, tid);
     }
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
@@ -280,7 +319,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_bf16(const u16* __restrict__ 
   }
 }
 
-__global__ __launch_bounds__(256) void attn_bwd_dkdv_bf16(const u16* __restrict__ qkv,
+__global__ __launch_bounds__(256) void attn_bwd_dkdv_bf16_g1(const u16* __restrict__ qkv,
                                                           const u16* __restrict__ d_o,
                                                           const float* __restrict__ lse,
                                                           const float* __restrict__ delta,
@@ -327,8 +366,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_bf16(const u16* __restrict_
   uint4 qr[4], dr[4];
   float lr_ = 0.f, dl_ = 0.f;
   auto load_q = [&](int qt) {
-    load_regs(qr, qbase, ld, qt * QB, T, tid);
-    load_regs(dr, dobase, ldo, qt * QB, T, tid);
+    load_regs<256>(qr, qbase, ld, qt * QB, T, tid);
+    load_regs<256>(dr, dobase, ldo, qt * QB, T, tid);
     if (tid < QB) {
       const int qq = qt * QB + tid;
       lr_ = qq < T ? lse[(int64_t)bh * T + qq] : 0.f;
@@ -338,8 +377,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_bf16(const u16* __restrict_
   load_q(0);
   for (int qt = 0; qt < nqt; ++qt) {
     __syncthreads();
-    store_regs<LDR>(Qs, qr, tid);
-    store_regs<LDR>(Ds, dr, tid);
+    store_regs<LDR, 256>(Qs, qr, tid);
+    store_regs<LDR, 256>(Ds, dr, tid);
     if (tid < QB) {
       lse_s[tid] = lr_;
       del_s[tid] = dl_;
@@ -375,25 +414,376 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_bf16(const u16* __restrict_
   }
 }
 
+// ---- two 16-row groups per wave
+template <int NW>
+__global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_bf16(const u16* __restrict__ qkv, u16* __restrict__ o,
+                                                         float* __restrict__ lse,
+                                                         const int64_t* __restrict__ lens, int T, int H,
+                                                         float scale) {
+  constexpr int NT = NW * 64, QBLK = NW * 32, PER = 1024 / NT;
+  __shared__ __attribute__((aligned(16))) u16 Ks[QB * LDR];
+  __shared__ __attribute__((aligned(16))) u16 Vs[QB * LDT];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, r16 = lane & 15;
+  const int q4 = r16 >> 2, p4 = r16 & 3;
+  const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
+  const int L = (int)min(lens[b], (int64_t)T);
+  const int64_t ld = 3LL * H * DH, ldo = (int64_t)H * DH;
+  const int q0 = blockIdx.x * QBLK;
+  const u16* base = qkv + (int64_t)b * T * ld;
+  u16* obase = o + (int64_t)b * T * ldo + h * DH;
+
+  if (q0 >= L) {  // fully padded query block: outputs are masked downstream; write zeros
+    for (int e = tid; e < QBLK * DH / 8; e += NT) {
+      const int row = e / (DH / 8), col = (e % (DH / 8)) * 8, q = q0 + row;
+      if (q < T) *reinterpret_cast<uint4*>(obase + (int64_t)q * ldo + col) = make_uint4(0u, 0u, 0u, 0u);
+    }
+    if (tid < QBLK && q0 + tid < T) lse[(int64_t)bh * T + q0 + tid] = 0.f;
+    return;
+  }
+  bf16x8 qf[2][4];
+#pragma unroll
+  for (int gq = 0; gq < 2; ++gq) {
+    const int q = q0 + wave * 32 + gq * 16 + r16;
+    load_frag(qf[gq], base + (int64_t)min(q, T - 1) * ld + h * DH, g);
+  }
+  float m_run[2] = {-INFINITY, -INFINITY}, l_run[2] = {0.f, 0.f};
+  f32x4 oacc[2][8];
+#pragma unroll
+  for (int gq = 0; gq < 2; ++gq)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) oacc[gq][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nkt = (L + QB - 1) / QB;
+  const u16* kbase = base + (int64_t)H * DH + h * DH;
+  const u16* vbase = base + 2LL * H * DH + h * DH;
+  uint4 kr[PER], vr[PER];
+  load_regs<NT>(kr, kbase, ld, 0, T, tid);
+  load_regs<NT>(vr, vbase, ld, 0, T, tid);
+  for (int kt = 0; kt < nkt; ++kt) {
+    __syncthreads();
+    store_regs<LDR, NT>(Ks, kr, tid);
+    store_regs<LDT, NT>(Vs, vr, tid);
+    __syncthreads();
+    if (kt + 1 < nkt) {  // next tile's loads in flight during this tile's MFMAs
+      load_regs<NT>(kr, kbase, ld, (kt + 1) * QB, T, tid);
+      load_regs<NT>(vr, vbase, ld, (kt + 1) * QB, T, tid);
+    }
+    f32x4 s[2][4];  // S^T[key 16 st + 4 g + r][query r16] per query group
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+      bf16x8 kfr[4];
+      row_frags<LDR>(kfr, Ks, 16 * st + r16, g);
+#pragma unroll
+      for (int gq = 0; gq < 2; ++gq) s[gq][st] = chain4(kfr, qf[gq]);
+    }
+#pragma unroll
+    for (int gq = 0; gq < 2; ++gq) {
+      float mt = -INFINITY;
+#pragma unroll
+      for (int st = 0; st < 4; ++st)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = kt * QB + 16 * st + 4 * g + r;
+          const float x = key < L ? s[gq][st][r] * scale : -INFINITY;
+          s[gq][st][r] = x;
+          mt = fmaxf(mt, x);
+        }
+      mt = group4_max(mt);
+      const float m_new = fmaxf(m_run[gq], mt);
+      const float alpha = __expf(m_run[gq] - m_new);
+      float ps = 0.f;
+#pragma unroll
+      for (int st = 0; st < 4; ++st)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float pv = __expf(s[gq][st][r] - m_new);
+          s[gq][st][r] = pv;
+          ps += pv;
+        }
+      ps = group4_sum(ps);
+      l_run[gq] = l_run[gq] * alpha + ps;
+      m_run[gq] = m_new;
+#pragma unroll
+      for (int ds = 0; ds < 8; ++ds) oacc[gq][ds] *= alpha;
+    }
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+      accum_t2<LDT>(oacc, Vs, 32 * c, pack8(s[0][2 * c], s[0][2 * c + 1]),
+                    pack8(s[1][2 * c], s[1][2 * c + 1]), g, q4, p4);
+  }
+#pragma unroll
+  for (int gq = 0; gq < 2; ++gq) {
+    const int q = q0 + wave * 32 + gq * 16 + r16;
+    if (q < T) {
+      const float inv = 1.f / l_run[gq];
+#pragma unroll
+      for (int ds = 0; ds < 8; ++ds)
+        store4_bf16(obase + (int64_t)q * ldo + 16 * ds + 4 * g, oacc[gq][ds] * inv);
+      if (g == 0) lse[(int64_t)bh * T + q] = m_run[gq] + __logf(l_run[gq]);
+    }
+  }
+}
+
+// dQ, plus delta[q] = sum_d dO[q, d] O[q, d] for the block's queries (written to `delta` for
+// the dK/dV kernel; padded queries get 0)
+template <int NW>
+__global__ __launch_bounds__(NW * 64, 8 / NW) void attn_bwd_dq_bf16(const u16* __restrict__ qkv,
+                                                            const u16* __restrict__ o,
+                                                            const u16* __restrict__ d_o,
+                                                            const float* __restrict__ lse,
+                                                            float* __restrict__ delta,
+                                                            u16* __restrict__ d_qkv,
+                                                            const int64_t* __restrict__ lens, int T,
+                                                            int H, float scale) {
+  constexpr int NT = NW * 64, QBLK = NW * 32, PER = 1024 / NT;
+  __shared__ __attribute__((aligned(16))) u16 Ks[QB * LDR];
+  __shared__ __attribute__((aligned(16))) u16 Vs[QB * LDR];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, r16 = lane & 15;
+  const int q4 = r16 >> 2, p4 = r16 & 3;
+  const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
+  const int L = (int)min(lens[b], (int64_t)T);
+  const int64_t ld = 3LL * H * DH, ldo = (int64_t)H * DH;
+  const int q0 = blockIdx.x * QBLK;
+  const u16* base = qkv + (int64_t)b * T * ld;
+  u16* dbase = d_qkv + (int64_t)b * T * ld + h * DH;
+
+  if (q0 >= L) {
+    for (int e = tid; e < QBLK * DH / 8; e += NT) {
+      const int row = e / (DH / 8), col = (e % (DH / 8)) * 8, qq = q0 + row;
+      if (qq < T) *reinterpret_cast<uint4*>(dbase + (int64_t)qq * ld + col) = make_uint4(0u, 0u, 0u, 0u);
+    }
+    if (tid < QBLK && q0 + tid < T) delta[(int64_t)bh * T + q0 + tid] = 0.f;
+    return;
+  }
+  bf16x8 qf[2][4], df[2][4];
+  float my_lse[2], my_delta[2];
+  bool qvalid[2];
+#pragma unroll
+  for (int gq = 0; gq < 2; ++gq) {
+    const int q = q0 + wave * 32 + gq * 16 + r16;
+    const int qc = min(q, T - 1);
+    load_frag(qf[gq], base + (int64_t)qc * ld + h * DH, g);
+    load_frag(df[gq], d_o + ((int64_t)b * T + qc) * ldo + h * DH, g);
+    bf16x8 of[4];
+    load_frag(of, o + ((int64_t)b * T + qc) * ldo + h * DH, g);
+    float part = 0.f;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) part += (float)of[c][e] * (float)df[gq][c][e];
+    qvalid[gq] = q < L;
+    my_delta[gq] = qvalid[gq] ? group4_sum(part) : 0.f;
+    my_lse[gq] = lse[(int64_t)bh * T + qc];
+    if (g == 0 && q < T) delta[(int64_t)bh * T + q] = my_delta[gq];
+  }
+
+  f32x4 dq[2][8];
+#pragma unroll
+  for (int gq = 0; gq < 2; ++gq)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dq[gq][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nkt = (L + QB - 1) / QB;
+  const u16* kbase = base + (int64_t)H * DH + h * DH;
+  const u16* vbase = base + 2LL * H * DH + h * DH;
+  uint4 kr[PER], vr[PER];
+  load_regs<NT>(kr, kbase, ld, 0, T, tid);
+  load_regs<NT>(vr, vbase, ld, 0, T, tid);
+  for (int kt = 0; kt < nkt; ++kt) {
+    __syncthreads();
+    store_regs<LDR, NT>(Ks, kr, tid);
+    store_regs<LDR, NT>(Vs, vr, tid);
+    __syncthreads();
+    if (kt + 1 < nkt) {
+      load_regs<NT>(kr, kbase, ld, (kt + 1) * QB, T, tid);
+      load_regs<NT>(vr, vbase, ld, (kt + 1) * QB, T, tid);
+    }
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      f32x4 dsv[2][2];  // [query group][half]
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        const int st = 2 * c + half;
+        bf16x8 kfr[4], vfr[4];
+        row_frags<LDR>(kfr, Ks, 16 * st + r16, g);
+        row_frags<LDR>(vfr, Vs, 16 * st + r16, g);
+#pragma unroll
+        for (int gq = 0; gq < 2; ++gq) {
+          const f32x4 s = chain4(kfr, qf[gq]);   // S^T[key][q]
+          const f32x4 dp = chain4(vfr, df[gq]);  // dP^T[key][q]
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int key = kt * QB + 16 * st + 4 * g + r;
+            const float pv = (key < L && qvalid[gq]) ? __expf(s[r] * scale - my_lse[gq]) : 0.f;
+            dsv[gq][half][r] = pv * (dp[r] - my_delta[gq]);
+          }
+        }
+      }
+      accum_t2<LDR>(dq, Ks, 32 * c, pack8(dsv[0][0], dsv[0][1]), pack8(dsv[1][0], dsv[1][1]), g,
+                    q4, p4);  // dQ^T += K^T dS^T
+    }
+  }
+#pragma unroll
+  for (int gq = 0; gq < 2; ++gq) {
+    const int q = q0 + wave * 32 + gq * 16 + r16;
+    if (q < T) {
+#pragma unroll
+      for (int ds = 0; ds < 8; ++ds)
+        store4_bf16(dbase + (int64_t)q * ld + 16 * ds + 4 * g, dq[gq][ds] * scale);
+    }
+  }
+}
+
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void attn_bwd_dkdv_bf16(const u16* __restrict__ qkv,
+                                                              const u16* __restrict__ d_o,
+                                                              const float* __restrict__ lse,
+                                                              const float* __restrict__ delta,
+                                                              u16* __restrict__ d_qkv,
+                                                              const int64_t* __restrict__ lens,
+                                                              int T, int H, float scale) {
+  constexpr int NT = NW * 64, KBLK = NW * 32, PER = 1024 / NT;
+  __shared__ __attribute__((aligned(16))) u16 Qs[QB * LDR];
+  __shared__ __attribute__((aligned(16))) u16 Ds[QB * LDR];
+  __shared__ float lse_s[QB], del_s[QB];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, r16 = lane & 15;
+  const int q4 = r16 >> 2, p4 = r16 & 3;
+  const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
+  const int L = (int)min(lens[b], (int64_t)T);
+  const int64_t ld = 3LL * H * DH, ldo = (int64_t)H * DH;
+  const int k0 = blockIdx.x * KBLK;
+  const u16* base = qkv + (int64_t)b * T * ld;
+  u16* dk_base = d_qkv + (int64_t)b * T * ld + (int64_t)H * DH + h * DH;
+  u16* dv_base = d_qkv + (int64_t)b * T * ld + 2LL * H * DH + h * DH;
+
+  if (k0 >= L) {
+    for (int e = tid; e < KBLK * DH / 8; e += NT) {
+      const int row = e / (DH / 8), col = (e % (DH / 8)) * 8, k = k0 + row;
+      if (k < T) {
+        *reinterpret_cast<uint4*>(dk_base + (int64_t)k * ld + col) = make_uint4(0u, 0u, 0u, 0u);
+        *reinterpret_cast<uint4*>(dv_base + (int64_t)k * ld + col) = make_uint4(0u, 0u, 0u, 0u);
+      }
+    }
+    return;
+  }
+  bf16x8 kf[2][4], vf[2][4];
+  bool kvalid[2];
+#pragma unroll
+  for (int kg = 0; kg < 2; ++kg) {
+    const int key = k0 + wave * 32 + kg * 16 + r16;
+    const int kc = min(key, T - 1);
+    load_frag(kf[kg], base + (int64_t)kc * ld + (int64_t)H * DH + h * DH, g);
+    load_frag(vf[kg], base + (int64_t)kc * ld + 2LL * H * DH + h * DH, g);
+    kvalid[kg] = key < L;
+  }
+  f32x4 dk[2][8], dv[2][8];
+#pragma unroll
+  for (int kg = 0; kg < 2; ++kg)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dk[kg][i] = dv[kg][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nqt = (L + QB - 1) / QB;
+  const u16* qbase = base + h * DH;
+  const u16* dobase = d_o + (int64_t)b * T * ldo + h * DH;
+  uint4 qr[PER], dr[PER];
+  float lr_ = 0.f, dl_ = 0.f;
+  auto load_q = [&](int qt) {
+    load_regs<NT>(qr, qbase, ld, qt * QB, T, tid);
+    load_regs<NT>(dr, dobase, ldo, qt * QB, T, tid);
+    if (tid < QB) {
+      const int qq = qt * QB + tid;
+      lr_ = qq < T ? lse[(int64_t)bh * T + qq] : 0.f;
+      dl_ = qq < T ? delta[(int64_t)bh * T + qq] : 0.f;
+    }
+  };
+  load_q(0);
+  for (int qt = 0; qt < nqt; ++qt) {
+    __syncthreads();
+    store_regs<LDR, NT>(Qs, qr, tid);
+    store_regs<LDR, NT>(Ds, dr, tid);
+    if (tid < QB) {
+      lse_s[tid] = lr_;
+      del_s[tid] = dl_;
+    }
+    __syncthreads();
+    if (qt + 1 < nqt) load_q(qt + 1);
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      f32x4 pp[2][2], dsv[2][2];  // [key group][half]
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        const int qs = 2 * c + half;
+        bf16x8 qfr[4], dfr[4];
+        row_frags<LDR>(qfr, Qs, 16 * qs + r16, g);
+        row_frags<LDR>(dfr, Ds, 16 * qs + r16, g);
+#pragma unroll
+        for (int kg = 0; kg < 2; ++kg) {
+          const f32x4 s = chain4(qfr, kf[kg]);   // S[q][key]
+          const f32x4 dp = chain4(dfr, vf[kg]);  // dP[q][key]
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int ql = 16 * qs + 4 * g + r, qq = qt * QB + ql;
+            const float pv = (qq < L && kvalid[kg]) ? __expf(s[r] * scale - lse_s[ql]) : 0.f;
+            pp[kg][half][r] = pv;
+            dsv[kg][half][r] = pv * (dp[r] - del_s[ql]);
+          }
+        }
+      }
+      accum_t2<LDR>(dv, Ds, 32 * c, pack8(pp[0][0], pp[0][1]), pack8(pp[1][0], pp[1][1]), g, q4,
+                    p4);  // dV^T += dO^T P
+      accum_t2<LDR>(dk, Qs, 32 * c, pack8(dsv[0][0], dsv[0][1]), pack8(dsv[1][0], dsv[1][1]), g,
+                    q4, p4);  // dK^T += Q^T dS
+    }
+  }
+#pragma unroll
+  for (int kg = 0; kg < 2; ++kg) {
+    const int key = k0 + wave * 32 + kg * 16 + r16;
+    if (key < T) {
+#pragma unroll
+      for (int ds = 0; ds < 8; ++ds) {
+        store4_bf16(dk_base + (int64_t)key * ld + 16 * ds + 4 * g, dk[kg][ds] * scale);
+        store4_bf16(dv_base + (int64_t)key * ld + 16 * ds + 4 * g, dv[kg][ds]);
+      }
+    }
+  }
+}
+
+// NW waves per workgroup (32 NW query / key rows): 4 from T = 256 on, 2 below (the encoder's
+// T = 128 keeps two workgroups per (utterance, head))
 int attn_fwd_bf16_launch(const void* qkv, void* o, float* lse, const int64_t* lens, int64_t batch,
                          int64_t seq_len, int heads, float scale, hipStream_t st) {
-  dim3 grid((unsigned)((seq_len + QB - 1) / QB), (unsigned)(batch * heads));
-  attn_fwd_bf16<<<grid, 256, 0, st>>>((const u16*)qkv, (u16*)o, lse, lens, (int)seq_len, heads, scale);
+  if (seq_len >= 256 && g_tune[FS2_TUNE_ATTN] >= 0) {
+    dim3 grid((unsigned)((seq_len + 127) / 128), (unsigned)(batch * heads));
+    attn_fwd_bf16<4><<<grid, 256, 0, st>>>((const u16*)qkv, (u16*)o, lse, lens, (int)seq_len, heads, scale);
+  } else {
+    dim3 grid((unsigned)((seq_len + QB - 1) / QB), (unsigned)(batch * heads));
+    attn_fwd_bf16_g1<<<grid, 256, 0, st>>>((const u16*)qkv, (u16*)o, lse, lens, (int)seq_len, heads, scale);
+  }
   return launch_status("fs2_attn_fwd(bf16)");
 }
 
 int attn_bwd_bf16_launch(const void* qkv, const void* o, const void* d_o, const float* lse,
                          void* d_qkv, const int64_t* lens, int64_t batch, int64_t seq_len,
                          int heads, float scale, float* ws, hipStream_t st) {
-  const int64_t rows = batch * seq_len;
-  const int64_t waves = rows * heads;
-  attn_bwd_delta_bf16<<<(unsigned)((waves * 64 + 255) / 256), 256, 0, st>>>(
-      (const u16*)o, (const u16*)d_o, ws, rows, (int)seq_len, heads);
-  dim3 grid((unsigned)((seq_len + QB - 1) / QB), (unsigned)(batch * heads));
-  attn_bwd_dq_bf16<<<grid, 256, 0, st>>>((const u16*)qkv, (const u16*)d_o, lse, ws, (u16*)d_qkv,
-                                         lens, (int)seq_len, heads, scale);
-  attn_bwd_dkdv_bf16<<<grid, 256, 0, st>>>((const u16*)qkv, (const u16*)d_o, lse, ws, (u16*)d_qkv,
-                                           lens, (int)seq_len, heads, scale);
+  const int tune = g_tune[FS2_TUNE_ATTN];
+  dim3 grid1((unsigned)((seq_len + QB - 1) / QB), (unsigned)(batch * heads));
+  dim3 grid2((unsigned)((seq_len + 127) / 128), (unsigned)(batch * heads));
+  if (seq_len >= 256 && tune >= 0) {  // dQ with delta fused
+    attn_bwd_dq_bf16<4><<<grid2, 256, 0, st>>>((const u16*)qkv, (const u16*)o, (const u16*)d_o, lse, ws,
+                                               (u16*)d_qkv, lens, (int)seq_len, heads, scale);
+  } else {
+    const int64_t rows = batch * seq_len;
+    attn_bwd_delta_bf16_g1<<<(unsigned)((rows * heads * 64 + 255) / 256), 256, 0, st>>>(
+        (const u16*)o, (const u16*)d_o, ws, rows, (int)seq_len, heads);
+    attn_bwd_dq_bf16_g1<<<grid1, 256, 0, st>>>((const u16*)qkv, (const u16*)d_o, lse, ws, (u16*)d_qkv,
+                                               lens, (int)seq_len, heads, scale);
+  }
+  if (seq_len >= 256 && tune != -1 && tune != 1)
+    attn_bwd_dkdv_bf16<4><<<grid2, 256, 0, st>>>((const u16*)qkv, (const u16*)d_o, lse, ws, (u16*)d_qkv,
+                                                 lens, (int)seq_len, heads, scale);
+  else
+    attn_bwd_dkdv_bf16_g1<<<grid1, 256, 0, st>>>((const u16*)qkv, (const u16*)d_o, lse, ws, (u16*)d_qkv,
+                                                 lens, (int)seq_len, heads, scale);
   return launch_status("fs2_attn_bwd(bf16)");
 }
 

@@ -472,12 +472,22 @@ void conv_gemm_halo(GldsArgs a) {
   const int64_t m0 = (int64_t)tm * BM;
   const int n0 = tn * BN;
   const bool skip = a.lens && rows_all_padding(a.lens, a.T, m0, m0 + BM < a.M ? m0 + BM : a.M);
+  // this wave's half of the tile (BM/2 rows) all padding: it stages its share of the tiles but
+  // issues no MFMAs (those outputs are masked downstream; the 256-row forward tiles of the
+  // decoder's k=9 conv hold ~13 % such rows)
+  const int64_t hr0 = m0 + wm * (BM / 2), hr1 = hr0 + BM / 2 < a.M ? hr0 + BM / 2 : a.M;
+  const bool half_pad = !VOC && (hr0 >= a.M || (a.lens && rows_all_padding(a.lens, a.T, hr0, hr1)));
   const int ncb_all = a.Cin / 64, cb0 = z * ncb_all / kz, cb1 = (z + 1) * ncb_all / kz;
 
   const int lrow = lane >> 3;
   const u16* zero = reinterpret_cast<const u16*>(g_zero_line);
   const int HR = BM + (a.taps - 1) * dil, HP = (HR + 7) / 8;
-  const int64_t u0 = (m0 / a.T) * a.T, u1 = u0 + a.T < a.M ? u0 + a.T : a.M;
+  const int64_t u0 = (m0 / a.T) * a.T;
+  // input rows past the utterance's length are zero in the FFT blocks (Layers.py:25,28) and in
+  // the upstream gradients: read them from the zero line (no HBM traffic).  Vocoder lens are
+  // row limits of another meaning: the whole padded utterance is staged there.
+  const int64_t ulen = (!VOC && a.lens) ? (a.lens[m0 / a.T] < a.T ? a.lens[m0 / a.T] : a.T) : a.T;
+  const int64_t u1 = u0 + ulen < a.M ? u0 + ulen : a.M;
   // halo piece p = wave + NWAVE q: rows h = 8 p + lrow, global row m0 - pad + h
   const u16* h_src[QMAX];
 #pragma unroll
@@ -520,6 +530,7 @@ void conv_gemm_halo(GldsArgs a) {
       glds16(b_src[i] ? b_src[i] + k0 : zero, Bs + slot * B_E + (wave * BW + i) * 8 * BK);
   };
   auto compute = [&](int j, int slot) {
+    if (half_pad) return;
     // fragment rows differ by multiples of 16, so one swizzle serves all of them.  All 16
     // fragment reads of the step are issued before the first MFMA: the waits before the
     // MFMAs are then counted (the second k-half's reads land under the first half's MFMAs)

@@ -720,6 +720,7 @@ class VarianceAdaptorFn(torch.autograd.Function):
 
     @staticmethod
     def forward(fctx, token, enc_out, m, speakers, src_lens, p_t, e_t, d_t, B, Ts, T_dec, ctx):
+        fctx.set_materialize_grads(False)  # unused outputs' gradients stay None (no zero fills)
         va = m.variance_adaptor
         x0, x0_t = K.rowvec_add(enc_out, speakers, m.speaker_emb.weight, B, Ts, copy=ctx.copy)
         log_d, s_d = va.duration_predictor.fwd(x0, x0_t, src_lens, B, Ts, ctx)
@@ -766,6 +767,7 @@ class VarianceAdaptorFn(torch.autograd.Function):
 class DecoderFn(torch.autograd.Function):
     @staticmethod
     def forward(fctx, token, x, x_t, dec, lens, B, T, ctx):
+        fctx.set_materialize_grads(False)  # the compute-copy side output gets no zero gradient
         x_t = x_t if x_t.numel() else None
         saved = []
         for layer in dec.layer_stack:
@@ -778,6 +780,8 @@ class DecoderFn(torch.autograd.Function):
 
     @staticmethod
     def backward(fctx, dx, _):
+        if dx is None:
+            dx = K.zeros(fctx.saved[0][0].shape, fctx.saved[0][0].device)
         dx = dx.contiguous()
         for layer, s in zip(reversed(fctx.dec.layer_stack), reversed(fctx.saved)):
             dx = layer.bwd(dx, s)

@@ -26,15 +26,19 @@ def timeit(run, n=20):
     return s.elapsed_time(e) / n * 1e3
 
 
-for name, T, lens in (("decoder", 512, np.asarray(b[7])), ("encoder", 128, np.asarray(b[4]))):
-    B, H, dh = 48, 2, 128
-    L = torch.tensor(lens, device=dev)
-    qkv = (torch.randn(B * T, 3 * H * dh, device=dev) * 0.5).to(torch.bfloat16)
-    o, lse = K.attn_fwd(qkv, L, B, T, H, dh, 1 / math.sqrt(dh))
-    do = torch.randn(B * T, H * dh, device=dev).to(torch.bfloat16)
-    tf = timeit(lambda: K.attn_fwd(qkv, L, B, T, H, dh, 1 / math.sqrt(dh)))
-    tb = timeit(lambda: K.attn_bwd(qkv, o, do, lse, L, B, T, H, dh, 1 / math.sqrt(dh)))
-    kv = np.ceil(lens / 64) * 64
-    fl = float(np.sum(4.0 * H * kv * kv * dh))
-    print(f"{name}: fwd {tf:6.1f} us ({fl / tf / 1e6:5.0f} TF)  bwd {tb:6.1f} us "
-          f"({2.5 * fl / tb / 1e6:5.0f} TF)", flush=True)
+for knob in ((-1, 0, 2) if "--variants" in sys.argv else (0,)):
+  K.lib.fs2_set_tuning(9, knob)  # FS2_TUNE_ATTN
+  print(f"== FS2_TUNE_ATTN = {knob}")
+  for name, T, lens in (("decoder", 512, np.asarray(b[7])), ("encoder", 128, np.asarray(b[4]))):
+      B, H, dh = 48, 2, 128
+      L = torch.tensor(lens, device=dev)
+      qkv = (torch.randn(B * T, 3 * H * dh, device=dev) * 0.5).to(torch.bfloat16)
+      o, lse = K.attn_fwd(qkv, L, B, T, H, dh, 1 / math.sqrt(dh))
+      do = torch.randn(B * T, H * dh, device=dev).to(torch.bfloat16)
+      tf = timeit(lambda: K.attn_fwd(qkv, L, B, T, H, dh, 1 / math.sqrt(dh)))
+      tb = timeit(lambda: K.attn_bwd(qkv, o, do, lse, L, B, T, H, dh, 1 / math.sqrt(dh)))
+      kv = np.ceil(lens / 64) * 64
+      fl = float(np.sum(4.0 * H * kv * kv * dh))
+      print(f"{name}: fwd {tf:6.1f} us ({fl / tf / 1e6:5.0f} TF)  bwd {tb:6.1f} us "
+            f"({2.5 * fl / tb / 1e6:5.0f} TF)", flush=True)
+K.lib.fs2_set_tuning(9, 0)

@@ -1,0 +1,186 @@
+"""Time the k=1 projection GEMMs of the FFT blocks alone at their step shapes and epilogues
+(SYN-48, utterance lengths passed as in the step), with compulsory HBM bytes and GB/s.
+
+    python scripts/k1_bench.py [--reps 20]
+"""
+import importlib
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+K = importlib.import_module("mid-attribute-speaker-generation_amd.kernels")
+PKG = importlib.import_module("mid-attribute-speaker-generation_amd")
+dev = "cuda:0"
+_b = PKG.data.syn_batch(48, 128, seed=0)
+LENS = {512: torch.tensor(_b[7], device=dev), 128: torch.tensor(_b[4], device=dev)}
+VALID = {512: int(np.sum(_b[7])), 128: int(np.sum(_b[4]))}
+bf, f32 = torch.bfloat16, torch.float32
+
+# name, T, cin, cout, kind: (bias?, epilogue, out dtype, aux dtype)
+SHAPES = [
+    ("dec qkv fwd", 512, 256, 768, "bias_bf16"),
+    ("dec fc fwd", 512, 256, 256, "bias_f32"),
+    ("dec w2 fwd", 512, 1024, 256, "bias_f32"),
+    ("dec w2 dgrad", 512, 256, 1024, "relumask_bf16"),
+    ("dec fc dgrad", 512, 256, 256, "plain_bf16"),
+    ("dec qkv dgrad", 512, 768, 256, "addaux_f32"),
+    ("enc qkv fwd", 128, 256, 768, "bias_bf16"),
+    ("enc fc fwd", 128, 256, 256, "bias_f32"),
+    ("enc w2 fwd", 128, 1024, 256, "bias_f32"),
+    ("enc w2 dgrad", 128, 256, 1024, "relumask_bf16"),
+    ("enc fc dgrad", 128, 256, 256, "plain_bf16"),
+    ("enc qkv dgrad", 128, 768, 256, "addaux_f32"),
+]
+
+
+def make(T, cin, cout, kind):
+    M = 48 * T
+    x = torch.randn(M, cin, device=dev).to(bf)
+    w = (torch.randn(cout, cin, device=dev) * 0.05).to(bf)
+    b = torch.randn(cout, device=dev)
+    V = VALID[T]
+    if kind == "bias_bf16":
+        return (lambda: K.conv_gemm(x, w, M, T, cin, cout, 1, 0, bias=b, out_dtype=bf, lens=LENS[T])), \
+            V * cin * 2 + M * cout * 2
+    if kind == "bias_f32":
+        return (lambda: K.conv_gemm(x, w, M, T, cin, cout, 1, 0, bias=b, lens=LENS[T])), \
+            V * cin * 2 + M * cout * 4
+    if kind == "relumask_bf16":
+        h = torch.randn(M, cout, device=dev).to(bf)
+        return (lambda: K.conv_gemm(x, w, M, T, cin, cout, 1, 0, flags=K.EPI_RELU_MASK_AUX, aux=h,
+                                    out_dtype=bf, lens=LENS[T])), V * cin * 2 + V * cout * 2 + M * cout * 2
+    if kind == "plain_bf16":
+        return (lambda: K.conv_gemm(x, w, M, T, cin, cout, 1, 0, out_dtype=bf, lens=LENS[T])), \
+            V * cin * 2 + M * cout * 2
+    if kind == "addaux_f32":
+        dx = torch.randn(M, cout, device=dev)
+        return (lambda: K.conv_gemm(x, w, M, T, cin, cout, 1, 0, flags=K.EPI_ADD_AUX, aux=dx, out=dx,
+                                    lens=LENS[T])), V * cin * 2 + V * cout * 4 + M * cout * 4
+    raise ValueError(kind)
+
+
+def check(T, cin, cout):
+    """Valid rows of the kernel's y = relu?(x W^T + b) against torch fp32 on the same bf16
+    operands."""
+    M = 48 * T
+    x = torch.randn(M, cin, device=dev).to(bf)
+    w = (torch.randn(cout, cin, device=dev) * 0.05).to(bf)
+    b = torch.randn(cout, device=dev)
+    aux = torch.randn(M, cout, device=dev)
+    y = K.conv_gemm(x, w, M, T, cin, cout, 1, 0, bias=b, flags=K.EPI_ADD_AUX, aux=aux, lens=LENS[T])
+    ref = x.float() @ w.float().t() + b + aux
+    valid = (torch.arange(T, device=dev)[None] < LENS[T][:, None]).reshape(-1)
+    err = (y[valid] - ref[valid]).abs().max().item() / ref[valid].abs().max().item()
+    return err
+
+
+WSHAPES = [  # weight gradients of the k=1 projections: name, T, c_in, c_out, bias gradient
+    ("dec qkv dW", 512, 256, 768, True),
+    ("dec fc dW", 512, 256, 256, False),
+    ("dec w2 dW", 512, 1024, 256, False),
+    ("enc qkv dW", 128, 256, 768, True),
+    ("enc fc dW", 128, 256, 256, False),
+    ("enc w2 dW", 128, 1024, 256, False),
+]
+
+
+def wgrad_set(reps):
+    tot = {128: 0.0, 512: 0.0}
+    for name, T, cin, cout, bias in WSHAPES:
+        M = 48 * T
+        V = VALID[T]
+        valid = (torch.arange(T, device=dev)[None] < LENS[T][:, None]).reshape(-1)
+        x = torch.randn(M, cin, device=dev).to(bf)
+        dy = (torch.randn(M, cout, device=dev) * valid[:, None]).to(bf)  # zero at padded rows, as in the step
+        dw = torch.zeros(cout, cin, device=dev)
+        db = torch.zeros(cout, device=dev) if bias else None
+        run = lambda: K.conv_wgrad(dy, x, dw, M, T, cin, cout, 1, 0, db=db, lens=LENS[T])
+        for _ in range(5):
+            run()
+        torch.cuda.synchronize()
+        # correctness on valid rows (fp32 reference of the same bf16 operands)
+        dw.zero_()
+        if db is not None:
+            db.zero_()
+        run()
+        ref = dy[valid].float().t() @ x[valid].float()
+        err = (dw - ref).abs().max().item() / ref.abs().max().item()
+        s_, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s_.record()
+        for _ in range(reps):
+            run()
+        e.record()
+        torch.cuda.synchronize()
+        us = s_.elapsed_time(e) / reps * 1e3
+        tot[T] += us
+        nbytes = V * (cin + cout) * 2 + cout * cin * 4 * 2
+        print(f"{name:16s} {us:7.1f} us  {nbytes / us / 1e3:6.0f} GB/s  "
+              f"{2.0 * V * cin * cout / us / 1e6:6.0f} TF/s  rel err {err:.1e}")
+    print(f"wgrad: decoder layer set {tot[512]:.1f} us, encoder {tot[128]:.1f} us; step ~ "
+          f"{6 * tot[512] + 4 * tot[128]:.0f} us", flush=True)
+
+
+def main():
+    reps = int(sys.argv[sys.argv.index("--reps") + 1]) if "--reps" in sys.argv else 20
+    if "--probe" in sys.argv:  # one shape, 10 launches (PMC passes): --probe <name>
+        i = sys.argv.index("--probe")
+        name = sys.argv[i + 1]
+        sh = [s_ for s_ in SHAPES if s_[0] == name][0]
+        run, _ = make(sh[1], sh[2], sh[3], sh[4])
+        for _ in range(10):
+            run()
+        torch.cuda.synchronize()
+        return
+    if "--wgrad" in sys.argv:
+        if "--sweep" in sys.argv:  # FS2_TUNE_WGRAD_STAGES x FS2_TUNE_WGRAD_TILE x splits
+            for tile in (64, 128):
+                for st in (1, 2, 3, 4):
+                    for sp in (0, 8, 16, 32):
+                        K.lib.fs2_set_tuning(2, tile)
+                        K.lib.fs2_set_tuning(1, st)
+                        K.lib.fs2_set_tuning(3, sp)
+                        print(f"== wgrad tile {tile} stages {st} splits {sp or 'auto'}")
+                        wgrad_set(reps)
+            for k in (1, 2, 3):
+                K.lib.fs2_set_tuning(k, 0)
+            return
+        wgrad_set(reps)
+        return
+    if "--stages" in sys.argv:  # the 4-wave tap-major kernel under FS2_TUNE_GEMM_STAGES
+        for st in (0, 1, 2, 3, 4):
+            K.lib.fs2_set_tuning(0, st)
+            print(f"== FS2_TUNE_GEMM_STAGES = {st}")
+            run_set(reps, [s_ for s_ in SHAPES if s_[1] == 512])
+        K.lib.fs2_set_tuning(0, 0)
+        return
+    run_set(reps, SHAPES)
+
+
+def run_set(reps, shapes):
+    runs = [(n, T, cin, cout) + make(T, cin, cout, kind) for n, T, cin, cout, kind in shapes]
+    for _ in range(2):  # clocks settle
+        for r in runs:
+            for _ in range(5):
+                r[4]()
+    torch.cuda.synchronize()
+    tot = {128: 0.0, 512: 0.0}
+    for name, T, cin, cout, run, nbytes in runs:
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(reps):
+            run()
+        e.record()
+        torch.cuda.synchronize()
+        us = s.elapsed_time(e) / reps * 1e3
+        tot[T] += us
+        fl = 2.0 * VALID[T] * cin * cout
+        print(f"{name:16s} {us:7.1f} us  {nbytes / us / 1e3:6.0f} GB/s  {fl / us / 1e6:6.0f} TF/s")
+    print(f"decoder layer set {tot[512]:.1f} us, encoder layer set {tot[128]:.1f} us; "
+          f"step ~ {6 * tot[512] + 4 * tot[128]:.0f} us", flush=True)
+
+
+if __name__ == "__main__":
+    main()

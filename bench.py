@@ -399,6 +399,10 @@ def main():
     M = importlib.import_module("mid-attribute-speaker-generation_amd.model")
     K = importlib.import_module("mid-attribute-speaker-generation_amd.kernels")
     TR = importlib.import_module("mid-attribute-speaker-generation_amd.train")
+    # FS2_TUNE="knob=value,...": kernel-selection knobs (include/fs2hip.h) for A/B runs
+    for kv in filter(None, os.environ.get("FS2_TUNE", "").split(",")):
+        knob, val = kv.split("=")
+        K.lib.fs2_set_tuning(int(knob), int(val))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:

@@ -218,11 +218,14 @@ int fs2_weight_prep_batch(int dtype, const int64_t* jobs, int n_jobs, int64_t n_
  *   FS2_TUNE_ATTN          bf16 attention at T >= 256: 0 = two 16-row groups per wave in the
  *                          forward, dQ (delta fused) and dK/dV kernels (automatic), -1 = one
  *                          group everywhere, 1 = two groups in the forward and dQ only
+ *   FS2_TUNE_HALO_DB       halo fwd/dX kernel, 2-slot weight ring: 0 = one halo stage, loaded
+ *                          at each channel block (default), 1 = double-buffered halo stage
+ *                          (the next channel block's rows in flight; A/B within run noise)
  * Process-wide; query workspace sizes after setting.                                 */
 enum { FS2_TUNE_GEMM_STAGES = 0, FS2_TUNE_WGRAD_STAGES = 1, FS2_TUNE_WGRAD_TILE = 2,
        FS2_TUNE_WGRAD_SPLITS = 3, FS2_TUNE_LEGACY_GEMM = 4, FS2_TUNE_NT_GROUP = 5,
        FS2_TUNE_NT_HALO = 6, FS2_TUNE_WGRAD_HALO = 7, FS2_TUNE_HALO_SPLITK = 8,
-       FS2_TUNE_ATTN = 9, FS2_TUNE_COUNT = 10 };
+       FS2_TUNE_ATTN = 9, FS2_TUNE_HALO_DB = 10, FS2_TUNE_COUNT = 11 };
 int fs2_set_tuning(int knob, int value);
 
 /* Weight (and optionally bias) gradient, accumulated into the fp32 master-gradient layout:

@@ -327,6 +327,51 @@ __global__ __launch_bounds__(256) void weight_prep_tiles(const int64_t* __restri
   const int nc = Cin - c0 < CT ? Cin - c0 : CT;
   const int run = nc * taps;  // contiguous source elements per row
   const int64_t Q = (int64_t)Cin * taps;
+  if constexpr (sizeof(OutT) == 2) {
+    // 16-B vector path (full tiles of aligned rows: every step weight but the odd edges):
+    // float4 source reads, 8 x bf16 = 16-B stores of w_fwd (8 channels of one (o, tap)) and
+    // w_bwd (8 output channels of one (c, tap))
+    const bool vec = no == 64 && nc == CT && (Q % 4) == 0 && (Cin % 8) == 0 && (Cout % 8) == 0 &&
+                     (((uintptr_t)w | (uintptr_t)wf | (uintptr_t)wb) & 15) == 0;
+    if (vec) {
+      const int run4 = run / 4;  // CT * taps is a multiple of 4 (CT = 32)
+      for (int e = threadIdx.x; e < 64 * run4; e += 256) {
+        const int r = e / run4, q4 = e - r * run4;
+        const f32x4 v = ld4(w + (int64_t)(o0 + r) * Q + (int64_t)c0 * taps + 4 * q4);
+        OutT* t = tile + r * LD + 4 * q4;
+        t[0] = f2bf(v.x);
+        t[1] = f2bf(v.y);
+        t[2] = f2bf(v.z);
+        t[3] = f2bf(v.w);
+      }
+      __syncthreads();
+      if (wf) {  // wf[o, j*Cin + c]: per (o, j) a run of CT = 4 x 8 channels
+        for (int e = threadIdx.x; e < 64 * taps * (CT / 8); e += 256) {
+          const int c8 = (e % (CT / 8)) * 8, rj = e / (CT / 8), j = rj % taps, r = rj / taps;
+          const OutT* t = tile + r * LD + c8 * taps + j;
+          uint4 o;
+          o.x = (uint32_t)t[0] | ((uint32_t)t[taps] << 16);
+          o.y = (uint32_t)t[2 * taps] | ((uint32_t)t[3 * taps] << 16);
+          o.z = (uint32_t)t[4 * taps] | ((uint32_t)t[5 * taps] << 16);
+          o.w = (uint32_t)t[6 * taps] | ((uint32_t)t[7 * taps] << 16);
+          *reinterpret_cast<uint4*>(wf + (int64_t)(o0 + r) * Q + (int64_t)j * Cin + c0 + c8) = o;
+        }
+      }
+      if (wb) {  // wb[c*taps + taps-1-j, o]: per (c, j) a run of 64 = 8 x 8 output channels
+        for (int e = threadIdx.x; e < CT * taps * 8; e += 256) {
+          const int r8 = (e & 7) * 8, cj = e >> 3, j = cj % taps, c = cj / taps;
+          const OutT* t = tile + r8 * LD + c * taps + j;
+          uint4 o;
+          o.x = (uint32_t)t[0] | ((uint32_t)t[LD] << 16);
+          o.y = (uint32_t)t[2 * LD] | ((uint32_t)t[3 * LD] << 16);
+          o.z = (uint32_t)t[4 * LD] | ((uint32_t)t[5 * LD] << 16);
+          o.w = (uint32_t)t[6 * LD] | ((uint32_t)t[7 * LD] << 16);
+          *reinterpret_cast<uint4*>(wb + ((int64_t)(c0 + c) * taps + (taps - 1 - j)) * Cout + o0 + r8) = o;
+        }
+      }
+      return;
+    }
+  }
   for (int e = threadIdx.x; e < no * run; e += 256) {
     const int r = e / run, q = e - r * run;
     const float v = w[(int64_t)(o0 + r) * Q + (int64_t)c0 * taps + q];

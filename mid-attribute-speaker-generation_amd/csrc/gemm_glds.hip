@@ -55,6 +55,7 @@ struct GldsArgs {
   u16* y2;              // FS2_EPI_Y2 bf16 output (ld = N)
   float alpha2;
   int kz;               // halo kernel: channel-block splits (0/1 = none; see halo_splitk_reduce)
+  int halo_db;          // halo kernel, BST == 2: double-buffered halo stage (FS2_TUNE_HALO_DB)
   float* slab;          // kz > 1: [kz][M][N] fp32 partial products
 };
 
@@ -98,6 +99,21 @@ FS2_DEV float bfv(u16 v) { return __uint_as_float(((uint32_t)v) << 16); }
 FS2_DEV u16 fbv(float f) {
   __bf16 b = (__bf16)f;
   return *reinterpret_cast<u16*>(&b);
+}
+
+// Wait until at most n (0..8, wave-uniform) vector-memory instructions are in flight.
+FS2_DEV void vm_wait_n(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+  }
 }
 
 // Wait until at most `ahead` tiles of PER LDS-DMA instructions each are still in flight.
@@ -446,11 +462,13 @@ void conv_gemm_halo(GldsArgs a) {
   constexpr int QMAX = (HMAX / 8 + NWAVE - 1) / NWAVE;  // 8-row halo pieces per wave
   constexpr int BW = BN / 8 / NWAVE;                // weight pieces per wave
   constexpr int A_E = HMAX * BK, B_E = BN * BK;
+  // BST == 2: two halo slots -- channel block cb + 1's rows are staged while cb's taps run
+  constexpr int NA = BST == 2 ? 2 : 1;
   constexpr int EPI_E = (BM / 2) * (BN + 4) * 2;
-  constexpr int SMEM_E = A_E + BST * B_E > EPI_E ? A_E + BST * B_E : EPI_E;
+  constexpr int SMEM_E = NA * A_E + BST * B_E > EPI_E ? NA * A_E + BST * B_E : EPI_E;
   __shared__ __attribute__((aligned(1024))) u16 smem[SMEM_E];
   u16* As = smem;
-  u16* Bs = smem + A_E;
+  u16* Bs = smem + NA * A_E;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -516,20 +534,23 @@ void conv_gemm_halo(GldsArgs a) {
   const int b_off[2] = {b_row * BK + ((0 + g) ^ (b_row & 7)) * 8, b_row * BK + ((4 + g) ^ (b_row & 7)) * 8};
   // step s = cb * taps + j: weight tile (tap j, channel block cb) into ring slot s % BST; the
   // halo of channel block cb is staged at j == 0
-  auto issue_a = [&](int cb) {
+  auto issue_a = [&](int cb, int aslot) {
 #pragma unroll
     for (int q = 0; q < QMAX; ++q) {
       const int pc = wave + NWAVE * q;
-      if (pc < HP) glds16(h_src[q] ? h_src[q] + cb * BK : zero, As + pc * 8 * BK);
+      if (pc < HP) glds16(h_src[q] ? h_src[q] + cb * BK : zero, As + aslot * A_E + pc * 8 * BK);
     }
   };
+  int qa = 0;  // this wave's halo pieces (its LDS-DMA count per halo stage)
+#pragma unroll
+  for (int q = 0; q < QMAX; ++q) qa += (wave + NWAVE * q) < HP ? 1 : 0;
   auto issue_b = [&](int cb, int j, int slot) {
     const int64_t k0 = (int64_t)j * a.Cin + cb * BK;
 #pragma unroll
     for (int i = 0; i < BW; ++i)
       glds16(b_src[i] ? b_src[i] + k0 : zero, Bs + slot * B_E + (wave * BW + i) * 8 * BK);
   };
-  auto compute = [&](int j, int slot) {
+  auto compute = [&](int j, int slot, int aslot) {
     if (half_pad) return;
     // fragment rows differ by multiples of 16, so one swizzle serves all of them.  All 16
     // fragment reads of the step are issued before the first MFMA: the waits before the
@@ -538,7 +559,7 @@ void conv_gemm_halo(GldsArgs a) {
     bf16x8g fa[2][MI], fb[2][NI];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      const u16* pa = As + ha * BK + ((ks * 4 + g) ^ sa) * 8;
+      const u16* pa = As + aslot * A_E + ha * BK + ((ks * 4 + g) ^ sa) * 8;
       const u16* pb = Bs + slot * B_E + b_off[ks];
 #pragma unroll
       for (int i = 0; i < MI; ++i) fa[ks][i] = *reinterpret_cast<const bf16x8g*>(pa + i * 16 * BK);
@@ -558,28 +579,57 @@ void conv_gemm_halo(GldsArgs a) {
     if constexpr (BST == 1) {
       for (int cb = 0; cb < ncb; ++cb) {
         for (int j = 0; j < a.taps; ++j) {
-          if (j == 0) issue_a(cb);
+          if (j == 0) issue_a(cb, 0);
           issue_b(cb, j, 0);
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           __builtin_amdgcn_s_barrier();
-          compute(j, 0);
+          compute(j, 0, 0);
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           __builtin_amdgcn_s_barrier();
         }
       }
+    } else if (BST == 2 && a.halo_db) {
+      // Step s = (cb, j) reads halo slot cb & 1 and weight slot s & 1.  Issue order per step
+      // (after the barrier): weight tile s + 1, then -- at j == 0 -- the halo of channel block
+      // cb + 1 into the other halo slot (free: block cb - 1's last reads finished before this
+      // step's barrier).  Loads complete in issue order, so waiting for weight tile s also
+      // covers every halo issued before it; only at j == 1 is the just-issued halo allowed to
+      // stay in flight (vmcnt = this wave's halo pieces), giving it a full step to land.
+      const int S = ncb * a.taps;
+      issue_a(0, 0);
+      issue_b(0, 0, 0);
+      int cb = 0, j = 0;
+      for (int s = 0; s < S; ++s) {
+        if (j == 1 && cb + 1 < ncb) vm_wait_n(qa);
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (s + 1 < S) {
+          const int cbn = j + 1 == a.taps ? cb + 1 : cb, jn = j + 1 == a.taps ? 0 : j + 1;
+          issue_b(cbn, jn, (s + 1) & 1);
+        }
+        if (j == 0 && cb + 1 < ncb) issue_a(cb + 1, (cb + 1) & 1);
+        compute(j, s & 1, cb & 1);
+        if (++j == a.taps) {
+          j = 0;
+          ++cb;
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
     } else {
       // weight-tile ring of BST slots, BST-1 tiles ahead: step s = (cb, j) reads slot s % BST
       // while tiles s+1 .. s+BST-1 are in flight.  At a channel-block boundary the single
       // halo buffer is reloaded after a barrier (everyone finished the previous block).
       const int S = ncb * a.taps;
-      issue_a(0);
+      issue_a(0, 0);
       for (int d = 0; d < BST - 1 && d < S; ++d) issue_b(d / a.taps, d % a.taps, d);
       int cb = 0, j = 0, slot = 0;
       for (int s = 0; s < S; ++s) {
         if (j == 0 && s > 0) {
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           __builtin_amdgcn_s_barrier();
-          issue_a(cb);
+          issue_a(cb, 0);
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         } else if (BST == 3 && s + 1 < S) {
           asm volatile("s_waitcnt vmcnt(%0)" ::"n"(BW) : "memory");  // tile s+1 may fly
@@ -593,7 +643,7 @@ void conv_gemm_halo(GldsArgs a) {
           const int cbn = sn / a.taps;
           issue_b(cbn, sn - cbn * a.taps, sn % BST);
         }
-        compute(j, slot);
+        compute(j, slot, 0);
         slot = slot + 1 == BST ? 0 : slot + 1;
         if (++j == a.taps) {
           j = 0;
@@ -1295,6 +1345,12 @@ static int halo_splitk(GldsArgs& a, unsigned grid, bool voc, bool hx64, hipStrea
   return kz;
 }
 
+// n-tiles per tile group of the halo kernels (FS2_TUNE_NT_GROUP; default: all of them)
+static int halo_group(int tiles_n) {
+  const int g = g_tune[FS2_TUNE_NT_GROUP];
+  return g > 0 && g < tiles_n ? g : tiles_n;
+}
+
 int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, int64_t ldy,
                           int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out, int taps,
                           int pad, const int64_t* lens, const float* bias, int flags,
@@ -1314,6 +1370,7 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
   GldsArgs a{(const u16*)x, ldx, (const u16*)wk, y, ldy, rows, seq_len, (int)c_in, (int)c_out,
              taps, pad, K, bias, flags, aux, ld_aux, 0, 0, vec, 1, lens,
              ve.dil, ve.alpha, ve.scale, (u16*)ve.y2, ve.alpha2};
+  a.halo_db = g_tune[FS2_TUNE_HALO_DB] > 0 ? 1 : 0;
   const bool tapaligned = c_in % 64 == 0;
   const bool voc = ve.dil != 1 || (flags & (FS2_EPI_LRELU | FS2_EPI_ACC_Y | FS2_EPI_Y2)) || !y;
   const int64_t big = ((rows + 127) / 128) * ((c_out + 127) / 128);
@@ -1361,7 +1418,7 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
     const int bm = h8 == 6 ? 128 : 256;
     a.tiles_m = (int)((rows + bm - 1) / bm);
     a.tiles_n = (int)((c_out + 127) / 128);
-    a.group = a.tiles_n;
+    a.group = halo_group(a.tiles_n);
     const unsigned grid = (unsigned)(a.tiles_m * a.tiles_n);
     if (h8 == 5) conv_gemm_halo<256, 128, 3, 16, false, 8><<<grid, 512, 0, st>>>(a);
     else if (h8 == 6) conv_gemm_halo<128, 128, 3, 16, false, 8><<<grid, 512, 0, st>>>(a);
@@ -1372,7 +1429,7 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
       g_tune[FS2_TUNE_NT_HALO] >= 0) {
     a.tiles_m = (int)((rows + halo_bm - 1) / halo_bm);
     a.tiles_n = (int)((c_out + (halo_wide ? 127 : 63)) / (halo_wide ? 128 : 64));
-    a.group = a.tiles_n;
+    a.group = halo_group(a.tiles_n);
     const unsigned grid = (unsigned)(a.tiles_m * a.tiles_n);
     // HX: halo rows beyond the tile, 16 (taps <= 17 undilated: the FFT/PostNet/VP convs) or
     // 64 (dilated vocoder convs; the larger A image leaves 2 blocks per CU)

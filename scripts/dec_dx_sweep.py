@@ -42,9 +42,18 @@ CONFIGS = ((0, 0, "auto"), (1, 0, "4-wave"), (4, 0, "3-slot"), (5, 0, "8w 256x12
 if not FWD:
     CONFIGS += ((0, 2, "128x64 kz2"), (0, 4, "128x64 kz4"), (2, 2, "128x128 kz2"),
                 (2, 3, "128x128 kz3"), (2, 4, "128x128 kz4"))
-for nt, sk, name in CONFIGS + CONFIGS:
+DB = [0]
+if "--db" in sys.argv:  # FS2_TUNE_HALO_DB: double-buffered halo stage on / off
+    CONFIGS = tuple((0, 0, f"auto db {d_}", 0, d_) for d_ in (0, -1))
+elif "--group" in sys.argv:  # FS2_TUNE_NT_GROUP: n-tiles per tile group (weight slice per XCD)
+    CONFIGS = tuple((0, 0, f"auto group {g_}", g_, 0) for g_ in (0, 1, 2, 4))
+else:
+    CONFIGS = tuple(c + (0, 0) for c in CONFIGS)
+for nt, sk, name, grp, db in CONFIGS + CONFIGS + CONFIGS:
     K.lib.fs2_set_tuning(6, nt)
     K.lib.fs2_set_tuning(8, sk)
+    K.lib.fs2_set_tuning(5, grp)
+    K.lib.fs2_set_tuning(10, db)
     for _ in range(3):
         run()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -62,3 +71,5 @@ for nt, sk, name in CONFIGS + CONFIGS:
           f"  max|diff| {err:.2e}", flush=True)
 K.lib.fs2_set_tuning(6, 0)
 K.lib.fs2_set_tuning(8, 0)
+K.lib.fs2_set_tuning(5, 0)
+K.lib.fs2_set_tuning(10, 0)

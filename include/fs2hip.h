@@ -221,11 +221,15 @@ int fs2_weight_prep_batch(int dtype, const int64_t* jobs, int n_jobs, int64_t n_
  *   FS2_TUNE_HALO_DB       halo fwd/dX kernel, 2-slot weight ring: 0 = one halo stage, loaded
  *                          at each channel block (default), 1 = double-buffered halo stage
  *                          (the next channel block's rows in flight; A/B within run noise)
+ *   FS2_TUNE_HALO_PIPE     halo fwd/dX kernel, 2-slot weight ring: 0 = fragment-pipelined
+ *                          loop (default: the next step's LDS fragments are read under the
+ *                          current step's second MFMA half; one barrier per step, mid-step),
+ *                          -1 = the loop that reads all of a step's fragments after its barrier
  * Process-wide; query workspace sizes after setting.                                 */
 enum { FS2_TUNE_GEMM_STAGES = 0, FS2_TUNE_WGRAD_STAGES = 1, FS2_TUNE_WGRAD_TILE = 2,
        FS2_TUNE_WGRAD_SPLITS = 3, FS2_TUNE_LEGACY_GEMM = 4, FS2_TUNE_NT_GROUP = 5,
        FS2_TUNE_NT_HALO = 6, FS2_TUNE_WGRAD_HALO = 7, FS2_TUNE_HALO_SPLITK = 8,
-       FS2_TUNE_ATTN = 9, FS2_TUNE_HALO_DB = 10, FS2_TUNE_COUNT = 11 };
+       FS2_TUNE_ATTN = 9, FS2_TUNE_HALO_DB = 10, FS2_TUNE_HALO_PIPE = 11, FS2_TUNE_COUNT = 12 };
 int fs2_set_tuning(int knob, int value);
 
 /* Weight (and optionally bias) gradient, accumulated into the fp32 master-gradient layout:

@@ -24,6 +24,7 @@
 // leave as 8-element row vectors: bias, residual/aux add, ReLU, ReLU-mask and the bf16 cast
 // are applied on 16-B (bf16) / 32-B (fp32) coalesced stores.
 #include <mutex>
+#include <type_traits>
 
 #include "common.hpp"
 
@@ -100,6 +101,10 @@ FS2_DEV u16 fbv(float f) {
   __bf16 b = (__bf16)f;
   return *reinterpret_cast<u16*>(&b);
 }
+
+// s_waitcnt lgkmcnt(0) with vmcnt / expcnt left at their maxima (gfx9 simm16 encoding), for
+// __builtin_amdgcn_s_waitcnt: unlike inline asm, the compiler's wait-count pass sees it.
+constexpr int kLgkm0 = 0xC07F;
 
 // Wait until at most n (0..8, wave-uniform) vector-memory instructions are in flight.
 FS2_DEV void vm_wait_n(int n) {
@@ -450,9 +455,10 @@ __global__ __launch_bounds__(256) void conv_gemm_nt_glds(GldsArgs a) {
 // of a 128 x 128 tile, and that traffic, not the MFMA, bounds the tap-major kernel
 // (per-CU vector-memory rate; profiles/).  LDS rows are swizzled chunk c -> c ^ (row & 7),
 // which keeps the 16-row fragment reads conflict-free at every row offset.
-template <int BM, int BN, int BST, int HX, bool VOC, int NWAVE = 4>
+template <int BM, int BN, int BST, int HX, bool VOC, int NWAVE = 4, bool PIPE = false>
 __global__ __launch_bounds__(NWAVE * 64, NWAVE == 8 ? 1 : BST == 1 ? 4 : (HX > 16 || BST > 2) ? 2 : 3)
 void conv_gemm_halo(GldsArgs a) {
+  static_assert(!PIPE || BST == 2, "the fragment-pipelined loop runs on the 2-slot weight ring");
   // NWAVE = 4: 2 x 2 waves; NWAVE = 8: 2 (rows) x 4 (columns) waves, one block per CU
   const int dil = VOC ? a.dil : 1;
   constexpr int BK = 64;
@@ -550,6 +556,23 @@ void conv_gemm_halo(GldsArgs a) {
     for (int i = 0; i < BW; ++i)
       glds16(b_src[i] ? b_src[i] + k0 : zero, Bs + slot * B_E + (wave * BW + i) * 8 * BK);
   };
+  // PIPE: one k-half (ks) of step (j, slot, aslot) into a register set, and its MFMAs
+  auto frag_ld = [&](int j, int slot, int aslot, int ks, bf16x8g (&fa)[MI], bf16x8g (&fb)[NI]) {
+    const int ha = a_row + j * dil, sa = ha & 7;
+    const u16* pa = As + aslot * A_E + ha * BK + ((ks * 4 + g) ^ sa) * 8;
+    const u16* pb = Bs + slot * B_E + b_off[ks];
+#pragma unroll
+    for (int i = 0; i < MI; ++i) fa[i] = *reinterpret_cast<const bf16x8g*>(pa + i * 16 * BK);
+#pragma unroll
+    for (int jj = 0; jj < NI; ++jj) fb[jj] = *reinterpret_cast<const bf16x8g*>(pb + jj * 16 * BK);
+  };
+  auto mfma_half = [&](const bf16x8g (&fa)[MI], const bf16x8g (&fb)[NI]) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int jj = 0; jj < NI; ++jj)
+        acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[jj], acc[i][jj], 0, 0, 0);
+  };
   auto compute = [&](int j, int slot, int aslot) {
     if (half_pad) return;
     // fragment rows differ by multiples of 16, so one swizzle serves all of them.  All 16
@@ -588,6 +611,82 @@ void conv_gemm_halo(GldsArgs a) {
           __builtin_amdgcn_s_barrier();
         }
       }
+    } else if constexpr (PIPE) {
+      // Fragment-pipelined 2-slot loop.  Step s = (cb, j) reads weight slot s & 1 and halo slot
+      // cb & 1 as two k-halves held in two register sets: set 1 (s, ks 1) is read while set 0's
+      // MFMAs issue; then ONE barrier, after which set 0 is refilled with step s + 1's first
+      // half under set 1's MFMAs -- a wave never waits on LDS right after the barrier.
+      // At the barrier of step s every wave has retired all its reads of step s (lgkmcnt(0)),
+      // so weight slot s & 1 takes tile s + 2 and, after cb's last tap, halo slot cb & 1 takes
+      // channel block cb + 2.  Tile s + 1 (and its halo, issued earlier) must have landed:
+      // it was issued at the previous barrier, followed at most by one halo (`pend` pieces of
+      // this wave), and loads retire in issue order.  A wave whose rows are all padding runs
+      // the same loads and barriers without fragments or MFMAs (a separate loop body, so the
+      // compute body has no per-step branches for the wait-count analysis to merge).
+      const int S = ncb * a.taps;
+      issue_a(0, 0);
+      issue_b(0, 0, 0);
+      issue_b(0, 1, 1);  // taps >= 2: step 1 = (0, 1)
+      int pend0 = 0;
+      if (ncb > 1) {
+        issue_a(1, 1);
+        pend0 = qa;
+      }
+      vm_wait_n(BW + pend0);  // halo 0 and weight tile 0 landed
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      auto pipe_loop = [&](auto with_mfma) {
+        constexpr bool C = decltype(with_mfma)::value;
+        bf16x8g fa0[MI], fb0[NI], fa1[MI], fb1[NI];
+        if constexpr (C) frag_ld(0, 0, 0, 0, fa0, fb0);
+        int cb = 0, j = 0, pend = pend0;
+        // steps 0 .. S-2 (the last step, with no successor, is peeled below: a loop body whose
+        // barrier half were conditional would merge two wait states before set 1's MFMAs)
+        for (int s = 0; s + 1 < S; ++s) {
+          const bool last_tap = j + 1 == a.taps;
+          const int jn = last_tap ? 0 : j + 1, cbn = last_tap ? cb + 1 : cb;
+          // set 0 landed under the previous step's second half (free wait).  The builtin form
+          // (not inline asm) lets the compiler's wait-count pass see it: with 2 x 10 reads in
+          // flight (beyond the 15-deep LDS counter) it would otherwise wait for set 1 as well
+          // before set 0's MFMAs.
+          __builtin_amdgcn_s_waitcnt(kLgkm0);
+          if constexpr (C) {
+            frag_ld(j, s & 1, cb & 1, 1, fa1, fb1);
+            mfma_half(fa0, fb0);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          vm_wait_n(pend);
+          __builtin_amdgcn_s_waitcnt(kLgkm0);
+          __builtin_amdgcn_s_barrier();
+          __builtin_amdgcn_sched_barrier(0);
+          pend = 0;
+          if (s + 2 < S) {
+            const bool l2 = jn + 1 == a.taps;
+            issue_b(l2 ? cbn + 1 : cbn, l2 ? 0 : jn + 1, s & 1);
+          }
+          if (last_tap && cb + 2 < ncb) {
+            issue_a(cb + 2, cb & 1);
+            pend = qa;
+          }
+          if constexpr (C) {
+            frag_ld(jn, (s + 1) & 1, cbn & 1, 0, fa0, fb0);
+            mfma_half(fa1, fb1);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          cb = cbn;
+          j = jn;
+        }
+        if constexpr (C) {
+          __builtin_amdgcn_s_waitcnt(kLgkm0);
+          frag_ld(j, (S - 1) & 1, cb & 1, 1, fa1, fb1);
+          mfma_half(fa0, fb0);
+          mfma_half(fa1, fb1);
+        }
+      };
+      if (half_pad) pipe_loop(std::false_type{});
+      else pipe_loop(std::true_type{});
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
     } else if (BST == 2 && a.halo_db) {
       // Step s = (cb, j) reads halo slot cb & 1 and weight slot s & 1.  Issue order per step
       // (after the barrier): weight tile s + 1, then -- at j == 0 -- the halo of channel block
@@ -1371,6 +1470,7 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
              taps, pad, K, bias, flags, aux, ld_aux, 0, 0, vec, 1, lens,
              ve.dil, ve.alpha, ve.scale, (u16*)ve.y2, ve.alpha2};
   a.halo_db = g_tune[FS2_TUNE_HALO_DB] > 0 ? 1 : 0;
+  const bool pipe = g_tune[FS2_TUNE_HALO_PIPE] >= 0;  // step A/B: 8.46 -> 8.39 ms
   const bool tapaligned = c_in % 64 == 0;
   const bool voc = ve.dil != 1 || (flags & (FS2_EPI_LRELU | FS2_EPI_ACC_Y | FS2_EPI_Y2)) || !y;
   const int64_t big = ((rows + 127) / 128) * ((c_out + 127) / 128);
@@ -1422,6 +1522,7 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
     const unsigned grid = (unsigned)(a.tiles_m * a.tiles_n);
     if (h8 == 5) conv_gemm_halo<256, 128, 3, 16, false, 8><<<grid, 512, 0, st>>>(a);
     else if (h8 == 6) conv_gemm_halo<128, 128, 3, 16, false, 8><<<grid, 512, 0, st>>>(a);
+    else if (pipe) conv_gemm_halo<256, 128, 2, 16, false, 8, true><<<grid, 512, 0, st>>>(a);
     else conv_gemm_halo<256, 128, 2, 16, false, 8><<<grid, 512, 0, st>>>(a);
     return launch_status("fs2_conv_gemm(bf16)");
   }
@@ -1438,6 +1539,11 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
   if (hx64) conv_gemm_halo<BM_, BN_, 2, 64, true><<<grid, 256, 0, st>>>(a);        \
   else if (voc) conv_gemm_halo<BM_, BN_, 2, 16, true><<<grid, 256, 0, st>>>(a);    \
   else conv_gemm_halo<BM_, BN_, BST_, 16, false><<<grid, 256, 0, st>>>(a);
+#define FS2_HALO2(BM_, BN_)                                                                  \
+  if (hx64) conv_gemm_halo<BM_, BN_, 2, 64, true><<<grid, 256, 0, st>>>(a);                  \
+  else if (voc) conv_gemm_halo<BM_, BN_, 2, 16, true><<<grid, 256, 0, st>>>(a);              \
+  else if (pipe) conv_gemm_halo<BM_, BN_, 2, 16, false, 4, true><<<grid, 256, 0, st>>>(a);   \
+  else conv_gemm_halo<BM_, BN_, 2, 16, false><<<grid, 256, 0, st>>>(a);
     if (g_tune[FS2_TUNE_NT_HALO] == 3) {  // single-buffered weight tile (A/B experiments)
       if (halo_wide && halo_bm == 128) { FS2_HALO(128, 128, 1) }
       else if (halo_wide) { FS2_HALO(64, 128, 1) }
@@ -1461,20 +1567,21 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
           halo_splitk_reduce<128><<<(unsigned)((n8 + 255) / 256 < 2048 ? (n8 + 255) / 256 : 2048),
                                     256, 0, st>>>(a);
         } else {
-          FS2_HALO(128, 128, 2)
+          FS2_HALO2(128, 128)
         }
-      } else if (halo_wide) { FS2_HALO(64, 128, 2) }
+      } else if (halo_wide) { FS2_HALO2(64, 128) }
       else if (halo_bm == 128) {
         // a forced split count (FS2_TUNE_HALO_SPLITK > 0) also applies to full 128x64 grids
         const int kz = g_tune[FS2_TUNE_HALO_SPLITK] > 0 ? halo_splitk(a, grid, voc, hx64, st) : 1;
         if (kz > 1) {
           a.kz = kz;
-          conv_gemm_halo<128, 64, 2, 16, false><<<grid * kz, 256, 0, st>>>(a);
+          if (pipe) conv_gemm_halo<128, 64, 2, 16, false, 4, true><<<grid * kz, 256, 0, st>>>(a);
+          else conv_gemm_halo<128, 64, 2, 16, false><<<grid * kz, 256, 0, st>>>(a);
           const int64_t n8 = rows * (c_out / 8);
           halo_splitk_reduce<128><<<(unsigned)((n8 + 255) / 256 < 2048 ? (n8 + 255) / 256 : 2048),
                                     256, 0, st>>>(a);
         } else {
-          FS2_HALO(128, 64, 2)
+          FS2_HALO2(128, 64)
         }
       } else {
         // under-filled 64x64 grid: with 128-row utterance multiples, 128x64 tiles split kz ways
@@ -1487,22 +1594,25 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
         const int kz = kz2 > 1 ? 1 : halo_splitk(a, grid, voc, hx64, st);
         if (kz2 > 1) {
           a2.kz = kz2;
-          conv_gemm_halo<128, 64, 2, 16, false><<<grid2 * kz2, 256, 0, st>>>(a2);
+          if (pipe) conv_gemm_halo<128, 64, 2, 16, false, 4, true><<<grid2 * kz2, 256, 0, st>>>(a2);
+          else conv_gemm_halo<128, 64, 2, 16, false><<<grid2 * kz2, 256, 0, st>>>(a2);
           const int64_t n8 = rows * (c_out / 8);
           halo_splitk_reduce<128><<<(unsigned)((n8 + 255) / 256 < 2048 ? (n8 + 255) / 256 : 2048),
                                     256, 0, st>>>(a2);
         } else if (kz > 1) {
           a.kz = kz;
-          conv_gemm_halo<64, 64, 2, 16, false><<<grid * kz, 256, 0, st>>>(a);
+          if (pipe) conv_gemm_halo<64, 64, 2, 16, false, 4, true><<<grid * kz, 256, 0, st>>>(a);
+          else conv_gemm_halo<64, 64, 2, 16, false><<<grid * kz, 256, 0, st>>>(a);
           const int64_t n8 = rows * (c_out / 8);
           halo_splitk_reduce<64><<<(unsigned)((n8 + 255) / 256 < 2048 ? (n8 + 255) / 256 : 2048),
                                    256, 0, st>>>(a);
         } else {
-          FS2_HALO(64, 64, 2)
+          FS2_HALO2(64, 64)
         }
       }
     }
 #undef FS2_HALO
+#undef FS2_HALO2
   } else if (big >= 512) {
     a.tiles_m = (int)((rows + 127) / 128);
     a.tiles_n = (int)((c_out + 127) / 128);

@@ -1,7 +1,10 @@
 """Time the k=1 projection GEMMs of the FFT blocks alone at their step shapes and epilogues
 (SYN-48, utterance lengths passed as in the step), with compulsory HBM bytes and GB/s.
 
-    python scripts/k1_bench.py [--reps 20]
+    python scripts/k1_bench.py [--reps 20] [--ab KNOB=V0/V1]
+
+--ab: every shape under fs2_set_tuning(KNOB, V0) and (KNOB, V1), alternating three times
+(best of each), with a bitwise comparison of the two outputs.
 """
 import importlib
 import os
@@ -123,8 +126,51 @@ def wgrad_set(reps):
           f"{6 * tot[512] + 4 * tot[128]:.0f} us", flush=True)
 
 
+def ab(spec, reps):
+    knob, vals = spec.split("=")
+    v0, v1 = (int(v) for v in vals.split("/"))
+    knob = int(knob)
+    tot = {v0: 0.0, v1: 0.0}
+    for name, T, cin, cout, kind in SHAPES:
+        M = 48 * T
+        x = torch.randn(M, cin, device=dev).to(bf)
+        w = (torch.randn(cout, cin, device=dev) * 0.05).to(bf)
+        b = torch.randn(cout, device=dev)
+        aux = torch.randn(M, cout, device=dev).to(bf if kind == "relumask_bf16" else torch.float32)
+        odt = bf if kind.endswith("bf16") else torch.float32
+        outs = {v: torch.empty(M, cout, device=dev, dtype=odt) for v in (v0, v1)}
+        kw = {"bias_bf16": dict(bias=b), "bias_f32": dict(bias=b),
+              "relumask_bf16": dict(flags=K.EPI_RELU_MASK_AUX, aux=aux), "plain_bf16": {},
+              "addaux_f32": dict(flags=K.EPI_ADD_AUX, aux=aux)}[kind]
+        res = {v0: [], v1: []}
+        for v in (v0, v1, v0, v1, v0, v1):
+            K.lib.fs2_set_tuning(knob, v)
+            run = lambda: K.conv_gemm(x, w, M, T, cin, cout, 1, 0, out=outs[v], lens=LENS[T], **kw)
+            for _ in range(10):
+                run()
+            torch.cuda.synchronize()
+            s_, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s_.record()
+            for _ in range(reps):
+                run()
+            e.record()
+            torch.cuda.synchronize()
+            res[v].append(s_.elapsed_time(e) / reps * 1e3)
+        K.lib.fs2_set_tuning(knob, 0)
+        t0, t1 = min(res[v0]), min(res[v1])
+        cnt = 6 if T == 512 else 4
+        tot[v0] += t0 * cnt
+        tot[v1] += t1 * cnt
+        print(f"{name:16s} [{knob}={v0}] {t0:6.1f} us  [{knob}={v1}] {t1:6.1f} us  "
+              f"bitwise {torch.equal(outs[v0], outs[v1])}", flush=True)
+    print(f"per step: [{knob}={v0}] {tot[v0]:.0f} us  [{knob}={v1}] {tot[v1]:.0f} us", flush=True)
+
+
 def main():
     reps = int(sys.argv[sys.argv.index("--reps") + 1]) if "--reps" in sys.argv else 20
+    if "--ab" in sys.argv:
+        ab(sys.argv[sys.argv.index("--ab") + 1], reps)
+        return
     if "--probe" in sys.argv:  # one shape, 10 launches (PMC passes): --probe <name>
         i = sys.argv.index("--probe")
         name = sys.argv[i + 1]

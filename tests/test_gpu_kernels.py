@@ -551,6 +551,18 @@ def test_conv_gemm_bf16_halo(B, T, cin, cout, k):
                 aux = rnd(B * T, cin, seed=45)
                 dx = K.conv_gemm(dy, wb, B * T, T, cout, cin, k, pad, flags=K.EPI_ADD_AUX, aux=aux)
                 close(dx, xr.grad + aux, 1e-5)
+                # FS2_TUNE_HALO_PIPE: the fragment-pipelined loop (default) issues the same
+                # MFMAs in the same order as the read-after-barrier loop: bitwise equal
+                K.lib.fs2_set_tuning(11, -1)
+                try:
+                    yl0 = K.conv_gemm(x, wf, B * T, T, cin, cout, k, pad, bias=b, lens=lens)
+                    dx0 = K.conv_gemm(dy, wb, B * T, T, cout, cin, k, pad, flags=K.EPI_ADD_AUX,
+                                      aux=aux, lens=lens)
+                finally:
+                    K.lib.fs2_set_tuning(11, 0)
+                dx1 = K.conv_gemm(dy, wb, B * T, T, cout, cin, k, pad, flags=K.EPI_ADD_AUX,
+                                  aux=aux, lens=lens)
+                assert torch.equal(yl0, yl) and torch.equal(dx0, dx1)
     finally:
         K.lib.fs2_set_tuning(6, 0)
 

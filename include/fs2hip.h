@@ -215,9 +215,11 @@ int fs2_weight_prep_batch(int dtype, const int64_t* jobs, int n_jobs, int64_t n_
  *   FS2_TUNE_HALO_SPLITK   64x64 halo fwd/dX on an under-filled grid (long-K encoder data
  *                          gradient): 0 = automatic channel-block split (128x64 tiles when
  *                          T % 128 == 0), -1 = off, -2 = 64x64 tiles only, n = n splits
- *   FS2_TUNE_ATTN          bf16 attention at T >= 256: 0 = two 16-row groups per wave in the
- *                          forward, dQ (delta fused) and dK/dV kernels (automatic), -1 = one
- *                          group everywhere, 1 = two groups in the forward and dQ only
+ *   FS2_TUNE_ATTN          bf16 attention: 0 = two 16-row groups per wave in the forward
+ *                          and dQ (delta fused) kernels at T >= 256, one 16-key group per wave
+ *                          at two workgroups per CU in dK/dV (automatic), -1 = one group
+ *                          everywhere, 1 = as 0 with the one-workgroup-per-CU dK/dV build,
+ *                          2 = two groups in dK/dV too, 3 = dK/dV at three workgroups per CU
  *   FS2_TUNE_HALO_DB       halo fwd/dX kernel, 2-slot weight ring: 0 = one halo stage, loaded
  *                          at each channel block (default), 1 = double-buffered halo stage
  *                          (the next channel block's rows in flight; A/B within run noise)

@@ -319,7 +319,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_bf16_g1(const u16* __restrict
   }
 }
 
-__global__ __launch_bounds__(256) void attn_bwd_dkdv_bf16_g1(const u16* __restrict__ qkv,
+template <int MINB>
+__global__ __launch_bounds__(256, MINB) void attn_bwd_dkdv_bf16_g1(const u16* __restrict__ qkv,
                                                           const u16* __restrict__ d_o,
                                                           const float* __restrict__ lse,
                                                           const float* __restrict__ delta,
@@ -778,12 +779,21 @@ int attn_bwd_bf16_launch(const void* qkv, const void* o, const void* d_o, const 
     attn_bwd_dq_bf16_g1<<<grid1, 256, 0, st>>>((const u16*)qkv, (const u16*)d_o, lse, ws, (u16*)d_qkv,
                                                lens, (int)seq_len, heads, scale);
   }
-  if (seq_len >= 256 && tune != -1 && tune != 1)
+  // dK/dV: one 16-key group per wave at two workgroups per CU (221 VGPRs) by default --
+  // decoder backward 99 -> 87 us against the two-group kernel, whose 415 registers allow one
+  // workgroup per CU (384 workgroups = 1.5 rounds of the CUs)
+  if (seq_len >= 256 && tune == 2)
     attn_bwd_dkdv_bf16<4><<<grid2, 256, 0, st>>>((const u16*)qkv, (const u16*)d_o, lse, ws, (u16*)d_qkv,
                                                  lens, (int)seq_len, heads, scale);
+  else if (tune == 3)
+    attn_bwd_dkdv_bf16_g1<3><<<grid1, 256, 0, st>>>((const u16*)qkv, (const u16*)d_o, lse, ws,
+                                                    (u16*)d_qkv, lens, (int)seq_len, heads, scale);
+  else if (tune == -1 || tune == 1)
+    attn_bwd_dkdv_bf16_g1<1><<<grid1, 256, 0, st>>>((const u16*)qkv, (const u16*)d_o, lse, ws,
+                                                    (u16*)d_qkv, lens, (int)seq_len, heads, scale);
   else
-    attn_bwd_dkdv_bf16_g1<<<grid1, 256, 0, st>>>((const u16*)qkv, (const u16*)d_o, lse, ws, (u16*)d_qkv,
-                                                 lens, (int)seq_len, heads, scale);
+    attn_bwd_dkdv_bf16_g1<2><<<grid1, 256, 0, st>>>((const u16*)qkv, (const u16*)d_o, lse, ws,
+                                                    (u16*)d_qkv, lens, (int)seq_len, heads, scale);
   return launch_status("fs2_attn_bwd(bf16)");
 }
 

@@ -359,7 +359,7 @@ def test_conv_gemm_bf16(B, T, cin, cout, k):
     close(db2, dy.float().sum(0) + 1, 1e-5)
 
 
-@pytest.mark.parametrize("knob", [0, 1, -1])  # FS2_TUNE_ATTN: two-group / mixed / one-group kernels
+@pytest.mark.parametrize("knob", [0, 1, -1, 2])  # FS2_TUNE_ATTN: kernel variants (fs2hip.h)
 @pytest.mark.parametrize("B,T,lens", [(2, 64, [64, 40]), (3, 130, [130, 77, 1]),
                                       (2, 512, [512, 300]), (3, 300, [300, 129, 64])])
 def test_attention_bf16(B, T, lens, knob):

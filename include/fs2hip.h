@@ -297,6 +297,13 @@ int fs2_ln_bwd(int dtype, const float* dout, const float* ddot, const float* dot
                float* dy,
                void* dy_t, float* dres, int dres_add, float* dgamma, float* dbeta, float* dw_dot,
                float* db_dot, float* dbias_in, float* ws, int64_t ws_bytes, void* stream);
+/* The parameter-gradient half of fs2_ln_bwd on its own: fs2_ln_bwd called with dgamma, dbeta,
+ * dw_dot, db_dot and dbias_in all NULL leaves its per-block partial sums in ws; this sums
+ * them into the given gradients (+=, fixed order) -- e.g. on another stream, off the data-
+ * gradient chain.  has_ddot: fs2_ln_bwd was called with ddot (the dw_dot / db_dot partials
+ * exist).  ws must hold fs2_ln_bwd's partials of the same rows.                          */
+int fs2_ln_bwd_final(int64_t rows, int d, const float* ws, int has_ddot, float* dgamma,
+                     float* dbeta, float* dw_dot, float* db_dot, float* dbias_in, void* stream);
 
 /* ---------------------------------------------------------------- BatchNorm (PostNet)
  * Training-mode BatchNorm1d over all rows (padded frames included) + optional tanh +

@@ -565,14 +565,24 @@ int fs2_ln_bwd(int dtype, const float* dout, const float* ddot, const float* dot
   else ln_bwd_f32<false><<<(unsigned)nblk, LN_BWD_WAVES * 64, 0, st>>>(a);
   int rc = launch_status("fs2_ln_bwd");
   if (rc) return rc;
+  return fs2_ln_bwd_final(rows, d, ws, ddot != nullptr, dgamma, dbeta, dw_dot, db_dot, dbias_in,
+                          stream);
+}
+
+int fs2_ln_bwd_final(int64_t rows, int d, const float* ws, int has_ddot, float* dgamma,
+                     float* dbeta, float* dw_dot, float* db_dot, float* dbias_in, void* stream) {
+  FS2_CHECK_ARG(d == LN_D, "fs2_ln_bwd_final: only d = 256 is supported (got %d)", d);
+  if (rows == 0) return FS2_OK;
+  const int64_t nblk = (rows + LN_ROWS - 1) / LN_ROWS;
+  float* w = const_cast<float*>(ws);
   ColsumJobs jobs{};
   jobs.acc = 1;
-  if (dgamma) jobs.add(ws, nblk, LN_D, dgamma);
-  if (dbeta) jobs.add(ws + nblk * LN_D, nblk, LN_D, dbeta);
-  if (ddot && dw_dot) jobs.add(ws + 2 * nblk * LN_D, nblk, LN_D, dw_dot);
-  if (ddot && db_dot) jobs.add(ws + 4 * nblk * LN_D, nblk, 1, db_dot);
-  if (dbias_in) jobs.add(ws + 3 * nblk * LN_D, nblk, LN_D, dbias_in);
-  return colsum_final_multi_launch(jobs, st);
+  if (dgamma) jobs.add(w, nblk, LN_D, dgamma);
+  if (dbeta) jobs.add(w + nblk * LN_D, nblk, LN_D, dbeta);
+  if (has_ddot && dw_dot) jobs.add(w + 2 * nblk * LN_D, nblk, LN_D, dw_dot);
+  if (has_ddot && db_dot) jobs.add(w + 4 * nblk * LN_D, nblk, 1, db_dot);
+  if (dbias_in) jobs.add(w + 3 * nblk * LN_D, nblk, LN_D, dbias_in);
+  return colsum_final_multi_launch(jobs, as_stream(stream));
 }
 
 int64_t fs2_bn_ws_bytes(int64_t rows, int64_t c) {

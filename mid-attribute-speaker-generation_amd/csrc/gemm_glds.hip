@@ -1508,11 +1508,15 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
   if (halo_bm == 128 && seq_len % 128 != 0 && seq_len % 64 == 0) halo_bm = 64;
   // 8-wave variants (FS2_TUNE_NT_HALO 5 / 6 / 7: 256x128 3-slot / 128x128 3-slot / 256x128
   // 2-slot), one block per CU with the weight prefetch in flight across the barrier
-  // Default for the wide forward shapes (c_in <= 512, >= 512 128x128 tiles, T % 256 == 0: the
-  // decoder FFN k=9 and PostNet 512 convs): 256 x 128 two-slot, 8 waves (k=9 decoder forward
-  // 114 -> 102 us alone, scripts/halo_check.py).  FS2_TUNE_NT_HALO 1 disables it.
+  // Default for the wide forward shapes (c_in <= 256, >= 512 128x128 tiles, T % 256 == 0: the
+  // decoder FFN k=9 forward): 256 x 128 two-slot, 8 waves (k=9 decoder forward 114 -> 102 us
+  // alone, scripts/halo_check.py).  FS2_TUNE_NT_HALO 1 disables it.
   int h8 = g_tune[FS2_TUNE_NT_HALO];
-  if (h8 == 0 && big >= 512 && c_in <= 512) h8 = 7;
+  // (C_in 512 -- the PostNet convs, forward and data gradient -- run faster on the 4-wave
+  // 128 x 128 tiles: 78 -> 73 us and 84 -> 77 us alone; the 8-wave tile's 384-block grid is
+  // 1.5 rounds of the CUs there)
+  if (h8 == 9) h8 = big >= 512 && c_in <= 512 ? 7 : 0;  // the earlier rule (A/B only)
+  else if (h8 == 0 && big >= 512 && c_in <= 256) h8 = 7;
   if ((h8 == 5 || h8 == 6 || h8 == 7) && taps > 1 && (taps - 1) * ve.dil <= 16 && tapaligned &&
       !voc && seq_len % (h8 == 6 ? 128 : 256) == 0) {
     const int bm = h8 == 6 ? 128 : 256;

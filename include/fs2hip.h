@@ -228,11 +228,14 @@ int fs2_weight_prep_batch(int dtype, const int64_t* jobs, int n_jobs, int64_t n_
  *                          loop (default: the next step's LDS fragments are read under the
  *                          current step's second MFMA half; one barrier per step, mid-step),
  *                          -1 = the loop that reads all of a step's fragments after its barrier
+ *   FS2_TUNE_NT_TILE       tap-major fwd/dX kernel (k = 1 projections, odd shapes): 0 = tile
+ *                          by grid size, 1 / 2 / 3 = force 128x128 / 128x64 / 64x64
  * Process-wide; query workspace sizes after setting.                                 */
 enum { FS2_TUNE_GEMM_STAGES = 0, FS2_TUNE_WGRAD_STAGES = 1, FS2_TUNE_WGRAD_TILE = 2,
        FS2_TUNE_WGRAD_SPLITS = 3, FS2_TUNE_LEGACY_GEMM = 4, FS2_TUNE_NT_GROUP = 5,
        FS2_TUNE_NT_HALO = 6, FS2_TUNE_WGRAD_HALO = 7, FS2_TUNE_HALO_SPLITK = 8,
-       FS2_TUNE_ATTN = 9, FS2_TUNE_HALO_DB = 10, FS2_TUNE_HALO_PIPE = 11, FS2_TUNE_COUNT = 12 };
+       FS2_TUNE_ATTN = 9, FS2_TUNE_HALO_DB = 10, FS2_TUNE_HALO_PIPE = 11, FS2_TUNE_NT_TILE = 12,
+       FS2_TUNE_COUNT = 13 };
 int fs2_set_tuning(int knob, int value);
 
 /* Weight (and optionally bias) gradient, accumulated into the fp32 master-gradient layout:

@@ -1617,12 +1617,12 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
     }
 #undef FS2_HALO
 #undef FS2_HALO2
-  } else if (big >= 512) {
+  } else if ((big >= 512 && g_tune[FS2_TUNE_NT_TILE] == 0) || g_tune[FS2_TUNE_NT_TILE] == 1) {
     a.tiles_m = (int)((rows + 127) / 128);
     a.tiles_n = (int)((c_out + 127) / 128);
     const int stages = tune ? tune : 1;
     FS2_NT(128, 128)
-  } else if (big >= 128) {
+  } else if ((big >= 128 && g_tune[FS2_TUNE_NT_TILE] == 0) || g_tune[FS2_TUNE_NT_TILE] == 2) {
     a.tiles_m = (int)((rows + 127) / 128);
     a.tiles_n = (int)((c_out + 63) / 64);
     const int stages = tune ? tune : 2;

@@ -21,6 +21,7 @@ order so gradient buckets complete front-to-back; kernels accumulate weight grad
 straight into the flat gradient buffer (``param.grad`` are views of it).
 """
 import math
+import os
 
 import numpy as np
 import torch
@@ -917,30 +918,43 @@ class FastSpeech2(nn.Module):
         K.seed_next(self._seed_state)
         return self._seed_state[2:3].clone()  # this forward's key (backward re-reads it)
 
-    def prep_weights(self):
-        """Re-lay out (and cast) every weight for the GEMMs: one batched launch per step; the
-        job table (pointers into the arena and the compute-weight buffers) is built once."""
+    def prep_weights(self, side=None):
+        """Re-lay out (and cast) every weight for the GEMMs, batched launches; the job tables
+        (pointers into the arena and the compute-weight buffers) are built once.  With a side
+        stream the encoder's weights are prepared on the current stream and everything after
+        them (variance predictors, decoder, PostNet, mel head) on ``side``, under the
+        encoder's forward; the caller joins ``side`` before the first of those layers."""
         cdt = self.compute_dtype
         if self._prep is None or self._prep[0] != cdt:
-            jobs = []
-            for b in list(self.encoder.layer_stack) + list(self.decoder.layer_stack):
-                b.prep(cdt, jobs)
+            enc_jobs, rest = [], []
+            for b in self.encoder.layer_stack:
+                b.prep(cdt, enc_jobs)
             va = self.variance_adaptor
             for v in (va.duration_predictor, va.pitch_predictor, va.energy_predictor):
-                v.prep(cdt, jobs)
-            self.postnet.prep(cdt, jobs)
-            _linear_prep(self.mel_linear, cdt, jobs=jobs)
+                v.prep(cdt, rest)
+            for b in self.decoder.layer_stack:
+                b.prep(cdt, rest)
+            self.postnet.prep(cdt, rest)
+            _linear_prep(self.mel_linear, cdt, jobs=rest)
             ct = K.lib.fs2_weight_prep_tile_channels(K.code(cdt))
-            rows, first = [], 0
-            for (w, co, ci, k, wf, wb) in jobs:
-                assert k <= 9
-                n = -(-co // 64) * -(-ci // ct)
-                rows.append([w, co, ci, k, wf, wb, first, first + n])
-                first += n
-            table = torch.tensor(rows, dtype=torch.int64).to(self._arena.flat.device)
-            self._prep = (cdt, table, len(rows), first)
-        cdt, table, n, n_tiles = self._prep
-        K.lib.fs2_weight_prep_batch(K.code(cdt), K.ptr(table), n, n_tiles, K.stream())
+
+            def table(jobs):
+                rows, first = [], 0
+                for (w, co, ci, k, wf, wb) in jobs:
+                    assert k <= 9
+                    n = -(-co // 64) * -(-ci // ct)
+                    rows.append([w, co, ci, k, wf, wb, first, first + n])
+                    first += n
+                t = torch.tensor(rows, dtype=torch.int64).to(self._arena.flat.device)
+                return t, len(rows), first
+            self._prep = (cdt, table(enc_jobs), table(rest))
+        cdt, (t0, n0, k0), (t1, n1, k1) = self._prep
+        K.lib.fs2_weight_prep_batch(K.code(cdt), K.ptr(t0), n0, k0, K.stream())
+        if side is None:
+            K.lib.fs2_weight_prep_batch(K.code(cdt), K.ptr(t1), n1, k1, K.stream())
+        else:
+            K.lib.fs2_stream_wait(side.cuda_stream, K.stream())
+            K.lib.fs2_weight_prep_batch(K.code(cdt), K.ptr(t1), n1, k1, side.cuda_stream)
 
     # -- forward ----------------------------------------------------------------------
     def forward(self, speakers, texts, src_lens, max_src_len, mels=None, mel_lens=None,
@@ -958,11 +972,12 @@ class FastSpeech2(nn.Module):
                                        max_mel_len, p_targets, e_targets, d_targets, p_control,
                                        e_control, d_control, accents, speaker_meta=speaker_meta)
         self.arena()
-        self.prep_weights()
+        side = self.side_stream() if self.training else None
+        self.prep_weights(side)  # A/B: 8.171 -> 8.152 ms against one launch on the main stream
         seed = self._step_seed() if (self.training and self.dropout) else 0
         ctx = StepCtx(seed, self.training, self.dropout, self.compute_dtype)
         ctx.hook = self._hooks["grad"]
-        ctx.side = self.side_stream() if self.training else None
+        ctx.side = side
         ctx.ws_cache = self._ws_cache
         B, Ts = texts.shape
         max_src_len = int(max_src_len)
@@ -979,6 +994,8 @@ class FastSpeech2(nn.Module):
                               B, Ts, ctx)
         speaker_emb_s = K.embedding_fwd(speakers.contiguous(), self.speaker_emb.weight)
         gmm = self.speaker_enc(speaker_meta)
+        if side is not None:  # the weights prepared on the side stream (prep_weights)
+            K.lib.fs2_stream_wait(K.stream(), side.cuda_stream)
         x_lr, log_d, p, e, mel_len, x_lr_t = VarianceAdaptorFn.apply(
             tok, enc, self, speakers.contiguous(), src_lens, p_targets, e_targets, d_targets, B, Ts,
             T_dec, ctx)

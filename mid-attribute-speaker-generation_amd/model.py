@@ -21,7 +21,6 @@ order so gradient buckets complete front-to-back; kernels accumulate weight grad
 straight into the flat gradient buffer (``param.grad`` are views of it).
 """
 import math
-import os
 
 import numpy as np
 import torch

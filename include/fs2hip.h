@@ -227,7 +227,9 @@ int fs2_weight_prep_batch(int dtype, const int64_t* jobs, int n_jobs, int64_t n_
  *   FS2_TUNE_HALO_PIPE     halo fwd/dX kernel, 2-slot weight ring: 0 = fragment-pipelined
  *                          loop (default: the next step's LDS fragments are read under the
  *                          current step's second MFMA half; one barrier per step, mid-step),
- *                          -1 = the loop that reads all of a step's fragments after its barrier
+ *                          -1 = the loop that reads all of a step's fragments after its barrier,
+ *                          2 = pipelined without the half-width body for waves whose second
+ *                          half of rows is past the utterance length (lens given)
  *   FS2_TUNE_NT_TILE       tap-major fwd/dX kernel (k = 1 projections, odd shapes): 0 = tile
  *                          by grid size, 1 / 2 / 3 = force 128x128 / 128x64 / 64x64
  * Process-wide; query workspace sizes after setting.                                 */

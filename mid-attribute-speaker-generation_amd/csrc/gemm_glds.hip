@@ -57,6 +57,7 @@ struct GldsArgs {
   float alpha2;
   int kz;               // halo kernel: channel-block splits (0/1 = none; see halo_splitk_reduce)
   int halo_db;          // halo kernel, BST == 2: double-buffered halo stage (FS2_TUNE_HALO_DB)
+  int no_trim;          // halo kernel, pipelined loop: no half-width body (FS2_TUNE_HALO_PIPE 2)
   float* slab;          // kz > 1: [kz][M][N] fp32 partial products
 };
 
@@ -512,6 +513,14 @@ void conv_gemm_halo(GldsArgs a) {
   // row limits of another meaning: the whole padded utterance is staged there.
   const int64_t ulen = (!VOC && a.lens) ? (a.lens[m0 / a.T] < a.T ? a.lens[m0 / a.T] : a.T) : a.T;
   const int64_t u1 = u0 + ulen < a.M ? u0 + ulen : a.M;
+  // this wave's 16-row fragments holding a row below the utterance's length (input rows past
+  // it are staged as zeros; outputs past it are masked downstream of the FFT / variance-
+  // predictor convs -- the only lens users of this kernel)
+  int mi_act = MI;
+  if (!VOC && a.lens && !a.no_trim) {
+    const int64_t nv = u1 - (m0 + wm * (BM / 2));
+    mi_act = nv <= 0 ? 0 : nv >= BM / 2 ? MI : (int)((nv + 15) / 16);
+  }
   // halo piece p = wave + NWAVE q: rows h = 8 p + lrow, global row m0 - pad + h
   const u16* h_src[QMAX];
 #pragma unroll
@@ -557,18 +566,23 @@ void conv_gemm_halo(GldsArgs a) {
       glds16(b_src[i] ? b_src[i] + k0 : zero, Bs + slot * B_E + (wave * BW + i) * 8 * BK);
   };
   // PIPE: one k-half (ks) of step (j, slot, aslot) into a register set, and its MFMAs
-  auto frag_ld = [&](int j, int slot, int aslot, int ks, bf16x8g (&fa)[MI], bf16x8g (&fb)[NI]) {
+  // (nact: compile-time count of this wave's 16-row fragments that hold a valid row; the
+  // others are neither read nor multiplied -- see mi_act below)
+  auto frag_ld = [&](auto nact, int j, int slot, int aslot, int ks, bf16x8g (&fa)[MI],
+                     bf16x8g (&fb)[NI]) {
+    constexpr int NACT = decltype(nact)::value;
     const int ha = a_row + j * dil, sa = ha & 7;
     const u16* pa = As + aslot * A_E + ha * BK + ((ks * 4 + g) ^ sa) * 8;
     const u16* pb = Bs + slot * B_E + b_off[ks];
 #pragma unroll
-    for (int i = 0; i < MI; ++i) fa[i] = *reinterpret_cast<const bf16x8g*>(pa + i * 16 * BK);
+    for (int i = 0; i < NACT; ++i) fa[i] = *reinterpret_cast<const bf16x8g*>(pa + i * 16 * BK);
 #pragma unroll
     for (int jj = 0; jj < NI; ++jj) fb[jj] = *reinterpret_cast<const bf16x8g*>(pb + jj * 16 * BK);
   };
-  auto mfma_half = [&](const bf16x8g (&fa)[MI], const bf16x8g (&fb)[NI]) {
+  auto mfma_half = [&](auto nact, const bf16x8g (&fa)[MI], const bf16x8g (&fb)[NI]) {
+    constexpr int NACT = decltype(nact)::value;
 #pragma unroll
-    for (int i = 0; i < MI; ++i)
+    for (int i = 0; i < NACT; ++i)
 #pragma unroll
       for (int jj = 0; jj < NI; ++jj)
         acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[jj], acc[i][jj], 0, 0, 0);
@@ -635,10 +649,10 @@ void conv_gemm_halo(GldsArgs a) {
       vm_wait_n(BW + pend0);  // halo 0 and weight tile 0 landed
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
-      auto pipe_loop = [&](auto with_mfma) {
-        constexpr bool C = decltype(with_mfma)::value;
+      auto pipe_loop = [&](auto nact) {
+        constexpr bool C = decltype(nact)::value > 0;
         bf16x8g fa0[MI], fb0[NI], fa1[MI], fb1[NI];
-        if constexpr (C) frag_ld(0, 0, 0, 0, fa0, fb0);
+        if constexpr (C) frag_ld(nact, 0, 0, 0, 0, fa0, fb0);
         int cb = 0, j = 0, pend = pend0;
         // steps 0 .. S-2 (the last step, with no successor, is peeled below: a loop body whose
         // barrier half were conditional would merge two wait states before set 1's MFMAs)
@@ -651,8 +665,8 @@ void conv_gemm_halo(GldsArgs a) {
           // before set 0's MFMAs.
           __builtin_amdgcn_s_waitcnt(kLgkm0);
           if constexpr (C) {
-            frag_ld(j, s & 1, cb & 1, 1, fa1, fb1);
-            mfma_half(fa0, fb0);
+            frag_ld(nact, j, s & 1, cb & 1, 1, fa1, fb1);
+            mfma_half(nact, fa0, fb0);
           }
           __builtin_amdgcn_sched_barrier(0);
           vm_wait_n(pend);
@@ -669,8 +683,8 @@ void conv_gemm_halo(GldsArgs a) {
             pend = qa;
           }
           if constexpr (C) {
-            frag_ld(jn, (s + 1) & 1, cbn & 1, 0, fa0, fb0);
-            mfma_half(fa1, fb1);
+            frag_ld(nact, jn, (s + 1) & 1, cbn & 1, 0, fa0, fb0);
+            mfma_half(nact, fa1, fb1);
           }
           __builtin_amdgcn_sched_barrier(0);
           cb = cbn;
@@ -678,13 +692,16 @@ void conv_gemm_halo(GldsArgs a) {
         }
         if constexpr (C) {
           __builtin_amdgcn_s_waitcnt(kLgkm0);
-          frag_ld(j, (S - 1) & 1, cb & 1, 1, fa1, fb1);
-          mfma_half(fa0, fb0);
-          mfma_half(fa1, fb1);
+          frag_ld(nact, j, (S - 1) & 1, cb & 1, 1, fa1, fb1);
+          mfma_half(nact, fa0, fb0);
+          mfma_half(nact, fa1, fb1);
         }
       };
-      if (half_pad) pipe_loop(std::false_type{});
-      else pipe_loop(std::true_type{});
+      // with lens, a wave whose rows past the first half of its fragments are all padding
+      // runs the half-width body (their outputs are masked downstream, as for half_pad)
+      if (half_pad) pipe_loop(std::integral_constant<int, 0>{});
+      else if (mi_act <= MI / 2) pipe_loop(std::integral_constant<int, MI / 2>{});
+      else pipe_loop(std::integral_constant<int, MI>{});
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
     } else if (BST == 2 && a.halo_db) {
@@ -1470,6 +1487,7 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
              taps, pad, K, bias, flags, aux, ld_aux, 0, 0, vec, 1, lens,
              ve.dil, ve.alpha, ve.scale, (u16*)ve.y2, ve.alpha2};
   a.halo_db = g_tune[FS2_TUNE_HALO_DB] > 0 ? 1 : 0;
+  a.no_trim = g_tune[FS2_TUNE_HALO_PIPE] == 2 ? 1 : 0;
   const bool pipe = g_tune[FS2_TUNE_HALO_PIPE] >= 0;  // step A/B: 8.46 -> 8.39 ms
   const bool tapaligned = c_in % 64 == 0;
   const bool voc = ve.dil != 1 || (flags & (FS2_EPI_LRELU | FS2_EPI_ACC_Y | FS2_EPI_Y2)) || !y;

@@ -268,10 +268,15 @@ def test_loss_curve_100_steps_vs_reference(dtype):
     assert got[-1, 0] < 0.5 * got[0, 0]  # it trains
 
 
-def test_step_vs_oracle_full_tensors():
-    """Same step on the CPU oracle: full output tensors and every parameter gradient."""
-    B, Ts = 4, 24
-    model, tr, batch = _hip_trainer(B, Ts, seed=3)
+# (1, 7, 10): a single 28-frame utterance.  Seeds are screened for ReLU kinks: with seed 5
+# a decoder FFN pre-activation is 1.2e-7 in the oracle, below the two fp32 implementations'
+# rounding difference, and its ReLU gradient flips (0.6 % on that layer's weight gradient,
+# less upstream) -- every seed 9-11 keeps all pre-activations above 1e-5.
+@pytest.mark.parametrize("B,Ts,seed", [(4, 24, 3), (1, 7, 10), (5, 40, 7)])
+def test_step_vs_oracle_full_tensors(B, Ts, seed):
+    """Same step on the CPU oracle: full output tensors and every parameter gradient (a
+    single short utterance and odd sizes included: grid edges, non-tile-multiple lengths)."""
+    model, tr, batch = _hip_trainer(B, Ts, seed=seed)
     out = model(*(batch[2:12]), accents=batch[13], speaker_meta=batch[12])
     losses = tr.Loss(batch[:12], out[:-2])
     losses[0].backward()
@@ -279,7 +284,7 @@ def test_step_vs_oracle_full_tensors():
     fs2_cpu.DROPOUT["enabled"] = False
     ref, _ = fs2_cpu.build("JVS-VCTK")
     ref.train()
-    cb = PKG.data.to_device(PKG.data.syn_batch(B, Ts, seed=3), "cpu")
+    cb = PKG.data.to_device(PKG.data.syn_batch(B, Ts, seed=seed), "cpu")
     ro = ref(*cb[2:12], accents=cb[13], speaker_meta=cb[12])
     rl = fs2_cpu.fs2_loss(cb[:12], ro[:-2])
     rl[0].backward()

@@ -167,6 +167,9 @@ def ab(spec, reps):
 
 
 def main():
+    for kv in filter(None, os.environ.get("FS2_TUNE", "").split(",")):  # "knob=value,..."
+        kn, v = kv.split("=")
+        K.lib.fs2_set_tuning(int(kn), int(v))
     reps = int(sys.argv[sys.argv.index("--reps") + 1]) if "--reps" in sys.argv else 20
     if "--ab" in sys.argv:
         ab(sys.argv[sys.argv.index("--ab") + 1], reps)

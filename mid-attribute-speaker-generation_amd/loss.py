@@ -13,7 +13,10 @@ from . import kernels as K
 
 class FS2LossFn(torch.autograd.Function):
     @staticmethod
-    def forward(fctx, mel_out, post_out, p, e, log_d, mels, p_t, e_t, d_t, src_pad, mel_pad, denoms):
+    def forward(fctx, mel_out, post_out, p, e, log_d, mels, p_t, e_t, d_t, src_pad, mel_pad, denoms,
+                g6buf):
+        fctx.set_materialize_grads(False)  # unused outputs' gradients stay None (no fills)
+        fctx.g6buf = g6buf
         T = mel_out.shape[1]
         args = (mel_out.contiguous(), post_out.contiguous(), mels.contiguous(), p.contiguous(),
                 e.contiguous(), log_d.contiguous(), p_t.contiguous().float(),
@@ -26,12 +29,20 @@ class FS2LossFn(torch.autograd.Function):
     @staticmethod
     def backward(fctx, *g):
         dev = fctx.ws.device
-        g6 = torch.stack([x.reshape(()) if x is not None else torch.zeros((), device=dev) for x in g])
+        buf = fctx.g6buf
+        if g[0] is not None and all(x is None for x in g[1:]) and buf is not None:
+            # the usual case (only the total loss back-propagated): one copy into a persistent
+            # [g, 0, 0, 0, 0, 0] buffer instead of five zero fills and a stack
+            buf[0:1].copy_(g[0].reshape(1))
+            g6 = buf
+        else:
+            g6 = torch.stack([x.reshape(()) if x is not None else torch.zeros((), device=dev)
+                              for x in g])
         a = fctx.args
         d_mel, d_post, d_p, d_e, d_d = K.fs2loss_bwd(a[0], a[1], a[2], a[3], a[4], a[5], a[6], a[7],
                                                      a[8], a[9], a[10], fctx.ws, g6.float().contiguous())
-        fctx.args = None
-        return (d_mel, d_post, d_p, d_e, d_d) + (None,) * 7
+        fctx.args = fctx.g6buf = None
+        return (d_mel, d_post, d_p, d_e, d_d) + (None,) * 8
 
 
 class FastSpeech2Loss(nn.Module):
@@ -43,12 +54,15 @@ class FastSpeech2Loss(nn.Module):
             assert preprocess_config[key]["feature"] == "phoneme_level", \
                 "frame-level variance losses are not built"
         self.denoms = None  # data-parallel: device [mel elements, phonemes] of the global batch
+        self._g6 = None  # persistent upstream-gradient vector (entries 1-5 stay zero)
 
     def forward(self, inputs, predictions):
         mels, _, _, p_t, e_t, d_t = inputs[6:12]
         (mel_out, post_out, p, e, log_d, _, src_masks, mel_masks, _, _) = predictions[:10]
+        if self._g6 is None or self._g6.device != mel_out.device:
+            self._g6 = torch.zeros(6, dtype=torch.float32, device=mel_out.device)
         return FS2LossFn.apply(mel_out, post_out, p, e, log_d, mels, p_t, e_t, d_t, src_masks,
-                               mel_masks, self.denoms)
+                               mel_masks, self.denoms, self._g6)
 
 
 class GMMMeanLogProbFn(torch.autograd.Function):

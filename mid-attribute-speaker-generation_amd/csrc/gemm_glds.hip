@@ -1090,7 +1090,14 @@ __global__ __launch_bounds__(256) void conv_wgrad_tn_glds(WgradGlds a) {
 // with the chunk swizzle ((R >> 1) & 3) << 1 and read with ds_read_b64_tr_b16 (rows
 // {4g+q} u {16+4g+q} of a 32-row step; a row offset j keeps the pair in one swizzle class).
 // Output: the same split-K slab layout (and bias slab) as conv_wgrad_tn_glds.
-template <int TAPS>
+//
+// WS = 1 (default): each wave owns 64 (o) x 16 (c) of the block tile for all taps instead of
+// a 32 x 32 quarter: the dy fragments (4 per k-step) are read once and reused by every tap,
+// and a tap costs ONE shifted x fragment for 4 MFMAs (the 32 x 32 quarter needs two for 4),
+// 26 instead of 40 fragment reads per wave and k-tile; the next tap's x fragment is read
+// under the current tap's MFMAs.  Each wave also carries the bias gradient of its 16 o rows
+// (one extra MFMA per k-step, evenly spread).  WS = 0: the 32 x 32 wave quarters of round 1.
+template <int TAPS, int WS>
 __global__ __launch_bounds__(256, 2) void conv_wgrad_halo(WgradGlds a) {
   constexpr int BO = 64, BC = 64, BK = 64, STAGES = 2;
   constexpr int HX = 8;                      // halo rows allocated (taps <= 9)
@@ -1175,16 +1182,16 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_halo(WgradGlds a) {
     }
   };
 
-  f32x4 acc[TAPS][2][2], accb[2];
+  constexpr int NA = WS ? 4 : 2, NB = WS ? 1 : 2;  // A (o) / B (c) fragments per wave
+  f32x4 acc[TAPS][NA][NB], accb[2];
 #pragma unroll
   for (int j = 0; j < TAPS; ++j)
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      acc[j][i][0] = f32x4{0.f, 0.f, 0.f, 0.f};
-      acc[j][i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
+    for (int i = 0; i < NA; ++i)
+#pragma unroll
+      for (int jj = 0; jj < NB; ++jj) acc[j][i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
   accb[0] = accb[1] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const bool do_bias = a.bslab != nullptr && tc == 0 && wn == 0;  // wave-uniform
+  const bool do_bias = a.bslab != nullptr && tc == 0 && (WS || wn == 0);  // wave-uniform
   bf16x8g ones;
 #pragma unroll
   for (int e = 0; e < 8; ++e) ones[e] = (__bf16)1.0f;
@@ -1201,6 +1208,30 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_halo(WgradGlds a) {
   auto compute = [&](int stage) {
     const u16* As = smem + stage * STAGE_E;
     const u16* Xs = As + A_E;
+    if constexpr (WS == 1) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8g fa[4], fb[2];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fa[i] = tr_frag(As, ks * 32, i * 16);
+        fb[0] = tr_frag(Xs, ks * 32, wave * 16);
+#pragma unroll
+        for (int j = 0; j < TAPS; ++j) {
+          if (j + 1 < TAPS) fb[(j + 1) & 1] = tr_frag(Xs, ks * 32 + j + 1, wave * 16);
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            acc[j][i][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j & 1], acc[j][i][0],
+                                                                   0, 0, 0);
+        }
+        if (do_bias) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (i == wave)
+              accb[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], ones, accb[0], 0, 0, 0);
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       bf16x8g fa[2];
@@ -1220,7 +1251,7 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_halo(WgradGlds a) {
         for (int i = 0; i < 2; ++i)
 #pragma unroll
           for (int jj = 0; jj < 2; ++jj)
-            acc[j][i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[jj], acc[j][i][jj], 0, 0, 0);
+            acc[j][i][jj % NB] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[jj], acc[j][i][jj % NB], 0, 0, 0);
       }
     }
   };
@@ -1229,10 +1260,10 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_halo(WgradGlds a) {
 
   if (do_bias && r16 == 0) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < (WS ? 1 : 2); ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int o = o0 + wm * 32 + i * 16 + 4 * g + r;
+        const int o = o0 + (WS ? wave * 16 : wm * 32 + i * 16) + 4 * g + r;
         a.bslab[(int64_t)z * a.Cout + o] = accb[i][r];
       }
   }
@@ -1241,13 +1272,13 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_halo(WgradGlds a) {
 #pragma unroll
   for (int j = 0; j < TAPS; ++j)
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < NA; ++i)
 #pragma unroll
-      for (int jj = 0; jj < 2; ++jj)
+      for (int jj = 0; jj < NB; ++jj)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int o = o0 + wm * 32 + i * 16 + 4 * g + r;
-          const int c = c0 + wn * 32 + jj * 16 + r16;
+          const int o = o0 + (WS ? i * 16 : wm * 32 + i * 16) + 4 * g + r;
+          const int c = c0 + (WS ? wave * 16 : wn * 32 + jj * 16) + r16;
           slab[(int64_t)o * a.Kp + (int64_t)j * a.Cin + c] = acc[j][i][jj][r];
         }
 }
@@ -1361,9 +1392,13 @@ int conv_wgrad_glds_launch(const void* dy, int64_t ldy, const void* x, int64_t l
     a.tiles_o = (int)(c_out / 64);
     a.tiles_k = (int)(c_in / 64);
     const unsigned hgrid = (unsigned)(a.tiles_o * a.tiles_k * splits);
-    if (taps == 9) conv_wgrad_halo<9><<<hgrid, 256, 0, st>>>(a);
-    else if (taps == 5) conv_wgrad_halo<5><<<hgrid, 256, 0, st>>>(a);
-    else conv_wgrad_halo<3><<<hgrid, 256, 0, st>>>(a);
+    const bool quarters = g_tune[FS2_TUNE_WGRAD_HALO] == 1;  // round-1 wave tiles (A/B)
+#define FS2_WH(T) (quarters ? conv_wgrad_halo<T, 0><<<hgrid, 256, 0, st>>>(a) \
+                            : conv_wgrad_halo<T, 1><<<hgrid, 256, 0, st>>>(a))
+    if (taps == 9) FS2_WH(9);
+    else if (taps == 5) FS2_WH(5);
+    else FS2_WH(3);
+#undef FS2_WH
   }
   const unsigned grid = (unsigned)(a.tiles_o * a.tiles_k * splits);
   const int stages = g_tune[FS2_TUNE_WGRAD_STAGES] >= 1 && g_tune[FS2_TUNE_WGRAD_STAGES] <= 4

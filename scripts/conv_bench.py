@@ -3,7 +3,7 @@ forward, data gradient and weight gradient (+ its split reduce), then the data g
 the weight gradient together on two streams as the step runs them (the weight gradients ride
 a side stream), to show what the overlap costs each.
 
-    python scripts/conv_bench.py [--reps 20] [--only dec] [--ab KNOB=V0/V1]
+    python scripts/conv_bench.py [--reps 20] [--only dec] [--ab KNOB=V0/V1] [--abw KNOB=V0/V1]
 
 --ab: forward and data gradient under fs2_set_tuning(KNOB, V0) and (KNOB, V1), alternating
 three times, with a bitwise comparison of the two outputs.
@@ -100,6 +100,47 @@ def ab(spec, reps, only):
         print(line + f"  bitwise fwd {eq_f} dgrad {eq_d}", flush=True)
 
 
+def abw(spec, reps, only):
+    """weight gradient (+ reduce) under two knob values, alternating; dW compared bitwise"""
+    knob, vals = spec.split("=")
+    v0, v1 = (int(v) for v in vals.split("/"))
+    knob = int(knob)
+    for name, T, cin, cout, k, cnt in SHAPES:
+        if only and not name.startswith(only):
+            continue
+        M, pad = 48 * T, (k - 1) // 2
+        lens = LENS[T]
+        valid = (torch.arange(T, device=dev)[None] < lens[:, None]).reshape(-1)
+        x = (torch.randn(M, cin, device=dev) * valid[:, None]).to(bf)
+        dy = (torch.randn(M, cout, device=dev) * valid[:, None]).to(bf)
+        dws = {v: torch.zeros(cout, cin, k, device=dev) for v in (v0, v1)}
+        dbs = {v: torch.zeros(cout, device=dev) for v in (v0, v1)}
+        res = {}
+        for v in (v0, v1, v0, v1, v0, v1):
+            K.lib.fs2_set_tuning(knob, v)
+            wsb = K.ws(K.lib.fs2_conv_wgrad_ws_bytes(M, cin, cout, k), dev)
+            wgr = lambda: K.conv_wgrad(dy, x, dws[v], M, T, cin, cout, k, pad, db=dbs[v],
+                                       ws_buf=wsb, lens=lens)
+            dws[v].zero_()
+            dbs[v].zero_()
+            wgr()
+            torch.cuda.synchronize()
+            snap = (dws[v].clone(), dbs[v].clone())
+            for _ in range(20):
+                wgr()
+            res.setdefault(v, []).append(timeit(wgr, reps))
+            dws[v].copy_(snap[0])
+            dbs[v].copy_(snap[1])
+        K.lib.fs2_set_tuning(knob, 0)
+        eq = torch.equal(dws[v0], dws[v1]) and torch.equal(dbs[v0], dbs[v1])
+        fl = 2.0 * VALID[T] * cin * cout * k / 1e6
+        line = f"{name:15s}"
+        for v in (v0, v1):
+            t = min(res[v])
+            line += f"  [{knob}={v}] wgrad+reduce {t:6.1f} us ({fl / t:4.0f} TF/s)"
+        print(line + f"  bitwise {eq}", flush=True)
+
+
 def probe(kind, only):
     """10 launches of one kernel (PMC passes): --probe fwd|dgrad|wgrad --only <shape>"""
     name, T, cin, cout, k, _ = [s_ for s_ in SHAPES if s_[0].startswith(only or "dec")][0]
@@ -141,6 +182,11 @@ def main():
         reps = int(sys.argv[sys.argv.index("--reps") + 1]) if "--reps" in sys.argv else 20
         only = sys.argv[sys.argv.index("--only") + 1] if "--only" in sys.argv else None
         ab(sys.argv[sys.argv.index("--ab") + 1], reps, only)
+        return
+    if "--abw" in sys.argv:
+        reps = int(sys.argv[sys.argv.index("--reps") + 1]) if "--reps" in sys.argv else 20
+        only = sys.argv[sys.argv.index("--only") + 1] if "--only" in sys.argv else None
+        abw(sys.argv[sys.argv.index("--abw") + 1], reps, only)
         return
     reps = int(sys.argv[sys.argv.index("--reps") + 1]) if "--reps" in sys.argv else 20
     only = sys.argv[sys.argv.index("--only") + 1] if "--only" in sys.argv else None

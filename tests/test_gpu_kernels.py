@@ -711,7 +711,7 @@ def test_conv_wgrad_halo(B, T, cin, cout, k):
     ref_conv(xr, wr, None, B, T, pad).backward(dy.float())
     out = {}
     try:
-        for mode in (0, -1):
+        for mode in (0, 1, -1):
             K.lib.fs2_set_tuning(7, mode)  # FS2_TUNE_WGRAD_HALO
             dw, db = torch.zeros_like(w), torch.zeros(cout, device=DEV)
             K.conv_wgrad(dy, x, dw, B * T, T, cin, cout, k, pad, db=db)
@@ -721,6 +721,8 @@ def test_conv_wgrad_halo(B, T, cin, cout, k):
     close(out[0][0], wr.grad, 1e-5)
     close(out[0][1], dy.float().sum(0), 1e-5)
     close(out[0][0], out[-1][0], 1e-5)
+    # the two halo wave layouts run the same MFMAs on the same fragments: bitwise equal
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
     # lens: zero dy rows past each length, skipped k-tiles change nothing (bitwise)
     lens = torch.tensor([T - (13 * u) % T for u in range(B)], device=DEV)
     padr = (torch.arange(T, device=DEV)[None] >= lens[:, None]).reshape(-1)

@@ -72,6 +72,22 @@ int fs2_conv_gemm(int dtype, const void* x, int64_t ldx, const void* wk, void* y
                   const int64_t* lens, const float* bias, int flags, const void* aux,
                   int64_t ld_aux, void* stream);
 
+/* bf16 Conv1d / Linear with the FFT block's post-LayerNorm fused into the epilogue
+ * (c_out = 256, the LayerNorm width; x, wk bf16 as fs2_conv_gemm):
+ *   z[r, :] = dropout(conv(x)[r, :] + bias, p_in) + res[r, :]      (res nullable)
+ *   out = (z - mean) * rstd * gamma + beta, out_t = bf16(out) (nullable), xhat, rstd saved;
+ *   rows t >= lens[b] are written as 0 (xhat / rstd left unwritten there).
+ * Bitwise equal to fs2_conv_gemm (fp32 y, FS2_EPI_BIAS) followed by fs2_ln_fwd(y, res, ...,
+ * p_out = 0, no head): one kernel instead of two, and y never goes to memory.  The dropout
+ * mask is fs2_ln_fwd's (seed, site_in), so fs2_ln_bwd is its backward.
+ * Replaces transformer/SubLayers.py:54-55 (fc, dropout, residual, layer_norm) and :88-91
+ * (w_2, dropout, residual, layer_norm).                                                  */
+int fs2_conv_gemm_ln(const void* x, int64_t ldx, const void* wk, int64_t rows, int64_t seq_len,
+                     int64_t c_in, int64_t c_out, int taps, int pad, const int64_t* lens,
+                     const float* bias, const float* res, const float* gamma, const float* beta,
+                     float* out, void* out_t, float* xhat, float* rstd, float p_in,
+                     const uint64_t* seed, uint64_t site_in, void* stream);
+
 /* Dilated Conv1d with the vocoder epilogue (HiFi-GAN generator, hifigan/models.py:19-178):
  *   v[r, o] = sum_{j, c} wk[o, j*c_in + c] * x[r + j*dilation - pad, c]   (zero outside the
  *   utterance of seq_len rows), then BIAS, ADD_AUX, ACC_Y, LRELU in that order; y stored
@@ -233,12 +249,13 @@ int fs2_weight_prep_batch(int dtype, const int64_t* jobs, int n_jobs, int64_t n_
  *                          half of rows is past the utterance length (lens given)
  *   FS2_TUNE_NT_TILE       tap-major fwd/dX kernel (k = 1 projections, odd shapes): 0 = tile
  *                          by grid size, 1 / 2 / 3 = force 128x128 / 128x64 / 64x64
+ *   FS2_TUNE_LN_TILE       fs2_conv_gemm_ln row tile: 0 = 64 x 256 (default), 1 = 128 x 256
  * Process-wide; query workspace sizes after setting.                                 */
 enum { FS2_TUNE_GEMM_STAGES = 0, FS2_TUNE_WGRAD_STAGES = 1, FS2_TUNE_WGRAD_TILE = 2,
        FS2_TUNE_WGRAD_SPLITS = 3, FS2_TUNE_LEGACY_GEMM = 4, FS2_TUNE_NT_GROUP = 5,
        FS2_TUNE_NT_HALO = 6, FS2_TUNE_WGRAD_HALO = 7, FS2_TUNE_HALO_SPLITK = 8,
        FS2_TUNE_ATTN = 9, FS2_TUNE_HALO_DB = 10, FS2_TUNE_HALO_PIPE = 11, FS2_TUNE_NT_TILE = 12,
-       FS2_TUNE_COUNT = 13 };
+       FS2_TUNE_LN_TILE = 13, FS2_TUNE_COUNT = 14 };
 int fs2_set_tuning(int knob, int value);
 
 /* Weight (and optionally bias) gradient, accumulated into the fp32 master-gradient layout:

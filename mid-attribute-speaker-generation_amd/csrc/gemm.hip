@@ -459,6 +459,22 @@ int fs2_conv_gemm_ex(int dtype, const void* x, int64_t ldx, const void* wk, void
   return launch_status("fs2_conv_gemm");
 }
 
+int fs2_conv_gemm_ln(const void* x, int64_t ldx, const void* wk, int64_t rows, int64_t seq_len,
+                     int64_t c_in, int64_t c_out, int taps, int pad, const int64_t* lens,
+                     const float* bias, const float* res, const float* gamma, const float* beta,
+                     float* out, void* out_t, float* xhat, float* rstd, float p_in,
+                     const uint64_t* seed, uint64_t site_in, void* stream) {
+  FS2_CHECK_ARG(rows >= 0 && seq_len > 0 && taps >= 1 && pad >= 0 && pad < taps,
+                "fs2_conv_gemm_ln: bad geometry");
+  FS2_CHECK_ARG(c_out == 256, "fs2_conv_gemm_ln: only c_out = 256 (the LayerNorm width) is built");
+  FS2_CHECK_ARG(gamma && beta && out && xhat && rstd, "fs2_conv_gemm_ln: missing LayerNorm tensors");
+  FS2_CHECK_ARG(!(p_in > 0.f) || seed, "fs2_conv_gemm_ln: dropout without seed");
+  if (rows == 0) return FS2_OK;
+  return conv_gemm_ln_glds_launch(x, ldx, wk, rows, seq_len, c_in, taps, pad, lens, bias, res,
+                                  gamma, beta, out, out_t, xhat, rstd, p_in, seed, site_in,
+                                  as_stream(stream));
+}
+
 int fs2_conv_gemm(int dtype, const void* x, int64_t ldx, const void* wk, void* y, int64_t ldy,
                   int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out, int taps, int pad,
                   const int64_t* lens, const float* bias, int flags, const void* aux,

@@ -59,6 +59,17 @@ struct GldsArgs {
   int halo_db;          // halo kernel, BST == 2: double-buffered halo stage (FS2_TUNE_HALO_DB)
   int no_trim;          // halo kernel, pipelined loop: no half-width body (FS2_TUNE_HALO_PIPE 2)
   float* slab;          // kz > 1: [kz][M][N] fp32 partial products
+  // LayerNorm epilogue (fs2_conv_gemm_ln; 256-wide tiles hold whole rows): ln_out != NULL
+  const float* ln_res;
+  const float* ln_gamma;
+  const float* ln_beta;
+  float* ln_out;
+  u16* ln_out_t;
+  float* ln_xhat;
+  float* ln_rstd;
+  const uint64_t* ln_seed;
+  uint64_t ln_site;
+  float ln_p;
 };
 
 // Are rows [r0, r1) all padding (t >= lens[b] for r = b*T + t)?  Scalar, block-uniform.
@@ -163,6 +174,86 @@ FS2_DEV void kloop(int nk, Issue&& issue, Compute&& compute) {
   }
 }
 
+// LayerNorm epilogue of a 256-wide tile (whole rows): the fs2_ln_fwd row computation on the
+// accumulators instead of a stored fp32 y -- z = dropout(acc + bias, p) + res, mean / variance
+// over the half-wave's 256 channels (8 per lane, the fs2_ln_fwd lane layout), out = xhat *
+// gamma + beta, padded rows written as 0 (xhat / rstd not written there: the backward skips
+// them).  Same operations in the same order as fs2_conv_gemm + fs2_ln_fwd: bitwise equal.
+template <int BM, int NWAVE, int WN>
+FS2_DEV void nt_epilogue_ln(const GldsArgs& a, f32x4 (&acc)[BM / 32][256 / WN / 16], u16* smem,
+                            int64_t m0, bool skip, int tid, int wm, int wn, int g, int r16) {
+  constexpr int MI = BM / 32, NI = 256 / WN / 16, EPI_LD = 256 + 4;
+  constexpr int RPP = NWAVE * 2;  // rows per pass: one per half-wave
+  float* Cs = reinterpret_cast<float*>(smem);
+  const int hl = tid & 31;
+  const uint64_t seed = a.ln_seed ? *a.ln_seed : 0ull;
+  const f32x4 ga0 = ld4(a.ln_gamma + 8 * hl), ga1 = ld4(a.ln_gamma + 8 * hl + 4);
+  const f32x4 be0 = ld4(a.ln_beta + 8 * hl), be1 = ld4(a.ln_beta + 8 * hl + 4);
+  f32x4 bi0 = f32x4{0.f, 0.f, 0.f, 0.f}, bi1 = bi0;
+  if ((a.flags & FS2_EPI_BIAS) && !skip) {
+    bi0 = ld4(a.bias + 8 * hl);
+    bi1 = ld4(a.bias + 8 * hl + 4);
+  }
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (wm == h) {
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            Cs[(i * 16 + 4 * g + r) * EPI_LD + wn * (256 / WN) + j * 16 + r16] = acc[i][j][r];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int p = 0; p < (BM / 2) / RPP; ++p) {
+      const int rr = p * RPP + (tid >> 5);
+      const int64_t m = m0 + h * (BM / 2) + rr;
+      if (m >= a.M) continue;  // half-wave uniform
+      const int64_t e0 = m * 256 + 8 * hl;
+      const bool pad = a.lens && (m % a.T) >= a.lens[m / a.T];
+      if (pad) {
+        const f32x4 zz = {0.f, 0.f, 0.f, 0.f};
+        st4(a.ln_out + e0, zz);
+        st4(a.ln_out + e0 + 4, zz);
+        if (a.ln_out_t) st8_bf16(a.ln_out_t + e0, zz, zz);
+        continue;
+      }
+      f32x4 z0 = *reinterpret_cast<const f32x4*>(Cs + rr * EPI_LD + 8 * hl);
+      f32x4 z1 = *reinterpret_cast<const f32x4*>(Cs + rr * EPI_LD + 8 * hl + 4);
+      z0 += bi0;
+      z1 += bi1;
+      if (a.ln_p > 0.f) {
+        f32x4 k0, k1;
+        dropout8(seed, a.ln_site, (uint64_t)e0, a.ln_p, k0, k1);
+        z0 *= k0;
+        z1 *= k1;
+      }
+      if (a.ln_res) {
+        z0 += ld4(a.ln_res + e0);
+        z1 += ld4(a.ln_res + e0 + 4);
+      }
+      const float mean =
+          half_sum((z0.x + z0.y + z0.z + z0.w) + (z1.x + z1.y + z1.z + z1.w)) * (1.f / 256);
+      const f32x4 c0 = z0 - mean, c1 = z1 - mean;
+      const float var = half_sum((c0.x * c0.x + c0.y * c0.y + c0.z * c0.z + c0.w * c0.w) +
+                                 (c1.x * c1.x + c1.y * c1.y + c1.z * c1.z + c1.w * c1.w)) *
+                        (1.f / 256);
+      const float rs = 1.f / sqrtf(var + 1e-5f);
+      const f32x4 xh0 = c0 * rs, xh1 = c1 * rs;
+      const f32x4 u0 = xh0 * ga0 + be0, u1 = xh1 * ga1 + be1;
+      st4(a.ln_out + e0, u0);
+      st4(a.ln_out + e0 + 4, u1);
+      if (a.ln_out_t) st8_bf16(a.ln_out_t + e0, u0, u1);
+      st4(a.ln_xhat + e0, xh0);
+      st4(a.ln_xhat + e0 + 4, xh1);
+      if (hl == 0) a.ln_rstd[m] = rs;
+    }
+    __syncthreads();
+  }
+}
+
 // Epilogue through LDS, one half (wm) at a time: bias, aux add, ReLU / ReLU-mask, bf16 cast
 // on 8-element row vectors (16-B / 32-B coalesced stores).  Shared by both NT kernels.
 template <int BM, int BN, bool VOC, int NWAVE = 4, int WN = 2>
@@ -170,6 +261,12 @@ FS2_DEV void nt_epilogue(const GldsArgs& a, f32x4 (&acc)[BM / 32][BN / WN / 16],
                          int64_t m0, int n0, bool skip, int tid, int wm, int wn, int g, int r16) {
   constexpr int MI = BM / 32, NI = BN / WN / 16;
   constexpr int EPI_LD = BN + 4;
+  if constexpr (BN == 256 && !VOC) {
+    if (a.ln_out) {
+      nt_epilogue_ln<BM, NWAVE, WN>(a, acc, smem, m0, skip, tid, wm, wn, g, r16);
+      return;
+    }
+  }
   if (skip && (a.flags & FS2_EPI_SKIP_NOSTORE)) return;  // block-uniform
   float* Cs = reinterpret_cast<float*>(smem);
   const bool out_bf16 = a.flags & FS2_EPI_OUT_BF16, aux_bf16 = a.flags & FS2_EPI_AUX_BF16;
@@ -1500,6 +1597,48 @@ static int halo_splitk(GldsArgs& a, unsigned grid, bool voc, bool hx64, hipStrea
 static int halo_group(int tiles_n) {
   const int g = g_tune[FS2_TUNE_NT_GROUP];
   return g > 0 && g < tiles_n ? g : tiles_n;
+}
+
+// fs2_conv_gemm_ln: the tap-major kernel on 64 x 256 tiles (whole 256-wide rows; 128 x 256
+// with FS2_TUNE_LN_TILE = 1) with the LayerNorm epilogue
+int conv_gemm_ln_glds_launch(const void* x, int64_t ldx, const void* wk, int64_t rows,
+                             int64_t seq_len, int64_t c_in, int taps, int pad, const int64_t* lens,
+                             const float* bias, const float* res, const float* gamma,
+                             const float* beta, float* out, void* out_t, float* xhat, float* rstd,
+                             float p_in, const uint64_t* seed, uint64_t site_in, hipStream_t st) {
+  auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  FS2_CHECK_ARG(c_in % 8 == 0 && ldx % 8 == 0 && al16(x) && al16(wk),
+                "fs2_conv_gemm_ln: c_in/ldx must be multiples of 8 and operands 16-B aligned");
+  FS2_CHECK_ARG(al16(out) && al16(xhat) && al16(gamma) && al16(beta) && al16(res) && al16(bias) &&
+                    al16(out_t),
+                "fs2_conv_gemm_ln: LayerNorm tensors must be 16-B aligned");
+  GldsArgs a{(const u16*)x, ldx, (const u16*)wk, nullptr, 256, rows, seq_len, (int)c_in, 256,
+             taps, pad, (int)(taps * c_in), bias, bias ? FS2_EPI_BIAS : 0, nullptr, 0, 0, 0, 1, 1,
+             lens, 1, 0.f, 1.f, nullptr, 0.f};
+  a.ln_res = res;
+  a.ln_gamma = gamma;
+  a.ln_beta = beta;
+  a.ln_out = out;
+  a.ln_out_t = (u16*)out_t;
+  a.ln_xhat = xhat;
+  a.ln_rstd = rstd;
+  a.ln_seed = p_in > 0.f ? seed : nullptr;
+  a.ln_site = site_in;
+  a.ln_p = p_in;
+  const bool wide = g_tune[FS2_TUNE_LN_TILE] == 1;
+  const int bm = wide ? 128 : 64;
+  a.tiles_m = (int)((rows + bm - 1) / bm);
+  a.tiles_n = 1;
+  const unsigned grid = (unsigned)a.tiles_m;
+  const bool tapaligned = c_in % 64 == 0;
+  if (wide) {
+    if (tapaligned) conv_gemm_nt_glds<128, 256, 2, true, false><<<grid, 256, 0, st>>>(a);
+    else conv_gemm_nt_glds<128, 256, 2, false, false><<<grid, 256, 0, st>>>(a);
+  } else {
+    if (tapaligned) conv_gemm_nt_glds<64, 256, 2, true, false><<<grid, 256, 0, st>>>(a);
+    else conv_gemm_nt_glds<64, 256, 2, false, false><<<grid, 256, 0, st>>>(a);
+  }
+  return launch_status("fs2_conv_gemm_ln");
 }
 
 int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, int64_t ldy,

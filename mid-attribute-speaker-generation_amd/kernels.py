@@ -92,6 +92,25 @@ def conv_gemm(x, wk, rows, seq_len, c_in, c_out, taps, pad, bias=None, flags=0, 
     return out
 
 
+def conv_gemm_ln(x, wk, rows, seq_len, c_in, c_out, taps, pad, gamma, beta, bias=None, res=None,
+                 lens=None, p_in=0.0, seed=0, site_in=0, copy=torch.bfloat16):
+    """bf16 conv/Linear with the post-LayerNorm fused in (fs2_conv_gemm_ln): returns
+    ``ln_fwd(conv_gemm(x) + bias, res=res, p_in=...)``'s (out fp32, out compute copy, xhat,
+    rstd), bitwise, without the fp32 intermediate."""
+    _dev(x, wk, gamma, beta, bias, res, lens)
+    if x.dtype != torch.bfloat16 or wk.dtype != torch.bfloat16:
+        raise RuntimeError("conv_gemm_ln: bf16 operands only")
+    out = torch.empty(rows, c_out, dtype=torch.float32, device=x.device)
+    out_t = _copy((rows, c_out), copy, x.device)
+    xhat = torch.empty_like(out)
+    rstd = torch.empty(rows, dtype=torch.float32, device=x.device)
+    sd = seed_arg(seed, x.device) if p_in > 0 else None
+    lib.fs2_conv_gemm_ln(ptr(x), c_in, ptr(wk), rows, seq_len, c_in, c_out, taps, pad, ptr(lens),
+                         ptr(bias), ptr(res), ptr(gamma), ptr(beta), ptr(out), ptr(out_t),
+                         ptr(xhat), ptr(rstd), p_in, ptr(sd), site_in, stream())
+    return out, out_t, xhat, rstd
+
+
 def conv_gemm_ex(x, wk, rows, seq_len, c_in, c_out, taps, pad, dilation=1, bias=None, flags=0,
                  aux=None, out=None, y2=None, alpha=0.1, scale=1.0, alpha2=0.1, lens=None):
     """Dilated conv with the vocoder epilogue (fs2_conv_gemm_ex): out and/or y2 (the

@@ -21,6 +21,7 @@ order so gradient buckets complete front-to-back; kernels accumulate weight grad
 straight into the flat gradient buffer (``param.grad`` are views of it).
 """
 import math
+import os
 
 import numpy as np
 import torch
@@ -162,6 +163,11 @@ class StepCtx:
             self.hook(params)
 
 
+# bf16 path: FFT-block post-LayerNorms fused into the fc / w_2 GEMM epilogues (fs2_conv_gemm_ln)
+FUSE_LN = os.environ.get("FS2_FUSE_LN", "1") != "0"  # step-level A/B switch
+FUSE_LN_MIN_ROWS = 16384
+
+
 def _t(f, t):
     """Compute-dtype view of an activation: the bf16 copy if one was made, else the fp32."""
     return f if t is None else t
@@ -291,19 +297,38 @@ class FFTBlock(nn.Module):
         qkv = K.conv_gemm(x_c, q._w_fwd, M, T, d, n3, 1, 0, bias=self._qkv_b, out_dtype=ctx.cdt,
                           lens=lens)
         o, lse = K.attn_fwd(qkv, lens, B, T, a.n_head, a.d_k, 1.0 / math.sqrt(a.d_k))
-        y1 = K.conv_gemm(o, a.fc._w_fwd, M, T, a.n_head * a.d_k, d, 1, 0, bias=a.fc.bias,
-                         lens=lens)
-        x1, x1_t, xh1, rs1, _ = K.ln_fwd(y1, a.layer_norm.weight, a.layer_norm.bias, res=x,
-                                         lens=lens, seq_len=T, p_in=p, seed=ctx.seed,
-                                         site_in=self.site, copy=ctx.copy)
+        hd = a.n_head * a.d_k
+        # bf16: the post-LNs run in the epilogues of fc and w_2 (fs2_conv_gemm_ln, bitwise
+        # equal to the two-launch form below, without the fp32 y round trip).  Decoder-sized
+        # grids only: at 6,144 rows (the encoder) its 96 64-row tiles under-fill the chip
+        # (scripts/ln_fuse_bench.py: decoder fc 31.7 -> 26.8 us, w_2 42.3 -> 37.4 us; encoder
+        # w_2 22.7 -> 29.5 us)
+        fuse = FUSE_LN and ctx.copy is not None and d == 256 and M >= FUSE_LN_MIN_ROWS
+        if fuse:
+            x1, x1_t, xh1, rs1 = K.conv_gemm_ln(
+                o, a.fc._w_fwd, M, T, hd, d, 1, 0, a.layer_norm.weight, a.layer_norm.bias,
+                bias=a.fc.bias, res=x, lens=lens, p_in=p, seed=ctx.seed, site_in=self.site,
+                copy=ctx.copy)
+        else:
+            y1 = K.conv_gemm(o, a.fc._w_fwd, M, T, hd, d, 1, 0, bias=a.fc.bias, lens=lens)
+            x1, x1_t, xh1, rs1, _ = K.ln_fwd(y1, a.layer_norm.weight, a.layer_norm.bias, res=x,
+                                             lens=lens, seq_len=T, p_in=p, seed=ctx.seed,
+                                             site_in=self.site, copy=ctx.copy)
         w1, w2 = f.w_1, f.w_2
         x1_c = _t(x1, x1_t)
         h = K.conv_gemm(x1_c, w1._w_fwd, M, T, d, w1.c_out, w1.k, w1.padding, bias=w1.bias,
                         flags=K.EPI_RELU, out_dtype=ctx.cdt, lens=lens)
-        y2 = K.conv_gemm(h, w2._w_fwd, M, T, w2.c_in, d, w2.k, w2.padding, bias=w2.bias, lens=lens)
-        x2, x2_t, xh2, rs2, _ = K.ln_fwd(y2, f.layer_norm.weight, f.layer_norm.bias, res=x1,
-                                         lens=lens, seq_len=T, p_in=p, seed=ctx.seed,
-                                         site_in=self.site + 1, copy=ctx.copy)
+        if fuse:
+            x2, x2_t, xh2, rs2 = K.conv_gemm_ln(
+                h, w2._w_fwd, M, T, w2.c_in, d, w2.k, w2.padding, f.layer_norm.weight,
+                f.layer_norm.bias, bias=w2.bias, res=x1, lens=lens, p_in=p, seed=ctx.seed,
+                site_in=self.site + 1, copy=ctx.copy)
+        else:
+            y2 = K.conv_gemm(h, w2._w_fwd, M, T, w2.c_in, d, w2.k, w2.padding, bias=w2.bias,
+                             lens=lens)
+            x2, x2_t, xh2, rs2, _ = K.ln_fwd(y2, f.layer_norm.weight, f.layer_norm.bias, res=x1,
+                                             lens=lens, seq_len=T, p_in=p, seed=ctx.seed,
+                                             site_in=self.site + 1, copy=ctx.copy)
         saved = (x_c, qkv, o, lse, x1_c, h, xh1, rs1, xh2, rs2, p, ctx, lens, B, T)
         return x2, x2_t, saved
 

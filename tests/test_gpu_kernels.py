@@ -440,6 +440,43 @@ def test_conv_gemm_bf16_pipeline_depths(stages, B, T, cin, cout, k):
             K.lib.fs2_set_tuning(knob, 0)
 
 
+@pytest.mark.parametrize("B,T,lens,cin,p,tile", [
+    (3, 50, [50, 17, 1], 256, 0.0, 0), (2, 200, [200, 130], 1024, 0.2, 0),
+    (4, 128, [128, 70, 33, 128], 256, 0.2, 1), (6, 512, [512, 300, 129, 128, 1, 400], 1024, 0.1, 0),
+    (5, 37, None, 256, 0.3, 1), (2, 64, [64, 9], 80, 0.1, 0)])
+def test_conv_gemm_ln(B, T, lens, cin, p, tile):
+    """fs2_conv_gemm_ln (GEMM + bias + dropout + residual + LayerNorm + row mask in one
+    kernel) equals fs2_conv_gemm (fp32 y) -> fs2_ln_fwd bitwise: out, its bf16 copy, and
+    xhat / rstd on the rows the backward reads; both row tiles (FS2_TUNE_LN_TILE)."""
+    M, d = B * T, 256
+    lt = None if lens is None else torch.tensor(lens, device=DEV)
+    x = bf(rnd(M, cin, seed=51))
+    w = bf(rnd(d, cin, 1, scale=1 / math.sqrt(cin), seed=52)).float()
+    b, res = rnd(d, seed=53), rnd(M, d, seed=54)
+    g, bt = 1 + 0.1 * rnd(d, seed=55), 0.1 * rnd(d, seed=56)
+    wf = torch.empty(d * cin, device=DEV, dtype=torch.bfloat16)
+    wb = torch.empty_like(wf)
+    K.weight_prep(w, d, cin, 1, wf, wb)
+    kw = dict(lens=lt, seq_len=T, p_in=p, seed=99, site_in=5, copy=torch.bfloat16)
+    y = K.conv_gemm(x, wf, M, T, cin, d, 1, 0, bias=b, lens=lt)
+    o0, t0, xh0, rs0, _ = K.ln_fwd(y, g, bt, res=res, **kw)
+    K.lib.fs2_set_tuning(13, tile)  # FS2_TUNE_LN_TILE
+    try:
+        o1, t1, xh1, rs1 = K.conv_gemm_ln(x, wf, M, T, cin, d, 1, 0, g, bt, bias=b, res=res,
+                                          lens=lt, p_in=p, seed=99, site_in=5)
+    finally:
+        K.lib.fs2_set_tuning(13, 0)
+    live = (torch.ones(M, dtype=torch.bool, device=DEV) if lt is None else
+            (torch.arange(T, device=DEV)[None] < lt[:, None]).reshape(-1))
+    assert torch.equal(o1, o0) and torch.equal(t1, t0)
+    assert torch.equal(xh1[live], xh0[live]) and torch.equal(rs1[live], rs0[live])
+    # and against fp32 math (no dropout: the reference's LayerNorm of the residual sum)
+    if p == 0:
+        ref = F.layer_norm(x.float() @ w.view(d, cin).t() + b + res, (d,), g, bt, 1e-5)
+        close(o1[live], ref[live], 2e-5)
+        assert torch.all(o1[~live] == 0)
+
+
 def test_conv_gemm_bf16_padding_tiles():
     """lens: all-padding 128-row tiles are written as zero rows (bias dropped) / aux, the
     rest exactly as without lens; the weight gradient with zero dy at padded rows is

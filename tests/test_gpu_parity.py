@@ -343,6 +343,31 @@ def test_step_bitwise_reproducible(dt):
         assert torch.equal(a, b)
 
 
+def test_fused_gemm_ln_step_bitwise():
+    """bf16: the FFT blocks' post-LayerNorms fused into the fc / w_2 GEMM epilogues
+    (fs2_conv_gemm_ln, model.FUSE_LN) give bitwise the weights, Adam moments and losses of
+    the two-launch form (conv_gemm -> ln_fwd) after 2 steps with dropout ON, at ragged
+    lengths (SYN-8 x 32: padded rows inside the 64-row tiles)."""
+    pp, mc, tc, path = PKG.config.load_configs("JVS-VCTK")
+    res = []
+    for fuse in (False, True):
+        M.FUSE_LN, M.FUSE_LN_MIN_ROWS = fuse, 0
+        try:
+            model = M.FastSpeech2(pp, mc, path, device=DEV, compute_dtype=torch.bfloat16)
+            PKG.seeded.load_seeded_(model)
+            model.train()
+            model.seed(21)
+            tr = T.Trainer(model, pp, mc, tc)
+            batch = PKG.data.to_device(PKG.data.syn_batch(8, 32, seed=6), DEV)
+            losses = [torch.stack(list(tr.step(batch)[0])).clone() for _ in range(2)]
+            torch.cuda.synchronize()
+            res.append((model.arena().flat.clone(), tr.opt.m.clone(), torch.stack(losses)))
+        finally:
+            M.FUSE_LN, M.FUSE_LN_MIN_ROWS = True, 16384
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+
+
 def test_graph_replay_matches_eager():
     """Trainer(graph=True): step 1 eager + capture, steps 2-4 replays of the captured step.
     With dropout ON (device-side per-step keys) the weights, Adam moments, LR and losses

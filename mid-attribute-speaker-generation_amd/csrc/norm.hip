@@ -10,8 +10,9 @@
 // Affine/linear-head gradients are reduced per 32-row block in registers + LDS and then
 // summed over blocks in a fixed order (bitwise reproducible).
 //
-// BatchNorm: two-pass column statistics over every (utterance, frame) row, padded frames
-// included (the reference's BatchNorm1d sees them, Layers.py:129-137).
+// BatchNorm: column statistics over every (utterance, frame) row, padded frames included (the
+// reference's BatchNorm1d sees them, Layers.py:129-137): per 64-row block its sum and centred
+// second moment in one pass, combined exactly over the blocks in a fixed order.
 #include <math.h>
 
 #include "common.hpp"
@@ -280,33 +281,6 @@ __global__ __launch_bounds__(LN_BWD_WAVES * 64) void ln_bwd_f32(LnBwd a) {
 // ------------------------------------------------------------------ BatchNorm
 constexpr int BN_ROWS = 64;  // rows per partial block: 1,536 blocks at 24,576 rows (latency-bound at 64)
 
-// Column partial sums over BN_ROWS-row chunks, 4 consecutive channels per lane (16-B loads):
-// block (x, y) covers channels [256x, 256x+256) of rows [BN_ROWS*y, BN_ROWS*(y+1)), four row
-// lanes summed in lane order.  MODE 0: sum z ; MODE 1: sum (z - mean)^2
-template <int MODE>
-__global__ __launch_bounds__(256) void bn_partial(const float* z, const float* mean, int64_t rows,
-                                                  int64_t c, float* part) {
-  const int tx = threadIdx.x & 63, ry = threadIdx.x >> 6;
-  const int64_t col = ((int64_t)blockIdx.x * 64 + tx) * 4;
-  const int64_t r0 = (int64_t)blockIdx.y * BN_ROWS;
-  __shared__ f32x4 red[4][64];
-  f32x4 s = {0.f, 0.f, 0.f, 0.f};
-  if (col < c) {
-    const f32x4 mu = MODE == 1 ? ld4(mean + col) : f32x4{0.f, 0.f, 0.f, 0.f};
-    const int64_t r1 = r0 + BN_ROWS < rows ? r0 + BN_ROWS : rows;
-#pragma unroll 4
-    for (int64_t r = r0 + ry; r < r1; r += 4) {
-      const f32x4 v = ld4(z + r * c + col);
-      if (MODE == 0) s += v;
-      else s += (v - mu) * (v - mu);
-    }
-  }
-  red[ry][tx] = s;
-  __syncthreads();
-  if (ry == 0 && col < c)
-    st4(part + (int64_t)blockIdx.y * c + col, ((red[0][tx] + red[1][tx]) + red[2][tx]) + red[3][tx]);
-}
-
 // in-order column sum of partial rows: 64 columns x 16 lanes per block (see colsum_final)
 FS2_DEV float col_reduce(const float* part, int64_t nparts, int64_t c, int64_t col, int tx, int ty,
                          float (*red)[65]) {
@@ -326,28 +300,78 @@ FS2_DEV float col_reduce(const float* part, int64_t nparts, int64_t c, int64_t c
   return t;
 }
 
-__global__ __launch_bounds__(1024) void bn_mean_final(const float* part, int64_t nparts, int64_t rows,
-                                                      int64_t c, float* mean) {
-  __shared__ float red[16][65];
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  const int64_t col = (int64_t)blockIdx.x * 64 + tx;
-  const float s = col_reduce(part, nparts, c, col, tx, ty, red);
-  if (ty == 0 && col < c) mean[col] = s / (float)rows;
+// Both statistics in one pass over z: a block sums its BN_ROWS rows per column (four row lanes,
+// added in lane order, as the round-2 mean pass did, so the mean is unchanged), then re-reads the same
+// rows (from L2) for its centred second moment M2_b = sum_r (z - mean_b)^2.  bn_stats_final
+// combines the blocks exactly: M2 = sum_b [M2_b + n_b (mean_b - mean)^2] (one launch and one HBM
+// pass of z fewer than the mean-then-variance pair, and no cancellation).
+__global__ __launch_bounds__(256) void bn_stats(const float* z, int64_t rows, int64_t c, float* psum,
+                                                float* pm2) {
+  const int tx = threadIdx.x & 63, ry = threadIdx.x >> 6;
+  const int64_t col = ((int64_t)blockIdx.x * 64 + tx) * 4;
+  const int64_t r0 = (int64_t)blockIdx.y * BN_ROWS;
+  const int64_t r1 = r0 + BN_ROWS < rows ? r0 + BN_ROWS : rows;
+  __shared__ f32x4 red[4][64];
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  if (col < c) {
+#pragma unroll 4
+    for (int64_t r = r0 + ry; r < r1; r += 4) s += ld4(z + r * c + col);
+  }
+  red[ry][tx] = s;
+  __syncthreads();
+  const f32x4 tot = ((red[0][tx] + red[1][tx]) + red[2][tx]) + red[3][tx];
+  const f32x4 mu = tot * (1.f / (float)(r1 - r0));
+  __syncthreads();
+  f32x4 q = {0.f, 0.f, 0.f, 0.f};
+  if (col < c) {
+#pragma unroll 4
+    for (int64_t r = r0 + ry; r < r1; r += 4) {
+      const f32x4 d = ld4(z + r * c + col) - mu;
+      q += d * d;
+    }
+  }
+  red[ry][tx] = q;
+  __syncthreads();
+  if (ry == 0 && col < c) {
+    st4(psum + (int64_t)blockIdx.y * c + col, tot);
+    st4(pm2 + (int64_t)blockIdx.y * c + col, ((red[0][tx] + red[1][tx]) + red[2][tx]) + red[3][tx]);
+  }
 }
 
-__global__ __launch_bounds__(1024) void bn_var_final(const float* part, int64_t nparts, int64_t rows,
-                                                     int64_t c, float eps, float mom,
-                                                     const float* mean, float* rm, float* rv,
-                                                     float* rstd) {
+// mean (in-order sum of the block sums), the exact block combination of the variance, rstd and
+// the running-statistics update, in one launch
+__global__ __launch_bounds__(1024) void bn_stats_final(const float* psum, const float* pm2,
+                                                       int64_t nparts, int64_t rows, int64_t c,
+                                                       float eps, float mom, float* mean, float* rm,
+                                                       float* rv, float* rstd) {
   __shared__ float red[16][65];
+  __shared__ float mu_s[64];
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int64_t col = (int64_t)blockIdx.x * 64 + tx;
-  const float s = col_reduce(part, nparts, c, col, tx, ty, red);
+  const float s = col_reduce(psum, nparts, c, col, tx, ty, red);
+  if (ty == 0) mu_s[tx] = s / (float)rows;
+  __syncthreads();
+  const float mu = mu_s[tx];
+  float q = 0.f;
+  if (col < c) {
+    for (int64_t p = ty; p < nparts; p += 16) {
+      const int64_t left = rows - p * BN_ROWS;
+      const float n = (float)(left < BN_ROWS ? left : BN_ROWS);
+      const float d = psum[p * c + col] / n - mu;
+      q += pm2[p * c + col] + n * d * d;
+    }
+  }
+  red[ty][tx] = q;
+  __syncthreads();
   if (ty != 0 || col >= c) return;
-  const float var = s / (float)rows;
+  float t = 0.f;
+#pragma unroll
+  for (int y = 0; y < 16; ++y) t += red[y][tx];
+  const float var = t / (float)rows;
+  mean[col] = mu;
   rstd[col] = 1.f / sqrtf(var + eps);
-  if (rm) rm[col] = (1.f - mom) * rm[col] + mom * mean[col];
-  if (rv) rv[col] = (1.f - mom) * rv[col] + mom * (rows > 1 ? s / (float)(rows - 1) : var);
+  if (rm) rm[col] = (1.f - mom) * rm[col] + mom * mu;
+  if (rv) rv[col] = (1.f - mom) * rv[col] + mom * (rows > 1 ? t / (float)(rows - 1) : var);
 }
 
 FS2_DEV f32x4 tanh4(f32x4 v) { return f32x4{tanhf(v.x), tanhf(v.y), tanhf(v.z), tanhf(v.w)}; }
@@ -604,11 +628,9 @@ int fs2_bn_fwd(int dtype, const float* z, int64_t rows, int64_t c, const float* 
   FS2_CHECK_ARG(c % 8 == 0, "fs2_bn_fwd: channel count must be a multiple of 8");
   dim3 grid((unsigned)((c + 255) / 256), (unsigned)nparts);
   const unsigned cg = (unsigned)((c + 63) / 64);
-  bn_partial<0><<<grid, 256, 0, st>>>(z, nullptr, rows, c, ws);
-  bn_mean_final<<<cg, 1024, 0, st>>>(ws, nparts, rows, c, mean);
-  bn_partial<1><<<grid, 256, 0, st>>>(z, mean, rows, c, ws);
-  bn_var_final<<<cg, 1024, 0, st>>>(ws, nparts, rows, c, eps, momentum, mean, running_mean,
-                                   running_var, rstd);
+  bn_stats<<<grid, 256, 0, st>>>(z, rows, c, ws, ws + nparts * c);
+  bn_stats_final<<<cg, 1024, 0, st>>>(ws, ws + nparts * c, nparts, rows, c, eps, momentum, mean,
+                                      running_mean, running_var, rstd);
   unsigned short* ot = dtype == FS2_BF16 ? (unsigned short*)out_t : nullptr;
   FS2_CHECK_ARG(out || ot, "fs2_bn_fwd: no output requested");
   bn_apply<<<ew_grid(rows * c / 8), 256, 0, st>>>(z, mean, rstd, gamma, beta, rows * c / 8, (int)c,

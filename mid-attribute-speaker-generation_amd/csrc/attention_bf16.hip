@@ -26,8 +26,14 @@ typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 namespace {
 constexpr int DH = 128;
 constexpr int QB = 64;
-constexpr int LDR = DH + 8;   // 272-B rows: conflict-free ds_read_b128 row fragments
-constexpr int LDT = DH + 16;  // 288-B rows: conflict-free ds_read_b64_tr_b16
+// LDS row strides of the 64 x 128 tiles.  288-B rows (72 dwords: row r starts at bank 8r mod
+// 64) are conflict-free both for ds_read_b128 row fragments (16 rows x 16 B in its 4 lane
+// groups) and for ds_read_b64_tr_b16 (8 rows x 32 B per 32-lane group); the dQ and dK/dV
+// kernels read the same K / Q / dO tiles both ways.  (272-B rows, round 2's row stride, were
+// 2-way conflicted on both: 22-43 % of the attention kernels' LDS cycles, SQ_LDS_BANK_CONFLICT;
+// 0 now, decoder backward 91 -> 87 us.)
+constexpr int LDR = DH + 16;
+constexpr int LDT = DH + 16;
 
 #define MFMA_BF16(a, b, c) __builtin_amdgcn_mfma_f32_16x16x32_bf16((a), (b), (c), 0, 0, 0)
 

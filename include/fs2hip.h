@@ -88,6 +88,24 @@ int fs2_conv_gemm_ln(const void* x, int64_t ldx, const void* wk, int64_t rows, i
                      float* out, void* out_t, float* xhat, float* rstd, float p_in,
                      const uint64_t* seed, uint64_t site_in, void* stream);
 
+/* bf16 Linear / Conv1d (c_out = 256) whose output is the upstream gradient of a post-
+ * LayerNorm, with that LayerNorm's backward in the epilogue:
+ *   dout[r, :] = conv(x)[r, :] + aux[r, :]                (aux: fp32 residual gradient, nullable)
+ *   then fs2_ln_bwd(dout, xhat, rstd, gamma, ..., p_in, site_in, dres, dres_add, dy_t = the bf16
+ *   dy copy, dgamma / dbeta / dbias_in accumulated; p_out = 0, no head, no ReLU input).
+ * dres and dy_t equal fs2_conv_gemm(FS2_EPI_ADD_AUX) followed by fs2_ln_bwd bitwise; the
+ * parameter gradients sum the same per-32-row block partials with another in-block order.
+ * ws: fs2_ln_bwd_ws_bytes(rows, 256).  In the FFT-block backward x is the attention input
+ * gradient (dqkv) and the LayerNorm is the PREVIOUS block's FFN post-LN: block i's QKV data
+ * gradient and block i-1's first backward op in one launch (transformer/SubLayers.py:38-40,91). */
+int fs2_conv_gemm_ln_bwd(const void* x, int64_t ldx, const void* wk, int64_t rows,
+                         int64_t seq_len, int64_t c_in, int64_t c_out, int taps, int pad,
+                         const int64_t* lens, const float* aux, const float* xhat,
+                         const float* rstd, const float* gamma, float* dgamma, float* dbeta,
+                         float* dbias_in, float p_in, const uint64_t* seed, uint64_t site_in,
+                         float* dres, int dres_add, void* dy_t, float* ws, int64_t ws_bytes,
+                         void* stream);
+
 /* Dilated Conv1d with the vocoder epilogue (HiFi-GAN generator, hifigan/models.py:19-178):
  *   v[r, o] = sum_{j, c} wk[o, j*c_in + c] * x[r + j*dilation - pad, c]   (zero outside the
  *   utterance of seq_len rows), then BIAS, ADD_AUX, ACC_Y, LRELU in that order; y stored

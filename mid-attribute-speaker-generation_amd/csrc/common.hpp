@@ -70,6 +70,12 @@ int conv_gemm_ln_glds_launch(const void* x, int64_t ldx, const void* wk, int64_t
                              const float* bias, const float* res, const float* gamma,
                              const float* beta, float* out, void* out_t, float* xhat, float* rstd,
                              float p_in, const uint64_t* seed, uint64_t site_in, hipStream_t st);
+int conv_gemm_lnbwd_glds_launch(const void* x, int64_t ldx, const void* wk, int64_t rows,
+                                int64_t seq_len, int64_t c_in, int taps, int pad,
+                                const int64_t* lens, const float* aux, const float* xhat,
+                                const float* rstd, const float* gamma, float p_in,
+                                const uint64_t* seed, uint64_t site_in, float* dres, int dres_add,
+                                void* dy_t, float* ws, hipStream_t st);
 int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, int64_t ldy,
                           int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out, int taps,
                           int pad, const int64_t* lens, const float* bias, int flags,

@@ -475,6 +475,27 @@ int fs2_conv_gemm_ln(const void* x, int64_t ldx, const void* wk, int64_t rows, i
                                   as_stream(stream));
 }
 
+int fs2_conv_gemm_ln_bwd(const void* x, int64_t ldx, const void* wk, int64_t rows,
+                         int64_t seq_len, int64_t c_in, int64_t c_out, int taps, int pad,
+                         const int64_t* lens, const float* aux, const float* xhat,
+                         const float* rstd, const float* gamma, float* dgamma, float* dbeta,
+                         float* dbias_in, float p_in, const uint64_t* seed, uint64_t site_in,
+                         float* dres, int dres_add, void* dy_t, float* ws, int64_t ws_bytes,
+                         void* stream) {
+  FS2_CHECK_ARG(rows >= 0 && seq_len > 0 && taps >= 1 && pad >= 0 && pad < taps,
+                "fs2_conv_gemm_ln_bwd: bad geometry");
+  FS2_CHECK_ARG(c_out == 256, "fs2_conv_gemm_ln_bwd: only c_out = 256 (the LayerNorm width) is built");
+  FS2_CHECK_ARG(xhat && rstd && gamma && dres, "fs2_conv_gemm_ln_bwd: missing LayerNorm tensors");
+  FS2_CHECK_ARG(!(p_in > 0.f) || seed, "fs2_conv_gemm_ln_bwd: dropout without seed");
+  FS2_CHECK_ARG(ws_bytes >= fs2_ln_bwd_ws_bytes(rows, 256), "fs2_conv_gemm_ln_bwd: workspace too small");
+  if (rows == 0) return FS2_OK;
+  int rc = conv_gemm_lnbwd_glds_launch(x, ldx, wk, rows, seq_len, c_in, taps, pad, lens, aux, xhat,
+                                       rstd, gamma, p_in, seed, site_in, dres, dres_add, dy_t, ws,
+                                       as_stream(stream));
+  if (rc) return rc;
+  return fs2_ln_bwd_final(rows, 256, ws, 0, dgamma, dbeta, nullptr, nullptr, dbias_in, stream);
+}
+
 int fs2_conv_gemm(int dtype, const void* x, int64_t ldx, const void* wk, void* y, int64_t ldy,
                   int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out, int taps, int pad,
                   const int64_t* lens, const float* bias, int flags, const void* aux,

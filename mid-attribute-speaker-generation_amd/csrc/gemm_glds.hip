@@ -70,6 +70,12 @@ struct GldsArgs {
   const uint64_t* ln_seed;
   uint64_t ln_site;
   float ln_p;
+  // LayerNorm-backward epilogue (fs2_conv_gemm_ln_bwd, ln_mode 1): ln_out = dres, ln_out_t =
+  // the bf16 dy copy, ln_xhat / ln_rstd read; column partials into ln_part ([4][ln_nblk][256])
+  int ln_mode;
+  int ln_dres_add;
+  float* ln_part;
+  int64_t ln_nblk;
 };
 
 // Are rows [r0, r1) all padding (t >= lens[b] for r = b*T + t)?  Scalar, block-uniform.
@@ -254,6 +260,107 @@ FS2_DEV void nt_epilogue_ln(const GldsArgs& a, f32x4 (&acc)[BM / 32][256 / WN / 
   }
 }
 
+// LayerNorm-BACKWARD epilogue of a 256-wide tile: the GEMM's rows are the upstream gradient of
+// a LayerNorm (dout = acc + aux, the residual-gradient add of fs2_conv_gemm's FS2_EPI_ADD_AUX),
+// and fs2_ln_bwd's row computation runs on them: dz = rstd (g dout - mean(g dout) - xhat
+// mean(g dout xhat)) into dres (written, or added with dres_add), dy = dz * dropout_in into the
+// bf16 copy, padded rows zero.  Each 32-row half of the tile is one fs2_ln_bwd block: its
+// column partials of dout xhat, dout and dy (dgamma, dbeta, the fused bias gradient) are summed
+// over the 8 half-waves in a fixed order into ln_part, reduced by fs2_ln_bwd_final.
+template <int BM, int NWAVE, int WN>
+FS2_DEV void nt_epilogue_lnbwd(const GldsArgs& a, f32x4 (&acc)[BM / 32][256 / WN / 16], u16* smem,
+                               int64_t m0, int tid, int wm, int wn, int g, int r16) {
+  static_assert(BM / 2 == 32 && NWAVE == 4, "one 32-row LayerNorm block per tile half");
+  constexpr int MI = BM / 32, NI = 256 / WN / 16, EPI_LD = 256 + 4;
+  float* Cs = reinterpret_cast<float*>(smem);
+  f32x4* red = reinterpret_cast<f32x4*>(Cs + 32 * EPI_LD);  // [3 kinds][8 half-waves][64]
+  const int hl = tid & 31, hw = tid >> 5;
+  const bool use_aux = a.flags & FS2_EPI_ADD_AUX;
+  const uint64_t seed = a.ln_seed ? *a.ln_seed : 0ull;
+  const f32x4 gam0 = ld4(a.ln_gamma + 8 * hl), gam1 = ld4(a.ln_gamma + 8 * hl + 4);
+  const f32x4 zz = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (wm == h) {
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            Cs[(i * 16 + 4 * g + r) * EPI_LD + wn * (256 / WN) + j * 16 + r16] = acc[i][j][r];
+    }
+    __syncthreads();
+    f32x4 pg0 = zz, pg1 = zz, pb0 = zz, pb1 = zz, py0 = zz, py1 = zz;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int rr = hw + 8 * p;
+      const int64_t m = m0 + h * 32 + rr;
+      if (m >= a.M) continue;  // half-wave uniform
+      const int64_t e0 = m * 256 + 8 * hl;
+      const bool pad = a.lens && (m % a.T) >= a.lens[m / a.T];
+      if (pad) {  // masked row: zero upstream gradient
+        if (!a.ln_dres_add) {
+          st4(a.ln_out + e0, zz);
+          st4(a.ln_out + e0 + 4, zz);
+        }
+        if (a.ln_out_t) st8_bf16(a.ln_out_t + e0, zz, zz);
+        continue;
+      }
+      f32x4 du0 = *reinterpret_cast<const f32x4*>(Cs + rr * EPI_LD + 8 * hl);
+      f32x4 du1 = *reinterpret_cast<const f32x4*>(Cs + rr * EPI_LD + 8 * hl + 4);
+      if (use_aux) {
+        const float* ap = (const float*)a.aux + m * a.ld_aux + 8 * hl;
+        du0 += ld4(ap);
+        du1 += ld4(ap + 4);
+      }
+      const f32x4 xh0 = ld4(a.ln_xhat + e0), xh1 = ld4(a.ln_xhat + e0 + 4);
+      pg0 += du0 * xh0;
+      pg1 += du1 * xh1;
+      pb0 += du0;
+      pb1 += du1;
+      const f32x4 dxh0 = du0 * gam0, dxh1 = du1 * gam1;
+      const float m1 = half_sum((dxh0.x + dxh0.y + dxh0.z + dxh0.w) + (dxh1.x + dxh1.y + dxh1.z + dxh1.w)) *
+                       (1.f / 256);
+      const float m2 = half_sum((dxh0.x * xh0.x + dxh0.y * xh0.y + dxh0.z * xh0.z + dxh0.w * xh0.w) +
+                                (dxh1.x * xh1.x + dxh1.y * xh1.y + dxh1.z * xh1.z + dxh1.w * xh1.w)) *
+                       (1.f / 256);
+      const float rs = a.ln_rstd[m];
+      const f32x4 dz0 = rs * (dxh0 - m1 - xh0 * m2), dz1 = rs * (dxh1 - m1 - xh1 * m2);
+      st4(a.ln_out + e0, a.ln_dres_add ? ld4(a.ln_out + e0) + dz0 : dz0);
+      st4(a.ln_out + e0 + 4, a.ln_dres_add ? ld4(a.ln_out + e0 + 4) + dz1 : dz1);
+      f32x4 dy0 = dz0, dy1 = dz1;
+      if (a.ln_p > 0.f) {
+        f32x4 mi0, mi1;
+        dropout8(seed, a.ln_site, (uint64_t)e0, a.ln_p, mi0, mi1);
+        dy0 *= mi0;
+        dy1 *= mi1;
+      }
+      if (a.ln_out_t) st8_bf16(a.ln_out_t + e0, dy0, dy1);
+      py0 += dy0;
+      py1 += dy1;
+    }
+    const int64_t blk = (m0 + h * 32) / 32;
+    const bool live = m0 + h * 32 < a.M;  // block-uniform
+    red[(0 * 8 + hw) * 64 + 2 * hl] = pg0;
+    red[(0 * 8 + hw) * 64 + 2 * hl + 1] = pg1;
+    red[(1 * 8 + hw) * 64 + 2 * hl] = pb0;
+    red[(1 * 8 + hw) * 64 + 2 * hl + 1] = pb1;
+    red[(2 * 8 + hw) * 64 + 2 * hl] = py0;
+    red[(2 * 8 + hw) * 64 + 2 * hl + 1] = py1;
+    __syncthreads();
+    if (live && tid < 3 * 64) {  // waves 0-2: one kind each, the 8 half-waves in order
+      const int kind = tid >> 6, q = tid & 63;
+      f32x4 s = red[(kind * 8) * 64 + q];
+#pragma unroll
+      for (int k = 1; k < 8; ++k) s += red[(kind * 8 + k) * 64 + q];
+      const int slot = kind == 2 ? 3 : kind;  // fs2_ln_bwd's part layout: dgamma, dbeta, -, dbias
+      st4(a.ln_part + ((int64_t)slot * a.ln_nblk + blk) * 256 + 4 * q, s);
+    }
+    __syncthreads();
+  }
+}
+
 // Epilogue through LDS, one half (wm) at a time: bias, aux add, ReLU / ReLU-mask, bf16 cast
 // on 8-element row vectors (16-B / 32-B coalesced stores).  Shared by both NT kernels.
 template <int BM, int BN, bool VOC, int NWAVE = 4, int WN = 2>
@@ -263,6 +370,12 @@ FS2_DEV void nt_epilogue(const GldsArgs& a, f32x4 (&acc)[BM / 32][BN / WN / 16],
   constexpr int EPI_LD = BN + 4;
   if constexpr (BN == 256 && !VOC) {
     if (a.ln_out) {
+      if constexpr (BM == 64) {
+        if (a.ln_mode == 1) {
+          nt_epilogue_lnbwd<BM, NWAVE, WN>(a, acc, smem, m0, tid, wm, wn, g, r16);
+          return;
+        }
+      }
       nt_epilogue_ln<BM, NWAVE, WN>(a, acc, smem, m0, skip, tid, wm, wn, g, r16);
       return;
     }
@@ -1639,6 +1752,42 @@ int conv_gemm_ln_glds_launch(const void* x, int64_t ldx, const void* wk, int64_t
     else conv_gemm_nt_glds<64, 256, 2, false, false><<<grid, 256, 0, st>>>(a);
   }
   return launch_status("fs2_conv_gemm_ln");
+}
+
+// fs2_conv_gemm_ln_bwd: the tap-major kernel on 64 x 256 tiles with the LayerNorm-backward
+// epilogue (ws = fs2_ln_bwd's partial layout; the caller runs fs2_ln_bwd_final)
+int conv_gemm_lnbwd_glds_launch(const void* x, int64_t ldx, const void* wk, int64_t rows,
+                                int64_t seq_len, int64_t c_in, int taps, int pad,
+                                const int64_t* lens, const float* aux, const float* xhat,
+                                const float* rstd, const float* gamma, float p_in,
+                                const uint64_t* seed, uint64_t site_in, float* dres, int dres_add,
+                                void* dy_t, float* ws, hipStream_t st) {
+  auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  FS2_CHECK_ARG(c_in % 8 == 0 && ldx % 8 == 0 && al16(x) && al16(wk),
+                "fs2_conv_gemm_ln_bwd: c_in/ldx must be multiples of 8 and operands 16-B aligned");
+  FS2_CHECK_ARG(al16(aux) && al16(xhat) && al16(gamma) && al16(dres) && al16(dy_t) && al16(ws),
+                "fs2_conv_gemm_ln_bwd: LayerNorm tensors must be 16-B aligned");
+  GldsArgs a{(const u16*)x, ldx, (const u16*)wk, nullptr, 256, rows, seq_len, (int)c_in, 256,
+             taps, pad, (int)(taps * c_in), nullptr, aux ? FS2_EPI_ADD_AUX : 0, aux, 256, 0, 0, 1,
+             1, lens, 1, 0.f, 1.f, nullptr, 0.f};
+  a.ln_gamma = gamma;
+  a.ln_out = dres;
+  a.ln_out_t = (u16*)dy_t;
+  a.ln_xhat = const_cast<float*>(xhat);
+  a.ln_rstd = const_cast<float*>(rstd);
+  a.ln_seed = p_in > 0.f ? seed : nullptr;
+  a.ln_site = site_in;
+  a.ln_p = p_in;
+  a.ln_mode = 1;
+  a.ln_dres_add = dres_add;
+  a.ln_part = ws;
+  a.ln_nblk = (rows + 31) / 32;
+  a.tiles_m = (int)((rows + 63) / 64);
+  a.tiles_n = 1;
+  const unsigned grid = (unsigned)a.tiles_m;
+  if (c_in % 64 == 0) conv_gemm_nt_glds<64, 256, 2, true, false><<<grid, 256, 0, st>>>(a);
+  else conv_gemm_nt_glds<64, 256, 2, false, false><<<grid, 256, 0, st>>>(a);
+  return launch_status("fs2_conv_gemm_ln_bwd");
 }
 
 int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, int64_t ldy,

@@ -111,6 +111,29 @@ def conv_gemm_ln(x, wk, rows, seq_len, c_in, c_out, taps, pad, gamma, beta, bias
     return out, out_t, xhat, rstd
 
 
+def conv_gemm_ln_bwd(x, wk, rows, seq_len, c_in, c_out, taps, pad, xhat, rstd, gamma, dgamma,
+                     dbeta, aux=None, lens=None, p_in=0.0, seed=0, site_in=0, dres=None,
+                     dres_add=False, dbias_in=None, copy=torch.bfloat16):
+    """bf16 conv/Linear whose output (+ aux) is a post-LayerNorm's upstream gradient, with that
+    LayerNorm's backward in the epilogue (fs2_conv_gemm_ln_bwd): returns ``ln_bwd(conv_gemm(x,
+    flags=ADD_AUX, aux=aux), ...)``'s (dy compute copy, dres); dgamma / dbeta / dbias_in
+    accumulate."""
+    _dev(x, wk, aux, xhat, rstd, gamma, dgamma, dbeta, dbias_in, lens, dres)
+    if x.dtype != torch.bfloat16 or wk.dtype != torch.bfloat16:
+        raise RuntimeError("conv_gemm_ln_bwd: bf16 operands only")
+    if dres is None:
+        dres = torch.empty(rows, c_out, dtype=torch.float32, device=x.device)
+    dy_t = _copy((rows, c_out), copy, x.device)
+    n = lib.fs2_ln_bwd_ws_bytes(rows, c_out)
+    w = ws(n, x.device)
+    sd = seed_arg(seed, x.device) if p_in > 0 else None
+    lib.fs2_conv_gemm_ln_bwd(ptr(x), c_in, ptr(wk), rows, seq_len, c_in, c_out, taps, pad,
+                             ptr(lens), ptr(aux), ptr(xhat), ptr(rstd), ptr(gamma), ptr(dgamma),
+                             ptr(dbeta), ptr(dbias_in), p_in, ptr(sd), site_in, ptr(dres),
+                             int(dres_add), ptr(dy_t), ptr(w), n, stream())
+    return dy_t, dres
+
+
 def conv_gemm_ex(x, wk, rows, seq_len, c_in, c_out, taps, pad, dilation=1, bias=None, flags=0,
                  aux=None, out=None, y2=None, alpha=0.1, scale=1.0, alpha2=0.1, lens=None):
     """Dilated conv with the vocoder epilogue (fs2_conv_gemm_ex): out and/or y2 (the

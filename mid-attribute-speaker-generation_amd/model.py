@@ -166,6 +166,8 @@ class StepCtx:
 # bf16 path: FFT-block post-LayerNorms fused into the fc / w_2 GEMM epilogues (fs2_conv_gemm_ln)
 FUSE_LN = os.environ.get("FS2_FUSE_LN", "1") != "0"  # step-level A/B switch
 FUSE_LN_MIN_ROWS = 16384
+# ... and each block's QKV data gradient carries the previous block's LN2 backward
+FUSE_LN_BWD = os.environ.get("FS2_FUSE_LN_BWD", "1") != "0"
 
 
 def _t(f, t):
@@ -332,7 +334,12 @@ class FFTBlock(nn.Module):
         saved = (x_c, qkv, o, lse, x1_c, h, xh1, rs1, xh2, rs2, p, ctx, lens, B, T)
         return x2, x2_t, saved
 
-    def bwd(self, dx2, saved):
+    def bwd(self, dx2, saved, ln2_done=None, prev=None):
+        """Block backward from the gradient of its output.  ``ln2_done`` = (dy2 copy, dx1):
+        this block's LN2 backward already ran in the epilogue of the following block's QKV data
+        gradient.  ``prev`` = (previous block, its saved tensors): run the previous block's LN2
+        backward in this block's QKV data-gradient epilogue (fs2_conv_gemm_ln_bwd) and return
+        its (dy2 copy, dx1) instead of dx."""
         a, f = self.slf_attn, self.pos_ffn
         x_c, qkv, o, lse, x1_c, h, xh1, rs1, xh2, rs2, p, ctx, lens, B, T = saved
         M, d = x_c.shape
@@ -341,12 +348,15 @@ class FFTBlock(nn.Module):
         seed, cdt = ctx.seed, ctx.cdt
         w1, w2 = f.w_1, f.w_2
         ln2, ln1 = f.layer_norm, a.layer_norm
-        # LN2 (masked; dropout before the residual add): dx1 starts as dz2
-        dx1 = torch.empty((M, d), dtype=torch.float32, device=x_c.device)
-        dy2, dy2_t = K.ln_bwd(xh2, rs2, ln2.weight, ln2.bias, _g(ln2.weight), _g(ln2.bias),
-                              dout=dx2, lens=lens, seq_len=T, p_in=p, seed=seed,
-                              site_in=self.site + 1, dres=dx1, dres_add=False, copy=ctx.copy,
-                              dbias_in=_g(w2.bias))
+        if ln2_done is not None:
+            dy2, dy2_t, dx1 = None, ln2_done[0], ln2_done[1]
+        else:
+            # LN2 (masked; dropout before the residual add): dx1 starts as dz2
+            dx1 = torch.empty((M, d), dtype=torch.float32, device=x_c.device)
+            dy2, dy2_t = K.ln_bwd(xh2, rs2, ln2.weight, ln2.bias, _g(ln2.weight), _g(ln2.bias),
+                                  dout=dx2, lens=lens, seq_len=T, p_in=p, seed=seed,
+                                  site_in=self.site + 1, dres=dx1, dres_add=False, copy=ctx.copy,
+                                  dbias_in=_g(w2.bias))
         dy2_c = _t(dy2, dy2_t)
         ctx.wgrad(dy2_c, h, _g(w2.weight), M, T, w2.c_in, d, w2.k, w2.padding, lens=lens)
         dh = K.conv_gemm(dy2_c, w2._w_bwd, M, T, d, w2.c_in, w2.k, w2.padding,
@@ -367,9 +377,36 @@ class FFTBlock(nn.Module):
         do = K.conv_gemm(dy1_c, a.fc._w_bwd, M, T, d, hd, 1, 0, out_dtype=cdt, lens=lens)
         dqkv = K.attn_bwd(qkv, o, do, lse, lens, B, T, a.n_head, a.d_k, 1.0 / math.sqrt(a.d_k))
         ctx.wgrad(dqkv, x_c, self._qkv_gw, M, T, d, n3, 1, 0, db=self._qkv_gb, lens=lens)
+        if prev is not None:
+            pb, ps = prev
+            pf = pb.pos_ffn
+            pl2 = pf.layer_norm
+            return K.conv_gemm_ln_bwd(
+                dqkv, q._w_bwd, M, T, n3, d, 1, 0, ps[8], ps[9], pl2.weight, _g(pl2.weight),
+                _g(pl2.bias), aux=dx, lens=lens, p_in=ps[10], seed=seed, site_in=pb.site + 1,
+                dbias_in=_g(pf.w_2.bias), copy=ctx.copy)
         K.conv_gemm(dqkv, q._w_bwd, M, T, n3, d, 1, 0, flags=K.EPI_ADD_AUX, aux=dx, out=dx,
                     lens=lens)
         return dx
+
+
+def _stack_bwd(layers, saved, dx, ctx):
+    """Backward through a stack of FFT blocks.  bf16, decoder-sized grids: each block's QKV data
+    gradient carries the previous block's LN2 backward in its epilogue (fs2_conv_gemm_ln_bwd),
+    and that block then starts from the (dy2 copy, dx1) it left."""
+    layers, saved = list(reversed(layers)), list(reversed(saved))
+    carry = None
+    for i, (layer, s) in enumerate(zip(layers, saved)):
+        M, d = s[0].shape
+        fuse = (FUSE_LN_BWD and ctx.copy is not None and d == 256 and M >= FUSE_LN_MIN_ROWS and
+                i + 1 < len(layers))
+        out = layer.bwd(dx, s, ln2_done=carry, prev=(layers[i + 1], saved[i + 1]) if fuse else None)
+        ctx.notify(fft_param_order(layer))
+        if fuse:
+            carry, dx = out, None
+        else:
+            carry, dx = None, out
+    return dx
 
 
 def _ffn_stack(config, side):
@@ -728,9 +765,7 @@ class EncoderFn(torch.autograd.Function):
     def backward(fctx, dx):
         enc = fctx.enc
         dx = dx.contiguous()
-        for layer, s in zip(reversed(enc.layer_stack), reversed(fctx.saved)):
-            dx = layer.bwd(dx, s)
-            fctx.ctx.notify(fft_param_order(layer))
+        dx = _stack_bwd(enc.layer_stack, fctx.saved, dx, fctx.ctx)
         texts, accents = fctx.ids
         K.embedding_bwd(dx, texts, _g(enc.src_word_emb.weight), 0)
         K.embedding_bwd(dx, accents, _g(enc.src_accent_emb.weight), 0)
@@ -808,9 +843,7 @@ class DecoderFn(torch.autograd.Function):
         if dx is None:
             dx = K.zeros(fctx.saved[0][0].shape, fctx.saved[0][0].device)
         dx = dx.contiguous()
-        for layer, s in zip(reversed(fctx.dec.layer_stack), reversed(fctx.saved)):
-            dx = layer.bwd(dx, s)
-            fctx.ctx.notify(fft_param_order(layer))
+        dx = _stack_bwd(fctx.dec.layer_stack, fctx.saved, dx, fctx.ctx)
         fctx.saved = None
         return None, dx, None, None, None, None, None, None
 

@@ -477,6 +477,48 @@ def test_conv_gemm_ln(B, T, lens, cin, p, tile):
         assert torch.all(o1[~live] == 0)
 
 
+@pytest.mark.parametrize("B,T,lens,cin,p,dres_add", [
+    (3, 50, [50, 17, 1], 768, 0.0, False), (2, 200, [200, 130], 768, 0.2, False),
+    (6, 512, [512, 300, 129, 128, 1, 400], 768, 0.1, True), (5, 37, None, 256, 0.3, False)])
+def test_conv_gemm_ln_bwd(B, T, lens, cin, p, dres_add):
+    """fs2_conv_gemm_ln_bwd (GEMM + residual-gradient add + LayerNorm backward in one kernel)
+    against fs2_conv_gemm(FS2_EPI_ADD_AUX) -> fs2_ln_bwd.  The upstream gradient (acc + aux) is
+    the same fp32 value in both; the row arithmetic is the same but compiled in another kernel
+    (the compiler may contract a product into an FMA differently), so dres agrees to fp32
+    rounding and its bf16 copy to one bf16 ulp; dgamma / dbeta / the fused bias gradient sum the
+    same 32-row block partials in another in-block order."""
+    M, d = B * T, 256
+    lt = None if lens is None else torch.tensor(lens, device=DEV)
+    x = bf(rnd(M, cin, seed=61))
+    w = bf(rnd(d, cin, 1, scale=1 / math.sqrt(cin), seed=62)).float()
+    wf = torch.empty(d * cin, device=DEV, dtype=torch.bfloat16)
+    wb = torch.empty_like(wf)
+    K.weight_prep(w, d, cin, 1, wf, wb)
+    aux = rnd(M, d, seed=63)
+    # a LayerNorm forward state to differentiate
+    y = rnd(M, d, seed=64)
+    g, bt = 1 + 0.1 * rnd(d, seed=65), 0.1 * rnd(d, seed=66)
+    _, _, xh, rs, _ = K.ln_fwd(y, g, bt, lens=lt, seq_len=T, p_in=p, seed=5, site_in=3)
+    dout = K.conv_gemm(x, wf, M, T, cin, d, 1, 0, flags=K.EPI_ADD_AUX, aux=aux)
+    grads = [torch.full((d,), 0.5, device=DEV) for _ in range(6)]
+    dres0 = rnd(M, d, seed=67) if dres_add else torch.empty(M, d, device=DEV)
+    dres1 = dres0.clone()
+    _, dyt0 = K.ln_bwd(xh, rs, g, bt, grads[0], grads[1], dout=dout, lens=lt, seq_len=T, p_in=p,
+                       seed=5, site_in=3, dres=dres0, dres_add=dres_add, copy=torch.bfloat16,
+                       dbias_in=grads[2])
+    dyt1, _ = K.conv_gemm_ln_bwd(x, wf, M, T, cin, d, 1, 0, xh, rs, g, grads[3], grads[4], aux=aux,
+                                 lens=lt, p_in=p, seed=5, site_in=3, dres=dres1,
+                                 dres_add=dres_add, dbias_in=grads[5])
+    live = (torch.ones(M, dtype=torch.bool, device=DEV) if lt is None else
+            (torch.arange(T, device=DEV)[None] < lt[:, None]).reshape(-1))
+    a1, a0 = dyt1.float(), dyt0.float()
+    assert bool(((a1 - a0).abs() <= a0.abs() * 2.0 ** -7).all()), "bf16 dy copies differ by > 1 ulp"
+    close(dres1[live], dres0[live], 1e-6)
+    assert torch.equal(dres1[~live], dres0[~live])
+    for a_, b_ in zip(grads[3:], grads[:3]):
+        close(a_, b_, 1e-5)
+
+
 def test_conv_gemm_bf16_padding_tiles():
     """lens: all-padding 128-row tiles are written as zero rows (bias dropped) / aux, the
     rest exactly as without lens; the weight gradient with zero dy at padded rows is

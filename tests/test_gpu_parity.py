@@ -351,7 +351,7 @@ def test_fused_gemm_ln_step_bitwise():
     pp, mc, tc, path = PKG.config.load_configs("JVS-VCTK")
     res = []
     for fuse in (False, True):
-        M.FUSE_LN, M.FUSE_LN_MIN_ROWS = fuse, 0
+        M.FUSE_LN, M.FUSE_LN_MIN_ROWS, M.FUSE_LN_BWD = fuse, 0, False
         try:
             model = M.FastSpeech2(pp, mc, path, device=DEV, compute_dtype=torch.bfloat16)
             PKG.seeded.load_seeded_(model)
@@ -363,9 +363,45 @@ def test_fused_gemm_ln_step_bitwise():
             torch.cuda.synchronize()
             res.append((model.arena().flat.clone(), tr.opt.m.clone(), torch.stack(losses)))
         finally:
-            M.FUSE_LN, M.FUSE_LN_MIN_ROWS = True, 16384
+            M.FUSE_LN, M.FUSE_LN_MIN_ROWS, M.FUSE_LN_BWD = True, 16384, True
     for a, b in zip(*res):
         assert torch.equal(a, b)
+
+
+def test_fused_gemm_ln_bwd_step():
+    """bf16: each FFT block's QKV data gradient carrying the previous block's LN2 backward
+    (fs2_conv_gemm_ln_bwd, model.FUSE_LN_BWD) against the two-launch form: one forward +
+    backward with dropout ON at ragged lengths, every parameter gradient to 2e-2 of its tensor's
+    scale (bf16 level: the fused row arithmetic agrees to fp32 rounding and its bf16 dy copy to
+    one ulp, test_conv_gemm_ln_bwd, and a one-ulp difference of a bf16 GEMM operand propagates
+    through the remaining blocks; a wrong or missing term is O(1)) and the losses equal.  After
+    Adam steps such differences are amplified wherever a gradient is near zero, so the check is
+    on the gradients."""
+    pp, mc, tc, path = PKG.config.load_configs("JVS-VCTK")
+    res = []
+    for fuse in (False, True):
+        M.FUSE_LN_BWD, M.FUSE_LN_MIN_ROWS = fuse, 0
+        try:
+            model = M.FastSpeech2(pp, mc, path, device=DEV, compute_dtype=torch.bfloat16)
+            PKG.seeded.load_seeded_(model)
+            model.train()
+            model.seed(23)
+            tr = T.Trainer(model, pp, mc, tc)
+            batch = PKG.data.to_device(PKG.data.syn_batch(8, 32, seed=7), DEV)
+            losses = T.train_step(model, tr.opt, tr.Loss, tr.eLoss, batch, update=False)[0]
+            torch.cuda.synchronize()
+            res.append((torch.stack(list(losses)).clone(),
+                        {n: M._g(p_).clone() for n, p_ in model.named_parameters()
+                         if hasattr(p_, "_fs2_grad")}))
+        finally:
+            M.FUSE_LN_BWD, M.FUSE_LN_MIN_ROWS = True, 16384
+    (l0, g0), (l1, g1) = res
+    assert torch.equal(l0, l1)  # the forward is untouched
+    def scale(n):  # gradients zero in exact arithmetic: their layer's weight-gradient scale
+        ref = n.rsplit(".", 1)[0] + ".weight" if _structural_zero(n) else n
+        return max(g0[ref].abs().max().item(), 1e-12)
+    worst = max(((g1[n] - g0[n]).abs().max().item() / scale(n), n) for n in g0)
+    assert worst[0] <= 2e-2, f"{worst[1]}: max abs err / scale {worst[0]:.3e}"
 
 
 def test_graph_replay_matches_eager():

@@ -26,7 +26,7 @@ def timeit(run, n=20):
     return s.elapsed_time(e) / n * 1e3
 
 
-for knob in ((0, 1, 2, 3, 0, 2) if "--variants" in sys.argv else (0,)):
+for knob in ((0, 1, 2, 3, 0, 2) if "--variants" in sys.argv else tuple(int(v) for v in sys.argv[sys.argv.index("--knobs") + 1].split(",")) if "--knobs" in sys.argv else (0,)):
   K.lib.fs2_set_tuning(9, knob)  # FS2_TUNE_ATTN
   print(f"== FS2_TUNE_ATTN = {knob}")
   for name, T, lens in (("decoder", 512, np.asarray(b[7])), ("encoder", 128, np.asarray(b[4]))):

@@ -361,6 +361,7 @@ __global__ __launch_bounds__(1024) void bn_stats_final(const float* psum, const 
   const float mu = mu_s[tx];
   float q = 0.f;
   if (col < c) {
+#pragma unroll 4
     for (int64_t p = ty; p < nparts; p += 16) {
       const int64_t left = rows - p * BN_ROWS;
       const float n = (float)(left < BN_ROWS ? left : BN_ROWS);

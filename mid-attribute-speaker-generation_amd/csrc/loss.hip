@@ -261,7 +261,11 @@ FS2_DEV float gmm_pi_gz(const float* pi, const float* resp, const float* g, int6
 // Blocks 0..: one thread per mu / sigma head output, looping over the batch in order.
 // Last block: the pi head -- (b, k) gradients for a chunk of the batch into LDS, then one
 // thread per (k, input) sums the chunk in batch order.  Deterministic throughout.
-__global__ __launch_bounds__(256) void gmm_head_bwd(const float* meta, const float* e,
+// 8 waves per block: for its 64 mu / sigma outputs (one per lane) wave w sums the batch rows
+// b = w, w + 8, ... in order, and the 8 wave partials are added in wave order through LDS (a
+// single thread walking all B rows was a chain of dependent divisions / exps: 40-60 us on the
+// step's critical path at B = 48).  The last block computes the pi head's gradients.
+__global__ __launch_bounds__(512) void gmm_head_bwd(const float* meta, const float* e,
                                                     const float* pi, const float* mu,
                                                     const float* sigma, const float* sigma_pre,
                                                     const float* resp, const float* g, int64_t B,
@@ -292,30 +296,49 @@ __global__ __launch_bounds__(256) void gmm_head_bwd(const float* meta, const flo
     }
     return;
   }
-  const int o = blockIdx.x * blockDim.x + threadIdx.x;
-  if (o >= 2 * KD) return;
+  __shared__ float red[8][9][64];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int o = blockIdx.x * 64 + lane;
+  const bool act = o < 2 * KD;
   const int kd = o < KD ? o : o - KD;
   const int k = kd / D, dd = kd - k * D;
   float acc_w[8] = {0, 0, 0, 0, 0, 0, 0, 0}, acc_b = 0.f;
-  for (int64_t b = 0; b < B; ++b) {
-    const int64_t idx = b * KD + kd;
-    const float gg = g[b] * resp[b * K + k];
-    const float sg = sigma[idx], df = e[b * D + dd] - mu[idx];
-    float gz;
-    if (o < KD) {  // mu
-      gz = gg * df / (sg * sg);
-    } else {  // sigma through softplus
-      const float dsg = gg * (df * df / (sg * sg * sg) - 1.f / sg);
-      const float x = sigma_pre[idx];
-      gz = dsg * (x > 20.f ? 1.f : 1.f / (1.f + expf(-x)));
+  if (act) {
+    for (int64_t b = w; b < B; b += 8) {
+      const int64_t idx = b * KD + kd;
+      const float gg = g[b] * resp[b * K + k];
+      const float sg = sigma[idx], df = e[b * D + dd] - mu[idx];
+      float gz;
+      if (o < KD) {  // mu
+        gz = gg * df / (sg * sg);
+      } else {  // sigma through softplus
+        const float dsg = gg * (df * df / (sg * sg * sg) - 1.f / sg);
+        const float x = sigma_pre[idx];
+        gz = dsg * (x > 20.f ? 1.f : 1.f / (1.f + expf(-x)));
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        if (i < in_dim) acc_w[i] += gz * meta[b * in_dim + i];
+      acc_b += gz;
     }
-    for (int i = 0; i < in_dim; ++i) acc_w[i] += gz * meta[b * in_dim + i];
-    acc_b += gz;
   }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) red[w][i][lane] = acc_w[i];
+  red[w][8][lane] = acc_b;
+  __syncthreads();
+  if (w != 0 || !act) return;
   float* dw = o < KD ? dw_mu : dw_s;
   float* db = o < KD ? db_mu : db_s;
-  for (int i = 0; i < in_dim; ++i) dw[kd * in_dim + i] += acc_w[i];
-  db[kd] += acc_b;
+  for (int i = 0; i < in_dim; ++i) {
+    float sw = red[0][i][lane];
+#pragma unroll
+    for (int v = 1; v < 8; ++v) sw += red[v][i][lane];
+    dw[kd * in_dim + i] += sw;
+  }
+  float sb = red[0][8][lane];
+#pragma unroll
+  for (int v = 1; v < 8; ++v) sb += red[v][8][lane];
+  db[kd] += sb;
 }
 
 __global__ void mean_k(const float* x, int64_t n, float* out, const float* den) {
@@ -447,7 +470,7 @@ int fs2_gmm_head_bwd(const float* meta, const float* e, const float* pi, const f
   FS2_CHECK_ARG(k >= 1 && k <= 16 && in_dim >= 1 && in_dim <= 8, "fs2_gmm_head_bwd: k <= 16, in_dim <= 8");
   FS2_CHECK_ARG(k * (in_dim + 1) <= 256, "fs2_gmm_head_bwd: k * (in_dim + 1) <= 256");
   const int64_t n = 2LL * k * d;
-  gmm_head_bwd<<<(unsigned)((n + 255) / 256 + 1), 256, 0, as_stream(stream)>>>(
+  gmm_head_bwd<<<(unsigned)((n + 63) / 64 + 1), 512, 0, as_stream(stream)>>>(
       meta, e, pi, mu, sigma, sigma_pre, resp, g_logp, batch, in_dim, k, d, dw_pi, db_pi, dw_sigma,
       db_sigma, dw_mu, db_mu);
   return launch_status("fs2_gmm_head_bwd");

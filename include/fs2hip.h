@@ -358,7 +358,9 @@ int fs2_bn_fwd(int dtype, const float* z, int64_t rows, int64_t c, const float* 
                float* running_var, float* mean, float* rstd, int act_tanh, float p,
                const uint64_t* seed, uint64_t site, const float* res, float* out, void* out_t,
                float* ws,
-               int64_t ws_bytes, void* stream);
+               int64_t ws_bytes, int64_t* num_batches_tracked, void* stream);
+/* (num_batches_tracked: nullable device int64, incremented with the running statistics --
+ *  BatchNorm1d's counter update, Layers.py:129-137, without a launch of its own.)        */
 /* Eval-mode BatchNorm1d (transformer/Layers.py:129-137 under model.eval()): normalise with
  * the running statistics, no dropout, no statistics update; mean / rstd (c floats each)
  * receive running_mean and 1/sqrt(running_var + eps).                                 */

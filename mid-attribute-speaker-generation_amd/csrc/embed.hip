@@ -130,18 +130,30 @@ __global__ __launch_bounds__(256) void rowvec_add_bwd(const float* __restrict__ 
                                                       const int64_t* __restrict__ ids, int64_t batch,
                                                       int64_t T, int d, float* dtab) {
   __shared__ f32x4 red[4][64];
+  __shared__ unsigned char hit[256];
   const int64_t b = blockIdx.x, id = ids[b];
-  for (int64_t j = 0; j < b; ++j)
-    if (ids[j] == id) return;  // block-uniform: an earlier utterance owns this id
+  // the id comparisons are made 256 at a time by the whole block (one serial global load per
+  // earlier utterance made the last blocks of a 48-utterance batch the launch's 21-us tail)
+  for (int64_t j0 = 0; j0 < b; j0 += 256) {
+    const int64_t j = j0 + threadIdx.x;
+    if (__syncthreads_or(j < b && ids[j] == id)) return;  // an earlier utterance owns this id
+  }
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   for (int c0 = 0; c0 < d; c0 += 256) {
     const int c = c0 + 4 * tx;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    if (c < d)
-      for (int64_t bb = b; bb < batch; ++bb) {
-        if (ids[bb] != id) continue;
-        for (int64_t t = ty; t < T; t += 4) acc += ld4(dout + (bb * T + t) * d + c);
-      }
+    for (int64_t q0 = b; q0 < batch; q0 += 256) {  // same rows, same order as one by one
+      __syncthreads();
+      hit[threadIdx.x] = q0 + threadIdx.x < batch && ids[q0 + threadIdx.x] == id;
+      __syncthreads();
+      const int64_t nq = batch - q0 < 256 ? batch - q0 : 256;
+      if (c < d)
+        for (int64_t u = 0; u < nq; ++u) {
+          if (!hit[u]) continue;
+          const int64_t bb = q0 + u;
+          for (int64_t t = ty; t < T; t += 4) acc += ld4(dout + (bb * T + t) * d + c);
+        }
+    }
     red[ty][tx] = acc;
     __syncthreads();
     if (ty == 0 && c < d)

@@ -350,7 +350,7 @@ __global__ __launch_bounds__(256) void bn_stats(const float* z, int64_t rows, in
 __global__ __launch_bounds__(1024) void bn_stats_final(const float* psum, const float* pm2,
                                                        int64_t nparts, int64_t rows, int64_t c,
                                                        float eps, float mom, float* mean, float* rm,
-                                                       float* rv, float* rstd) {
+                                                       float* rv, float* rstd, int64_t* nbt) {
   __shared__ float red[16][65];
   __shared__ float mu_s[64];
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
@@ -380,6 +380,7 @@ __global__ __launch_bounds__(1024) void bn_stats_final(const float* psum, const 
   rstd[col] = 1.f / sqrtf(var + eps);
   if (rm) rm[col] = (1.f - mom) * rm[col] + mom * mu;
   if (rv) rv[col] = (1.f - mom) * rv[col] + mom * (rows > 1 ? t / (float)(rows - 1) : var);
+  if (nbt && col == 0) nbt[0] += 1;
 }
 
 FS2_DEV f32x4 tanh4(f32x4 v) { return f32x4{tanhf(v.x), tanhf(v.y), tanhf(v.z), tanhf(v.w)}; }
@@ -627,7 +628,7 @@ int fs2_bn_fwd(int dtype, const float* z, int64_t rows, int64_t c, const float* 
                float* running_var, float* mean, float* rstd, int act_tanh, float p,
                const uint64_t* seed, uint64_t site, const float* res, float* out, void* out_t,
                float* ws,
-               int64_t ws_bytes, void* stream) {
+               int64_t ws_bytes, int64_t* num_batches_tracked, void* stream) {
   if (int rc = copy_dtype_ok(dtype, "fs2_bn_fwd")) return rc;
   FS2_CHECK_ARG(rows > 0 && c > 0, "fs2_bn_fwd: empty input");
   FS2_CHECK_ARG(ws_bytes >= fs2_bn_ws_bytes(rows, c), "fs2_bn_fwd: workspace too small");
@@ -638,7 +639,7 @@ int fs2_bn_fwd(int dtype, const float* z, int64_t rows, int64_t c, const float* 
   const unsigned cg = (unsigned)((c + 63) / 64);
   bn_stats<<<grid, 256, 0, st>>>(z, rows, c, ws, ws + nparts * c);
   bn_stats_final<<<cg, 1024, 0, st>>>(ws, ws + nparts * c, nparts, rows, c, eps, momentum, mean,
-                                      running_mean, running_var, rstd);
+                                      running_mean, running_var, rstd, num_batches_tracked);
   unsigned short* ot = dtype == FS2_BF16 ? (unsigned short*)out_t : nullptr;
   FS2_CHECK_ARG(out || ot, "fs2_bn_fwd: no output requested");
   bn_apply<<<ew_grid(rows * c / 8), 256, 0, st>>>(z, mean, rstd, gamma, beta, rows * c / 8, (int)c,

@@ -310,9 +310,10 @@ def ln_bwd(xhat, rstd, gamma, beta, dgamma, dbeta, dout=None, ddot=None, dot_w=N
 
 # ------------------------------------------------------------------ BatchNorm
 def bn_fwd(z, gamma, beta, running_mean, running_var, act_tanh, p, seed, site, res=None,
-           eps=1e-5, momentum=0.1, copy=None, want_out=True):
-    """(out fp32 or None when only the copy is wanted, out copy or None, mean, rstd)."""
-    _dev(z, gamma, beta, running_mean, running_var, res)
+           eps=1e-5, momentum=0.1, copy=None, want_out=True, num_batches_tracked=None):
+    """(out fp32 or None when only the copy is wanted, out copy or None, mean, rstd);
+    ``num_batches_tracked`` (device int64) is incremented in the statistics launch."""
+    _dev(z, gamma, beta, running_mean, running_var, res, num_batches_tracked)
     rows, c = z.shape
     out = torch.empty_like(z) if (want_out or copy is None) else None
     out_t = _copy(z.shape, copy, z.device)
@@ -324,7 +325,7 @@ def bn_fwd(z, gamma, beta, running_mean, running_var, act_tanh, p, seed, site, r
     lib.fs2_bn_fwd(BF16 if copy is not None else F32, ptr(z), rows, c, ptr(gamma), ptr(beta), eps,
                    momentum, ptr(running_mean), ptr(running_var), ptr(mean), ptr(rstd),
                    int(act_tanh), p, ptr(sd), site, ptr(res), ptr(out), ptr(out_t), ptr(w), n,
-                   stream())
+                   ptr(num_batches_tracked), stream())
     return out, out_t, mean, rstd
 
 

@@ -572,9 +572,9 @@ class PostNet(nn.Module):
             last = i == n - 1
             out, out_t, mean, rstd = K.bn_fwd(z, bn.weight, bn.bias, rm, rv, not last, p, ctx.seed,
                                               self.site + i, res=x if last else None,
-                                              copy=None if last else ctx.copy, want_out=last)
-            if self.training:
-                K.add_i64_(bn.num_batches_tracked, 1)
+                                              copy=None if last else ctx.copy, want_out=last,
+                                              num_batches_tracked=bn.num_batches_tracked
+                                              if self.training else None)
             saved.append((a_c, z, mean, rstd))
             a_c = _t(out, out_t)
         return out, (saved, p, ctx, T)

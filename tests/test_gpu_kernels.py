@@ -191,7 +191,9 @@ def test_batchnorm(act, res):
     g, b = 1 + 0.1 * rnd(c, seed=2), 0.1 * rnd(c, seed=3)
     rm, rv = torch.zeros(c, device=DEV), torch.ones(c, device=DEV)
     r = rnd(M, c, seed=4) if res else None
-    out, _, mean, rstd = K.bn_fwd(z, g, b, rm, rv, act, 0.0, 1, 2, res=r)
+    nbt = torch.tensor(5, dtype=torch.int64, device=DEV)
+    out, _, mean, rstd = K.bn_fwd(z, g, b, rm, rv, act, 0.0, 1, 2, res=r, num_batches_tracked=nbt)
+    assert nbt.item() == 6  # BatchNorm1d's counter, advanced in the statistics launch
     zr, gr, br = z.clone().requires_grad_(), g.clone().requires_grad_(), b.clone().requires_grad_()
     rm2, rv2 = torch.zeros(c, device=DEV), torch.ones(c, device=DEV)
     ref = F.batch_norm(zr, rm2, rv2, gr, br, training=True, momentum=0.1, eps=1e-5)

@@ -281,20 +281,21 @@ __global__ __launch_bounds__(LN_BWD_WAVES * 64) void ln_bwd_f32(LnBwd a) {
 // ------------------------------------------------------------------ BatchNorm
 constexpr int BN_ROWS = 64;  // rows per partial block: 1,536 blocks at 24,576 rows (latency-bound at 64)
 
-// in-order column sum of partial rows: 64 columns x 16 lanes per block (see colsum_final)
+// in-order column sum of partial rows: 32 columns x 32 part lanes per block, 8 loads in flight
+// per lane (the 64 x 16 layout with 4 took 24 dependent rounds at the PostNet's 384 parts)
 FS2_DEV float col_reduce(const float* part, int64_t nparts, int64_t c, int64_t col, int tx, int ty,
-                         float (*red)[65]) {
+                         float (*red)[33]) {
   float s = 0.f;
   if (col < c) {
-#pragma unroll 4
-    for (int64_t p = ty; p < nparts; p += 16) s += part[p * c + col];
+#pragma unroll 8
+    for (int64_t p = ty; p < nparts; p += 32) s += part[p * c + col];
   }
   red[ty][tx] = s;
   __syncthreads();
   float t = 0.f;
   if (ty == 0) {
 #pragma unroll
-    for (int y = 0; y < 16; ++y) t += red[y][tx];
+    for (int y = 0; y < 32; ++y) t += red[y][tx];
   }
   __syncthreads();
   return t;
@@ -351,18 +352,18 @@ __global__ __launch_bounds__(1024) void bn_stats_final(const float* psum, const 
                                                        int64_t nparts, int64_t rows, int64_t c,
                                                        float eps, float mom, float* mean, float* rm,
                                                        float* rv, float* rstd, int64_t* nbt) {
-  __shared__ float red[16][65];
-  __shared__ float mu_s[64];
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  const int64_t col = (int64_t)blockIdx.x * 64 + tx;
+  __shared__ float red[32][33];
+  __shared__ float mu_s[32];
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const int64_t col = (int64_t)blockIdx.x * 32 + tx;
   const float s = col_reduce(psum, nparts, c, col, tx, ty, red);
   if (ty == 0) mu_s[tx] = s / (float)rows;
   __syncthreads();
   const float mu = mu_s[tx];
   float q = 0.f;
   if (col < c) {
-#pragma unroll 4
-    for (int64_t p = ty; p < nparts; p += 16) {
+#pragma unroll 8
+    for (int64_t p = ty; p < nparts; p += 32) {
       const int64_t left = rows - p * BN_ROWS;
       const float n = (float)(left < BN_ROWS ? left : BN_ROWS);
       const float d = psum[p * c + col] / n - mu;
@@ -374,7 +375,7 @@ __global__ __launch_bounds__(1024) void bn_stats_final(const float* psum, const 
   if (ty != 0 || col >= c) return;
   float t = 0.f;
 #pragma unroll
-  for (int y = 0; y < 16; ++y) t += red[y][tx];
+  for (int y = 0; y < 32; ++y) t += red[y][tx];
   const float var = t / (float)rows;
   mean[col] = mu;
   rstd[col] = 1.f / sqrtf(var + eps);
@@ -385,116 +386,186 @@ __global__ __launch_bounds__(1024) void bn_stats_final(const float* psum, const 
 
 FS2_DEV f32x4 tanh4(f32x4 v) { return f32x4{tanhf(v.x), tanhf(v.y), tanhf(v.z), tanhf(v.w)}; }
 
-// out = act(BN(z)) * dropout (+ res), 8 consecutive elements (same row) per lane
-__global__ __launch_bounds__(256) void bn_apply(const float* z, const float* mean, const float* rstd,
-                                                const float* gamma, const float* beta, int64_t n8,
-                                                int c, int act_tanh, float p, const uint64_t* seed_p,
-                                                uint64_t site, const float* res, float* out,
-                                                unsigned short* out_t) {
+// column of element e0 (32-bit division when the tensor allows: the 64-bit one is a long
+// instruction sequence per lane)
+FS2_DEV int col_of(int64_t e0, int c, bool wide) {
+  return wide ? (int)(e0 % c) : (int)((uint32_t)e0 % (uint32_t)c);
+}
+
+// out = act(BN(z)) * dropout (+ res), G groups of 8 consecutive elements (same row) per lane,
+// every group's loads issued first.  Launched with G = 1: G = 2 measured 35 us against 23 us at
+// 24,576 x 512 (a lane stride of 64 B leaves each 16-B load instruction a quarter coalesced)
+template <int G>
+__global__ __launch_bounds__(256) void bn_apply(const float* __restrict__ z, const float* mean,
+                                                const float* rstd, const float* gamma,
+                                                const float* beta, int64_t nq, int c, bool wide,
+                                                int act_tanh, float p, const uint64_t* seed_p,
+                                                uint64_t site, const float* __restrict__ res,
+                                                float* __restrict__ out,
+                                                unsigned short* __restrict__ out_t) {
   const uint64_t seed = seed_p ? *seed_p : 0ull;
-  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n8;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nq;
        q += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t e0 = q * 8;
-    const int col = (int)(e0 % c);
-    f32x4 v0 = (ld4(z + e0) - ld4(mean + col)) * ld4(rstd + col) * ld4(gamma + col) + ld4(beta + col);
-    f32x4 v1 = (ld4(z + e0 + 4) - ld4(mean + col + 4)) * ld4(rstd + col + 4) * ld4(gamma + col + 4) +
-               ld4(beta + col + 4);
-    if (act_tanh) {
-      v0 = tanh4(v0);
-      v1 = tanh4(v1);
-    }
-    if (p > 0.f) {
-      f32x4 m0, m1;
-      dropout8(seed, site, (uint64_t)e0, p, m0, m1);
-      v0 *= m0;
-      v1 *= m1;
-    }
-    if (res) {
-      v0 += ld4(res + e0);
-      v1 += ld4(res + e0 + 4);
-    }
-    if (out) {
-      st4(out + e0, v0);
-      st4(out + e0 + 4, v1);
-    }
-    if (out_t) st8_bf16(out_t + e0, v0, v1);
-  }
-}
-
-// g = dout * mask * act'(a) for 8 consecutive elements (one Philox call); also returns xhat
-FS2_DEV void bn_g8(const float* dout, const float* z, const float* mean, const float* rstd,
-                   const float* gamma, const float* beta, int col, int act_tanh, float p,
-                   uint64_t seed, uint64_t site, int64_t e0, f32x4 (&g)[2], f32x4 (&xh)[2]) {
-  f32x4 m[2] = {{1.f, 1.f, 1.f, 1.f}, {1.f, 1.f, 1.f, 1.f}};
-  if (p > 0.f) dropout8(seed, site, (uint64_t)e0, p, m[0], m[1]);
+    const int64_t e0 = q * 8 * G;
+    const int col = col_of(e0, c, wide);
+    f32x4 zv[G][2], rv[G][2];
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int cc = col + 4 * h;
-    xh[h] = (ld4(z + e0 + 4 * h) - ld4(mean + cc)) * ld4(rstd + cc);
-    g[h] = ld4(dout + e0 + 4 * h) * m[h];
-    if (act_tanh) {
-      const f32x4 t = tanh4(xh[h] * ld4(gamma + cc) + ld4(beta + cc));
-      g[h] *= 1.f - t * t;
+    for (int g = 0; g < G; ++g) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        zv[g][h] = ld4(z + e0 + 8 * g + 4 * h);
+        rv[g][h] = res ? ld4(res + e0 + 8 * g + 4 * h) : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int cc = col + 8 * g;
+      const int64_t eg = e0 + 8 * g;
+      f32x4 v0 = (zv[g][0] - ld4(mean + cc)) * ld4(rstd + cc) * ld4(gamma + cc) + ld4(beta + cc);
+      f32x4 v1 = (zv[g][1] - ld4(mean + cc + 4)) * ld4(rstd + cc + 4) * ld4(gamma + cc + 4) +
+                 ld4(beta + cc + 4);
+      if (act_tanh) {
+        v0 = tanh4(v0);
+        v1 = tanh4(v1);
+      }
+      if (p > 0.f) {
+        f32x4 m0, m1;
+        dropout8(seed, site, (uint64_t)eg, p, m0, m1);
+        v0 *= m0;
+        v1 *= m1;
+      }
+      if (res) {
+        v0 += rv[g][0];
+        v1 += rv[g][1];
+      }
+      if (out) {
+        st4(out + eg, v0);
+        st4(out + eg + 4, v1);
+      }
+      if (out_t) st8_bf16(out_t + eg, v0, v1);
     }
   }
 }
 
-// column partials of g and g*xhat: block (x, y) covers channels [512x, 512x+512) (8 per
-// lane) of rows [BN_ROWS*y, BN_ROWS*(y+1)); wave ry takes rows r0 + ry + 8i, and the eight
-// row-group (wave) partials are summed in wave order.  8 waves per block: the PostNet shape
-// gives only 1.5 blocks per CU, so the row groups are what keeps enough loads in flight
+// column partials of g and g*xhat over the BN_BWD_ROWS rows of block x.  The lane layout follows
+// the width: cg = c / 8 column groups (8 channels per lane) x rl row lanes (host: the largest
+// power of two with cg * rl <= 512, rl <= BN_BWD_ROWS), so the 80-channel PostNet output keeps
+// 320 lanes busy rather than 10 of 64.  Row lane ry takes rows r0 + ry + rl*i in order, loading
+// BN_BWD_BATCH rows of dout and z before any arithmetic, and the row-lane partials are summed in
+// row-lane order.  32-row blocks (768 at the SYN-48 shape, all resident at 121 VGPRs) measured
+// 21.8 / 7.7 us at c = 512 / 80 against 26.6 / 12.8 us for 64-row blocks of one-row-at-a-time
+// waves (16-row blocks: 24.0 / 10.3 us, the finals then read twice the parts).
+constexpr int BN_BWD_BATCH = 2;  // rows loaded ahead per lane
+constexpr int BN_BWD_ROWS = 32;  // rows per partial block of the backward
 __global__ __launch_bounds__(512) void bn_bwd_partial(const float* dout, const float* z,
                                                       const float* mean, const float* rstd,
                                                       const float* gamma, const float* beta,
-                                                      int64_t rows, int64_t c, int act_tanh,
-                                                      float p, const uint64_t* seed_p,
+                                                      int64_t rows, int64_t c, int rl,
+                                                      int act_tanh, float p, const uint64_t* seed_p,
                                                       uint64_t site, float* part_g, float* part_gx) {
   const uint64_t seed = seed_p ? *seed_p : 0ull;
-  const int tx = threadIdx.x & 63, ry = threadIdx.x >> 6;
-  const int64_t col = ((int64_t)blockIdx.x * 64 + tx) * 8;
-  const int64_t r0 = (int64_t)blockIdx.y * BN_ROWS;
-  __shared__ f32x4 red[2][8][128];
+  const int cg = (int)(c >> 3);
+  const int t = threadIdx.x, gx = t % cg, ry = t / cg;
+  const int col = gx * 8;
+  const int64_t r0 = (int64_t)blockIdx.x * BN_BWD_ROWS;
+  const int64_t r1 = r0 + BN_BWD_ROWS < rows ? r0 + BN_BWD_ROWS : rows;
+  __shared__ f32x4 red[2][1024];
   f32x4 sg[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}}, sgx[2] = {sg[0], sg[0]};
-  if (col < c) {
-    const int64_t r1 = r0 + BN_ROWS < rows ? r0 + BN_ROWS : rows;
-    for (int64_t r = r0 + ry; r < r1; r += 8) {
-      f32x4 g[2], xh[2];
-      bn_g8(dout, z, mean, rstd, gamma, beta, (int)col, act_tanh, p, seed, site, r * c + col, g, xh);
+  if (ry < rl) {
+    f32x4 mu[2], rs[2], ga[2], be[2];
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        sg[h] += g[h];
-        sgx[h] += g[h] * xh[h];
+    for (int h = 0; h < 2; ++h) {
+      mu[h] = ld4(mean + col + 4 * h);
+      rs[h] = ld4(rstd + col + 4 * h);
+      ga[h] = ld4(gamma + col + 4 * h);
+      be[h] = ld4(beta + col + 4 * h);
+    }
+    for (int64_t rb = r0 + ry; rb < r1; rb += (int64_t)rl * BN_BWD_BATCH) {
+      f32x4 dv[BN_BWD_BATCH][2], zv[BN_BWD_BATCH][2];
+#pragma unroll
+      for (int i = 0; i < BN_BWD_BATCH; ++i) {
+        const int64_t r = rb + (int64_t)rl * i;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          dv[i][h] = r < r1 ? ld4(dout + r * c + col + 4 * h) : f32x4{0.f, 0.f, 0.f, 0.f};
+          zv[i][h] = r < r1 ? ld4(z + r * c + col + 4 * h) : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < BN_BWD_BATCH; ++i) {
+        const int64_t r = rb + (int64_t)rl * i;
+        if (r >= r1) break;
+        f32x4 m[2] = {{1.f, 1.f, 1.f, 1.f}, {1.f, 1.f, 1.f, 1.f}};
+        if (p > 0.f) dropout8(seed, site, (uint64_t)(r * c + col), p, m[0], m[1]);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {  // g = dout * mask * act'(a), xhat = (z - mean) * rstd
+          const f32x4 xh = (zv[i][h] - mu[h]) * rs[h];
+          f32x4 g = dv[i][h] * m[h];
+          if (act_tanh) {
+            const f32x4 th = tanh4(xh * ga[h] + be[h]);
+            g *= 1.f - th * th;
+          }
+          sg[h] += g;
+          sgx[h] += g * xh;
+        }
       }
     }
   }
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
-    red[0][ry][2 * tx + h] = sg[h];
-    red[1][ry][2 * tx + h] = sgx[h];
+    red[0][2 * t + h] = sg[h];
+    red[1][2 * t + h] = sgx[h];
   }
   __syncthreads();
-  if (ry == 0 && col < c) {
+  if (t < cg) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const int q = 2 * tx + h;
-      st4(part_g + (int64_t)blockIdx.y * c + col + 4 * h,
-          ((((((red[0][0][q] + red[0][1][q]) + red[0][2][q]) + red[0][3][q]) + red[0][4][q]) +
-            red[0][5][q]) + red[0][6][q]) + red[0][7][q]);
-      st4(part_gx + (int64_t)blockIdx.y * c + col + 4 * h,
-          ((((((red[1][0][q] + red[1][1][q]) + red[1][2][q]) + red[1][3][q]) + red[1][4][q]) +
-            red[1][5][q]) + red[1][6][q]) + red[1][7][q]);
+      f32x4 a = red[0][2 * t + h], b = red[1][2 * t + h];
+      for (int y = 1; y < rl; ++y) {
+        a += red[0][2 * (y * cg + t) + h];
+        b += red[1][2 * (y * cg + t) + h];
+      }
+      st4(part_g + (int64_t)blockIdx.x * c + col + 4 * h, a);
+      st4(part_gx + (int64_t)blockIdx.x * c + col + 4 * h, b);
     }
   }
+}
+
+// in-order column sums of two partial arrays at once: 32 columns x 32 part lanes per block, so
+// each lane has nparts / 32 loads of each array in flight (the 64 x 16 layout ran two serial
+// reductions of 24 dependent rounds each: ~10 us at the PostNet's 384 parts)
+FS2_DEV void col_reduce2(const float* pa, const float* pb, int64_t nparts, int64_t c, int64_t col,
+                         int tx, int ty, float (*red)[2][33], float& sa, float& sb) {
+  float a = 0.f, b = 0.f;
+  if (col < c) {
+#pragma unroll 8
+    for (int64_t p = ty; p < nparts; p += 32) {
+      a += pa[p * c + col];
+      b += pb[p * c + col];
+    }
+  }
+  red[ty][0][tx] = a;
+  red[ty][1][tx] = b;
+  __syncthreads();
+  sa = sb = 0.f;
+  if (ty == 0) {
+#pragma unroll
+    for (int y = 0; y < 32; ++y) {
+      sa += red[y][0][tx];
+      sb += red[y][1][tx];
+    }
+  }
+  __syncthreads();
 }
 
 __global__ __launch_bounds__(1024) void bn_bwd_final(const float* part_g, const float* part_gx,
                                                      int64_t nparts, int64_t c, float* sums,
                                                      float* dgamma, float* dbeta) {
-  __shared__ float red[16][65];
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  const int64_t col = (int64_t)blockIdx.x * 64 + tx;
-  const float sg = col_reduce(part_g, nparts, c, col, tx, ty, red);
-  const float sgx = col_reduce(part_gx, nparts, c, col, tx, ty, red);
+  __shared__ float red[32][2][33];
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const int64_t col = (int64_t)blockIdx.x * 32 + tx;
+  float sg, sgx;
+  col_reduce2(part_g, part_gx, nparts, c, col, tx, ty, red, sg, sgx);
   if (ty != 0 || col >= c) return;
   sums[col] = sg;
   sums[c + col] = sgx;
@@ -502,32 +573,55 @@ __global__ __launch_bounds__(1024) void bn_bwd_final(const float* part_g, const 
   if (dgamma) dgamma[col] += sgx;
 }
 
-__global__ __launch_bounds__(256) void bn_bwd_apply(const float* dout, const float* z,
+template <int G>
+__global__ __launch_bounds__(256) void bn_bwd_apply(const float* __restrict__ dout,
+                                                    const float* __restrict__ z,
                                                     const float* mean, const float* rstd,
                                                     const float* gamma, const float* beta,
-                                                    const float* sums, int64_t n8, int64_t rows,
-                                                    int c, int act_tanh, float p,
-                                                    const uint64_t* seed_p, uint64_t site, float* dz,
-                                                    unsigned short* dz_t) {
+                                                    const float* sums, int64_t nq, int64_t rows,
+                                                    int c, bool wide, int act_tanh, float p,
+                                                    const uint64_t* seed_p, uint64_t site,
+                                                    float* __restrict__ dz,
+                                                    unsigned short* __restrict__ dz_t) {
   const uint64_t seed = seed_p ? *seed_p : 0ull;
   const float inv_m = 1.f / (float)rows;
-  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n8;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nq;
        q += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t e0 = q * 8;
-    const int col = (int)(e0 % c);
-    f32x4 g[2], xh[2], v[2];
-    bn_g8(dout, z, mean, rstd, gamma, beta, col, act_tanh, p, seed, site, e0, g, xh);
+    const int64_t e0 = q * 8 * G;
+    const int col = col_of(e0, c, wide);
+    f32x4 dv[G][2], zv[G][2];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int cc = col + 4 * h;
-      v[h] = ld4(gamma + cc) * ld4(rstd + cc) *
-             (g[h] - ld4(sums + cc) * inv_m - xh[h] * ld4(sums + c + cc) * inv_m);
+    for (int g = 0; g < G; ++g) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        dv[g][h] = ld4(dout + e0 + 8 * g + 4 * h);
+        zv[g][h] = ld4(z + e0 + 8 * g + 4 * h);
+      }
     }
-    if (dz) {
-      st4(dz + e0, v[0]);
-      st4(dz + e0 + 4, v[1]);
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int64_t eg = e0 + 8 * g;
+      f32x4 m[2] = {{1.f, 1.f, 1.f, 1.f}, {1.f, 1.f, 1.f, 1.f}};
+      if (p > 0.f) dropout8(seed, site, (uint64_t)eg, p, m[0], m[1]);
+      f32x4 v[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {  // g = dout * mask * act'(a) as in the partials, then dz
+        const int cc = col + 8 * g + 4 * h;
+        const f32x4 rs = ld4(rstd + cc);
+        const f32x4 xh = (zv[g][h] - ld4(mean + cc)) * rs;
+        f32x4 gr = dv[g][h] * m[h];
+        if (act_tanh) {
+          const f32x4 t = tanh4(xh * ld4(gamma + cc) + ld4(beta + cc));
+          gr *= 1.f - t * t;
+        }
+        v[h] = ld4(gamma + cc) * rs * (gr - ld4(sums + cc) * inv_m - xh * ld4(sums + c + cc) * inv_m);
+      }
+      if (dz) {
+        st4(dz + eg, v[0]);
+        st4(dz + eg + 4, v[1]);
+      }
+      if (dz_t) st8_bf16(dz_t + eg, v[0], v[1]);
     }
-    if (dz_t) st8_bf16(dz_t + e0, v[0], v[1]);
   }
 }
 
@@ -535,6 +629,16 @@ static unsigned ew_grid(int64_t n) {
   int64_t b = (n + 255) / 256;
   if (b > 8192) b = 8192;
   return (unsigned)(b < 1 ? 1 : b);
+}
+
+static void bn_apply_launch(const float* z, const float* mean, const float* rstd,
+                            const float* gamma, const float* beta, int64_t rows, int64_t c,
+                            int act_tanh, float p, const uint64_t* seed, uint64_t site,
+                            const float* res, float* out, unsigned short* ot, hipStream_t st) {
+  const bool wide = rows * c >= (int64_t(1) << 32);
+  bn_apply<1><<<ew_grid(rows * c / 8), 256, 0, st>>>(z, mean, rstd, gamma, beta, rows * c / 8,
+                                                     (int)c, wide, act_tanh, p, seed, site, res,
+                                                     out, ot);
 }
 
 }  // namespace fs2
@@ -619,7 +723,8 @@ int fs2_ln_bwd_final(int64_t rows, int d, const float* ws, int has_ddot, float* 
 }
 
 int64_t fs2_bn_ws_bytes(int64_t rows, int64_t c) {
-  const int64_t nparts = (rows + BN_ROWS - 1) / BN_ROWS;
+  const int64_t nf = (rows + BN_ROWS - 1) / BN_ROWS, nb = (rows + BN_BWD_ROWS - 1) / BN_BWD_ROWS;
+  const int64_t nparts = nf > nb ? nf : nb;
   return (2 * nparts * c + 2 * c) * 4;
 }
 
@@ -636,14 +741,13 @@ int fs2_bn_fwd(int dtype, const float* z, int64_t rows, int64_t c, const float* 
   const int64_t nparts = (rows + BN_ROWS - 1) / BN_ROWS;
   FS2_CHECK_ARG(c % 8 == 0, "fs2_bn_fwd: channel count must be a multiple of 8");
   dim3 grid((unsigned)((c + 255) / 256), (unsigned)nparts);
-  const unsigned cg = (unsigned)((c + 63) / 64);
+  const unsigned cg = (unsigned)((c + 31) / 32);
   bn_stats<<<grid, 256, 0, st>>>(z, rows, c, ws, ws + nparts * c);
   bn_stats_final<<<cg, 1024, 0, st>>>(ws, ws + nparts * c, nparts, rows, c, eps, momentum, mean,
                                       running_mean, running_var, rstd, num_batches_tracked);
   unsigned short* ot = dtype == FS2_BF16 ? (unsigned short*)out_t : nullptr;
   FS2_CHECK_ARG(out || ot, "fs2_bn_fwd: no output requested");
-  bn_apply<<<ew_grid(rows * c / 8), 256, 0, st>>>(z, mean, rstd, gamma, beta, rows * c / 8, (int)c,
-                                                  act_tanh, p, seed, site, res, out, ot);
+  bn_apply_launch(z, mean, rstd, gamma, beta, rows, c, act_tanh, p, seed, site, res, out, ot, st);
   return launch_status("fs2_bn_fwd");
 }
 
@@ -668,8 +772,8 @@ int fs2_bn_eval_fwd(int dtype, const float* z, int64_t rows, int64_t c, const fl
   FS2_CHECK_ARG(out || ot, "fs2_bn_eval_fwd: no output requested");
   bn_eval_stats<<<(unsigned)((c + 255) / 256), 256, 0, st>>>(running_mean, running_var, c, eps,
                                                              mean, rstd);
-  bn_apply<<<ew_grid(rows * c / 8), 256, 0, st>>>(z, mean, rstd, gamma, beta, rows * c / 8, (int)c,
-                                                  act_tanh, 0.f, nullptr, 0, res, out, ot);
+  bn_apply_launch(z, mean, rstd, gamma, beta, rows, c, act_tanh, 0.f, nullptr, 0, res, out, ot,
+                  st);
   return launch_status("fs2_bn_eval_fwd");
 }
 
@@ -682,21 +786,24 @@ int fs2_bn_bwd(int dtype, const float* dout, const float* z, const float* mean, 
   FS2_CHECK_ARG(rows > 0 && c > 0, "fs2_bn_bwd: empty input");
   FS2_CHECK_ARG(ws_bytes >= fs2_bn_ws_bytes(rows, c), "fs2_bn_bwd: workspace too small");
   hipStream_t st = as_stream(stream);
-  const int64_t nparts = (rows + BN_ROWS - 1) / BN_ROWS;
+  const int64_t nparts = (rows + BN_BWD_ROWS - 1) / BN_BWD_ROWS;
   float* part_g = ws;
   float* part_gx = ws + nparts * c;
   float* sums = ws + 2 * nparts * c;
   FS2_CHECK_ARG(c % 8 == 0, "fs2_bn_bwd: channel count must be a multiple of 8");
   unsigned short* zt = dtype == FS2_BF16 ? (unsigned short*)dz_t : nullptr;
   FS2_CHECK_ARG(dz || zt, "fs2_bn_bwd: no output requested");
-  dim3 grid((unsigned)((c + 511) / 512), (unsigned)nparts);
-  bn_bwd_partial<<<grid, 512, 0, st>>>(dout, z, mean, rstd, gamma, beta, rows, c, act_tanh, p,
-                                       seed, site, part_g, part_gx);
-  bn_bwd_final<<<(unsigned)((c + 63) / 64), 1024, 0, st>>>(part_g, part_gx, nparts, c, sums,
+  FS2_CHECK_ARG(c <= 4096, "fs2_bn_bwd: at most 4096 channels (got %lld)", (long long)c);
+  int rl = 1;  // row lanes: the largest power of two with (c / 8) * rl <= 512, rl <= BN_ROWS
+  while (rl < BN_BWD_ROWS && (c / 8) * rl * 2 <= 512) rl *= 2;
+  bn_bwd_partial<<<(unsigned)nparts, 512, 0, st>>>(dout, z, mean, rstd, gamma, beta, rows, c, rl,
+                                                   act_tanh, p, seed, site, part_g, part_gx);
+  bn_bwd_final<<<(unsigned)((c + 31) / 32), 1024, 0, st>>>(part_g, part_gx, nparts, c, sums,
                                                              dgamma, dbeta);
-  bn_bwd_apply<<<ew_grid(rows * c / 8), 256, 0, st>>>(dout, z, mean, rstd, gamma, beta, sums,
-                                                      rows * c / 8, rows, (int)c, act_tanh, p,
-                                                      seed, site, dz, zt);
+  const bool wide = rows * c >= (int64_t(1) << 32);
+  bn_bwd_apply<1><<<ew_grid(rows * c / 8), 256, 0, st>>>(dout, z, mean, rstd, gamma, beta, sums,
+                                                           rows * c / 8, rows, (int)c, wide,
+                                                           act_tanh, p, seed, site, dz, zt);
   return launch_status("fs2_bn_bwd");
 }
 

@@ -386,63 +386,57 @@ __global__ __launch_bounds__(1024) void bn_stats_final(const float* psum, const 
 
 FS2_DEV f32x4 tanh4(f32x4 v) { return f32x4{tanhf(v.x), tanhf(v.y), tanhf(v.z), tanhf(v.w)}; }
 
-// column of element e0 (32-bit division when the tensor allows: the 64-bit one is a long
-// instruction sequence per lane)
-FS2_DEV int col_of(int64_t e0, int c, bool wide) {
-  return wide ? (int)(e0 % c) : (int)((uint32_t)e0 % (uint32_t)c);
+
+// out = act(BN(z)) * dropout (+ res), 8 consecutive elements (same row) per lane
+__global__ __launch_bounds__(256) void bn_apply(const float* z, const float* mean, const float* rstd,
+                                                const float* gamma, const float* beta, int64_t n8,
+                                                int c, int act_tanh, float p, const uint64_t* seed_p,
+                                                uint64_t site, const float* res, float* out,
+                                                unsigned short* out_t) {
+  const uint64_t seed = seed_p ? *seed_p : 0ull;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n8;
+       q += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e0 = q * 8;
+    const int col = (int)(e0 % c);
+    f32x4 v0 = (ld4(z + e0) - ld4(mean + col)) * ld4(rstd + col) * ld4(gamma + col) + ld4(beta + col);
+    f32x4 v1 = (ld4(z + e0 + 4) - ld4(mean + col + 4)) * ld4(rstd + col + 4) * ld4(gamma + col + 4) +
+               ld4(beta + col + 4);
+    if (act_tanh) {
+      v0 = tanh4(v0);
+      v1 = tanh4(v1);
+    }
+    if (p > 0.f) {
+      f32x4 m0, m1;
+      dropout8(seed, site, (uint64_t)e0, p, m0, m1);
+      v0 *= m0;
+      v1 *= m1;
+    }
+    if (res) {
+      v0 += ld4(res + e0);
+      v1 += ld4(res + e0 + 4);
+    }
+    if (out) {
+      st4(out + e0, v0);
+      st4(out + e0 + 4, v1);
+    }
+    if (out_t) st8_bf16(out_t + e0, v0, v1);
+  }
 }
 
-// out = act(BN(z)) * dropout (+ res), G groups of 8 consecutive elements (same row) per lane,
-// every group's loads issued first.  Launched with G = 1: G = 2 measured 35 us against 23 us at
-// 24,576 x 512 (a lane stride of 64 B leaves each 16-B load instruction a quarter coalesced)
-template <int G>
-__global__ __launch_bounds__(256) void bn_apply(const float* __restrict__ z, const float* mean,
-                                                const float* rstd, const float* gamma,
-                                                const float* beta, int64_t nq, int c, bool wide,
-                                                int act_tanh, float p, const uint64_t* seed_p,
-                                                uint64_t site, const float* __restrict__ res,
-                                                float* __restrict__ out,
-                                                unsigned short* __restrict__ out_t) {
-  const uint64_t seed = seed_p ? *seed_p : 0ull;
-  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nq;
-       q += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t e0 = q * 8 * G;
-    const int col = col_of(e0, c, wide);
-    f32x4 zv[G][2], rv[G][2];
+// g = dout * mask * act'(a) for 8 consecutive elements (one Philox call); also returns xhat
+FS2_DEV void bn_g8(const float* dout, const float* z, const float* mean, const float* rstd,
+                   const float* gamma, const float* beta, int col, int act_tanh, float p,
+                   uint64_t seed, uint64_t site, int64_t e0, f32x4 (&g)[2], f32x4 (&xh)[2]) {
+  f32x4 m[2] = {{1.f, 1.f, 1.f, 1.f}, {1.f, 1.f, 1.f, 1.f}};
+  if (p > 0.f) dropout8(seed, site, (uint64_t)e0, p, m[0], m[1]);
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        zv[g][h] = ld4(z + e0 + 8 * g + 4 * h);
-        rv[g][h] = res ? ld4(res + e0 + 8 * g + 4 * h) : f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-    }
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      const int cc = col + 8 * g;
-      const int64_t eg = e0 + 8 * g;
-      f32x4 v0 = (zv[g][0] - ld4(mean + cc)) * ld4(rstd + cc) * ld4(gamma + cc) + ld4(beta + cc);
-      f32x4 v1 = (zv[g][1] - ld4(mean + cc + 4)) * ld4(rstd + cc + 4) * ld4(gamma + cc + 4) +
-                 ld4(beta + cc + 4);
-      if (act_tanh) {
-        v0 = tanh4(v0);
-        v1 = tanh4(v1);
-      }
-      if (p > 0.f) {
-        f32x4 m0, m1;
-        dropout8(seed, site, (uint64_t)eg, p, m0, m1);
-        v0 *= m0;
-        v1 *= m1;
-      }
-      if (res) {
-        v0 += rv[g][0];
-        v1 += rv[g][1];
-      }
-      if (out) {
-        st4(out + eg, v0);
-        st4(out + eg + 4, v1);
-      }
-      if (out_t) st8_bf16(out_t + eg, v0, v1);
+  for (int h = 0; h < 2; ++h) {
+    const int cc = col + 4 * h;
+    xh[h] = (ld4(z + e0 + 4 * h) - ld4(mean + cc)) * ld4(rstd + cc);
+    g[h] = ld4(dout + e0 + 4 * h) * m[h];
+    if (act_tanh) {
+      const f32x4 t = tanh4(xh[h] * ld4(gamma + cc) + ld4(beta + cc));
+      g[h] *= 1.f - t * t;
     }
   }
 }
@@ -573,55 +567,32 @@ __global__ __launch_bounds__(1024) void bn_bwd_final(const float* part_g, const 
   if (dgamma) dgamma[col] += sgx;
 }
 
-template <int G>
-__global__ __launch_bounds__(256) void bn_bwd_apply(const float* __restrict__ dout,
-                                                    const float* __restrict__ z,
+__global__ __launch_bounds__(256) void bn_bwd_apply(const float* dout, const float* z,
                                                     const float* mean, const float* rstd,
                                                     const float* gamma, const float* beta,
-                                                    const float* sums, int64_t nq, int64_t rows,
-                                                    int c, bool wide, int act_tanh, float p,
-                                                    const uint64_t* seed_p, uint64_t site,
-                                                    float* __restrict__ dz,
-                                                    unsigned short* __restrict__ dz_t) {
+                                                    const float* sums, int64_t n8, int64_t rows,
+                                                    int c, int act_tanh, float p,
+                                                    const uint64_t* seed_p, uint64_t site, float* dz,
+                                                    unsigned short* dz_t) {
   const uint64_t seed = seed_p ? *seed_p : 0ull;
   const float inv_m = 1.f / (float)rows;
-  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nq;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n8;
        q += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t e0 = q * 8 * G;
-    const int col = col_of(e0, c, wide);
-    f32x4 dv[G][2], zv[G][2];
+    const int64_t e0 = q * 8;
+    const int col = (int)(e0 % c);
+    f32x4 g[2], xh[2], v[2];
+    bn_g8(dout, z, mean, rstd, gamma, beta, col, act_tanh, p, seed, site, e0, g, xh);
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        dv[g][h] = ld4(dout + e0 + 8 * g + 4 * h);
-        zv[g][h] = ld4(z + e0 + 8 * g + 4 * h);
-      }
+    for (int h = 0; h < 2; ++h) {
+      const int cc = col + 4 * h;
+      v[h] = ld4(gamma + cc) * ld4(rstd + cc) *
+             (g[h] - ld4(sums + cc) * inv_m - xh[h] * ld4(sums + c + cc) * inv_m);
     }
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      const int64_t eg = e0 + 8 * g;
-      f32x4 m[2] = {{1.f, 1.f, 1.f, 1.f}, {1.f, 1.f, 1.f, 1.f}};
-      if (p > 0.f) dropout8(seed, site, (uint64_t)eg, p, m[0], m[1]);
-      f32x4 v[2];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {  // g = dout * mask * act'(a) as in the partials, then dz
-        const int cc = col + 8 * g + 4 * h;
-        const f32x4 rs = ld4(rstd + cc);
-        const f32x4 xh = (zv[g][h] - ld4(mean + cc)) * rs;
-        f32x4 gr = dv[g][h] * m[h];
-        if (act_tanh) {
-          const f32x4 t = tanh4(xh * ld4(gamma + cc) + ld4(beta + cc));
-          gr *= 1.f - t * t;
-        }
-        v[h] = ld4(gamma + cc) * rs * (gr - ld4(sums + cc) * inv_m - xh * ld4(sums + c + cc) * inv_m);
-      }
-      if (dz) {
-        st4(dz + eg, v[0]);
-        st4(dz + eg + 4, v[1]);
-      }
-      if (dz_t) st8_bf16(dz_t + eg, v[0], v[1]);
+    if (dz) {
+      st4(dz + e0, v[0]);
+      st4(dz + e0 + 4, v[1]);
     }
+    if (dz_t) st8_bf16(dz_t + e0, v[0], v[1]);
   }
 }
 
@@ -629,16 +600,6 @@ static unsigned ew_grid(int64_t n) {
   int64_t b = (n + 255) / 256;
   if (b > 8192) b = 8192;
   return (unsigned)(b < 1 ? 1 : b);
-}
-
-static void bn_apply_launch(const float* z, const float* mean, const float* rstd,
-                            const float* gamma, const float* beta, int64_t rows, int64_t c,
-                            int act_tanh, float p, const uint64_t* seed, uint64_t site,
-                            const float* res, float* out, unsigned short* ot, hipStream_t st) {
-  const bool wide = rows * c >= (int64_t(1) << 32);
-  bn_apply<1><<<ew_grid(rows * c / 8), 256, 0, st>>>(z, mean, rstd, gamma, beta, rows * c / 8,
-                                                     (int)c, wide, act_tanh, p, seed, site, res,
-                                                     out, ot);
 }
 
 }  // namespace fs2
@@ -747,7 +708,8 @@ int fs2_bn_fwd(int dtype, const float* z, int64_t rows, int64_t c, const float* 
                                       running_mean, running_var, rstd, num_batches_tracked);
   unsigned short* ot = dtype == FS2_BF16 ? (unsigned short*)out_t : nullptr;
   FS2_CHECK_ARG(out || ot, "fs2_bn_fwd: no output requested");
-  bn_apply_launch(z, mean, rstd, gamma, beta, rows, c, act_tanh, p, seed, site, res, out, ot, st);
+  bn_apply<<<ew_grid(rows * c / 8), 256, 0, st>>>(z, mean, rstd, gamma, beta, rows * c / 8, (int)c,
+                                                  act_tanh, p, seed, site, res, out, ot);
   return launch_status("fs2_bn_fwd");
 }
 
@@ -772,8 +734,8 @@ int fs2_bn_eval_fwd(int dtype, const float* z, int64_t rows, int64_t c, const fl
   FS2_CHECK_ARG(out || ot, "fs2_bn_eval_fwd: no output requested");
   bn_eval_stats<<<(unsigned)((c + 255) / 256), 256, 0, st>>>(running_mean, running_var, c, eps,
                                                              mean, rstd);
-  bn_apply_launch(z, mean, rstd, gamma, beta, rows, c, act_tanh, 0.f, nullptr, 0, res, out, ot,
-                  st);
+  bn_apply<<<ew_grid(rows * c / 8), 256, 0, st>>>(z, mean, rstd, gamma, beta, rows * c / 8, (int)c,
+                                                  act_tanh, 0.f, nullptr, 0, res, out, ot);
   return launch_status("fs2_bn_eval_fwd");
 }
 
@@ -800,10 +762,9 @@ int fs2_bn_bwd(int dtype, const float* dout, const float* z, const float* mean, 
                                                    act_tanh, p, seed, site, part_g, part_gx);
   bn_bwd_final<<<(unsigned)((c + 31) / 32), 1024, 0, st>>>(part_g, part_gx, nparts, c, sums,
                                                              dgamma, dbeta);
-  const bool wide = rows * c >= (int64_t(1) << 32);
-  bn_bwd_apply<1><<<ew_grid(rows * c / 8), 256, 0, st>>>(dout, z, mean, rstd, gamma, beta, sums,
-                                                           rows * c / 8, rows, (int)c, wide,
-                                                           act_tanh, p, seed, site, dz, zt);
+  bn_bwd_apply<<<ew_grid(rows * c / 8), 256, 0, st>>>(dout, z, mean, rstd, gamma, beta, sums,
+                                                      rows * c / 8, rows, (int)c, act_tanh, p,
+                                                      seed, site, dz, zt);
   return launch_status("fs2_bn_bwd");
 }
 

@@ -156,20 +156,25 @@ __global__ __launch_bounds__(LN_BWD_WAVES * 64) void ln_bwd_f32(LnBwd a) {
   // few blocks per CU, so the loads of all IT = LN_ROWS / NSLOT iterations must be in flight together
   // (one pair at a time left the kernel latency-bound at ~1 TB/s).
   constexpr int IT = LN_ROWS / NSLOT;
-  f32x4 XH[IT][2], DU[IT][2];
+  f32x4 XH[IT][2], DU[IT][2], DR[IT][2];  // DR: the residual gradient added to (dres_add)
   float RS[IT], RD[IT];
   bool LIVE[IT];
+  const bool dres_rd = a.dres && a.dres_add;
 #pragma unroll
   for (int it = 0; it < IT; ++it) {
     const int64_t r = rbeg + 2 * (wave + LN_BWD_WAVES * it) + half;
     LIVE[it] = r < a.rows && !row_padded(a.lens, a.T, r);
-    XH[it][0] = XH[it][1] = DU[it][0] = DU[it][1] = zz;
+    XH[it][0] = XH[it][1] = DU[it][0] = DU[it][1] = DR[it][0] = DR[it][1] = zz;
     RS[it] = RD[it] = 0.f;
     if (LIVE[it]) {
       const int64_t e0 = r * LN_D + c8;
       RD[it] = a.rstd[r];
       XH[it][0] = ld4(a.xhat + e0);
       XH[it][1] = ld4(a.xhat + e0 + 4);
+      if (dres_rd) {  // fetched with the row, not after its reduction (a second latency wait)
+        DR[it][0] = ld4(a.dres + e0);
+        DR[it][1] = ld4(a.dres + e0 + 4);
+      }
       if constexpr (DDOT) {
         RS[it] = a.ddot[r];  // the dot gradient rides in RS until the row is reduced
       } else {
@@ -225,8 +230,8 @@ __global__ __launch_bounds__(LN_BWD_WAVES * 64) void ln_bwd_f32(LnBwd a) {
     const float rs = RD[it];
     const f32x4 dz0 = rs * (dxh0 - m1 - xh0 * m2), dz1 = rs * (dxh1 - m1 - xh1 * m2);
     if (a.dres) {
-      st4(a.dres + e0, a.dres_add ? ld4(a.dres + e0) + dz0 : dz0);
-      st4(a.dres + e0 + 4, a.dres_add ? ld4(a.dres + e0 + 4) + dz1 : dz1);
+      st4(a.dres + e0, a.dres_add ? DR[it][0] + dz0 : dz0);
+      st4(a.dres + e0 + 4, a.dres_add ? DR[it][1] + dz1 : dz1);
     }
     f32x4 dy0 = dz0, dy1 = dz1;
     if (a.p_in > 0.f) {

@@ -47,3 +47,9 @@ for p in (0.0, 0.2):
     t = timeit(run)
     byt = V * d * (4 + 4 + 4 + 2) + (M - V) * d * 6
     print(f"ln_bwd  p={p}: {t:7.1f} us  {byt / t / 1e3:7.0f} GB/s", flush=True)
+    run = lambda: K.ln_bwd(xh, rs, g, b, dg, db, dout=dx2, lens=lens, seq_len=T, p_in=p, seed=SEED,
+                           site_in=3, dres=dres, dres_add=True, copy=torch.bfloat16,
+                           dbias_in=dbi)
+    t = timeit(run)
+    byt = V * d * (4 + 4 + 8 + 2) + (M - V) * d * 6
+    print(f"ln_bwd+ p={p}: {t:7.1f} us  {byt / t / 1e3:7.0f} GB/s  (dres +=)", flush=True)

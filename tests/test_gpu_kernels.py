@@ -697,6 +697,26 @@ def test_conv_gemm_bf16_halo_splitk(B, T, cin, cout, k, flags):
         K.lib.fs2_set_tuning(8, 0)
 
 
+@pytest.mark.parametrize("M,c", [(333, 8), (97, 24), (65, 4096), (32, 512), (2, 80)])
+def test_batchnorm_widths(M, c):
+    """BatchNorm forward/backward at the edges of the backward partials' lane layout (c / 8
+    column lanes x up to 32 row lanes of a 32-row block: one column group, a non-power-of-two
+    count, 512 groups with one row lane, exactly one block, two rows) against autograd."""
+    z = rnd(M, c, seed=21) * 2 + 0.3
+    g, b = 1 + 0.1 * rnd(c, seed=22), 0.1 * rnd(c, seed=23)
+    out, _, mean, rstd = K.bn_fwd(z, g, b, None, None, True, 0.0, 1, 2)
+    zr, gr, br = z.clone().requires_grad_(), g.clone().requires_grad_(), b.clone().requires_grad_()
+    ref = torch.tanh(F.batch_norm(zr, None, None, gr, br, training=True, eps=1e-5))
+    close(out, ref, 2e-5)
+    dout = rnd(M, c, seed=24)
+    ref.backward(dout)
+    dg, db = torch.zeros(c, device=DEV), torch.zeros(c, device=DEV)
+    dz, _ = K.bn_bwd(dout, z, mean, rstd, g, b, dg, db, True, 0.0, 1, 2)
+    close(dz, zr.grad)
+    close(dg, gr.grad)
+    close(db, br.grad)
+
+
 @pytest.mark.parametrize("c,act", [(512, True), (80, False)])
 def test_batchnorm_dropout(c, act):
     """PostNet BatchNorm with dropout (p = 0.5): keep-rate of the 16-bit Philox draws, and the

@@ -301,6 +301,10 @@ def test_grad_norm_adam():
     nc = torch.empty(2, device=DEV)
     K.grad_norm(g, 1.0, nc)
     close(nc[0], g.norm(), 1e-6)
+    big = rnd(4 * 1024 * 256 * 5 + 4 * 777 + 3, seed=3)  # several grid-stride trips + tail
+    nc_big = torch.empty(2, device=DEV)
+    K.grad_norm(big, 1.0, nc_big)
+    close(nc_big[0], big.double().norm(), 1e-6)
     pr = p.clone().requires_grad_()
     opt = torch.optim.Adam([pr], lr=1e-3, betas=(0.9, 0.98), eps=1e-9)
     for t in range(1, 4):

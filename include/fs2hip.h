@@ -349,8 +349,10 @@ int fs2_ln_bwd_final(int64_t rows, int d, const float* ws, int has_ddot, float* 
 
 /* ---------------------------------------------------------------- BatchNorm (PostNet)
  * Training-mode BatchNorm1d over all rows (padded frames included) + optional tanh +
- * dropout (transformer/Layers.py:129-137).  Stats are exact two-pass (mean, then centred
- * sum of squares); running stats updated with momentum, unbiased variance.  c % 8 == 0.
+ * dropout (transformer/Layers.py:129-137).  Stats in one pass: per 64-row block its column
+ * sum and centred second moment, combined exactly (M2 = sum_b [M2_b + n_b (mean_b - mean)^2])
+ * in a fixed order; running stats updated with momentum, unbiased variance.  c % 8 == 0;
+ * fs2_bn_bwd also c <= 4096.  ws: fs2_bn_ws_bytes(rows, c) bytes, for either call.
  * out / dz may be NULL when the bf16 copy (out_t / dz_t) is requested.               */
 int64_t fs2_bn_ws_bytes(int64_t rows, int64_t c);
 int fs2_bn_fwd(int dtype, const float* z, int64_t rows, int64_t c, const float* gamma,

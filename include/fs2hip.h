@@ -93,8 +93,10 @@ int fs2_conv_gemm_ln(const void* x, int64_t ldx, const void* wk, int64_t rows, i
  *   dout[r, :] = conv(x)[r, :] + aux[r, :]                (aux: fp32 residual gradient, nullable)
  *   then fs2_ln_bwd(dout, xhat, rstd, gamma, ..., p_in, site_in, dres, dres_add, dy_t = the bf16
  *   dy copy, dgamma / dbeta / dbias_in accumulated; p_out = 0, no head, no ReLU input).
- * dres and dy_t equal fs2_conv_gemm(FS2_EPI_ADD_AUX) followed by fs2_ln_bwd bitwise; the
- * parameter gradients sum the same per-32-row block partials with another in-block order.
+ * Against fs2_conv_gemm(FS2_EPI_ADD_AUX) followed by fs2_ln_bwd (the contract its test
+ * checks): dres equal to fp32 rounding (the row arithmetic is compiled in another kernel and
+ * contracted differently), the bf16 dy copy within 1 bf16 ulp, and the parameter gradients
+ * summed from per-32-row block partials in another in-block order.
  * ws: fs2_ln_bwd_ws_bytes(rows, 256).  In the FFT-block backward x is the attention input
  * gradient (dqkv) and the LayerNorm is the PREVIOUS block's FFN post-LN: block i's QKV data
  * gradient and block i-1's first backward op in one launch (transformer/SubLayers.py:38-40,91). */
@@ -268,12 +270,15 @@ int fs2_weight_prep_batch(int dtype, const int64_t* jobs, int n_jobs, int64_t n_
  *   FS2_TUNE_NT_TILE       tap-major fwd/dX kernel (k = 1 projections, odd shapes): 0 = tile
  *                          by grid size, 1 / 2 / 3 = force 128x128 / 128x64 / 64x64
  *   FS2_TUNE_LN_TILE       fs2_conv_gemm_ln row tile: 0 = 64 x 256 (default), 1 = 128 x 256
+ *   FS2_TUNE_HALO_WV       fwd/dX Conv1d with 3 or 9 taps: 1 = the halo kernel with the weight
+ *                          operand streamed into registers (conv_gemm_halo_wv; grids of >= 512
+ *                          tiles), 2 = also on smaller grids, 0 = automatic (currently off)
  * Process-wide; query workspace sizes after setting.                                 */
 enum { FS2_TUNE_GEMM_STAGES = 0, FS2_TUNE_WGRAD_STAGES = 1, FS2_TUNE_WGRAD_TILE = 2,
        FS2_TUNE_WGRAD_SPLITS = 3, FS2_TUNE_LEGACY_GEMM = 4, FS2_TUNE_NT_GROUP = 5,
        FS2_TUNE_NT_HALO = 6, FS2_TUNE_WGRAD_HALO = 7, FS2_TUNE_HALO_SPLITK = 8,
        FS2_TUNE_ATTN = 9, FS2_TUNE_HALO_DB = 10, FS2_TUNE_HALO_PIPE = 11, FS2_TUNE_NT_TILE = 12,
-       FS2_TUNE_LN_TILE = 13, FS2_TUNE_COUNT = 14 };
+       FS2_TUNE_LN_TILE = 13, FS2_TUNE_HALO_WV = 14, FS2_TUNE_COUNT = 15 };
 int fs2_set_tuning(int knob, int value);
 
 /* Weight (and optionally bias) gradient, accumulated into the fp32 master-gradient layout:

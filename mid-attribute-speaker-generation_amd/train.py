@@ -13,8 +13,13 @@ Data parallel: one process per GPU, batch sharded by utterance.
   buffer.  The buffer is laid out in reverse backward order, every block's backward reports
   its parameters as final (``StepCtx.notify``), and a bucket's all-reduce is launched as soon
   as all of its parameters are final, so communication overlaps the rest of the backward.
+  Each all-reduce runs on a communication stream that waits on events recorded on the main
+  compute stream and on the weight-gradient side stream at launch time: neither compute
+  stream ever waits for a bucket (only the clip at the end of the step waits for them all).
 * BatchNorm statistics stay per rank (DataParallel's per-replica semantics).
 """
+import warnings
+
 import torch
 import torch.distributed as dist
 
@@ -98,7 +103,11 @@ class GradBuckets:
             self.ranges.append((arena.offsets[idxs[0]],
                                 arena.offsets[last] + arena.params[last].numel()))
         self.sizes = [len(idxs) for idxs in buckets]
-        self.join = None
+        # producers of the gradients besides the current stream (the weight-gradient side
+        # stream): a callable returning the streams, each waited for by event at a launch
+        self.producers = None
+        self.comm = torch.cuda.Stream(device=arena.grad.device) if arena.grad.is_cuda else None
+        self.log = None  # optional list: bucket launches are appended (tests)
         del index
         self.reset()
 
@@ -108,10 +117,24 @@ class GradBuckets:
         self.works = []
 
     def _launch(self, b):
-        if self.join is not None:
-            self.join()  # weight gradients computed on the side stream are part of the bucket
         s, e = self.ranges[b]
-        self.works.append(dist.all_reduce(self.arena.grad[s:e], group=self.group, async_op=True))
+        if self.log is not None:
+            self.log.append(b)
+        if self.comm is None:
+            self.works.append(dist.all_reduce(self.arena.grad[s:e], group=self.group,
+                                              async_op=True))
+            return
+        # the bucket's gradients are complete in stream order on the current stream and on
+        # the producer streams: the communication stream waits on an event of each (the
+        # compute streams themselves never wait for the collective)
+        for st in [torch.cuda.current_stream()] + list(self.producers() if self.producers else ()):
+            if st is not None:
+                ev = torch.cuda.Event()
+                ev.record(st)
+                self.comm.wait_event(ev)
+        with torch.cuda.stream(self.comm):
+            self.works.append(dist.all_reduce(self.arena.grad[s:e], group=self.group,
+                                              async_op=True))
 
     def ready(self, params):
         for p in params:
@@ -126,6 +149,8 @@ class GradBuckets:
             self.next += 1
         for w in self.works:
             w.wait()  # stream-ordered: the clip/Adam kernels queue behind the collectives
+        if self.comm is not None:
+            torch.cuda.current_stream().wait_stream(self.comm)
         self.reset()
 
 
@@ -155,6 +180,11 @@ class Trainer:
         if self.grad_acc < 1:
             raise ValueError("grad_acc_step must be >= 1")
         self.batch_step = int(current_step) + 1
+        if self.graph_mode and self.grad_acc > 1:
+            # the captured step is one whole optimiser step; accumulated micro-batches (whose
+            # update flag alternates) run eagerly -- say so instead of dropping the mode silently
+            warnings.warn("Trainer(graph=True) with grad_acc_step > 1 runs eager steps "
+                          "(HIP-graph replay captures whole optimiser steps only)", stacklevel=2)
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
         self.buckets = None
@@ -163,7 +193,7 @@ class Trainer:
             with torch.no_grad():  # identical initial weights on every rank
                 dist.broadcast(arena.flat, src=0, group=process_group)
             self.buckets = GradBuckets(arena, process_group, bucket_bytes)
-            self.buckets.join = model.join_side
+            self.buckets.producers = lambda: (model._side,)
             model._hooks["grad"] = self.buckets.ready
 
     def _global_denominators(self, batch):

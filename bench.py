@@ -196,12 +196,26 @@ class BlockTimer:
         self._f, self._b = Fn.forward, Fn.backward
         me = self
 
+        self.ops = None  # OpTimer: per-op spans (this pass puts the GPU behind the host first)
+
+        def spin():
+            if me.ops is not None:
+                try:
+                    torch.cuda._sleep(8_000_000)  # a few ms: the host enqueues the pass meanwhile
+                except Exception:
+                    pass
+
         def fwd(fctx, *a):
             if not me.on:
                 return me._f(fctx, *a)
+            spin()
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
+            if me.ops is not None:
+                me.ops.phase = "fwd"
             r = me._f(fctx, *a)
+            if me.ops is not None:
+                me.ops.phase = None
             e.record()
             me.ev.append(("fwd", s, e))
             return r
@@ -209,9 +223,14 @@ class BlockTimer:
         def bwd(fctx, *a):
             if not me.on:
                 return me._b(fctx, *a)
+            spin()
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
+            if me.ops is not None:
+                me.ops.phase = "bwd"
             r = me._b(fctx, *a)
+            if me.ops is not None:
+                me.ops.phase = None
             me.model.join_side()  # the decoder's weight gradients belong to its backward
             e.record()
             me.ev.append(("bwd", s, e))
@@ -224,6 +243,101 @@ class BlockTimer:
         f = [s.elapsed_time(e) for k, s, e in self.ev if k == "fwd"]
         b = [s.elapsed_time(e) for k, s, e in self.ev if k == "bwd"]
         return (float(np.median(f)), float(np.median(b))) if f and b else (None, None)
+
+
+class OpTimer:
+    """Per-op spans of the decoder's FFT blocks inside the training step (the north star's
+    fft_block broken down): every kernel call made while ``phase`` is "fwd" / "bwd" (set by
+    BlockTimer around DecoderFn) is bracketed by HIP events on the stream it runs on (the
+    weight gradients on the side stream) and labelled by its role in the block.  Before each
+    decoder pass a spin kernel (torch.cuda._sleep) puts the GPU behind the host, so the spans
+    carry no host launch gaps; the side-stream weight gradients still share the CUs with the
+    main-stream chain as in every step."""
+
+    FNS = ("conv_gemm", "conv_gemm_ln", "conv_gemm_ln_bwd", "attn_fwd", "attn_bwd", "ln_fwd",
+           "ln_bwd", "conv_wgrad")
+    FWD = {(256, 768, 1): "qkv", (256, 256, 1): "fc", (256, 1024, 9): "w1_k9",
+           (1024, 256, 1): "w2"}
+    BWD = {(256, 1024, 1): "w2_dgrad", (1024, 256, 9): "w1_k9_dgrad", (256, 256, 1): "fc_dgrad",
+           (768, 256, 1): "qkv_dgrad"}
+    WGRAD = {(1024, 256, 1): "w2_wgrad", (256, 1024, 9): "w1_k9_wgrad", (256, 256, 1): "fc_wgrad",
+             (256, 768, 1): "qkv_wgrad"}
+
+    def __init__(self, K, valid_by_T, sq_by_T):
+        self.K, self.valid_by_T, self.sq_by_T = K, valid_by_T, sq_by_T
+        self.phase = None
+        self.rec = []  # (op, start event, end event, flop)
+        self._streams = {}
+        self._orig = {n: getattr(K, n) for n in self.FNS}
+
+    def _stream(self, handle):
+        if handle is None:
+            return torch.cuda.current_stream()
+        s = self._streams.get(handle)
+        if s is None:
+            s = self._streams[handle] = torch.cuda.ExternalStream(handle)
+        return s
+
+    def _label(self, name, a, kw):
+        if name == "attn_fwd":  # (qkv, lens, batch, seq_len, heads, d_head, scale)
+            return "attention", 4.0 * a[4] * a[5] * self.sq_by_T.get(a[3], a[2] * a[3] * a[3])
+        if name == "attn_bwd":  # (qkv, o, d_o, lse, lens, batch, seq_len, heads, d_head, scale)
+            return "attention_bwd", 10.0 * a[7] * a[8] * self.sq_by_T.get(a[6], a[5] * a[6] * a[6])
+        if name in ("ln_fwd", "ln_bwd"):
+            return name, 0.0
+        rows, T, c_in, c_out, taps = a[2], a[3], a[4], a[5], a[6]
+        if name == "conv_wgrad":
+            rows, T, c_in, c_out, taps = a[3], a[4], a[5], a[6], a[7]
+        r = self.valid_by_T.get(T, rows) if kw.get("lens") is not None else rows
+        fl = 2.0 * r * c_in * c_out * taps
+        key = (c_in, c_out, taps)
+        if name == "conv_wgrad":
+            return self.WGRAD.get(key, f"wgrad{key}"), fl
+        if name == "conv_gemm_ln":
+            return self.FWD.get(key, f"gemm{key}") + "+ln", fl
+        if name == "conv_gemm_ln_bwd":
+            return "qkv_dgrad+ln2_bwd", fl
+        tab = self.FWD if self.phase == "fwd" else self.BWD
+        return tab.get(key, f"gemm{key}"), fl
+
+    def install(self):
+        me = self
+
+        def wrap(name, fn):
+            def f(*a, **kw):
+                if me.phase is None:
+                    return fn(*a, **kw)
+                op, fl = me._label(name, a, kw)
+                st = me._stream(kw.get("on_stream"))
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record(st)
+                y = fn(*a, **kw)
+                e.record(st)
+                me.rec.append((("fwd:" if me.phase == "fwd" else "bwd:") + op, s, e, fl))
+                return y
+            return f
+        for n, fn in self._orig.items():
+            setattr(self.K, n, wrap(n, fn))
+
+    def table(self, blocks, peak, wall_ms):
+        torch.cuda.synchronize()
+        agg = {}
+        for op, s, e, fl in self.rec:
+            a = agg.setdefault(op, [0.0, 0.0, 0])
+            a[0] += s.elapsed_time(e)
+            a[1] += fl
+            a[2] += 1
+        out, tot = {}, 0.0
+        for op, (ms, fl, n) in agg.items():
+            per = ms / blocks
+            tot += per
+            d = {"ms_per_block": round(per, 4), "calls_per_block": round(n / blocks, 2),
+                 "share_of_block": round(per / wall_ms, 3) if wall_ms else None}
+            if fl > 0:
+                d["gflop"] = round(fl / blocks / 1e9, 2)
+                d["frac"] = round(fl / (ms / 1e3) / 1e12 / peak, 4)
+            out[op] = d
+        return out, round(tot, 4)
 
 
 # ----------------------------------------------------------------------------- PMC traffic
@@ -546,6 +660,29 @@ def main():
                 fb.update(gflop_padded=gf_pad, achieved_padded=round(gf_pad / blk_ms, 1),
                           frac_padded=round(gf_pad / blk_ms / peak, 4))
             out["fft_block"] = fb
+        # per-op attribution of the block: 3 more steps with every decoder kernel call timed
+        ot = OpTimer(K, {T_m: frames_local, T_s: int(src.sum())},
+                     {T_m: float((mel ** 2).sum()), T_s: float((src ** 2).sum())})
+        ot.install()
+        bt.ops, bt.ev, bt.on = ot, [], True
+        for _ in range(3):
+            trainer.step(batch)
+        bt.on, bt.ops = False, None
+        for n, fn in ot._orig.items():
+            setattr(K, n, fn)
+        f2, b2 = bt.result()
+        if rank == 0 and f_ms is not None and f2 is not None:
+            L = len(model.decoder.layer_stack)
+            wall = (f2 + b2) / L
+            ops, tot = ot.table(3 * L, peak, wall)
+            out["fft_block"]["ops"] = ops
+            out["fft_block"]["ops_basis"] = (
+                "3 further steps, every kernel call inside DecoderFn forward / backward between HIP "
+                "events on its own stream (weight gradients: the side stream, concurrent with the "
+                "main-stream chain), after a spin kernel that puts the GPU behind the host; "
+                "ms per block = total / (3 steps x 6 layers); frac on valid-frame FLOP")
+            out["fft_block"]["ops_wall_ms_per_block"] = round(wall, 4)
+            out["fft_block"]["ops_sum_ms_per_block"] = tot
 
     # the reference's precision (fp32), N = 1, a short companion measurement
     if world == 1 and args.dtype == "bf16" and not args.no_f32 and not args.use_clf:

@@ -270,15 +270,12 @@ int fs2_weight_prep_batch(int dtype, const int64_t* jobs, int n_jobs, int64_t n_
  *   FS2_TUNE_NT_TILE       tap-major fwd/dX kernel (k = 1 projections, odd shapes): 0 = tile
  *                          by grid size, 1 / 2 / 3 = force 128x128 / 128x64 / 64x64
  *   FS2_TUNE_LN_TILE       fs2_conv_gemm_ln row tile: 0 = 64 x 256 (default), 1 = 128 x 256
- *   FS2_TUNE_HALO_WV       fwd/dX Conv1d with 3 or 9 taps: 1 = the halo kernel with the weight
- *                          operand streamed into registers (conv_gemm_halo_wv; grids of >= 512
- *                          tiles), 2 = also on smaller grids, 0 = automatic (currently off)
  * Process-wide; query workspace sizes after setting.                                 */
 enum { FS2_TUNE_GEMM_STAGES = 0, FS2_TUNE_WGRAD_STAGES = 1, FS2_TUNE_WGRAD_TILE = 2,
        FS2_TUNE_WGRAD_SPLITS = 3, FS2_TUNE_LEGACY_GEMM = 4, FS2_TUNE_NT_GROUP = 5,
        FS2_TUNE_NT_HALO = 6, FS2_TUNE_WGRAD_HALO = 7, FS2_TUNE_HALO_SPLITK = 8,
        FS2_TUNE_ATTN = 9, FS2_TUNE_HALO_DB = 10, FS2_TUNE_HALO_PIPE = 11, FS2_TUNE_NT_TILE = 12,
-       FS2_TUNE_LN_TILE = 13, FS2_TUNE_HALO_WV = 14, FS2_TUNE_COUNT = 15 };
+       FS2_TUNE_LN_TILE = 13, FS2_TUNE_COUNT = 14 };
 int fs2_set_tuning(int knob, int value);
 
 /* Weight (and optionally bias) gradient, accumulated into the fp32 master-gradient layout:

@@ -32,7 +32,6 @@ namespace fs2 {
 
 typedef __bf16 bf16x8g __attribute__((ext_vector_type(8)));
 typedef unsigned short u16;
-typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
 
 __device__ __attribute__((aligned(128))) uint4 g_zero_line[8];  // zero source for OOB chunks
 
@@ -107,14 +106,6 @@ FS2_DEV int m_interleave(int tm, int tiles_m, bool on) {
   int s = tiles_m / 8 + 1;
   while (igcd(s, tiles_m) != 1) ++s;
   return (int)(((int64_t)tm * s) % tiles_m);
-}
-
-template <int I, int N, typename F>
-FS2_DEV void static_for(F&& f) {
-  if constexpr (I < N) {
-    f(std::integral_constant<int, I>{});
-    static_for<I + 1, N>(f);
-  }
 }
 
 FS2_DEV void glds16(const void* src, u16* lds_wave_base) {
@@ -372,14 +363,12 @@ FS2_DEV void nt_epilogue_lnbwd(const GldsArgs& a, f32x4 (&acc)[BM / 32][256 / WN
 
 // Epilogue through LDS, one half (wm) at a time: bias, aux add, ReLU / ReLU-mask, bf16 cast
 // on 8-element row vectors (16-B / 32-B coalesced stores).  Shared by both NT kernels.
-// WM row-waves (2, or 4 for conv_gemm_halo_wv): wave wm owns rows wm * BM / WM .. of the tile,
-// so tile half h is written by the waves with wm / (WM / 2) == h.
-template <int BM, int BN, bool VOC, int NWAVE = 4, int WN = 2, int WM = 2>
-FS2_DEV void nt_epilogue(const GldsArgs& a, f32x4 (&acc)[BM / WM / 16][BN / WN / 16], u16* smem,
+template <int BM, int BN, bool VOC, int NWAVE = 4, int WN = 2>
+FS2_DEV void nt_epilogue(const GldsArgs& a, f32x4 (&acc)[BM / 32][BN / WN / 16], u16* smem,
                          int64_t m0, int n0, bool skip, int tid, int wm, int wn, int g, int r16) {
-  constexpr int MI = BM / WM / 16, NI = BN / WN / 16;
+  constexpr int MI = BM / 32, NI = BN / WN / 16;
   constexpr int EPI_LD = BN + 4;
-  if constexpr (BN == 256 && !VOC && WM == 2) {
+  if constexpr (BN == 256 && !VOC) {
     if (a.ln_out) {
       if constexpr (BM == 64) {
         if (a.ln_mode == 1) {
@@ -396,15 +385,14 @@ FS2_DEV void nt_epilogue(const GldsArgs& a, f32x4 (&acc)[BM / WM / 16][BN / WN /
   const bool out_bf16 = a.flags & FS2_EPI_OUT_BF16, aux_bf16 = a.flags & FS2_EPI_AUX_BF16;
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
-    if (wm / (WM / 2) == h) {
-      const int rb = (wm % (WM / 2)) * (BM / WM);
+    if (wm == h) {
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < NI; ++j)
 #pragma unroll
           for (int r = 0; r < 4; ++r)
-            Cs[(rb + i * 16 + 4 * g + r) * EPI_LD + wn * (BN / WN) + j * 16 + r16] = acc[i][j][r];
+            Cs[(i * 16 + 4 * g + r) * EPI_LD + wn * (BN / WN) + j * 16 + r16] = acc[i][j][r];
     }
     __syncthreads();
     constexpr int TPR = BN / 8;           // threads per row
@@ -1004,190 +992,6 @@ void conv_gemm_halo(GldsArgs a) {
   nt_epilogue<BM, BN, VOC, NWAVE, WN>(a, acc, smem, m0, n0, skip, tid, wm, wn, g, r16);
 }
 
-// ------------------------------------------------------------------ halo, weights in registers
-// conv_gemm_halo_wv: the halo Conv1d (TAPS taps, compile time; Cin % 64 == 0, T % BM == 0,
-// N % BN == 0) with the weight operand streamed straight into registers instead of an LDS ring.
-// Only the x rows of a 64-channel block (the tile's BM rows plus the tap halo, zero outside the
-// utterance) go through LDS, staged once per channel block by plain 16-B loads into registers
-// and ds_write_b128 into the other of two LDS slots while the block's taps run; tap j reads
-// them at row offset j (the chunk swizzle c ^ (row & 7) of conv_gemm_halo).  A wave's B
-// fragments are 16-B runs of the K-contiguous weight rows (w_fwd[o][j*Cin + c]): one
-// global_load_dwordx4 per lane and fragment, issued three steps ahead into a register ring of
-// three step slots (TAPS % 3 == 0, so step (cb, j) always uses slot j % 3).
-// Against conv_gemm_halo: LDS carries the x fragments alone (MI reads per NI x MI MFMAs), there
-// is one barrier per channel block instead of one per (channel block, tap) step, and waves run
-// their taps independently between the barriers.  WM x WN waves of (BM / WM) x (BN / WN).
-template <int BM, int BN, int WM, int WN, int TAPS, int MINW>
-__global__ __launch_bounds__(WM * WN * 64, MINW) void conv_gemm_halo_wv(GldsArgs a) {
-  static_assert(TAPS % 3 == 0 && TAPS <= 9, "three-slot weight ring: TAPS in {3, 9}");
-  constexpr int NWAVE = WM * WN, NT = NWAVE * 64, BK = 64;
-  constexpr int RW = BM / WM, CW = BN / WN, MI = RW / 16, NI = CW / 16;
-  static_assert(MI % 2 == 0 && NI >= 1, "wave tile");
-  constexpr int HP = (BM + TAPS - 1 + 7) / 8;      // 8-row halo pieces needed
-  constexpr int QW = (HP * 64 + NT - 1) / NT;      // 16-B halo chunks per thread
-  constexpr int HROWS = QW * NT / 8;               // halo rows allocated per slot
-  constexpr int A_E = HROWS * BK;
-  constexpr int EPI_E = (BM / 2) * (BN + 4) * 2;
-  constexpr int SMEM_E = 2 * A_E > EPI_E ? 2 * A_E : EPI_E;
-  __shared__ __attribute__((aligned(1024))) u16 smem[SMEM_E];
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave / WN, wn = wave % WN;
-  const int g = lane >> 4, r16 = lane & 15;
-
-  const int nwg = a.tiles_m * a.tiles_n;
-  const int orig = blockIdx.x, xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
-  const int gfull = a.tiles_m * a.group;
-  const int ng = wg / gfull, rem = wg - ng * gfull;
-  const int gsz = a.tiles_n - ng * a.group < a.group ? a.tiles_n - ng * a.group : a.group;
-  const int tm = m_interleave(rem / gsz, a.tiles_m, a.lens != nullptr);
-  const int tn = ng * a.group + (rem - (rem / gsz) * gsz);
-  const int64_t m0 = (int64_t)tm * BM;
-  const int n0 = tn * BN;
-  const bool skip = a.lens && rows_all_padding(a.lens, a.T, m0, m0 + BM < a.M ? m0 + BM : a.M);
-
-  const int64_t u0 = (m0 / a.T) * a.T;
-  const int64_t ulen = a.lens ? (a.lens[m0 / a.T] < a.T ? a.lens[m0 / a.T] : a.T) : a.T;
-  const int64_t u1 = u0 + ulen < a.M ? u0 + ulen : a.M;
-  // this wave's 16-row fragments holding a row below the utterance's length (x rows past it
-  // are staged as zeros; outputs past it are masked downstream, as in conv_gemm_halo)
-  const int64_t nv = u1 - (m0 + wm * RW);
-  const int nact = nv <= 0 ? 0 : nv >= RW ? MI : (int)((nv + 15) / 16);
-
-  // halo chunk q of this thread: row h = (tid + NT q) / 8, logical chunk c = tid & 7, stored at
-  // physical chunk c ^ (h & 7).  The next channel block's halo is streamed in CPT chunks per
-  // tap (loaded at tap j, stored at tap j + 1), so only CPT 16-B registers are held.
-  constexpr int CPT = (QW + TAPS - 2) / (TAPS - 1);
-  // halo rows by buffer loads from a descriptor on the tile's utterance [u0, u1): rows outside
-  // it (negative offsets wrap past the record count) read as zeros in hardware, so the loads
-  // are unconditional; the channel block goes in the scalar offset
-  const int hc = tid & 7, h0 = tid >> 3;
-  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<u16*>(a.x + u0 * a.ldx), (short)0, (int)((u1 - u0) * a.ldx * 2), 0x00020000);
-  auto h_voff = [&](int q) {
-    const int h = h0 + (NT / 8) * q;
-    return (int)(((m0 - u0 - a.pad + h) * a.ldx + hc * 8) * 2);
-  };
-  auto h_off = [&](int q) {
-    const int h = h0 + (NT / 8) * q;
-    return h * BK + ((hc ^ (h & 7)) << 3);
-  };
-  auto h_ld = [&](int q, int cb) {
-    return __builtin_amdgcn_raw_buffer_load_b128(xrs, h_voff(q), cb * BK * 2, 0);
-  };
-  // B fragments by buffer loads from a descriptor on the block's BN weight rows (built from
-  // block-uniform values): per-lane offset (r16 * K + 8 g) * 2 B in voffset, everything else
-  // (wave column, fragment, tap, channel block, k-half) in the scalar offset -- no 64-bit
-  // address registers per load
-  const int K = a.K;
-  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<u16*>(a.w + (int64_t)n0 * K), (short)0, BN * K * 2, 0x00020000);
-  const int w_voff = (r16 * K + g * 8) * 2;
-  const int w_sbase = wn * CW * K * 2;
-  const int a_row = wm * RW + r16;
-  const int ncb = a.Cin / 64;
-
-  f32x4 acc[MI][NI];
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // weights of step (cb, j), both k-halves, into a ring slot
-  auto w_load = [&](int cb, int j, bf16x8g (&w)[NI][2]) {
-    const int so = w_sbase + (j * a.Cin + cb * BK) * 2;
-#pragma unroll
-    for (int jj = 0; jj < NI; ++jj)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-        w[jj][ks] = __builtin_bit_cast(
-            bf16x8g, __builtin_amdgcn_raw_buffer_load_b128(wrs, w_voff, so + (jj * 16 * K + ks * 32) * 2, 0));
-  };
-
-  auto run = [&](auto nact_c) {
-    constexpr int NA = decltype(nact_c)::value;
-    bf16x8g wr0[NI][2], wr1[NI][2], wr2[NI][2];
-    bf16x8g fa0[MI], fa1[MI];
-    u32x4v hr[2][CPT];
-    auto a_read = [&](int slot, int j, int ks, bf16x8g (&fa)[MI]) {
-      const int ha = a_row + j;
-      const u16* pa = smem + slot * A_E + ha * BK + ((ks * 4 + g) ^ (ha & 7)) * 8;
-#pragma unroll
-      for (int i = 0; i < NA; ++i) fa[i] = *reinterpret_cast<const bf16x8g*>(pa + i * 16 * BK);
-    };
-    auto mfma = [&](const bf16x8g (&fa)[MI], const bf16x8g (&w)[NI][2], int ks) {
-#pragma unroll
-      for (int i = 0; i < NA; ++i)
-#pragma unroll
-        for (int jj = 0; jj < NI; ++jj)
-          acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], w[jj][ks], acc[i][jj], 0, 0, 0);
-    };
-    // halo of channel block 0 (all chunks; then the ring loads)
-    {
-      u32x4v h0r[QW];
-#pragma unroll
-      for (int q = 0; q < QW; ++q) h0r[q] = h_ld(q, 0);
-#pragma unroll
-      for (int q = 0; q < QW; ++q)
-        *reinterpret_cast<u32x4v*>(smem + h_off(q)) = h0r[q];
-    }
-    if constexpr (NA > 0) {
-      w_load(0, 0, wr0);
-      w_load(0, 1, wr1);
-    }
-    for (int cb = 0; cb < ncb; ++cb) {
-      __syncthreads();  // halo cb visible; every wave is done with slot (cb + 1) & 1
-      const int slot = cb & 1;
-      const int cbn = cb + 1 < ncb ? cb + 1 : cb;
-      static_for<0, TAPS>([&](auto jc) {
-        constexpr int j = decltype(jc)::value;
-        // ring slots named statically (a runtime-indexed register array goes to scratch):
-        // step (cb, j) reads slot j % 3; slot (j + 2) % 3 (read at tap j - 1) takes step s + 2
-        bf16x8g (&w)[NI][2] = j % 3 == 0 ? wr0 : j % 3 == 1 ? wr1 : wr2;
-        bf16x8g (&wn2)[NI][2] = j % 3 == 0 ? wr2 : j % 3 == 1 ? wr0 : wr1;
-        __builtin_amdgcn_sched_barrier(0);
-        // issue: weights of step s + 2, then the next block's halo chunks [CPT j, CPT (j + 1))
-        if constexpr (NA > 0) {
-          if constexpr (j + 2 < TAPS) w_load(cb, j + 2, wn2);
-          else w_load(cbn, j + 2 - TAPS, wn2);
-        }
-        if constexpr (j + 1 < TAPS && CPT * j < QW) {
-#pragma unroll
-          for (int c = 0; c < CPT; ++c)
-            if (CPT * j + c < QW) hr[j & 1][c] = h_ld(CPT * j + c, cbn);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        if constexpr (NA > 0) {
-          if constexpr (j == 0) a_read(slot, 0, 0, fa0);
-          a_read(slot, j, 1, fa1);
-          mfma(fa0, w, 0);
-          if constexpr (j + 1 < TAPS) a_read(slot, j + 1, 0, fa0);
-          mfma(fa1, w, 1);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        // store the chunks loaded at tap j - 1 (landed: only this tap's loads are younger than
-        // what the next tap's MFMAs need anyway).  Unconditional: after the last block the
-        // other slot is dead.
-        if constexpr (j >= 1 && CPT * (j - 1) < QW) {
-#pragma unroll
-          for (int c = 0; c < CPT; ++c)
-            if (CPT * (j - 1) + c < QW)
-              *reinterpret_cast<u32x4v*>(smem + (slot ^ 1) * A_E + h_off(CPT * (j - 1) + c)) = hr[(j - 1) & 1][c];
-        }
-      });
-    }
-  };
-  if (!skip) {
-    if (nact == 0) run(std::integral_constant<int, 0>{});
-    else if (nact <= MI / 2) run(std::integral_constant<int, MI / 2>{});
-    else run(std::integral_constant<int, MI>{});
-  }
-  __syncthreads();
-  nt_epilogue<BM, BN, false, NWAVE, WN, WM>(a, acc, smem, m0, n0, skip, tid, wm, wn, g, r16);
-}
-
 // Split-K epilogue of the halo kernel: y = epilogue(sum_z slab[z]) in split order, 8 columns
 // per thread, with nt_epilogue's non-vocoder semantics (bias, aux add, ReLU / ReLU mask, bf16
 // cast; tiles of BM rows that are all padding get no bias, as in the unsplit kernel).
@@ -1286,6 +1090,26 @@ struct WgradGlds {
 
 typedef short s16x4g __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4g lds_s16x4g;
+
+// ds_read_b64_tr_b16 as inline asm.  The builtin's memory operand carries no alias scope, so
+// hipcc's wait-count pass makes every such read wait for ALL LDS-DMA in flight (vmcnt(0)):
+// issued after the next k-tile's DMA it drained the prefetch every k-tile, serialising the
+// weight-gradient loops on one global round trip.  The asm read is invisible to that pass:
+// the caller orders it after the DMA of the tile it reads (counted vmcnt + barrier, as the
+// k-loops do) and waits for its result with lgkm_wait<N>() before use.
+FS2_DEV s16x4g ds_tr16(const u16* p) {
+  s16x4g r;
+  const uint32_t a = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) u16*)p;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(a));
+  return r;
+}
+// s_waitcnt lgkmcnt(N), then a scheduling fence: register-only MFMAs must not be hoisted
+// above the wait (the asm reads' results are unknown to the compiler)
+template <int N>
+FS2_DEV void lgkm_wait() {
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
 
 template <int BT, int STAGES>
 __global__ __launch_bounds__(256) void conv_wgrad_tn_glds(WgradGlds a) {
@@ -1413,23 +1237,41 @@ __global__ __launch_bounds__(256) void conv_wgrad_tn_glds(WgradGlds a) {
 
   // transposed fragment: 16 columns at col0, k-step ks; rows {4g+q} and {16+4g+q}
   const int swz = swz_of(4 * g + q);
-  auto tr_frag = [&](const u16* img, int col0, int ks) -> bf16x8g {
+  // transposed fragment halves (asm reads, see ds_tr16): rows ks*32 + {4g+q} and + 16
+  auto tr_lo = [&](const u16* img, int col0, int ks, int hi) -> s16x4g {
     const int lc = (col0 >> 3) + (p >> 1);
-    const int off = (ks * 32 + 4 * g + q) * BT + ((lc ^ swz) << 3) + ((p & 1) << 2);
-    const s16x4g lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4g*)(img + off));
-    const s16x4g hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4g*)(img + off + 16 * BT));
+    const int off = (ks * 32 + 4 * g + q + 16 * hi) * BT + ((lc ^ swz) << 3) + ((p & 1) << 2);
+    return ds_tr16(img + off);
+  };
+  auto cat = [](s16x4g lo, s16x4g hi) {
     return __builtin_bit_cast(bf16x8g, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
   };
+  // both k-halves' fragment reads issued up front; the first half's MFMAs start once its reads
+  // (the older 2 (MI + NI)) landed
   auto compute = [&](int stage) {
     const u16* As = smem + stage * STAGE_E;
     const u16* Bs = As + IMG;
+    s16x4g ra[2][MI][2], rb[2][NI][2];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) ra[ks][i][h] = tr_lo(As, wm * (BM / 2) + i * 16, ks, h);
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) rb[ks][j][h] = tr_lo(Bs, wn * (BN / 2) + j * 16, ks, h);
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      if (ks == 0) lgkm_wait<(2 * (MI + NI) < 15 ? 2 * (MI + NI) : 15)>();  // 4-bit counter
+      else lgkm_wait<0>();
       bf16x8g fa[MI], fb[NI];
 #pragma unroll
-      for (int i = 0; i < MI; ++i) fa[i] = tr_frag(As, wm * (BM / 2) + i * 16, ks);
+      for (int i = 0; i < MI; ++i) fa[i] = cat(ra[ks][i][0], ra[ks][i][1]);
 #pragma unroll
-      for (int j = 0; j < NI; ++j) fb[j] = tr_frag(Bs, wn * (BN / 2) + j * 16, ks);
+      for (int j = 0; j < NI; ++j) fb[j] = cat(rb[ks][j][0], rb[ks][j][1]);
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -1611,6 +1453,16 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_halo(WgradGlds a) {
     const s16x4g hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4g*)(img + off + 16 * 64));
     return __builtin_bit_cast(bf16x8g, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
   };
+  // the same fragment by two asm reads (see ds_tr16: the builtin made every read wait for the
+  // next k-tile's DMA); the caller waits with lgkm_wait before use
+  auto tr_frag_asm = [&](const u16* img, int rb, int col0) -> bf16x8g {
+    const int R = rb + 4 * g + q;
+    const int lc = (col0 >> 3) + (p >> 1);
+    const int off = R * 64 + ((lc ^ swz(R)) << 3) + ((p & 1) << 2);
+    const s16x4g lo = ds_tr16(img + off);
+    const s16x4g hi = ds_tr16(img + off + 16 * 64);
+    return __builtin_bit_cast(bf16x8g, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+  };
   auto compute = [&](int stage) {
     const u16* As = smem + stage * STAGE_E;
     const u16* Xs = As + A_E;
@@ -1619,11 +1471,16 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_halo(WgradGlds a) {
       for (int ks = 0; ks < 2; ++ks) {
         bf16x8g fa[4], fb[2];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) fa[i] = tr_frag(As, ks * 32, i * 16);
-        fb[0] = tr_frag(Xs, ks * 32, wave * 16);
+        for (int i = 0; i < 4; ++i) fa[i] = tr_frag_asm(As, ks * 32, i * 16);
+        fb[0] = tr_frag_asm(Xs, ks * 32, wave * 16);
 #pragma unroll
         for (int j = 0; j < TAPS; ++j) {
-          if (j + 1 < TAPS) fb[(j + 1) & 1] = tr_frag(Xs, ks * 32 + j + 1, wave * 16);
+          if (j + 1 < TAPS) {
+            fb[(j + 1) & 1] = tr_frag_asm(Xs, ks * 32 + j + 1, wave * 16);
+            lgkm_wait<2>();  // all but the next tap's x fragment landed
+          } else {
+            lgkm_wait<0>();
+          }
 #pragma unroll
           for (int i = 0; i < 4; ++i)
             acc[j][i][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j & 1], acc[j][i][0],
@@ -2048,25 +1905,6 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
   // Default for the wide forward shapes (c_in <= 256, >= 512 128x128 tiles, T % 256 == 0: the
   // decoder FFN k=9 forward): 256 x 128 two-slot, 8 waves (k=9 decoder forward 114 -> 102 us
   // alone, scripts/halo_check.py).  FS2_TUNE_NT_HALO 1 disables it.
-  // weights-in-registers halo kernel (FS2_TUNE_HALO_WV): 256 x 128 tiles of 8 waves (64 x 64
-  // each) for the wide forward shapes, 128 x 64 tiles of 4 waves (64 x 32) otherwise
-  const int wv = g_tune[FS2_TUNE_HALO_WV];
-  if (wv > 0 && !voc && (taps == 9 || taps == 3) && tapaligned && g_tune[FS2_TUNE_NT_HALO] >= 0) {
-    const bool wide = big >= 512 && c_in <= 256 && c_out % 128 == 0 && seq_len % 256 == 0;
-    const int bm = wide ? 256 : 128, bn = wide ? 128 : 64;
-    const int64_t tiles = ((rows + bm - 1) / bm) * (c_out / bn);
-    if (c_out % bn == 0 && seq_len % bm == 0 && (wide || tiles >= 512 || wv == 2)) {
-      a.tiles_m = (int)((rows + bm - 1) / bm);
-      a.tiles_n = (int)(c_out / bn);
-      a.group = halo_group(a.tiles_n);
-      const unsigned grid = (unsigned)(a.tiles_m * a.tiles_n);
-      if (wide && taps == 9) conv_gemm_halo_wv<256, 128, 4, 2, 9, 2><<<grid, 512, 0, st>>>(a);
-      else if (wide) conv_gemm_halo_wv<256, 128, 4, 2, 3, 2><<<grid, 512, 0, st>>>(a);
-      else if (taps == 9) conv_gemm_halo_wv<128, 64, 2, 2, 9, 3><<<grid, 256, 0, st>>>(a);
-      else conv_gemm_halo_wv<128, 64, 2, 2, 3, 3><<<grid, 256, 0, st>>>(a);
-      return launch_status("fs2_conv_gemm(bf16)");
-    }
-  }
   int h8 = g_tune[FS2_TUNE_NT_HALO];
   // (C_in 512 -- the PostNet convs, forward and data gradient -- run faster on the 4-wave
   // 128 x 128 tiles: 78 -> 73 us and 84 -> 77 us alone; the 8-wave tile's 384-block grid is

@@ -140,17 +140,26 @@ def _emulate(globs, acc=1):
     t = tr.Trainer(model, pp, mc, tc)
     shards = [[_shard(pkg, r, "cuda:0", m) for r in range(2)] for m in range(acc)]
     grads = []
+    arena = model.arena()
     for _ in range(2):
-        for m in range(acc):
-            glob = globs[m].cuda()
-            t.Loss.denoms, t.eLoss.denom = glob[0:2], glob[2:3]
-            for b in shards[m]:
+        # each rank's micro-batches accumulate in its own buffer, then the two buffers are
+        # summed: the fp32 addition order of the ranks' local accumulation + the all-reduce
+        per_rank = []
+        for r in range(2):
+            for m in range(acc):
+                glob = globs[m].cuda()
+                t.Loss.denoms, t.eLoss.denom = glob[0:2], glob[2:3]
+                b = shards[m][r]
                 out_ = model(*(b[2:12]), accents=b[13], speaker_meta=b[12])
                 loss = t.Loss(b[:12], out_[:-2])[0]
                 (loss / acc if acc != 1 else loss).backward()
                 el = -t.eLoss(out_[-1], out_[-2])
                 (el / acc if acc != 1 else el).backward()
-        model.join_side()
+            model.join_side()
+            per_rank.append(arena.grad.clone())
+            t.opt.zero_grad()
+        with torch.no_grad():
+            arena.grad.copy_(per_rank[0] + per_rank[1])
         grads.append(model.arena().grad.detach().cpu().clone())
         t.opt.clip_grad_norm_(t.clip)
         t.opt.step_and_update_lr()

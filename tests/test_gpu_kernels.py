@@ -656,48 +656,6 @@ def test_conv_gemm_bf16_halo(B, T, cin, cout, k):
         K.lib.fs2_set_tuning(6, 0)
 
 
-@pytest.mark.parametrize("B,T,cin,cout,k", [(48, 512, 256, 1024, 9), (48, 512, 1024, 256, 9),
-                                            (8, 256, 256, 256, 3), (4, 512, 512, 128, 9)])
-def test_conv_gemm_bf16_halo_wv(B, T, cin, cout, k):
-    """The halo kernel with the weight operand streamed into registers (FS2_TUNE_HALO_WV: 8-wave
-    256 x 128 tiles on the wide forward shape, 4-wave 128 x 64 otherwise) against fp32 math on the
-    same bf16 data, and bitwise against the LDS-ring halo kernel: per accumulator it issues the
-    same MFMAs in the same (channel block, tap, k-half) order.  With lens, the valid rows."""
-    pad = (k - 1) // 2
-    x = bf(rnd(B * T, cin, seed=46))
-    w = bf(rnd(cout, cin, k, scale=1 / math.sqrt(cin * k), seed=47)).float()
-    b = rnd(cout, seed=48)
-    wf = torch.empty(cout * cin * k, device=DEV, dtype=torch.bfloat16)
-    wb = torch.empty(cout * cin * k, device=DEV, dtype=torch.bfloat16)
-    K.weight_prep(w, cout, cin, k, wf, wb)
-    lens = torch.tensor([T - (37 * u) % T for u in range(B)], device=DEV)
-    lens[-1] = 1
-    valid = (torch.arange(T, device=DEV)[None] < lens[:, None]).reshape(-1)
-    dy = bf(rnd(B * T, cout, seed=49) * valid[:, None])
-    aux = rnd(B * T, cin, seed=50)
-
-    def run(wv):
-        K.lib.fs2_set_tuning(14, wv)
-        try:
-            return (K.conv_gemm(x, wf, B * T, T, cin, cout, k, pad, bias=b, flags=K.EPI_RELU),
-                    K.conv_gemm(x, wf, B * T, T, cin, cout, k, pad, bias=b, flags=K.EPI_RELU,
-                                out_dtype=torch.bfloat16, lens=lens),
-                    K.conv_gemm(dy, wb, B * T, T, cout, cin, k, pad, flags=K.EPI_ADD_AUX, aux=aux,
-                                lens=lens))
-        finally:
-            K.lib.fs2_set_tuning(14, 0)
-    y0, yl0, d0 = run(-1)
-    y1, yl1, d1 = run(2)
-    ref = torch.relu(ref_conv(x.float(), w, b, B, T, pad))
-    close(y1, ref, 1e-5)
-    assert torch.equal(y0, y1)
-    assert torch.equal(yl0[valid], yl1[valid]) and torch.equal(d0[valid], d1[valid])
-    assert torch.isfinite(yl1.float()).all() and torch.isfinite(d1).all()
-    xr, wr = (x.float() * valid[:, None]).clone().requires_grad_(), w.clone().requires_grad_()
-    ref_conv(xr, wr, b, B, T, pad).backward(dy.float())
-    close(d1[valid], (xr.grad + aux)[valid], 1e-5)
-
-
 @pytest.mark.parametrize("B,T,cin,cout,k,flags", [
     (48, 128, 1024, 256, 9, "add_aux"), (48, 128, 1024, 256, 9, "bias_relu_bf16"),
     (8, 64, 512, 256, 5, "relu_mask_bf16")])

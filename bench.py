@@ -519,6 +519,9 @@ def main():
         K.lib.fs2_set_tuning(int(knob), int(val))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    if os.environ.get("FS2_MAIN_PRIORITY"):  # A/B: the step's main chain on a prioritised stream
+        main_stream = torch.cuda.Stream(dev, priority=int(os.environ["FS2_MAIN_PRIORITY"]))
+        torch.cuda.set_stream(main_stream)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 

@@ -64,7 +64,10 @@ class _Lib:
                     f"libfs2hip.so not found at {LIB_PATH}; build it with "
                     "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)")
             dll = ctypes.CDLL(LIB_PATH)
+            override = bool(os.environ.get("FS2HIP_LIB"))
             for name, (res, args) in self._sigs.items():
+                if override and not hasattr(dll, name):
+                    continue  # an older library selected for an A/B run: only its own entry points
                 fn = getattr(dll, name)
                 fn.restype = res
                 fn.argtypes = args

@@ -398,6 +398,14 @@ static int wgrad_splits(int64_t rows, int64_t c_in, int64_t c_out, int taps) {
     const int s = g_tune[FS2_TUNE_WGRAD_SPLITS];
     return s < 1 ? 1 : s > 64 ? 64 : s;
   }
+  if (taps == 1 && k1_split_rule()) {
+    // wgrad_k1_glds: 128 x 128 tiles at one block per CU -- about 256 blocks, each split at
+    // least 8 k-tiles of 64 rows
+    const int64_t t1 = ((c_out + 127) / 128) * ((c_in + 127) / 128);
+    int64_t s = (256 + t1 / 2) / t1;
+    if (s > rows / 512) s = rows / 512;
+    return (int)(s < 1 ? 1 : s);
+  }
   const int64_t Kp = (int64_t)taps * c_in;
   const int bt = wgrad_tile(rows, c_in, c_out, taps);
   const int64_t tiles = ((c_out + bt - 1) / bt) * ((Kp + bt - 1) / bt);

@@ -108,6 +108,20 @@ FS2_DEV int m_interleave(int tm, int tiles_m, bool on) {
   return (int)(((int64_t)tm * s) % tiles_m);
 }
 
+// LDS-DMA through a buffer descriptor (buffer_load_dwordx4 ... lds): per-lane 32-bit byte offset
+// in voffset, the wave-uniform rest in soffset, no 64-bit address arithmetic per load; bytes
+// past the descriptor's record count read as zeros.
+FS2_DEV void glds16_buf(__amdgpu_buffer_rsrc_t r, u16* lds_wave_base, uint32_t voff, uint32_t soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(
+      r, (__attribute__((address_space(3))) void*)lds_wave_base, 16, voff, soff, 0, 0);
+}
+// a block-uniform buffer descriptor over [p, p + bytes)
+FS2_DEV __amdgpu_buffer_rsrc_t buf_rsrc(const void* p, int64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0,
+                                           (int)(bytes < 0x7fffffff ? bytes : 0x7fffffff), 0x00020000);
+}
+constexpr uint32_t kOOB = 0x80000000u;  // a voffset past every record count: reads zeros
+
 FS2_DEV void glds16(const void* src, u16* lds_wave_base) {
   __builtin_amdgcn_global_load_lds(
       (const __attribute__((address_space(1))) void*)src,
@@ -180,6 +194,15 @@ FS2_DEV void kloop(int nk, Issue&& issue, Compute&& compute) {
   }
 }
 
+// Workgroup barrier of the epilogues: LDS writes retired (lgkmcnt(0)), then a raw s_barrier.
+// __syncthreads() would also wait vmcnt(0), draining any LDS-DMA still in flight -- in the
+// persistent GEMM that is the next tile's k-steps; at the end of the other kernels no DMA is
+// in flight and the two are the same.  (The epilogues share no global memory between threads.)
+FS2_DEV void epi_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+}
+
 // LayerNorm epilogue of a 256-wide tile (whole rows): the fs2_ln_fwd row computation on the
 // accumulators instead of a stored fp32 y -- z = dropout(acc + bias, p) + res, mean / variance
 // over the half-wave's 256 channels (8 per lane, the fs2_ln_fwd lane layout), out = xhat *
@@ -211,7 +234,7 @@ FS2_DEV void nt_epilogue_ln(const GldsArgs& a, f32x4 (&acc)[BM / 32][256 / WN / 
           for (int r = 0; r < 4; ++r)
             Cs[(i * 16 + 4 * g + r) * EPI_LD + wn * (256 / WN) + j * 16 + r16] = acc[i][j][r];
     }
-    __syncthreads();
+    epi_barrier();
 #pragma unroll
     for (int p = 0; p < (BM / 2) / RPP; ++p) {
       const int rr = p * RPP + (tid >> 5);
@@ -256,7 +279,7 @@ FS2_DEV void nt_epilogue_ln(const GldsArgs& a, f32x4 (&acc)[BM / 32][256 / WN / 
       st4(a.ln_xhat + e0 + 4, xh1);
       if (hl == 0) a.ln_rstd[m] = rs;
     }
-    __syncthreads();
+    epi_barrier();
   }
 }
 
@@ -290,7 +313,7 @@ FS2_DEV void nt_epilogue_lnbwd(const GldsArgs& a, f32x4 (&acc)[BM / 32][256 / WN
           for (int r = 0; r < 4; ++r)
             Cs[(i * 16 + 4 * g + r) * EPI_LD + wn * (256 / WN) + j * 16 + r16] = acc[i][j][r];
     }
-    __syncthreads();
+    epi_barrier();
     f32x4 pg0 = zz, pg1 = zz, pb0 = zz, pb1 = zz, py0 = zz, py1 = zz;
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
@@ -348,7 +371,7 @@ FS2_DEV void nt_epilogue_lnbwd(const GldsArgs& a, f32x4 (&acc)[BM / 32][256 / WN
     red[(1 * 8 + hw) * 64 + 2 * hl + 1] = pb1;
     red[(2 * 8 + hw) * 64 + 2 * hl] = py0;
     red[(2 * 8 + hw) * 64 + 2 * hl + 1] = py1;
-    __syncthreads();
+    epi_barrier();
     if (live && tid < 3 * 64) {  // waves 0-2: one kind each, the 8 half-waves in order
       const int kind = tid >> 6, q = tid & 63;
       f32x4 s = red[(kind * 8) * 64 + q];
@@ -357,7 +380,7 @@ FS2_DEV void nt_epilogue_lnbwd(const GldsArgs& a, f32x4 (&acc)[BM / 32][256 / WN
       const int slot = kind == 2 ? 3 : kind;  // fs2_ln_bwd's part layout: dgamma, dbeta, -, dbias
       st4(a.ln_part + ((int64_t)slot * a.ln_nblk + blk) * 256 + 4 * q, s);
     }
-    __syncthreads();
+    epi_barrier();
   }
 }
 
@@ -394,7 +417,7 @@ FS2_DEV void nt_epilogue(const GldsArgs& a, f32x4 (&acc)[BM / 32][BN / WN / 16],
           for (int r = 0; r < 4; ++r)
             Cs[(i * 16 + 4 * g + r) * EPI_LD + wn * (BN / WN) + j * 16 + r16] = acc[i][j][r];
     }
-    __syncthreads();
+    epi_barrier();
     constexpr int TPR = BN / 8;           // threads per row
     constexpr int RPP = NWAVE * 64 / TPR; // rows per pass
     const int cc = (tid % TPR) * 8;
@@ -520,12 +543,16 @@ FS2_DEV void nt_epilogue(const GldsArgs& a, f32x4 (&acc)[BM / 32][BN / WN / 16],
         }
       }
     }
-    __syncthreads();
+    epi_barrier();
   }
 }
 
-template <int BM, int BN, int STAGES, bool TAPALIGNED, bool VOC>
+// K1: taps == 1 and K % 64 == 0 (the Linear / 1x1 projections) -- A and B stage through buffer
+// descriptors based at the tile's first row: per-lane 32-bit offsets fixed over the k loop, the
+// k-step in the scalar offset, rows past M / N out of the descriptors' range (zeros).
+template <int BM, int BN, int STAGES, bool TAPALIGNED, bool VOC, bool K1 = false>
 __global__ __launch_bounds__(256) void conv_gemm_nt_glds(GldsArgs a) {
+  static_assert(!K1 || (TAPALIGNED && !VOC), "K1: taps == 1, K % 64 == 0, no vocoder epilogue");
   const int dil = VOC ? a.dil : 1;
   constexpr int BK = 64;
   constexpr int AW = BM / 32, BW = BN / 32;  // glds per wave per tile (8 rows each)
@@ -587,6 +614,27 @@ __global__ __launch_bounds__(256) void conv_gemm_nt_glds(GldsArgs a) {
   }
 
   const int nk = (a.K + BK - 1) / BK;
+  // K1 staging: descriptors over the tile's BM rows of x / BN rows of w
+  const auto x_rs = buf_rsrc(a.x + m0 * a.ldx, (a.M - m0 < BM ? a.M - m0 : BM) * a.ldx * 2);
+  const auto w_rs = buf_rsrc(a.w + (int64_t)n0 * a.K, (int64_t)(a.N - n0 < BN ? a.N - n0 : BN) * a.K * 2);
+  uint32_t a_vo[K1 ? AW : 1], b_vo[K1 ? BW : 1];
+  if constexpr (K1) {
+#pragma unroll
+    for (int i = 0; i < AW; ++i)
+      a_vo[i] = (uint32_t)((((wave * AW + i) * 8 + lrow) * a.ldx + a_lc[i] * 8) * 2);
+#pragma unroll
+    for (int i = 0; i < BW; ++i)
+      b_vo[i] = (uint32_t)((((wave * BW + i) * 8 + lrow) * a.K + b_lc[i] * 8) * 2);
+  }
+  auto issue_k1 = [&](int kt, int stage) {
+    u16* As = smem + stage * STAGE_E;
+    u16* Bs = As + BM * BK;
+    const uint32_t k0 = (uint32_t)(kt * BK * 2);
+#pragma unroll
+    for (int i = 0; i < AW; ++i) glds16_buf(x_rs, As + (wave * AW + i) * 8 * BK, a_vo[i], k0);
+#pragma unroll
+    for (int i = 0; i < BW; ++i) glds16_buf(w_rs, Bs + (wave * BW + i) * 8 * BK, b_vo[i], k0);
+  };
   auto issue = [&](int kt, int stage) {
     u16* As = smem + stage * STAGE_E;
     u16* Bs = As + BM * BK;
@@ -651,9 +699,153 @@ __global__ __launch_bounds__(256) void conv_gemm_nt_glds(GldsArgs a) {
     }
   };
 
-  if (!skip) kloop<STAGES, AW + BW>(nk, issue, compute);
+  if (!skip) {
+    if constexpr (K1) kloop<STAGES, AW + BW>(nk, issue_k1, compute);
+    else kloop<STAGES, AW + BW>(nk, issue, compute);
+  }
 
   nt_epilogue<BM, BN, VOC>(a, acc, smem, m0, n0, skip, tid, wm, wn, g, r16);
+}
+
+// ------------------------------------------------------------------------ persistent k = 1 GEMM
+// gemm_nt_persist: the tap-major kernel's tiles and epilogues for the Linear / 1x1 Conv1d
+// projections (taps = 1, K % 64 == 0), persistent: one workgroup per CU slot walks a list of
+// tiles, and its LDS-DMA ring of STAGES k-tile slots runs across tile boundaries -- the next
+// tile's first k-steps are in flight while the current tile's epilogue (through its own LDS
+// region, raw barriers that leave the DMA pending) stores.  The short-K projections (K = 256:
+// four k-steps) were bound by that per-tile chain of load latency -> MFMA -> store, not by
+// bytes or MFMAs (profiles/r2_hipblaslt_vs_ours.txt).  Each XCD takes a contiguous range of
+// tiles, n fastest (a row band's A tile is re-read by the n-tiles from its XCD's L2); with
+// lens the m-tiles are interleaved as in conv_gemm_nt_glds and all-padding tiles run no
+// k-steps (epilogue only).
+template <int BM, int BN, int STAGES>
+__global__ __launch_bounds__(256, 1) void gemm_nt_persist(GldsArgs a) {
+  constexpr int BK = 64;
+  constexpr int AW = BM / 32, BW = BN / 32;  // glds per wave per k-step
+  constexpr int MI = BM / 32, NI = BN / 32;
+  constexpr int STAGE_E = (BM + BN) * BK;
+  constexpr int EPI_LD = BN + 4;
+  // epilogue region: the fp32 half tile (+ nt_epilogue_lnbwd's reduction rows on 64 x 256 tiles)
+  constexpr int EPI_E = (BM / 2) * EPI_LD * 2 + (BM == 64 && BN == 256 ? 3 * 8 * 64 * 8 : 0);
+  __shared__ __attribute__((aligned(1024))) u16 smem[STAGES * STAGE_E + EPI_E];
+  u16* epi = smem + STAGES * STAGE_E;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int g = lane >> 4, r16 = lane & 15;
+
+  // this workgroup's tiles: XCD x = blockIdx % 8 owns tiles [T x / 8, T (x + 1) / 8), its
+  // workgroups take every gx-th of them
+  const int T = a.tiles_m * a.tiles_n, G = gridDim.x;
+  const int xcd = blockIdx.x & 7, jx = blockIdx.x >> 3, gx = (G - xcd + 7) >> 3;
+  const int t_beg = (int)((int64_t)T * xcd / 8) + jx, t_end = (int)((int64_t)T * (xcd + 1) / 8);
+  const int nk = a.K / BK;
+  auto tile_of = [&](int t, int64_t& m0, int& n0) {
+    const int tm = m_interleave(t / a.tiles_n, a.tiles_m, a.lens != nullptr);
+    m0 = (int64_t)tm * BM;
+    n0 = (t % a.tiles_n) * BN;
+  };
+  auto steps_of = [&](int t) {  // k-steps of tile t (0: all rows padding)
+    int64_t m0;
+    int n0;
+    tile_of(t, m0, n0);
+    const bool skip = a.lens && rows_all_padding(a.lens, a.T, m0, m0 + BM < a.M ? m0 + BM : a.M);
+    return skip ? 0 : nk;
+  };
+
+  // per-lane staging: A row R = (wave AW + i) * 8 + lane / 8 (logical chunk (lane & 7) ^
+  // ((R >> 1) & 7)), B row likewise
+  const int lrow = lane >> 3;
+  int a_lc[AW], b_lc[BW];
+#pragma unroll
+  for (int i = 0; i < AW; ++i) a_lc[i] = (lane & 7) ^ ((((wave * AW + i) * 8 + lrow) >> 1) & 7);
+#pragma unroll
+  for (int i = 0; i < BW; ++i) b_lc[i] = (lane & 7) ^ ((((wave * BW + i) * 8 + lrow) >> 1) & 7);
+  const u16* zero = reinterpret_cast<const u16*>(g_zero_line);
+  auto issue = [&](int t, int kt, int slot) {
+    int64_t m0;
+    int n0;
+    tile_of(t, m0, n0);
+    u16* As = smem + slot * STAGE_E;
+    u16* Bs = As + BM * BK;
+    const int k0 = kt * BK;
+#pragma unroll
+    for (int i = 0; i < AW; ++i) {
+      const int64_t m = m0 + (wave * AW + i) * 8 + lrow;
+      glds16(m < a.M ? a.x + m * a.ldx + k0 + a_lc[i] * 8 : zero, As + (wave * AW + i) * 8 * BK);
+    }
+#pragma unroll
+    for (int i = 0; i < BW; ++i) {
+      const int n = n0 + (wave * BW + i) * 8 + lrow;
+      glds16(n < a.N ? a.w + (int64_t)n * a.K + k0 + b_lc[i] * 8 : zero, Bs + (wave * BW + i) * 8 * BK);
+    }
+  };
+
+  f32x4 acc[MI][NI];
+  const int sw = (r16 >> 1) & 7;
+  const int fo0 = r16 * BK + ((0 * 4 + g) ^ sw) * 8;
+  const int fo1 = r16 * BK + ((1 * 4 + g) ^ sw) * 8;
+  auto compute = [&](int slot) {
+    const u16* As = smem + slot * STAGE_E + wm * (BM / 2) * BK;
+    const u16* Bs = smem + slot * STAGE_E + BM * BK + wn * (BN / 2) * BK;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int fo = ks ? fo1 : fo0;
+      bf16x8g fa[MI], fb[NI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) fa[i] = *reinterpret_cast<const bf16x8g*>(As + i * 16 * BK + fo);
+#pragma unroll
+      for (int j = 0; j < NI; ++j) fb[j] = *reinterpret_cast<const bf16x8g*>(Bs + j * 16 * BK + fo);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  // issue cursor (tile it, k-step ik) over the flattened (tile, k-step) stream; `ahead` steps
+  // issued beyond the one being consumed
+  int it = t_beg, ik = 0;
+  while (it < t_end && steps_of(it) == 0) it += gx;
+  auto advance = [&]() {
+    if (++ik == nk) {
+      ik = 0;
+      do it += gx; while (it < t_end && steps_of(it) == 0);
+    }
+  };
+  int issued = 0, consumed = 0;
+  for (int d = 0; d < STAGES - 1 && it < t_end; ++d) {
+    issue(it, ik, issued % STAGES);
+    ++issued;
+    advance();
+  }
+  for (int t = t_beg; t < t_end; t += gx) {
+    int64_t m0;
+    int n0;
+    tile_of(t, m0, n0);
+    const int ns = steps_of(t);
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int kt = 0; kt < ns; ++kt) {
+      // step `consumed` landed: at most (issued - consumed - 1) younger steps stay in flight
+      const int ahead = issued - consumed - 1;
+      vm_wait_tiles<AW + BW>(ahead < STAGES - 2 ? ahead : STAGES - 2);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (it < t_end) {  // refill the slot consumed last step (every wave is past its reads)
+        issue(it, ik, issued % STAGES);
+        ++issued;
+        advance();
+      }
+      compute(consumed % STAGES);
+      ++consumed;
+    }
+    nt_epilogue<BM, BN, false>(a, acc, epi, m0, n0, ns == 0, tid, wm, wn, g, r16);
+  }
 }
 
 // ------------------------------------------------------------------------ halo variant
@@ -731,21 +923,25 @@ void conv_gemm_halo(GldsArgs a) {
     const int64_t nv = u1 - (m0 + wm * (BM / 2));
     mi_act = nv <= 0 ? 0 : nv >= BM / 2 ? MI : (int)((nv + 15) / 16);
   }
-  // halo piece p = wave + NWAVE q: rows h = 8 p + lrow, global row m0 - pad + h
-  const u16* h_src[QMAX];
+  // halo piece p = wave + NWAVE q: rows h = 8 p + lrow, global row m0 - pad + h.  Buffer
+  // descriptors based at the tile's first halo row / first weight row; a lane whose row lies
+  // outside the utterance (or past N) carries an out-of-range offset and stages zeros.  The
+  // channel block and tap advance in the scalar offset.
+  const auto x_rs = buf_rsrc(a.x + (m0 - a.pad) * a.ldx + cb0 * BK, (int64_t)HMAX * a.ldx * 2);
+  const auto w_rs = buf_rsrc(a.w + (int64_t)n0 * a.K + cb0 * BK, (int64_t)BN * a.K * 2);
+  uint32_t h_vo[QMAX];
 #pragma unroll
   for (int q = 0; q < QMAX; ++q) {
     const int h = (wave + NWAVE * q) * 8 + lrow;
     const int64_t gr = m0 - a.pad + h;
     const int lc = (lane & 7) ^ (h & 7);
-    h_src[q] = (gr >= u0 && gr < u1) ? a.x + gr * a.ldx + lc * 8 + cb0 * BK : nullptr;
+    h_vo[q] = (gr >= u0 && gr < u1) ? (uint32_t)((h * a.ldx + lc * 8) * 2) : kOOB;
   }
-  const u16* b_src[BW];
+  uint32_t b_vo[BW];
 #pragma unroll
   for (int i = 0; i < BW; ++i) {
     const int R = (wave * BW + i) * 8 + lrow;
-    const int n = n0 + R;
-    b_src[i] = n < a.N ? a.w + (int64_t)n * a.K + ((lane & 7) ^ (R & 7)) * 8 + cb0 * BK : nullptr;
+    b_vo[i] = n0 + R < a.N ? (uint32_t)((R * a.K + ((lane & 7) ^ (R & 7)) * 8) * 2) : kOOB;
   }
 
   f32x4 acc[MI][NI];
@@ -763,17 +959,16 @@ void conv_gemm_halo(GldsArgs a) {
 #pragma unroll
     for (int q = 0; q < QMAX; ++q) {
       const int pc = wave + NWAVE * q;
-      if (pc < HP) glds16(h_src[q] ? h_src[q] + cb * BK : zero, As + aslot * A_E + pc * 8 * BK);
+      if (pc < HP) glds16_buf(x_rs, As + aslot * A_E + pc * 8 * BK, h_vo[q], (uint32_t)(cb * BK * 2));
     }
   };
   int qa = 0;  // this wave's halo pieces (its LDS-DMA count per halo stage)
 #pragma unroll
   for (int q = 0; q < QMAX; ++q) qa += (wave + NWAVE * q) < HP ? 1 : 0;
   auto issue_b = [&](int cb, int j, int slot) {
-    const int64_t k0 = (int64_t)j * a.Cin + cb * BK;
+    const uint32_t k0 = (uint32_t)((j * a.Cin + cb * BK) * 2);
 #pragma unroll
-    for (int i = 0; i < BW; ++i)
-      glds16(b_src[i] ? b_src[i] + k0 : zero, Bs + slot * B_E + (wave * BW + i) * 8 * BK);
+    for (int i = 0; i < BW; ++i) glds16_buf(w_rs, Bs + slot * B_E + (wave * BW + i) * 8 * BK, b_vo[i], k0);
   };
   // PIPE: one k-half (ks) of step (j, slot, aslot) into a register set, and its MFMAs
   // (nact: compile-time count of this wave's 16-row fragments that hold a valid row; the
@@ -1328,6 +1523,225 @@ __global__ __launch_bounds__(256) void conv_wgrad_tn_glds(WgradGlds a) {
   }
 }
 
+// k = 1 weight gradient (Linear / 1x1 Conv1d): a 128 (o) x 128 (c) output tile per block of 8
+// waves.  Wave w owns the 64 x 64 quadrant w & 3 over rows 32 (w >> 2) .. +31 of each 64-row
+// k-tile, and the two row halves of a quadrant are summed through LDS at the end.  The k-tiles
+// (dy [64 rows][128 o] and x [64 rows][128 c], 256-B rows, LDS-DMA) run through a 4-slot ring
+// with three tiles in flight (counted vmcnt, raw barrier: 96 KB in flight per CU).  Against
+// conv_wgrad_tn_glds (64 x 64 tiles of 2 x 2 waves of 32 x 32, one tile in flight): a quarter of
+// the L2 -> LDS operand traffic per FLOP (each staged row feeds 128 x 128 outputs), every
+// transposed fragment read feeds 4 MFMAs instead of 2, and the load latency is covered -- that
+// kernel measured MFMA-busy 0.09 at the decoder QKV shape, 39 % of its wave cycles waiting on the
+// next tile's DMA (profiles/r3_wgrad_pmc.txt).  Same split-K slab layout (slab[z][o][c], bias
+// slab[z][o]) and wgrad_reduce_k1.  The bias gradient rides on the dy fragments of the blocks
+// of the first c tile (an MFMA against a ones fragment).
+__global__ __launch_bounds__(512, 1) void wgrad_k1_glds(WgradGlds a) {
+  constexpr int BO = 128, BC = 128, BK = 64, NT = 512, STAGES = 4;
+  constexpr int IMG = BK * 128;          // one operand image: [64 rows][128] bf16 (256-B rows)
+  constexpr int STAGE_E = 2 * IMG;       // dy image then x image (32 KB)
+  constexpr int EPI_LD = 64 + 4;         // fp32 epilogue rows of a 64 x 64 quadrant
+  constexpr int EPI_B = (4 * 64 * EPI_LD + 4 * 64) * 4;
+  constexpr int SMEM_B = STAGES * STAGE_E * 2 > EPI_B ? STAGES * STAGE_E * 2 : EPI_B;
+  constexpr int MAXKT = 1024;
+  __shared__ __attribute__((aligned(1024))) u16 smem[SMEM_B / 2 + MAXKT + 64];
+  short* ktl = reinterpret_cast<short*>(smem + SMEM_B / 2);
+  int* wcnt = reinterpret_cast<int*>(smem + SMEM_B / 2 + MAXKT);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int quad = wave & 3, half = wave >> 2;
+  const int qo = (quad >> 1) * 64, qc = (quad & 1) * 64;
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3, r16 = lane & 15;
+
+  const int per_split = a.tiles_o * a.tiles_k;
+  const int nwg = per_split * a.splits;
+  const int orig = blockIdx.x, xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int z = wg / per_split, rem = wg - z * per_split;
+  const int tc = rem % a.tiles_k, to = rem / a.tiles_k;
+  const int o0 = to * BO, c0 = tc * BC;
+  const int64_t r_begin = (int64_t)z * a.rows_per_split;
+  int64_t r_end = r_begin + a.rows_per_split;
+  if (r_end > a.M) r_end = a.M;
+  const int nk_all = r_end > r_begin ? (int)((r_end - r_begin + BK - 1) / BK) : 0;
+  // ordered list of the split's k-tiles holding a real row (as conv_wgrad_tn_glds)
+  const bool use_list = a.lens != nullptr && nk_all <= MAXKT;
+  int nk = nk_all;
+  if (use_list) {
+    int total = 0;
+    for (int cc0 = 0; cc0 < nk_all; cc0 += NT) {
+      const int kt = cc0 + tid;
+      bool v = false;
+      if (kt < nk_all) {
+        const int64_t k0 = r_begin + (int64_t)kt * BK;
+        v = !rows_all_padding(a.lens, a.T, k0, k0 + BK < r_end ? k0 + BK : r_end);
+      }
+      const uint64_t mask = __ballot(v);
+      if (lane == 0) wcnt[wave] = __popcll(mask);
+      __syncthreads();
+      int before = total;
+      for (int w = 0; w < wave; ++w) before += wcnt[w];
+      const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
+      if (v) ktl[before + below] = (short)kt;
+      for (int w = 0; w < 8; ++w) total += wcnt[w];
+      __syncthreads();
+    }
+    nk = total;
+  }
+
+  // staging: a wave-instruction fills 4 image rows x 256 B; image row R = (2 wave + i) * 4 +
+  // lane / 16 (i < 2), physical 16-B chunk lane & 15 holding logical chunk (lane & 15) ^
+  // swz(R), swz(R) = (R & 7) << 1 (the BT = 128 swizzle of conv_wgrad_tn_glds: a 32-lane
+  // transposed read hits 16 distinct bank slots)
+  auto swz = [](int R) { return (R & 7) << 1; };
+  // buffer descriptors over the split's rows of dy and x (the k-tile advance rides in the scalar
+  // offset); a lane whose chunk lies past the channel count, or whose row lies past the split's
+  // end, selects an out-of-range voffset and stages zeros.  The row clip is the voffset select,
+  // not the record count, so it holds whether or not the range check sees the scalar offset.
+  const auto dy_rs = buf_rsrc(a.dy + r_begin * a.ldy, (r_end - r_begin) * a.ldy * 2);
+  const auto x_rs = buf_rsrc(a.x + r_begin * a.ldx, (r_end - r_begin) * a.ldx * 2);
+  int Rl[2];
+  uint32_t a_vo[2], b_vo[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int R = (wave * 2 + i) * 4 + (lane >> 4);
+    const int lc = (lane & 15) ^ swz(R);
+    Rl[i] = R;
+    a_vo[i] = o0 + lc * 8 < a.Cout ? (uint32_t)((R * a.ldy + o0 + lc * 8) * 2) : kOOB;
+    b_vo[i] = c0 + lc * 8 < a.Cin ? (uint32_t)((R * a.ldx + c0 + lc * 8) * 2) : kOOB;
+  }
+  const int rows = (int)(r_end - r_begin);
+  auto issue = [&](int kt, int stage) {
+    u16* As = smem + stage * STAGE_E;
+    u16* Bs = As + IMG;
+    const int tile = __builtin_amdgcn_readfirstlane(use_list ? (int)ktl[kt] : kt);
+    const int lim = rows - tile * BK;  // rows of this k-tile inside the split
+    const uint32_t sa = (uint32_t)(tile * BK * a.ldy * 2), sb = (uint32_t)(tile * BK * a.ldx * 2);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const bool ok = Rl[i] < lim;
+      glds16_buf(dy_rs, As + (wave * 2 + i) * 4 * 128, ok ? a_vo[i] : kOOB, sa);
+      glds16_buf(x_rs, Bs + (wave * 2 + i) * 4 * 128, ok ? b_vo[i] : kOOB, sb);
+    }
+  };
+
+  f32x4 acc[4][4], accb[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    accb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  // bias gradient: the waves of the c-half-0 quadrants of the first c tile (block-uniform tile
+  // test, wave-uniform quadrant test)
+  const bool do_bias = a.bslab != nullptr && tc == 0 && (quad & 1) == 0;
+  bf16x8g ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = (__bf16)1.0f;
+  // transposed fragment halves of this wave's 32 rows (asm reads, see ds_tr16)
+  const int rbase = half * 32 + 4 * g + q, sw = swz(rbase);
+  auto tr = [&](const u16* img, int col0, int hi) -> s16x4g {
+    const int lc = (col0 >> 3) + (p >> 1);
+    return ds_tr16(img + (rbase + 16 * hi) * 128 + ((lc ^ sw) << 3) + ((p & 1) << 2));
+  };
+  auto cat = [](s16x4g lo, s16x4g hi) {
+    return __builtin_bit_cast(bf16x8g, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+  };
+  auto compute = [&](int stage) {
+    const u16* As = smem + stage * STAGE_E;
+    const u16* Bs = As + IMG;
+    s16x4g ra[4][2], rb[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      ra[i][0] = tr(As, qo + i * 16, 0);
+      ra[i][1] = tr(As, qo + i * 16, 1);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      rb[j][0] = tr(Bs, qc + j * 16, 0);
+      rb[j][1] = tr(Bs, qc + j * 16, 1);
+    }
+    bf16x8g fa[4];
+    // c fragment j's MFMAs wait only for the reads up to it (4-bit counter: the 16th read
+    // issues once the first has retired, so 6 - 2 j younger reads remain in flight)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (j == 0) lgkm_wait<6>();
+      else if (j == 1) lgkm_wait<4>();
+      else if (j == 2) lgkm_wait<2>();
+      else lgkm_wait<0>();
+      if (j == 0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fa[i] = cat(ra[i][0], ra[i][1]);
+      }
+      const bf16x8g fb = cat(rb[j][0], rb[j][1]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb, acc[i][j], 0, 0, 0);
+    }
+    if (do_bias) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], ones, accb[i], 0, 0, 0);
+    }
+  };
+
+  kloop<STAGES, 4>(nk, issue, compute);
+
+  // the two row halves of each quadrant through LDS: half 1 writes, half 0 adds and stores
+  float* Cs = reinterpret_cast<float*>(smem);
+  float* Bp = Cs + 4 * 64 * EPI_LD;
+  if (half == 1) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          Cs[(quad * 64 + i * 16 + 4 * g + r) * EPI_LD + j * 16 + r16] = acc[i][j][r];
+    if (do_bias && r16 == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Bp[quad * 64 + i * 16 + 4 * g + r] = accb[i][r];
+    }
+  }
+  __syncthreads();
+  if (half == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          Cs[(quad * 64 + i * 16 + 4 * g + r) * EPI_LD + j * 16 + r16] += acc[i][j][r];
+    if (do_bias && r16 == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Bp[quad * 64 + i * 16 + 4 * g + r] += accb[i][r];
+    }
+  }
+  __syncthreads();
+  {
+    // 128 x 128 outputs, 32 per thread: row o = tid / 4, 32 consecutive c; quadrant rows
+    const int o = tid >> 2, cc = (tid & 3) * 32;
+    const int qd = (o >> 6) * 2 + (cc >> 6), ro = o & 63, co = cc & 63;
+    float* slab = a.slab + (int64_t)z * a.Cout * a.Kp;
+    if (o0 + o < a.Cout) {
+#pragma unroll
+      for (int v = 0; v < 8; ++v) {
+        const f32x4 t = *reinterpret_cast<const f32x4*>(Cs + (qd * 64 + ro) * EPI_LD + co + 4 * v);
+        if (c0 + cc + 4 * v < a.Cin)
+          *reinterpret_cast<f32x4*>(slab + (int64_t)(o0 + o) * a.Kp + c0 + cc + 4 * v) = t;
+      }
+    }
+    if (a.bslab != nullptr && tc == 0 && tid < BO && o0 + tid < a.Cout)
+      a.bslab[(int64_t)z * a.Cout + o0 + tid] = Bp[((tid >> 6) * 2) * 64 + (tid & 63)];
+  }
+}
+
 // Halo weight gradient for Conv1d with 2 <= taps <= 9 (C_in, C_out multiples of 64, T a
 // multiple of 64): a block owns a 64 (o) x 64 (c) tile for ALL taps.  Per 64-row k-tile it
 // stages the dy tile (64 x 64) and the x rows of the tile plus the tap halo
@@ -1469,21 +1883,26 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_halo(WgradGlds a) {
     if constexpr (WS == 1) {
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        bf16x8g fa[4], fb[2];
+        // x fragments two taps ahead in a ring of three: tap j's MFMAs wait only for the reads
+        // up to its fragment (the LDS latency exceeds one tap's 4 MFMAs)
+        bf16x8g fa[4], fb[3];
 #pragma unroll
         for (int i = 0; i < 4; ++i) fa[i] = tr_frag_asm(As, ks * 32, i * 16);
         fb[0] = tr_frag_asm(Xs, ks * 32, wave * 16);
+        if (TAPS > 1) fb[1] = tr_frag_asm(Xs, ks * 32 + 1, wave * 16);
 #pragma unroll
         for (int j = 0; j < TAPS; ++j) {
-          if (j + 1 < TAPS) {
-            fb[(j + 1) & 1] = tr_frag_asm(Xs, ks * 32 + j + 1, wave * 16);
-            lgkm_wait<2>();  // all but the next tap's x fragment landed
+          if (j + 2 < TAPS) {
+            fb[(j + 2) % 3] = tr_frag_asm(Xs, ks * 32 + j + 2, wave * 16);
+            lgkm_wait<4>();  // all but the x fragments of taps j + 1, j + 2 landed
+          } else if (j + 1 < TAPS) {
+            lgkm_wait<2>();
           } else {
             lgkm_wait<0>();
           }
 #pragma unroll
           for (int i = 0; i < 4; ++i)
-            acc[j][i][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j & 1], acc[j][i][0],
+            acc[j][i][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j % 3], acc[j][i][0],
                                                                    0, 0, 0);
         }
         if (do_bias) {
@@ -1634,6 +2053,38 @@ __global__ __launch_bounds__(256) void wgrad_reduce_taps(const float* __restrict
   }
 }
 
+// taps > 1, one workgroup per output row o: the S slab rows (taps * Cin contiguous floats each)
+// are summed in split order with 16-B loads, S loads in flight per chunk, into LDS, then added
+// to dw[o][c][j] in output order (the [j][c] -> [c][j] transpose through LDS; coalesced 4-B
+// read-modify-writes).  Same split order as wgrad_reduce_taps (bitwise equal), a quarter of its
+// workgroups, every slab row read as one contiguous run.
+constexpr int RROW_MAX = 9 * 1024;
+__global__ __launch_bounds__(256) void wgrad_reduce_rows(const float* __restrict__ slab,
+                                                         const float* __restrict__ bslab,
+                                                         int splits, int Cout, int Cin, int taps,
+                                                         float* dw, float* db) {
+  __shared__ float row[RROW_MAX];
+  const int o = blockIdx.x, Kp = taps * Cin;
+  const int64_t total = (int64_t)Cout * Kp;
+  const float* src = slab + (int64_t)o * Kp;
+  for (int e4 = threadIdx.x; e4 < Kp / 4; e4 += 256) {
+    f32x4 s = ld4(src + 4 * e4);
+    for (int z = 1; z < splits; ++z) s += ld4(src + z * total + 4 * e4);
+    *reinterpret_cast<f32x4*>(row + 4 * e4) = s;
+  }
+  __syncthreads();
+  float* out = dw + (int64_t)o * Kp;
+  for (int e = threadIdx.x; e < Kp; e += 256) {
+    const int c = e / taps, j = e - c * taps;
+    out[e] += row[j * Cin + c];
+  }
+  if (db && threadIdx.x == 0) {
+    float b = 0.f;
+    for (int z = 0; z < splits; ++z) b += bslab[(int64_t)z * Cout + o];
+    db[o] += b;
+  }
+}
+
 int conv_wgrad_glds_launch(const void* dy, int64_t ldy, const void* x, int64_t ldx, float* dw,
                            float* db, int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out,
                            int taps, int pad, const int64_t* lens, int splits, int tile, float* ws,
@@ -1648,6 +2099,19 @@ int conv_wgrad_glds_launch(const void* dy, int64_t ldy, const void* x, int64_t l
   WgradGlds a{(const u16*)dy, ldy, (const u16*)x, ldx, ws, bslab, rows, seq_len, (int)c_in,
               (int)c_out, taps, pad, (int)Kp, rps, (int)((c_out + tile - 1) / tile),
               (int)((Kp + tile - 1) / tile), splits, lens};
+  // wgrad_k1_glds stages through buffer descriptors with 32-bit byte offsets within a split
+  const bool off32 = (rps + 64) * (ldx > ldy ? ldx : ldy) * 2 < ((int64_t)1 << 31);
+  if (taps == 1 && k1_split_rule() && c_in % 8 == 0 && off32) {
+    // k = 1: 128 x 128 tiles of 8 waves (wgrad_k1_glds), splits in 64-row k-tiles
+    a.tiles_o = (int)((c_out + 127) / 128);
+    a.tiles_k = (int)((c_in + 127) / 128);
+    const unsigned g1 = (unsigned)(a.tiles_o * a.tiles_k * splits);
+    wgrad_k1_glds<<<g1, 512, 0, st>>>(a);
+    const int64_t total = c_out * c_in;
+    wgrad_reduce_k1<<<(unsigned)((total / 4 + 63) / 64), 256, 0, st>>>(ws, bslab, splits,
+                                                                     (int)c_out, total, dw, db);
+    return launch_status("fs2_conv_wgrad(bf16)");
+  }
   const bool halo = taps >= 2 && taps <= 9 && (taps == 3 || taps == 5 || taps == 9) &&
                     c_in % 64 == 0 && c_out % 64 == 0 && seq_len % 64 == 0 &&
                     g_tune[FS2_TUNE_WGRAD_HALO] >= 0;
@@ -1688,6 +2152,9 @@ int conv_wgrad_glds_launch(const void* dy, int64_t ldy, const void* x, int64_t l
     const int64_t total = c_out * c_in;  // multiple of 64 (both channel counts % 8 == 0)
     wgrad_reduce_k1<<<(unsigned)((total / 4 + 63) / 64), 256, 0, st>>>(ws, bslab, splits,
                                                                      (int)c_out, total, dw, db);
+  } else if (taps * c_in <= RROW_MAX && c_in % 4 == 0 && g_tune[FS2_TUNE_WGRAD_K1] != -2) {
+    wgrad_reduce_rows<<<(unsigned)c_out, 256, 0, st>>>(ws, bslab, splits, (int)c_out, (int)c_in,
+                                                       taps, dw, db);
   } else {
     dim3 rg((unsigned)((c_in + 63) / 64), (unsigned)c_out);
     wgrad_reduce_taps<<<rg, 256, 0, st>>>(ws, bslab, splits, (int)c_out, (int)c_in, taps, dw, db);
@@ -1695,6 +2162,26 @@ int conv_wgrad_glds_launch(const void* dy, int64_t ldy, const void* x, int64_t l
   return launch_status("fs2_conv_wgrad(bf16)");
 }
 
+
+static int cu_count() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
+      n = v;
+    else
+      n = 256;
+  }
+  return n;
+}
+
+// gemm_nt_persist launch: one workgroup per CU (at most one per tile)
+template <int BM, int BN, int S>
+static void launch_persist(GldsArgs a, hipStream_t st) {
+  const int T = a.tiles_m * a.tiles_n, n = cu_count();
+  gemm_nt_persist<BM, BN, S><<<(unsigned)(T < n ? T : n), 256, 0, st>>>(a);
+}
 
 template <int BM, int BN, int S>
 static void launch_nt(GldsArgs a, bool tapaligned, bool voc, hipStream_t st) {
@@ -1706,6 +2193,8 @@ static void launch_nt(GldsArgs a, bool tapaligned, bool voc, hipStream_t st) {
   if (voc) {  // vocoder convs: one pipeline depth, dilation + the extended epilogue
     if (tapaligned) conv_gemm_nt_glds<BM, BN, 2, true, true><<<grid, 256, 0, st>>>(a);
     else conv_gemm_nt_glds<BM, BN, 2, false, true><<<grid, 256, 0, st>>>(a);
+  } else if (tapaligned && a.taps == 1 && g_tune[FS2_TUNE_NT_K1] >= 0) {
+    conv_gemm_nt_glds<BM, BN, S, true, false, true><<<grid, 256, 0, st>>>(a);
   } else if (tapaligned) {
     conv_gemm_nt_glds<BM, BN, S, true, false><<<grid, 256, 0, st>>>(a);
   } else {
@@ -1797,11 +2286,18 @@ int conv_gemm_ln_glds_launch(const void* x, int64_t ldx, const void* wk, int64_t
   a.tiles_n = 1;
   const unsigned grid = (unsigned)a.tiles_m;
   const bool tapaligned = c_in % 64 == 0;
+  if (!wide && taps == 1 && tapaligned && g_tune[FS2_TUNE_PERSIST] > 0 &&
+      a.tiles_m >= 2 * cu_count()) {
+    launch_persist<64, 256, 2>(a, st);
+    return launch_status("fs2_conv_gemm_ln");
+  }
+  const bool k1 = tapaligned && taps == 1 && g_tune[FS2_TUNE_NT_K1] >= 0;
   if (wide) {
     if (tapaligned) conv_gemm_nt_glds<128, 256, 2, true, false><<<grid, 256, 0, st>>>(a);
     else conv_gemm_nt_glds<128, 256, 2, false, false><<<grid, 256, 0, st>>>(a);
   } else {
-    if (tapaligned) conv_gemm_nt_glds<64, 256, 2, true, false><<<grid, 256, 0, st>>>(a);
+    if (k1) conv_gemm_nt_glds<64, 256, 2, true, false, true><<<grid, 256, 0, st>>>(a);
+    else if (tapaligned) conv_gemm_nt_glds<64, 256, 2, true, false><<<grid, 256, 0, st>>>(a);
     else conv_gemm_nt_glds<64, 256, 2, false, false><<<grid, 256, 0, st>>>(a);
   }
   return launch_status("fs2_conv_gemm_ln");
@@ -1838,7 +2334,11 @@ int conv_gemm_lnbwd_glds_launch(const void* x, int64_t ldx, const void* wk, int6
   a.tiles_m = (int)((rows + 63) / 64);
   a.tiles_n = 1;
   const unsigned grid = (unsigned)a.tiles_m;
-  if (c_in % 64 == 0) conv_gemm_nt_glds<64, 256, 2, true, false><<<grid, 256, 0, st>>>(a);
+  if (taps == 1 && c_in % 64 == 0 && g_tune[FS2_TUNE_PERSIST] > 0 && a.tiles_m >= 2 * cu_count())
+    launch_persist<64, 256, 2>(a, st);
+  else if (c_in % 64 == 0 && taps == 1 && g_tune[FS2_TUNE_NT_K1] >= 0)
+    conv_gemm_nt_glds<64, 256, 2, true, false, true><<<grid, 256, 0, st>>>(a);
+  else if (c_in % 64 == 0) conv_gemm_nt_glds<64, 256, 2, true, false><<<grid, 256, 0, st>>>(a);
   else conv_gemm_nt_glds<64, 256, 2, false, false><<<grid, 256, 0, st>>>(a);
   return launch_status("fs2_conv_gemm_ln_bwd");
 }
@@ -2011,6 +2511,12 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
     }
 #undef FS2_HALO
 #undef FS2_HALO2
+  } else if (taps == 1 && !voc && tapaligned && g_tune[FS2_TUNE_PERSIST] > 0 &&
+             big >= 2 * cu_count()) {
+    // persistent projection GEMM (gemm_nt_persist): 128 x 128 tiles, 3-slot ring across tiles
+    a.tiles_m = (int)((rows + 127) / 128);
+    a.tiles_n = (int)((c_out + 127) / 128);
+    launch_persist<128, 128, 3>(a, st);
   } else if ((big >= 512 && g_tune[FS2_TUNE_NT_TILE] == 0) || g_tune[FS2_TUNE_NT_TILE] == 1) {
     a.tiles_m = (int)((rows + 127) / 128);
     a.tiles_n = (int)((c_out + 127) / 128);

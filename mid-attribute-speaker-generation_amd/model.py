@@ -954,7 +954,10 @@ class FastSpeech2(nn.Module):
         if not self.overlap_wgrad:
             return None
         if self._side is None:
-            self._side = torch.cuda.Stream(device=self.encoder.position_enc.device)
+            # FS2_SIDE_PRIORITY: stream priority of the weight-gradient stream (torch's scale:
+            # lower = higher priority; the main chain runs on the current stream)
+            prio = int(os.environ.get("FS2_SIDE_PRIORITY", "0"))
+            self._side = torch.cuda.Stream(device=self.encoder.position_enc.device, priority=prio)
         return self._side
 
     def join_side(self):

@@ -411,6 +411,88 @@ def test_norm_copies_bf16():
     assert torch.equal(K.cast_bf16(x), x.to(torch.bfloat16))
 
 
+@pytest.mark.parametrize("B,T,cin,cout,kind", [
+    (48, 512, 256, 768, "bias_bf16"), (48, 512, 1024, 256, "add_aux"),
+    (48, 512, 256, 1024, "relu_mask_bf16"), (40, 512, 768, 256, "plain"), (48, 512, 256, 256, "ln"),
+    (48, 512, 768, 256, "ln_bwd")])
+def test_gemm_persistent(B, T, cin, cout, kind):
+    """The persistent projection GEMM (FS2_TUNE_PERSIST = 1: one workgroup per CU walks its tiles,
+    the LDS-DMA ring runs across tile boundaries) issues the same MFMAs in the same order per
+    tile and the same epilogue as the per-tile launch grid: bitwise equal, with utterance
+    lengths (all-padding tiles skipped), for the plain / bias / aux / ReLU-mask epilogues and the
+    fused LayerNorm forward and backward epilogues (xhat / rstd compared on the rows the forward
+    writes: valid ones)."""
+    x = bf(rnd(B * T, cin, seed=61))
+    w = bf(rnd(cout, cin, scale=1 / math.sqrt(cin), seed=62))
+    b = rnd(cout, seed=63)
+    lens = torch.tensor([T - (41 * u) % T for u in range(B)], device=DEV)
+    lens[-1] = 3
+    valid = (torch.arange(T, device=DEV)[None] < lens[:, None]).reshape(-1)
+    aux = rnd(B * T, cout, seed=64)
+    g, be = 1 + 0.1 * rnd(cout, seed=65), 0.1 * rnd(cout, seed=66)
+
+    def run(knob):
+        K.lib.fs2_set_tuning(15, knob)
+        try:
+            if kind == "bias_bf16":
+                return [K.conv_gemm(x, w, B * T, T, cin, cout, 1, 0, bias=b, out_dtype=torch.bfloat16,
+                                    lens=lens)]
+            if kind == "add_aux":
+                return [K.conv_gemm(x, w, B * T, T, cin, cout, 1, 0, flags=K.EPI_ADD_AUX, aux=aux,
+                                    lens=lens)]
+            if kind == "relu_mask_bf16":
+                return [K.conv_gemm(x, w, B * T, T, cin, cout, 1, 0, flags=K.EPI_RELU_MASK_AUX,
+                                    aux=bf(aux), out_dtype=torch.bfloat16, lens=lens)]
+            if kind == "plain":
+                return [K.conv_gemm(x, w, B * T, T, cin, cout, 1, 0)]
+            if kind == "ln":
+                out, out_t, xh, rs = K.conv_gemm_ln(x, w, B * T, T, cin, cout, 1, 0, g, be, bias=b,
+                                                    res=aux, lens=lens, copy=torch.bfloat16)
+                return [out, out_t, xh[valid], rs[valid]]
+            xh = rnd(B * T, cout, seed=67)
+            rs = 1 + rnd(B * T, seed=68).abs()
+            dg, db, dbi = (torch.zeros(cout, device=DEV) for _ in range(3))
+            dy_t, dres = K.conv_gemm_ln_bwd(x, w, B * T, T, cin, cout, 1, 0, xh, rs, g, dg, db,
+                                            aux=aux, lens=lens, dbias_in=dbi, copy=torch.bfloat16)
+            return [dy_t, dres, dg, db, dbi]
+        finally:
+            K.lib.fs2_set_tuning(15, 0)
+    r0, r1 = run(0), run(1)
+    for a0, a1 in zip(r0, r1):
+        assert torch.equal(a0, a1)
+
+
+@pytest.mark.parametrize("B,T,cin,cout", [(48, 512, 256, 768), (48, 512, 1024, 256),
+                                          (48, 128, 256, 256), (3, 200, 256, 80), (5, 77, 72, 24),
+                                          (1, 1000, 1024, 256)])
+def test_wgrad_k1(B, T, cin, cout):
+    """The k = 1 weight gradient (wgrad_k1_glds: 64 x 64 tiles, 128-row k-tiles over the block's
+    4 waves, split-K slabs + wgrad_reduce_k1) with its fused bias gradient, accumulating into
+    existing gradients, against fp32 math on the same bf16 data -- with and without utterance
+    lengths (all-padding k-tiles skipped; dy is zero on padded rows as in the step), at forced
+    split counts, and against the tap-major kernel (FS2_TUNE_WGRAD_K1 = -1)."""
+    x = bf(rnd(B * T, cin, seed=31))
+    lens = torch.tensor([T - (53 * u) % T for u in range(B)], device=DEV)
+    lens[-1] = max(1, T // 7)
+    valid = (torch.arange(T, device=DEV)[None] < lens[:, None]).reshape(-1)
+    dy = bf(rnd(B * T, cout, seed=32) * valid[:, None])
+    ref_w = dy.float().t() @ x.float()
+    ref_b = dy.float().sum(0)
+    try:
+        for knob, splits, use_lens in ((0, 0, False), (0, 0, True), (0, 1, True), (0, 7, False),
+                                       (0, 64, True), (-1, 0, True)):
+            K.lib.fs2_set_tuning(14, knob)
+            K.lib.fs2_set_tuning(3, splits)  # FS2_TUNE_WGRAD_SPLITS
+            dw, db = torch.ones(cout, cin, device=DEV), torch.ones(cout, device=DEV)
+            K.conv_wgrad(dy, x, dw, B * T, T, cin, cout, 1, 0, db=db,
+                         lens=lens if use_lens else None)
+            close(dw, ref_w + 1, 1e-5)
+            close(db, ref_b + 1, 1e-5)
+    finally:
+        K.lib.fs2_set_tuning(14, 0)
+        K.lib.fs2_set_tuning(3, 0)
+
+
 @pytest.mark.parametrize("stages", [1, 2, 3, 4])
 @pytest.mark.parametrize("B,T,cin,cout,k", [(2, 70, 256, 512, 9), (3, 50, 80, 256, 5),
                                             (1, 200, 512, 80, 5)])

@@ -270,21 +270,29 @@ int fs2_weight_prep_batch(int dtype, const int64_t* jobs, int n_jobs, int64_t n_
  *   FS2_TUNE_NT_TILE       tap-major fwd/dX kernel (k = 1 projections, odd shapes): 0 = tile
  *                          by grid size, 1 / 2 / 3 = force 128x128 / 128x64 / 64x64
  *   FS2_TUNE_LN_TILE       fs2_conv_gemm_ln row tile: 0 = 64 x 256 (default), 1 = 128 x 256
- *   FS2_TUNE_WGRAD_K1      k = 1 weight gradient: 0 = 128 x 128 tiles of 8 waves, buffer-
- *                          descriptor staging (default), -1 = the tap-major kernel;
+ *   FS2_TUNE_WGRAD_K1      k = 1 weight gradient: 0 = 64 x 64 tiles with the 128-row k-tiles
+ *                          split over 4 waves (default), 1 = 128 x 128 tiles of 8 waves
+ *                          (both: buffer-descriptor staging), -1 = the tap-major kernel;
  *                          -2 = also the round-2 split reduce for taps > 1 (A/B)
  *   FS2_TUNE_PERSIST       k = 1 projections (fs2_conv_gemm, _ln, _ln_bwd) on grids of >= 2
  *                          tiles per CU: 1 = persistent GEMM (ring across tiles), 0 = per-tile
  *                          launch grid (default)
  *   FS2_TUNE_NT_K1         k = 1 projections on the tap-major kernel: 0 = buffer-descriptor
  *                          staging build (default), -1 = the general tap-walking build (A/B)
+ *   FS2_TUNE_ATTN_DMA      bf16 attention at T >= 256: 0 = K / V (Q / dO) tiles by LDS-DMA into
+ *                          a 2-slot ring, exp2-folded softmax (default), 1 = 3-slot forward ring
+ *                          at one workgroup per CU, -1 = the register-staged kernels (A/B)
+ *   FS2_TUNE_WGRAD_FUSE    k = 1 weight gradient (FS2_TUNE_WGRAD_K1 = 0): 0 = split slabs summed
+ *                          by a reduce launch (default), 1 = the last split to finish a tile sums
+ *                          them in split order inside the kernel (no reduce launch)
  * Process-wide; query workspace sizes after setting.                                 */
 enum { FS2_TUNE_GEMM_STAGES = 0, FS2_TUNE_WGRAD_STAGES = 1, FS2_TUNE_WGRAD_TILE = 2,
        FS2_TUNE_WGRAD_SPLITS = 3, FS2_TUNE_LEGACY_GEMM = 4, FS2_TUNE_NT_GROUP = 5,
        FS2_TUNE_NT_HALO = 6, FS2_TUNE_WGRAD_HALO = 7, FS2_TUNE_HALO_SPLITK = 8,
        FS2_TUNE_ATTN = 9, FS2_TUNE_HALO_DB = 10, FS2_TUNE_HALO_PIPE = 11, FS2_TUNE_NT_TILE = 12,
        FS2_TUNE_LN_TILE = 13, FS2_TUNE_WGRAD_K1 = 14, FS2_TUNE_PERSIST = 15,
-       FS2_TUNE_NT_K1 = 16, FS2_TUNE_COUNT = 17 };
+       FS2_TUNE_NT_K1 = 16, FS2_TUNE_ATTN_DMA = 17,
+       FS2_TUNE_WGRAD_FUSE = 18, FS2_TUNE_COUNT = 19 };
 int fs2_set_tuning(int knob, int value);
 
 /* Weight (and optionally bias) gradient, accumulated into the fp32 master-gradient layout:

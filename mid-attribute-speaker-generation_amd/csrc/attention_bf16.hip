@@ -14,6 +14,8 @@
 // are taken as rows {32c + 4g + r} u {32c + 16 + 4g + r} on both operands.
 #include <math.h>
 
+#include <type_traits>
+
 #include "common.hpp"
 
 namespace fs2 {
@@ -755,11 +757,471 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dkdv_bf16(const u16* __restr
   }
 }
 
+// ---- LDS-DMA staged kernels (T >= 256; FS2_TUNE_ATTN_DMA = 0, default) -------------------
+// The K / V (Q / dO) tiles arrive by buffer_load ... lds into a ring of LDS slots: no register
+// round trip, no ds_write, ONE barrier per tile, and the next tile's DMA in flight under the
+// current tile's MFMAs.  Tile image: 64 rows x 256 B, 16-B chunk ch of row r stored at chunk
+// ch ^ ((r & 7) << 1).  That one image is conflict-free for both reads the kernels make of it:
+// the row-fragment reads (ds_read_b128 of the 16x16x32 operand: rows r16, chunks g + 4c) and
+// the transposed reads (ds_read_b64_tr_b16: rows 4g + q of an 8-aligned group, chunks
+// 2 ds + p / 2).  A DMA wave-instruction writes its 64 x 16 B contiguously (4 rows), so the
+// swizzle is applied on the source side: lane i of the instruction staging rows 4I .. 4I + 3
+// fetches logical chunk (i & 15) ^ swz(row) of row 4I + i / 16.
+// Softmax VALU work, which at d_head = 128 costs more issue cycles per score than the MFMAs
+// (v_exp_f32 is quarter rate): scores stay unscaled, the row maximum is taken on them (scale
+// > 0), and p = exp2(fma(s, scale log2 e, -m')) is one FMA + v_exp_f32 per score; keys are
+// masked only in the last (partial) key tile; invalid queries carry lse = +inf into the
+// backward (p = 0 with no per-score select); the O *= alpha rescale is skipped when no lane's
+// running maximum moved (alpha == 1 exactly: the skip is exact).  Results match the
+// register-staged kernels to fp32 rounding of the exponent argument (tests: within 2e-3).
+namespace {
+constexpr int IMG = 64 * DH;  // elements of one tile image
+
+FS2_DEV int swz(int r) { return (r & 7) << 1; }
+
+// per-lane LDS-DMA sources of a 64-row tile staged by NW waves (16 / NW instructions each)
+template <int NW>
+struct TileDma {
+  static constexpr int NI = 16 / NW;
+  uint32_t vo[NI];
+  int row[NI];
+  FS2_DEV void init(int64_t ld, int wave, int lane) {
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int I = wave * NI + j, r = 4 * I + (lane >> 4);
+      row[j] = r;
+      vo[j] = (uint32_t)((r * ld + (((lane & 15) ^ swz(r)) << 3)) * 2);
+    }
+  }
+  // rows t0 .. t0 + 63 of the [nrows][ld] matrix behind rs into img (rows past nrows: zeros)
+  FS2_DEV void issue(__amdgpu_buffer_rsrc_t rs, u16* img, int t0, int nrows, int64_t ld,
+                     int wave) const {
+    const int lim = nrows - t0;
+    const uint32_t so = (uint32_t)(t0 * ld * 2);
+#pragma unroll
+    for (int j = 0; j < NI; ++j) glds16_buf(rs, img + (wave * NI + j) * 512, row[j] < lim ? vo[j] : kOOB, so);
+  }
+};
+
+// per-lane read offsets into a tile image: row fragments (chunks g + 4c of row r16) and
+// transposed blocks (rows 4g + q, columns 16 ds + 4p)
+struct ImgRd {
+  int ro[4], to[8];
+  FS2_DEV void init(int g, int r16, int q, int p) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) ro[c] = r16 * DH + (((g + 4 * c) ^ swz(r16)) << 3);
+    const int r = 4 * g + q;
+#pragma unroll
+    for (int ds = 0; ds < 8; ++ds) to[ds] = r * DH + (((2 * ds + (p >> 1)) ^ swz(r)) << 3) + 4 * (p & 1);
+  }
+  // the 4 row fragments of rows row0 + r16 (row0 % 16 == 0)
+  FS2_DEV void rows(bf16x8 (&f)[4], const u16* img, int row0) const {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) f[c] = *reinterpret_cast<const bf16x8*>(img + row0 * DH + ro[c]);
+  }
+  // transposed fragment of columns 16 ds .. over rows {rb + 4g + q} u {rb + 16 + 4g + q}
+  FS2_DEV bf16x8 tr(const u16* img, int rb, int ds) const {
+    const u16* p0 = img + rb * DH + to[ds];
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0 + 16 * DH));
+    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+  }
+};
+
+FS2_DEV f32x4 chain4_img(const ImgRd& rd, const u16* img, int row0, const bf16x8 (&b)[4]) {
+  bf16x8 a[4];
+  rd.rows(a, img, row0);
+  return chain4(a, b);
+}
+
+// The ring: slot s of STAGES holds NM tile images; prologue issues tiles 0 .. STAGES-2; per tile
+// kt: counted vmcnt (tile kt landed), barrier (visible to all waves, and every wave is done with
+// tile kt-1 whose slot the refill overwrites), refill with tile kt + STAGES - 1, compute.
+// The last tile (the only one holding keys / queries past the length) runs a separate body,
+// peeled out of the loop (a branch between two inlined bodies inside it spilled registers).
+template <int STAGES, int PER, typename Issue, typename Full, typename Last>
+FS2_DEV void tile_loop(int nt, Issue&& issue, Full&& full, Last&& last) {
+  for (int t = 0; t < STAGES - 1 && t < nt; ++t) issue(t, t);
+  auto step = [&](int kt) {
+    const int ahead = nt - 1 - kt < STAGES - 2 ? nt - 1 - kt : STAGES - 2;
+    vm_wait_tiles<PER>(ahead);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (kt + STAGES - 1 < nt) issue(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
+  };
+  for (int kt = 0; kt + 1 < nt; ++kt) {
+    step(kt);
+    full(kt, kt % STAGES);
+  }
+  if (nt > 0) {
+    step(nt - 1);
+    last(nt - 1, (nt - 1) % STAGES);
+  }
+}
+}  // namespace
+
+// forward: 4 waves x 32 queries (two 16-row groups per wave), K / V tiles by LDS-DMA
+template <int STAGES>
+__global__ __launch_bounds__(256, STAGES == 2 ? 2 : 1) void attn_fwd_dma(
+    const u16* __restrict__ qkv, u16* __restrict__ o, float* __restrict__ lse,
+    const int64_t* __restrict__ lens, int T, int H, float scale) {
+  constexpr int NW = 4, NT = 256, QBLK = 128;
+  __shared__ __attribute__((aligned(1024))) u16 smem[STAGES * 2 * IMG];
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, r16 = lane & 15;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int q4 = r16 >> 2, p4 = r16 & 3;
+  const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
+  const int L = (int)min(lens[b], (int64_t)T);
+  const int64_t ld = 3LL * H * DH, ldo = (int64_t)H * DH;
+  const int q0 = blockIdx.x * QBLK;
+  const u16* base = qkv + (int64_t)b * T * ld;
+  u16* obase = o + (int64_t)b * T * ldo + h * DH;
+
+  if (q0 >= L) {
+    for (int e = tid; e < QBLK * DH / 8; e += NT) {
+      const int row = e / (DH / 8), col = (e % (DH / 8)) * 8, q = q0 + row;
+      if (q < T) *reinterpret_cast<uint4*>(obase + (int64_t)q * ldo + col) = make_uint4(0u, 0u, 0u, 0u);
+    }
+    if (tid < QBLK && q0 + tid < T) lse[(int64_t)bh * T + q0 + tid] = 0.f;
+    return;
+  }
+  const auto k_rs = buf_rsrc(base + (int64_t)H * DH + h * DH, (int64_t)T * ld * 2);
+  const auto v_rs = buf_rsrc(base + 2LL * H * DH + h * DH, (int64_t)T * ld * 2);
+  TileDma<NW> dma;
+  dma.init(ld, wave, lane);
+  ImgRd rd;
+  rd.init(g, r16, q4, p4);
+  const int nkt = (L + QB - 1) / QB;
+  auto issue = [&](int kt, int slot) {
+    u16* Ks = smem + slot * 2 * IMG;
+    dma.issue(k_rs, Ks, kt * QB, T, ld, wave);
+    dma.issue(v_rs, Ks + IMG, kt * QB, T, ld, wave);
+  };
+
+  bf16x8 qf[2][4];
+#pragma unroll
+  for (int gq = 0; gq < 2; ++gq) {
+    const int q = q0 + wave * 32 + gq * 16 + r16;
+    load_frag(qf[gq], base + (int64_t)min(q, T - 1) * ld + h * DH, g);
+  }
+  float m_run[2] = {-INFINITY, -INFINITY}, l_run[2] = {0.f, 0.f};
+  f32x4 oacc[2][8];
+#pragma unroll
+  for (int gq = 0; gq < 2; ++gq)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) oacc[gq][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const float c2 = scale * 1.4426950408889634f;  // scores -> log2 units
+  auto body = [&](auto mask_c, int kt, int slot) {
+    constexpr bool MASK = decltype(mask_c)::value;
+    const u16* Ks = smem + slot * 2 * IMG;
+    const u16* Vs = Ks + IMG;
+    f32x4 s[2][4];
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+      bf16x8 kfr[4];
+      rd.rows(kfr, Ks, 16 * st);
+#pragma unroll
+      for (int gq = 0; gq < 2; ++gq) s[gq][st] = chain4(kfr, qf[gq]);
+    }
+    float alpha[2];
+#pragma unroll
+    for (int gq = 0; gq < 2; ++gq) {
+      float mt = -INFINITY;
+#pragma unroll
+      for (int st = 0; st < 4; ++st)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          if (MASK && kt * QB + 16 * st + 4 * g + r >= L) s[gq][st][r] = -INFINITY;
+          mt = fmaxf(mt, s[gq][st][r]);
+        }
+      mt = group4_max(mt);
+      const float m_new = fmaxf(m_run[gq], mt * c2);
+      alpha[gq] = __builtin_amdgcn_exp2f(m_run[gq] - m_new);
+      float ps = 0.f;
+#pragma unroll
+      for (int st = 0; st < 4; ++st)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float pv = __builtin_amdgcn_exp2f(fmaf(s[gq][st][r], c2, -m_new));
+          s[gq][st][r] = pv;
+          ps += pv;
+        }
+      ps = group4_sum(ps);
+      l_run[gq] = l_run[gq] * alpha[gq] + ps;
+      m_run[gq] = m_new;
+    }
+    // O *= alpha unless no lane's maximum moved (then alpha == 1 everywhere: exact skip); on
+    // the first tile O is zero
+    if (kt > 0 && __ballot(alpha[0] != 1.f || alpha[1] != 1.f)) {
+#pragma unroll
+      for (int gq = 0; gq < 2; ++gq)
+#pragma unroll
+        for (int ds = 0; ds < 8; ++ds) oacc[gq][ds] *= alpha[gq];
+    }
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const bf16x8 w0 = pack8(s[0][2 * c], s[0][2 * c + 1]), w1 = pack8(s[1][2 * c], s[1][2 * c + 1]);
+#pragma unroll
+      for (int ds = 0; ds < 8; ++ds) {
+        const bf16x8 a = rd.tr(Vs, 32 * c, ds);
+        oacc[0][ds] = MFMA_BF16(a, w0, oacc[0][ds]);
+        oacc[1][ds] = MFMA_BF16(a, w1, oacc[1][ds]);
+      }
+    }
+  };
+  tile_loop<STAGES, 2 * TileDma<NW>::NI>(nkt, issue, [&](int kt, int slot) { body(std::false_type{}, kt, slot); },
+      [&](int kt, int slot) { body(std::true_type{}, kt, slot); });
+#pragma unroll
+  for (int gq = 0; gq < 2; ++gq) {
+    const int q = q0 + wave * 32 + gq * 16 + r16;
+    if (q < T) {
+      const float inv = 1.f / l_run[gq];
+#pragma unroll
+      for (int ds = 0; ds < 8; ++ds)
+        store4_bf16(obase + (int64_t)q * ldo + 16 * ds + 4 * g, oacc[gq][ds] * inv);
+      if (g == 0) lse[(int64_t)bh * T + q] = (m_run[gq] + __log2f(l_run[gq])) * 0.6931471805599453f;
+    }
+  }
+}
+
+// dQ (+ delta), 4 waves x 32 queries, K / V tiles by LDS-DMA
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq_dma(
+    const u16* __restrict__ qkv, const u16* __restrict__ o, const u16* __restrict__ d_o,
+    const float* __restrict__ lse, float* __restrict__ delta, u16* __restrict__ d_qkv,
+    const int64_t* __restrict__ lens, int T, int H, float scale) {
+  constexpr int NW = 4, NT = 256, QBLK = 128, STAGES = 2;
+  __shared__ __attribute__((aligned(1024))) u16 smem[STAGES * 2 * IMG];
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, r16 = lane & 15;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int q4 = r16 >> 2, p4 = r16 & 3;
+  const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
+  const int L = (int)min(lens[b], (int64_t)T);
+  const int64_t ld = 3LL * H * DH, ldo = (int64_t)H * DH;
+  const int q0 = blockIdx.x * QBLK;
+  const u16* base = qkv + (int64_t)b * T * ld;
+  u16* dbase = d_qkv + (int64_t)b * T * ld + h * DH;
+
+  if (q0 >= L) {
+    for (int e = tid; e < QBLK * DH / 8; e += NT) {
+      const int row = e / (DH / 8), col = (e % (DH / 8)) * 8, qq = q0 + row;
+      if (qq < T) *reinterpret_cast<uint4*>(dbase + (int64_t)qq * ld + col) = make_uint4(0u, 0u, 0u, 0u);
+    }
+    if (tid < QBLK && q0 + tid < T) delta[(int64_t)bh * T + q0 + tid] = 0.f;
+    return;
+  }
+  const auto k_rs = buf_rsrc(base + (int64_t)H * DH + h * DH, (int64_t)T * ld * 2);
+  const auto v_rs = buf_rsrc(base + 2LL * H * DH + h * DH, (int64_t)T * ld * 2);
+  TileDma<NW> dma;
+  dma.init(ld, wave, lane);
+  ImgRd rd;
+  rd.init(g, r16, q4, p4);
+  const int nkt = (L + QB - 1) / QB;
+  auto issue = [&](int kt, int slot) {
+    u16* Ks = smem + slot * 2 * IMG;
+    dma.issue(k_rs, Ks, kt * QB, T, ld, wave);
+    dma.issue(v_rs, Ks + IMG, kt * QB, T, ld, wave);
+  };
+  issue(0, 0);  // the first tile's DMA flies under the delta computation
+
+  bf16x8 qf[2][4], df[2][4];
+  float my_lse[2], my_delta[2];
+  bool qvalid[2];
+#pragma unroll
+  for (int gq = 0; gq < 2; ++gq) {
+    const int q = q0 + wave * 32 + gq * 16 + r16;
+    const int qc = min(q, T - 1);
+    load_frag(qf[gq], base + (int64_t)qc * ld + h * DH, g);
+    load_frag(df[gq], d_o + ((int64_t)b * T + qc) * ldo + h * DH, g);
+    bf16x8 of[4];
+    load_frag(of, o + ((int64_t)b * T + qc) * ldo + h * DH, g);
+    float part = 0.f;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) part += (float)of[c][e] * (float)df[gq][c][e];
+    qvalid[gq] = q < L;
+    my_delta[gq] = qvalid[gq] ? group4_sum(part) : 0.f;
+    // lse in log2 units; an invalid query's +inf makes every p of its column 0
+    my_lse[gq] = qvalid[gq] ? lse[(int64_t)bh * T + qc] * 1.4426950408889634f : INFINITY;
+    if (g == 0 && q < T) delta[(int64_t)bh * T + q] = my_delta[gq];
+  }
+  const float c2 = scale * 1.4426950408889634f;
+
+  f32x4 dq[2][8];
+#pragma unroll
+  for (int gq = 0; gq < 2; ++gq)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dq[gq][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto body = [&](auto mask_c, int kt, int slot) {
+    constexpr bool MASK = decltype(mask_c)::value;
+    const u16* Ks = smem + slot * 2 * IMG;
+    const u16* Vs = Ks + IMG;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      f32x4 dsv[2][2];
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        const int st = 2 * c + half;
+        bf16x8 kfr[4], vfr[4];
+        rd.rows(kfr, Ks, 16 * st);
+        rd.rows(vfr, Vs, 16 * st);
+#pragma unroll
+        for (int gq = 0; gq < 2; ++gq) {
+          const f32x4 s = chain4(kfr, qf[gq]);
+          const f32x4 dp = chain4(vfr, df[gq]);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float pv = __builtin_amdgcn_exp2f(fmaf(s[r], c2, -my_lse[gq]));
+            if (MASK && kt * QB + 16 * st + 4 * g + r >= L) pv = 0.f;
+            dsv[gq][half][r] = pv * (dp[r] - my_delta[gq]);
+          }
+        }
+      }
+      const bf16x8 w0 = pack8(dsv[0][0], dsv[0][1]), w1 = pack8(dsv[1][0], dsv[1][1]);
+#pragma unroll
+      for (int ds = 0; ds < 8; ++ds) {
+        const bf16x8 a = rd.tr(Ks, 32 * c, ds);
+        dq[0][ds] = MFMA_BF16(a, w0, dq[0][ds]);
+        dq[1][ds] = MFMA_BF16(a, w1, dq[1][ds]);
+      }
+    }
+  };
+  // tile 0 is already in flight: the ring starts at tile 1
+  tile_loop<STAGES, 2 * TileDma<NW>::NI>(nkt, [&](int kt, int slot) { if (kt > 0) issue(kt, slot); },
+                                        [&](int kt, int slot) { body(std::false_type{}, kt, slot); },
+      [&](int kt, int slot) { body(std::true_type{}, kt, slot); });
+#pragma unroll
+  for (int gq = 0; gq < 2; ++gq) {
+    const int q = q0 + wave * 32 + gq * 16 + r16;
+    if (q < T) {
+#pragma unroll
+      for (int ds = 0; ds < 8; ++ds)
+        store4_bf16(dbase + (int64_t)q * ld + 16 * ds + 4 * g, dq[gq][ds] * scale);
+    }
+  }
+}
+
+// dK / dV: 4 waves x 16 keys, Q / dO tiles (+ the tile's lse / delta) by LDS-DMA
+__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_dma(
+    const u16* __restrict__ qkv, const u16* __restrict__ d_o, const float* __restrict__ lse,
+    const float* __restrict__ delta, u16* __restrict__ d_qkv, const int64_t* __restrict__ lens,
+    int T, int H, float scale) {
+  constexpr int NW = 4, STAGES = 2;
+  constexpr int SLOT_E = 2 * IMG + 2 * QB * 2;  // Q image, dO image, lse[64], delta[64] (fp32)
+  __shared__ __attribute__((aligned(1024))) u16 smem[STAGES * SLOT_E];
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, r16 = lane & 15;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int q4 = r16 >> 2, p4 = r16 & 3;
+  const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
+  const int L = (int)min(lens[b], (int64_t)T);
+  const int64_t ld = 3LL * H * DH, ldo = (int64_t)H * DH;
+  const int k0 = blockIdx.x * QB;
+  const u16* base = qkv + (int64_t)b * T * ld;
+  u16* dk_base = d_qkv + (int64_t)b * T * ld + (int64_t)H * DH + h * DH;
+  u16* dv_base = d_qkv + (int64_t)b * T * ld + 2LL * H * DH + h * DH;
+
+  if (k0 >= L) {
+    for (int e = tid; e < QB * DH / 8; e += 256) {
+      const int row = e / (DH / 8), col = (e % (DH / 8)) * 8, k = k0 + row;
+      if (k < T) {
+        *reinterpret_cast<uint4*>(dk_base + (int64_t)k * ld + col) = make_uint4(0u, 0u, 0u, 0u);
+        *reinterpret_cast<uint4*>(dv_base + (int64_t)k * ld + col) = make_uint4(0u, 0u, 0u, 0u);
+      }
+    }
+    return;
+  }
+  const auto q_rs = buf_rsrc(base + h * DH, (int64_t)T * ld * 2);
+  const auto d_rs = buf_rsrc(d_o + (int64_t)b * T * ldo + h * DH, (int64_t)T * ldo * 2);
+  const auto l_rs = buf_rsrc(lse + (int64_t)bh * T, (int64_t)T * 4);
+  const auto e_rs = buf_rsrc(delta + (int64_t)bh * T, (int64_t)T * 4);
+  TileDma<NW> dq_dma, do_dma;
+  dq_dma.init(ld, wave, lane);
+  do_dma.init(ldo, wave, lane);
+  ImgRd rd;
+  rd.init(g, r16, q4, p4);
+  const int nqt = (L + QB - 1) / QB;
+  auto issue = [&](int qt, int slot) {
+    u16* Qs = smem + slot * SLOT_E;
+    dq_dma.issue(q_rs, Qs, qt * QB, T, ld, wave);
+    do_dma.issue(d_rs, Qs + IMG, qt * QB, T, ldo, wave);
+    // wave 0: the tile's lse, wave 1: its delta (queries past T read as 0)
+    if (wave < 2)
+      glds4_buf(wave == 0 ? l_rs : e_rs, Qs + 2 * IMG + wave * 2 * QB,
+                lane < T - qt * QB ? (uint32_t)(lane * 4) : kOOB, (uint32_t)(qt * QB * 4));
+  };
+
+  const int key = k0 + wave * 16 + r16;
+  const int kc = min(key, T - 1);
+  bf16x8 kf[4], vf[4];
+  load_frag(kf, base + (int64_t)kc * ld + (int64_t)H * DH + h * DH, g);
+  load_frag(vf, base + (int64_t)kc * ld + 2LL * H * DH + h * DH, g);
+  const bool kvalid = key < L;
+
+  f32x4 dk[8], dv[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) dk[i] = dv[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const float c2 = scale * 1.4426950408889634f;
+  auto body = [&](auto mask_c, int qt, int slot) {
+    constexpr bool MASK = decltype(mask_c)::value;
+    const u16* Qs = smem + slot * SLOT_E;
+    const u16* Ds = Qs + IMG;
+    const float* lse_s = reinterpret_cast<const float*>(Qs + 2 * IMG);
+    const float* del_s = lse_s + QB;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      f32x4 pp[2], dsv[2];
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        const int qs = 2 * c + half;
+        const f32x4 s = chain4_img(rd, Qs, 16 * qs, kf);
+        const f32x4 dp = chain4_img(rd, Ds, 16 * qs, vf);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int ql = 16 * qs + 4 * g + r;
+          float pv = __builtin_amdgcn_exp2f(fmaf(s[r], c2, -lse_s[ql] * 1.4426950408889634f));
+          if (MASK && qt * QB + ql >= L) pv = 0.f;
+          pp[half][r] = pv;
+          dsv[half][r] = pv * (dp[r] - del_s[ql]);
+        }
+      }
+      const bf16x8 wp = pack8(pp[0], pp[1]), wd = pack8(dsv[0], dsv[1]);
+#pragma unroll
+      for (int ds = 0; ds < 8; ++ds) dv[ds] = MFMA_BF16(rd.tr(Ds, 32 * c, ds), wp, dv[ds]);
+#pragma unroll
+      for (int ds = 0; ds < 8; ++ds) dk[ds] = MFMA_BF16(rd.tr(Qs, 32 * c, ds), wd, dk[ds]);
+    }
+  };
+  // with 2 slots every wait drains the wave's DMA (vmcnt(0)): the per-wave count may differ
+  tile_loop<STAGES, 1>(nqt, issue, [&](int qt, int slot) { body(std::false_type{}, qt, slot); },
+      [&](int qt, int slot) { body(std::true_type{}, qt, slot); });
+  if (!kvalid) {  // padded keys: zero gradients (their p were not masked per score)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dk[i] = dv[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  if (key < T) {
+#pragma unroll
+    for (int ds = 0; ds < 8; ++ds) {
+      store4_bf16(dk_base + (int64_t)key * ld + 16 * ds + 4 * g, dk[ds] * scale);
+      store4_bf16(dv_base + (int64_t)key * ld + 16 * ds + 4 * g, dv[ds]);
+    }
+  }
+}
+
 // NW waves per workgroup (32 NW query / key rows): 4 from T = 256 on, 2 below (the encoder's
 // T = 128 keeps two workgroups per (utterance, head))
 int attn_fwd_bf16_launch(const void* qkv, void* o, float* lse, const int64_t* lens, int64_t batch,
                          int64_t seq_len, int heads, float scale, hipStream_t st) {
-  if (seq_len >= 256 && g_tune[FS2_TUNE_ATTN] >= 0) {
+  const int dma = g_tune[FS2_TUNE_ATTN_DMA];
+  if (seq_len >= 256 && g_tune[FS2_TUNE_ATTN] >= 0 && dma >= 0) {
+    dim3 grid((unsigned)((seq_len + 127) / 128), (unsigned)(batch * heads));
+    if (dma == 1)
+      attn_fwd_dma<3><<<grid, 256, 0, st>>>((const u16*)qkv, (u16*)o, lse, lens, (int)seq_len, heads, scale);
+    else
+      attn_fwd_dma<2><<<grid, 256, 0, st>>>((const u16*)qkv, (u16*)o, lse, lens, (int)seq_len, heads, scale);
+  } else if (seq_len >= 256 && g_tune[FS2_TUNE_ATTN] >= 0) {
     dim3 grid((unsigned)((seq_len + 127) / 128), (unsigned)(batch * heads));
     attn_fwd_bf16<4><<<grid, 256, 0, st>>>((const u16*)qkv, (u16*)o, lse, lens, (int)seq_len, heads, scale);
   } else {
@@ -775,7 +1237,11 @@ int attn_bwd_bf16_launch(const void* qkv, const void* o, const void* d_o, const 
   const int tune = g_tune[FS2_TUNE_ATTN];
   dim3 grid1((unsigned)((seq_len + QB - 1) / QB), (unsigned)(batch * heads));
   dim3 grid2((unsigned)((seq_len + 127) / 128), (unsigned)(batch * heads));
-  if (seq_len >= 256 && tune >= 0) {  // dQ with delta fused
+  const bool dma = seq_len >= 256 && g_tune[FS2_TUNE_ATTN_DMA] >= 0 && (tune == 0 || tune == 1);
+  if (dma) {  // dQ with delta fused, LDS-DMA staged
+    attn_bwd_dq_dma<<<grid2, 256, 0, st>>>((const u16*)qkv, (const u16*)o, (const u16*)d_o, lse, ws,
+                                           (u16*)d_qkv, lens, (int)seq_len, heads, scale);
+  } else if (seq_len >= 256 && tune >= 0) {  // dQ with delta fused
     attn_bwd_dq_bf16<4><<<grid2, 256, 0, st>>>((const u16*)qkv, (const u16*)o, (const u16*)d_o, lse, ws,
                                                (u16*)d_qkv, lens, (int)seq_len, heads, scale);
   } else {
@@ -788,7 +1254,10 @@ int attn_bwd_bf16_launch(const void* qkv, const void* o, const void* d_o, const 
   // dK/dV: one 16-key group per wave at two workgroups per CU (221 VGPRs) by default --
   // decoder backward 99 -> 87 us against the two-group kernel, whose 415 registers allow one
   // workgroup per CU (384 workgroups = 1.5 rounds of the CUs)
-  if (seq_len >= 256 && tune == 2)
+  if (dma && tune == 0)
+    attn_bwd_dkdv_dma<<<grid1, 256, 0, st>>>((const u16*)qkv, (const u16*)d_o, lse, ws, (u16*)d_qkv,
+                                             lens, (int)seq_len, heads, scale);
+  else if (seq_len >= 256 && tune == 2)
     attn_bwd_dkdv_bf16<4><<<grid2, 256, 0, st>>>((const u16*)qkv, (const u16*)d_o, lse, ws, (u16*)d_qkv,
                                                  lens, (int)seq_len, heads, scale);
   else if (tune == 3)

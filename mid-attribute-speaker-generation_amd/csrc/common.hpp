@@ -1,7 +1,7 @@
 // Shared device helpers for the gfx950 kernels of libfs2hip.so.
 //
-// Wave64 everywhere: lane = threadIdx.x & 63; cross-lane reductions use __shfl_xor over
-// 64 lanes.  Dropout masks come from a counter-based Philox4x32-10 stream keyed by
+// Wave64 everywhere: lane = threadIdx.x & 63; cross-lane reductions use permlane swaps for
+// the 16- / 32-lane exchanges and __shfl_xor below.  Dropout masks come from a counter-based Philox4x32-10 stream keyed by
 // (seed, site offset, element index), so backward recomputes the forward mask instead of
 // storing it.
 #pragma once
@@ -85,7 +85,7 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
 int conv_wgrad_glds_launch(const void* dy, int64_t ldy, const void* x, int64_t ldx, float* dw,
                            float* db, int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out,
                            int taps, int pad, const int64_t* lens, int splits, int tile, float* ws,
-                           hipStream_t st);
+                           unsigned* ctr, hipStream_t st);
 int conv_wgrad_bf16_launch(const void* dy, int64_t ldy, const void* x, int64_t ldx, float* slab,
                            int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out, int taps,
                            int pad, int splits, hipStream_t st);
@@ -100,26 +100,73 @@ int colsum_bf16_launch(const void* x, int64_t ldx, int64_t rows, int64_t cols, f
                        float* ws, hipStream_t st);
 
 // ------------------------------------------------------------------ wave reductions
+// Exchanges across 16- and 32-lane distances go through v_permlane16_swap / v_permlane32_swap
+// (VALU, no LDS round trip as ds_bpermute): with both operands = v the pair {r[0], r[1]} holds
+// this lane's value and its partner's (lane ^ 16, lane ^ 32), so the sums / maxima are the
+// __shfl_xor ones bitwise (a + b == b + a).
+FS2_DEV float x16_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+FS2_DEV float x32_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+FS2_DEV float x16_max(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+FS2_DEV float x32_max(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
 FS2_DEV float wave_sum(float v) {
+  v = x32_sum(v);
+  v = x16_sum(v);
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
 FS2_DEV float wave_max(float v) {
+  v = x32_max(v);
+  v = x16_max(v);
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  for (int o = 8; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
   return v;
 }
 // reduce across the 4 lane-groups of 16 (lanes l, l^16, l^32, l^48)
-FS2_DEV float group4_sum(float v) {
-  v += __shfl_xor(v, 16, 64);
-  v += __shfl_xor(v, 32, 64);
-  return v;
+FS2_DEV float group4_sum(float v) { return x32_sum(x16_sum(v)); }
+FS2_DEV float group4_max(float v) { return x32_max(x16_max(v)); }
+
+// ------------------------------------------------------------------ LDS-DMA through buffers
+// buffer_load_dwordx4 ... lds: the wave's 64 x 16 B land contiguously at lds_wave_base; the
+// per-lane byte offset rides in voffset, the wave-uniform rest in soffset; offsets past the
+// descriptor's record count read as zeros.
+FS2_DEV void glds16_buf(__amdgpu_buffer_rsrc_t r, void* lds_wave_base, uint32_t voff, uint32_t soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(
+      r, (__attribute__((address_space(3))) void*)lds_wave_base, 16, voff, soff, 0, 0);
 }
-FS2_DEV float group4_max(float v) {
-  v = fmaxf(v, __shfl_xor(v, 16, 64));
-  v = fmaxf(v, __shfl_xor(v, 32, 64));
-  return v;
+// the dword form: lane i's 4 B land at lds_wave_base + 4 i
+FS2_DEV void glds4_buf(__amdgpu_buffer_rsrc_t r, void* lds_wave_base, uint32_t voff, uint32_t soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(
+      r, (__attribute__((address_space(3))) void*)lds_wave_base, 4, voff, soff, 0, 0);
+}
+// a block-uniform buffer descriptor over [p, p + bytes)
+FS2_DEV __amdgpu_buffer_rsrc_t buf_rsrc(const void* p, int64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0,
+                                           (int)(bytes < 0x7fffffff ? bytes : 0x7fffffff), 0x00020000);
+}
+constexpr uint32_t kOOB = 0x80000000u;  // a voffset past every record count: reads zeros
+
+// Wait until at most `ahead` tiles of PER LDS-DMA instructions each are still in flight.
+template <int PER>
+FS2_DEV void vm_wait_tiles(int ahead) {
+  switch (ahead) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER) : "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * PER) : "memory"); break;
+  }
 }
 
 // ------------------------------------------------------------------ Philox4x32-10
@@ -212,8 +259,9 @@ FS2_DEV void st8_bf16(void* p, f32x4 a, f32x4 b) {
 }
 // sum over the 32 lanes of a half-wave (every lane gets the half's sum)
 FS2_DEV float half_sum(float v) {
+  v = x16_sum(v);
 #pragma unroll
-  for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
 

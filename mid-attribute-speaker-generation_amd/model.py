@@ -111,6 +111,11 @@ def sinusoid_table(n_position, d_hid):
 # ----------------------------------------------------------------------------- runtime state
 
 
+# FS2_SERIAL_WGRAD_TAPS="9" (A/B): weight gradients of these kernel widths run on the main
+# stream, serially after the data gradient, instead of concurrently on the side stream
+_SERIAL_TAPS = frozenset(int(t) for t in os.environ.get("FS2_SERIAL_WGRAD_TAPS", "").split(",") if t)
+
+
 class StepCtx:
     """Per-forward state: compute dtype of the GEMM operands, one Philox seed per step (one
     site id per dropout call, assigned at construction)."""
@@ -132,7 +137,7 @@ class StepCtx:
         """Weight (+bias) gradient GEMM.  Nothing in the backward waits for it, so with a
         side stream it runs concurrently with the data-gradient chain on the main stream
         (the small GEMMs of a block fill the GPU together); ``join`` orders it back."""
-        if self.side is None:
+        if self.side is None or taps in _SERIAL_TAPS:
             return K.conv_wgrad(dy, x, dw, rows, seq_len, c_in, c_out, taps, pad, db=db,
                                 lens=lens)
         # one workspace for every side-stream weight gradient (they run in stream order);

@@ -11,6 +11,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 PKG = importlib.import_module("mid-attribute-speaker-generation_amd")
 K = importlib.import_module("mid-attribute-speaker-generation_amd.kernels")
 dev = "cuda:0"
+for kv in filter(None, os.environ.get("FS2_TUNE", "").split(",")):  # knob=value A/B
+    K.lib.fs2_set_tuning(int(kv.split("=")[0]), int(kv.split("=")[1]))
 b = PKG.data.syn_batch(48, 128, seed=0)
 
 

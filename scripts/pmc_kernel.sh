@@ -31,7 +31,7 @@ for kn, d in acc.items():
         print(f"   -> wait_any {sum(d['SQ_WAIT_ANY'])/len(d['SQ_WAIT_ANY'])/W:.2f}, wait_inst {sum(d['SQ_WAIT_INST_ANY'])/len(d['SQ_WAIT_INST_ANY'])/W:.2f}, active {sum(d['SQ_ACTIVE_INST_ANY'])/len(d['SQ_ACTIVE_INST_ANY'])/W:.2f} of wave cycles")
     if g and d.get("SQ_VALU_MFMA_BUSY_CYCLES"):
         G = sum(g) / len(g)
-        print(f"   -> MFMA busy {sum(d['SQ_VALU_MFMA_BUSY_CYCLES'])/len(d['SQ_VALU_MFMA_BUSY_CYCLES'])/(1024*G/8):.3f} (of 1024 SIMDs x GRBM/8), kernel {G/2.4e3:.1f} us at 2.4 GHz")
+        print(f"   -> MFMA busy {sum(d['SQ_VALU_MFMA_BUSY_CYCLES'])/len(d['SQ_VALU_MFMA_BUSY_CYCLES'])/(1024*G/8):.3f} (of 1024 SIMDs x GRBM/8), kernel {G/8/2.4e3:.1f} us at 2.4 GHz (GRBM summed over 8 XCDs)")
     if d.get("FETCH_SIZE") and d.get("WRITE_SIZE"):
         print(f"   -> HBM-side bytes: fetch x2 {2*sum(d['FETCH_SIZE'])/len(d['FETCH_SIZE'])/1024:.1f} MB, write {sum(d['WRITE_SIZE'])/len(d['WRITE_SIZE'])/1024:.1f} MB")
 PY

@@ -392,6 +392,40 @@ def _attention_bf16(B, T, lens):
     close(dqkv.float(), qr.grad, 3e-2)
 
 
+@pytest.mark.parametrize("B,T,lens", [(3, 512, [512, 300, 1]), (3, 300, [300, 129, 64]),
+                                      (2, 256, [256, 200])])
+def test_attention_dma_vs_register_staged(B, T, lens):
+    """The LDS-DMA staged attention kernels (FS2_TUNE_ATTN_DMA = 0 / 1: 2- / 3-slot forward
+    ring; exp2 with the scale folded into one FMA, last-tile-only key masks, exact rescale skip)
+    against the register-staged ones (-1) on the same inputs: outputs within one bf16 rounding,
+    lse within fp32 rounding of the exponent argument, gradients within 2e-3 of their scale,
+    padded gradient rows exactly zero in both (T = 300: a partial last tile, rows past T staged
+    as zeros by the descriptor range)."""
+    H, dh = 2, 128
+    lens_t = torch.tensor(lens, device=DEV)
+    qkv = bf(rnd(B * T, 3 * H * dh, seed=11))
+    valid = (torch.arange(T, device=DEV)[None, :] < lens_t[:, None]).reshape(-1)
+    do = bf(rnd(B * T, H * dh, seed=12) * valid[:, None])
+    res = {}
+    try:
+        for knob in (-1, 0, 1):
+            K.lib.fs2_set_tuning(17, knob)
+            o, lse = K.attn_fwd(qkv, lens_t, B, T, H, dh, 1 / math.sqrt(dh))
+            dqkv = K.attn_bwd(qkv, o, do, lse, lens_t, B, T, H, dh, 1 / math.sqrt(dh))
+            res[knob] = (o, lse, dqkv)
+    finally:
+        K.lib.fs2_set_tuning(17, 0)
+    pad = ~valid
+    for knob in (0, 1):
+        o, lse, dqkv = res[knob]
+        o0, lse0, dqkv0 = res[-1]
+        close(o.float(), o0.float(), 8e-3)
+        close(lse, lse0, 1e-5)
+        close(dqkv.float(), dqkv0.float(), 2e-3)
+        # padded rows of d_qkv are exact zeros (dQ of padded queries, dK / dV of padded keys)
+        assert not dqkv[pad].any() and not dqkv0[pad].any(), knob
+
+
 def test_norm_copies_bf16():
     M, d = 300, 256
     y, r = rnd(M, d, seed=1), rnd(M, d, seed=2)
@@ -466,8 +500,9 @@ def test_gemm_persistent(B, T, cin, cout, kind):
                                           (48, 128, 256, 256), (3, 200, 256, 80), (5, 77, 72, 24),
                                           (1, 1000, 1024, 256)])
 def test_wgrad_k1(B, T, cin, cout):
-    """The k = 1 weight gradient (wgrad_k1_glds: 64 x 64 tiles, 128-row k-tiles over the block's
-    4 waves, split-K slabs + wgrad_reduce_k1) with its fused bias gradient, accumulating into
+    """The k = 1 weight gradient (wgrad_k1_q: 64 x 64 tiles, 128-row k-tiles over the block's
+    4 waves; wgrad_k1_glds with FS2_TUNE_WGRAD_K1 = 1: 128 x 128 tiles of 8 waves; split-K
+    slabs + wgrad_reduce_k1) with its fused bias gradient, accumulating into
     existing gradients, against fp32 math on the same bf16 data -- with and without utterance
     lengths (all-padding k-tiles skipped; dy is zero on padded rows as in the step), at forced
     split counts, and against the tap-major kernel (FS2_TUNE_WGRAD_K1 = -1)."""
@@ -479,10 +514,14 @@ def test_wgrad_k1(B, T, cin, cout):
     ref_w = dy.float().t() @ x.float()
     ref_b = dy.float().sum(0)
     try:
-        for knob, splits, use_lens in ((0, 0, False), (0, 0, True), (0, 1, True), (0, 7, False),
-                                       (0, 64, True), (-1, 0, True)):
+        for knob, splits, use_lens, fuse in (
+                (0, 0, False, 0), (0, 0, True, 0), (0, 1, True, 0), (0, 7, False, 0),
+                (0, 64, True, 0), (0, 0, False, 1), (0, 0, True, 1), (0, 1, True, 1),
+                (0, 7, True, 1), (1, 0, False, 0), (1, 0, True, 0), (1, 7, True, 0),
+                (-1, 0, True, 0)):
             K.lib.fs2_set_tuning(14, knob)
             K.lib.fs2_set_tuning(3, splits)  # FS2_TUNE_WGRAD_SPLITS
+            K.lib.fs2_set_tuning(18, fuse)  # FS2_TUNE_WGRAD_FUSE: in-kernel split reduce
             dw, db = torch.ones(cout, cin, device=DEV), torch.ones(cout, device=DEV)
             K.conv_wgrad(dy, x, dw, B * T, T, cin, cout, 1, 0, db=db,
                          lens=lens if use_lens else None)
@@ -491,6 +530,7 @@ def test_wgrad_k1(B, T, cin, cout):
     finally:
         K.lib.fs2_set_tuning(14, 0)
         K.lib.fs2_set_tuning(3, 0)
+        K.lib.fs2_set_tuning(18, 0)
 
 
 @pytest.mark.parametrize("stages", [1, 2, 3, 4])

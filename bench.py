@@ -375,7 +375,7 @@ def probe_alg_bytes(syn):
 
 
 def hbm_traffic(timeout=300):
-    """Per-launch memory-side bytes of the probe's halo-conv launches from rocprofv3 PMC
+    """Per-launch memory-side bytes of the probe's k=9 conv launches from rocprofv3 PMC
     counters: FETCH_SIZE and WRITE_SIZE (KiB) in separate passes (they do not fit one TCC
     pass), FETCH_SIZE doubled (gfx950 reports half the bytes of 16-B-per-lane streaming
     reads; MI355X_MICROARCH.md, HBM).  These count L2 misses, Infinity-Cache hits included."""
@@ -402,10 +402,11 @@ def hbm_traffic(timeout=300):
                 return None, f"{ctr} pass failed (rc {r.returncode})"
             vals = []
             for row in csv.DictReader(open(files[0])):
-                if "conv_gemm_halo" in row.get("Kernel_Name", "") and row.get("Counter_Name") == ctr:
+                kn = row.get("Kernel_Name", "")
+                if ("conv_gemm_halo" in kn or "conv_gemm_tapreg" in kn) and row.get("Counter_Name") == ctr:
                     vals.append(float(row["Counter_Value"]))
             if not vals:
-                return None, f"{ctr}: no conv_gemm_halo dispatches"
+                return None, f"{ctr}: no conv_gemm_halo / conv_gemm_tapreg dispatches"
             per[ctr] = float(np.mean(vals))
     return (per["FETCH_SIZE"] * 2.0 + per["WRITE_SIZE"]) * 1024.0, per
 

@@ -285,6 +285,10 @@ int fs2_weight_prep_batch(int dtype, const int64_t* jobs, int n_jobs, int64_t n_
  *   FS2_TUNE_WGRAD_FUSE    k = 1 weight gradient (FS2_TUNE_WGRAD_K1 = 0): 0 = split slabs summed
  *                          by a reduce launch (default), 1 = the last split to finish a tile sums
  *                          them in split order inside the kernel (no reduce launch)
+ *   FS2_TUNE_TAPREG        fwd/dX Conv1d taps 5 / 9 (C_in % 64 == 0): 0 = the tap-register halo
+ *                          kernel where its grid fills the chip (default), -1 = off (the halo
+ *                          kernels above), 1 = force its 4-wave 128 x 64 tiles, 2 = force its
+ *                          8-wave 256 x 128 tiles (when T allows)
  * Process-wide; query workspace sizes after setting.                                 */
 enum { FS2_TUNE_GEMM_STAGES = 0, FS2_TUNE_WGRAD_STAGES = 1, FS2_TUNE_WGRAD_TILE = 2,
        FS2_TUNE_WGRAD_SPLITS = 3, FS2_TUNE_LEGACY_GEMM = 4, FS2_TUNE_NT_GROUP = 5,
@@ -292,7 +296,7 @@ enum { FS2_TUNE_GEMM_STAGES = 0, FS2_TUNE_WGRAD_STAGES = 1, FS2_TUNE_WGRAD_TILE 
        FS2_TUNE_ATTN = 9, FS2_TUNE_HALO_DB = 10, FS2_TUNE_HALO_PIPE = 11, FS2_TUNE_NT_TILE = 12,
        FS2_TUNE_LN_TILE = 13, FS2_TUNE_WGRAD_K1 = 14, FS2_TUNE_PERSIST = 15,
        FS2_TUNE_NT_K1 = 16, FS2_TUNE_ATTN_DMA = 17,
-       FS2_TUNE_WGRAD_FUSE = 18, FS2_TUNE_COUNT = 19 };
+       FS2_TUNE_WGRAD_FUSE = 18, FS2_TUNE_TAPREG = 19, FS2_TUNE_COUNT = 20 };
 int fs2_set_tuning(int knob, int value);
 
 /* Weight (and optionally bias) gradient, accumulated into the fp32 master-gradient layout:

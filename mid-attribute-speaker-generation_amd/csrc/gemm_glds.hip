@@ -359,14 +359,20 @@ FS2_DEV void nt_epilogue_lnbwd(const GldsArgs& a, f32x4 (&acc)[BM / 32][256 / WN
   }
 }
 
-// Epilogue through LDS, one half (wm) at a time: bias, aux add, ReLU / ReLU-mask, bf16 cast
-// on 8-element row vectors (16-B / 32-B coalesced stores).  Shared by both NT kernels.
-template <int BM, int BN, bool VOC, int NWAVE = 4, int WN = 2>
-FS2_DEV void nt_epilogue(const GldsArgs& a, f32x4 (&acc)[BM / 32][BN / WN / 16], u16* smem,
+// Epilogue through LDS, one half of the tile's rows at a time: bias, aux add, ReLU / ReLU-mask,
+// bf16 cast on 8-element row vectors (16-B / 32-B coalesced stores).  Shared by the NT kernels.
+// WM waves per column of the tile (each BM / WM rows, MI = BM / WM / 16 fragments; WM / 2 per
+// half).  SROW > 0 (conv_gemm_tapreg): fragment i of a wave holds the rows i + SROW * m
+// (m = 0..15) of its band; the fragments are staged as usual and the store pass maps each
+// output row back to its (fragment, m) slot.
+template <int BM, int BN, bool VOC, int NWAVE = 4, int WN = 2, int WM = 2, int SROW = 0>
+FS2_DEV void nt_epilogue(const GldsArgs& a, f32x4 (&acc)[BM / WM / 16][BN / WN / 16], u16* smem,
                          int64_t m0, int n0, bool skip, int tid, int wm, int wn, int g, int r16) {
-  constexpr int MI = BM / 32, NI = BN / WN / 16;
+  constexpr int MI = BM / WM / 16, NI = BN / WN / 16;
+  constexpr int WR = BM / WM, WPH = WM / 2;  // rows per wave, waves per half
+  static_assert(WM % 2 == 0 && (SROW == 0 || MI % SROW == 0), "epilogue layout");
   constexpr int EPI_LD = BN + 4;
-  if constexpr (BN == 256 && !VOC) {
+  if constexpr (BN == 256 && !VOC && WM == 2 && SROW == 0) {
     if (a.ln_out) {
       if constexpr (BM == 64) {
         if (a.ln_mode == 1) {
@@ -383,14 +389,15 @@ FS2_DEV void nt_epilogue(const GldsArgs& a, f32x4 (&acc)[BM / 32][BN / WN / 16],
   const bool out_bf16 = a.flags & FS2_EPI_OUT_BF16, aux_bf16 = a.flags & FS2_EPI_AUX_BF16;
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
-    if (wm == h) {
+    if (wm / WPH == h) {
+      const int rb = (wm % WPH) * WR;
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < NI; ++j)
 #pragma unroll
           for (int r = 0; r < 4; ++r)
-            Cs[(i * 16 + 4 * g + r) * EPI_LD + wn * (BN / WN) + j * 16 + r16] = acc[i][j][r];
+            Cs[(rb + i * 16 + 4 * g + r) * EPI_LD + wn * (BN / WN) + j * 16 + r16] = acc[i][j][r];
     }
     epi_barrier();
     constexpr int TPR = BN / 8;           // threads per row
@@ -402,9 +409,14 @@ FS2_DEV void nt_epilogue(const GldsArgs& a, f32x4 (&acc)[BM / 32][BN / WN / 16],
       const int rr = p * RPP + tid / TPR;
       const int64_t m = m0 + h * (BM / 2) + rr;
       if (m >= a.M || n >= a.N) continue;
+      int rq = rr;
+      if constexpr (SROW > 0) {  // row b + i + SROW * q of a band of 16 * SROW rows
+        const int w = rr / WR, rw = rr % WR, bnd = rw / (16 * SROW), rb2 = rw % (16 * SROW);
+        rq = w * WR + (bnd * SROW + rb2 % SROW) * 16 + rb2 / SROW;
+      }
       float v[8];
-      const f32x4 lo = *reinterpret_cast<const f32x4*>(Cs + rr * EPI_LD + cc);
-      const f32x4 hi = *reinterpret_cast<const f32x4*>(Cs + rr * EPI_LD + cc + 4);
+      const f32x4 lo = *reinterpret_cast<const f32x4*>(Cs + rq * EPI_LD + cc);
+      const f32x4 hi = *reinterpret_cast<const f32x4*>(Cs + rq * EPI_LD + cc + 4);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         v[e] = lo[e];
@@ -1230,6 +1242,221 @@ __global__ __launch_bounds__(256) void halo_splitk_reduce(GldsArgs a) {
       st4(yp + 4, f32x4{v[4], v[5], v[6], v[7]});
     }
   }
+}
+
+// fn(integral_constant<0>), ..., fn(integral_constant<N - 1>), in order
+template <int N, typename Fn>
+FS2_DEV void static_for(Fn&& fn) {
+  if constexpr (N > 0) {
+    static_for<N - 1>(fn);
+    fn(std::integral_constant<int, N - 1>{});
+  }
+}
+
+// ---------------------------------------------------------------- tap-register halo Conv1d
+// conv_gemm_tapreg: the halo Conv1d (C_in % 64 == 0, taps > 1, undilated, every row tile inside
+// one utterance) with each A fragment of a channel block read from LDS ONCE for all taps.
+//
+// A wave owns a band of 16 S rows x WC columns.  Its output fragment i (i < S) holds the band
+// rows i + S m (m = 0..15), so tap j of fragment i needs the input rows i + j + S m: halo
+// fragment F[i + j], where F[f] = rows f + S m of the band's halo (f < S + taps - 1).  The
+// S + taps - 1 halo fragments of a channel block are each read from LDS once and held in a
+// rolling register window (tap j uses F[j .. j + S - 1]: one new fragment per tap and k-half);
+// the k=9 decoder forward (64 x 64 per wave) reads 24 + 72 fragments per 288 MFMAs, the halo
+// kernel's 128 x 32 wave tile 180.  Same MFMAs per output in the same (channel block, tap, k-half) order as the halo
+// kernels: bitwise equal where both compute.
+// LDS halo image: halo row h sits at position (h mod S) * RS + h / S, so every F[f] reads 16
+// consecutive positions (chunk swizzle c ^ (h / S & 7): conflict-free ds_read_b128); the LDS-DMA
+// source row of each position is fixed per block (zero line outside the utterance / length).
+// Weight tiles (tap j, channel block cb) stream through a WS-slot ring, one barrier per tap;
+// channel block cb + 1's halo is staged at tap 0 of block cb (two halo slots).
+// Weight and halo registers rotate by k-half: after a tap's half-0 MFMAs the next tap's half-0
+// weights and halo fragment (at the last tap the next block's first S halo fragments) are read
+// under the half-1 MFMAs, and vice versa -- one register set of each.
+// A wave whose band lies past the utterance's length stages its share but issues no MFMAs
+// (those rows are masked downstream, as in conv_gemm_halo).
+template <int BM, int BN, int WGM, int WGN, int S, int TAPS, int WS, int MINB>
+__global__ __launch_bounds__(WGM * WGN * 64, MINB) void conv_gemm_tapreg(GldsArgs a) {
+  constexpr int NW = WGM * WGN, BK = 64;
+  constexpr int WR = 16 * S, WC = BN / WGN, NI = WC / 16;
+  static_assert(BM == WGM * WR && WC % 16 == 0 && WGM % 2 == 0, "tile");
+  constexpr int NF = S + TAPS - 1;
+  constexpr int HR = BM + TAPS - 1, RS = (HR + S - 1) / S, HP = (S * RS + 7) / 8;
+  constexpr int QMAX = (HP + NW - 1) / NW, BWP = BN / 8 / NW;
+  static_assert(BN % (8 * NW) == 0, "weight pieces");
+  constexpr int D = WS == 2 ? 2 : WS - 1;  // tile s + D is issued at step s
+  static_assert(D <= 3 && TAPS >= D && (D - 2) * BWP + QMAX <= 8, "vmcnt bookkeeping");
+  constexpr int A_E = HP * 8 * BK, B_E = BN * BK;
+  constexpr int EPI_E = (BM / 2) * (BN + 4) * 2;
+  constexpr int SMEM_E = 2 * A_E + WS * B_E > EPI_E ? 2 * A_E + WS * B_E : EPI_E;
+  __shared__ __attribute__((aligned(1024))) u16 smem[SMEM_E];
+  u16* As = smem;
+  u16* Bs = smem + 2 * A_E;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WGN, wn = wave % WGN;
+  const int g = lane >> 4, r16 = lane & 15, lrow = lane >> 3;
+  // block -> tile: XCD-contiguous runs, n fastest within a group (as conv_gemm_halo)
+  const int nwg = a.tiles_m * a.tiles_n;
+  const int orig = blockIdx.x, xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int gfull = a.tiles_m * a.group;
+  const int ng = wg / gfull, rem = wg - ng * gfull;
+  const int gsz = a.tiles_n - ng * a.group < a.group ? a.tiles_n - ng * a.group : a.group;
+  const int tm = m_interleave(rem / gsz, a.tiles_m, a.lens != nullptr);
+  const int tn = ng * a.group + (rem - (rem / gsz) * gsz);
+  const int64_t m0 = (int64_t)tm * BM;
+  const int n0 = tn * BN;
+  const bool skip = a.lens && rows_all_padding(a.lens, a.T, m0, m0 + BM < a.M ? m0 + BM : a.M);
+  const int64_t u0 = (m0 / a.T) * a.T;
+  const int64_t ulen = a.lens ? (a.lens[m0 / a.T] < a.T ? a.lens[m0 / a.T] : a.T) : a.T;
+  const int64_t u1 = u0 + ulen < a.M ? u0 + ulen : a.M;
+  const bool band_pad = m0 + wm * WR >= u1;
+
+  // halo piece pc = wave + NW q: positions 8 pc + lrow, position P = res * RS + qq holds halo
+  // row h = qq * S + res (global row m0 - pad + h)
+  const auto x_rs = buf_rsrc(a.x + (m0 - a.pad) * a.ldx, (int64_t)HR * a.ldx * 2);
+  const auto w_rs = buf_rsrc(a.w + (int64_t)n0 * a.K, (int64_t)BN * a.K * 2);
+  uint32_t h_vo[QMAX];
+  int qa = 0;
+#pragma unroll
+  for (int q = 0; q < QMAX; ++q) {
+    const int pc = wave + NW * q, P = pc * 8 + lrow;
+    const int res = P / RS, qq = P - res * RS, h = qq * S + res;
+    const int64_t gr = m0 - a.pad + h;
+    const int lc = (lane & 7) ^ (qq & 7);
+    h_vo[q] = (pc < HP && res < S && h < HR && gr >= u0 && gr < u1)
+                  ? (uint32_t)((h * a.ldx + lc * 8) * 2) : kOOB;
+    qa += pc < HP ? 1 : 0;
+  }
+  uint32_t b_vo[BWP];
+#pragma unroll
+  for (int i = 0; i < BWP; ++i) {
+    const int R = (wave * BWP + i) * 8 + lrow;
+    b_vo[i] = n0 + R < a.N ? (uint32_t)((R * a.K + ((lane & 7) ^ (R & 7)) * 8) * 2) : kOOB;
+  }
+  auto issue_a = [&](int cb, int slot) {
+#pragma unroll
+    for (int q = 0; q < QMAX; ++q) {
+      const int pc = wave + NW * q;
+      if (pc < HP) glds16_buf(x_rs, As + slot * A_E + pc * 8 * BK, h_vo[q], (uint32_t)(cb * BK * 2));
+    }
+  };
+  auto issue_b = [&](int t) {  // weight tile t = (channel block t / TAPS, tap t % TAPS)
+    const int cb = t / TAPS, j = t - cb * TAPS;
+    const uint32_t k0 = (uint32_t)((j * a.Cin + cb * BK) * 2);
+    u16* dst = Bs + (t % WS) * B_E + wave * BWP * 8 * BK;
+#pragma unroll
+    for (int i = 0; i < BWP; ++i) glds16_buf(w_rs, dst + i * 8 * BK, b_vo[i], k0);
+  };
+
+  f32x4 acc[S][NI];
+#pragma unroll
+  for (int i = 0; i < S; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8g F[NF][2], Bw[NI][2];
+  // F[f] of this lane: position (f % S) * RS + wm * 16 + f / S + r16, swizzle key = its offset
+  // within the residue class mod 8 = (r16 + f / S) & 7 -- one of (NF - 1) / S + 1 lane patterns
+  // per k-half (the rest of the address is a compile-time offset)
+  constexpr int NQ = (NF - 1) / S + 1;
+  const u16* fa[NQ][2];
+#pragma unroll
+  for (int d = 0; d < NQ; ++d)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+      fa[d][ks] = As + (r16 + wm * 16 + d) * BK + (((ks * 4 + g) ^ ((r16 + d) & 7)) * 8);
+  const int b_row = wn * WC + r16;
+  const u16* fb[2] = {Bs + b_row * BK + ((g ^ (b_row & 7)) * 8),
+                      Bs + b_row * BK + (((4 + g) ^ (b_row & 7)) * 8)};
+  auto rd_f = [&](int cb, int f, int ks) {
+    F[f][ks] = *reinterpret_cast<const bf16x8g*>(fa[f / S][ks] + (cb & 1) * A_E + (f % S) * RS * BK);
+  };
+  auto rd_b = [&](int t, int ks) {
+    const int so = (t % WS) * B_E;
+#pragma unroll
+    for (int jj = 0; jj < NI; ++jj) Bw[jj][ks] = *reinterpret_cast<const bf16x8g*>(fb[ks] + so + jj * 16 * BK);
+  };
+  auto mfma_half = [&](auto jc, int ks) {
+    constexpr int J = decltype(jc)::value;
+#pragma unroll
+    for (int i = 0; i < S; ++i)
+#pragma unroll
+      for (int jj = 0; jj < NI; ++jj)
+        acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(F[i + J][ks], Bw[jj][ks], acc[i][jj], 0, 0, 0);
+  };
+
+  if (!skip) {
+    const int ncb = a.Cin / BK, Stot = ncb * TAPS;
+    // prologue: halo 0, tiles 0 .. D-1
+    issue_a(0, 0);
+    issue_b(0);
+    int pend = 0;
+#pragma unroll
+    for (int d = 1; d < D; ++d)
+      if (d < Stot) {
+        issue_b(d);
+        pend += BWP;
+      }
+    vm_wait_n(pend);  // halo 0 and tile 0 landed
+    __builtin_amdgcn_s_barrier();
+    auto run = [&](auto cc) {
+      constexpr bool C = decltype(cc)::value;
+      if constexpr (C) {
+#pragma unroll
+        for (int f = 0; f < S; ++f) {
+          rd_f(0, f, 0);
+          rd_f(0, f, 1);
+        }
+        rd_b(0, 0);
+        rd_b(0, 1);
+      }
+      for (int cb = 0; cb < ncb; ++cb) {
+        const bool more = cb + 1 < ncb;
+        auto step = [&](auto jc) {
+          constexpr int J = decltype(jc)::value;
+          const int s = cb * TAPS + J;
+          // tile s + 1 landed (this wave's pieces); later DMA may stay in flight: tiles
+          // s + 2 .. s + D - 1 and the halo issued at tap 0 when that came after tile s + 1
+          int n = 0;
+          if (D == 3 && s + 2 < Stot) n += BWP;
+          if (J >= 1 && J <= D - 1 && more) n += qa;
+          vm_wait_n(n);
+          if constexpr (WS == 2) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_s_barrier();
+          __builtin_amdgcn_sched_barrier(0);
+          if (s + D < Stot) issue_b(s + D);
+          // block cb + 1's halo into the slot block cb - 1 used (its last reads, at tap
+          // TAPS - 2, were consumed by the MFMAs of tap TAPS - 1: done before this barrier)
+          if (J == 0 && more) issue_a(cb + 1, (cb + 1) & 1);
+          if constexpr (C) {
+            // tap J uses F[J .. J + S - 1]; F[J] is dead after it, F[J + S] is new at J + 1
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+              mfma_half(jc, ks);
+              __builtin_amdgcn_sched_barrier(0);
+              if (s + 1 < Stot) rd_b(s + 1, ks);
+              if constexpr (J + 1 < TAPS) {
+                rd_f(cb, J + S, ks);
+              } else if (more) {
+#pragma unroll
+                for (int f = 0; f < S; ++f) rd_f(cb + 1, f, ks);
+              }
+              __builtin_amdgcn_sched_barrier(0);
+            }
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        };
+        static_for<TAPS>(step);
+      }
+    };
+    if (band_pad) run(std::false_type{});
+    else run(std::true_type{});
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+  nt_epilogue<BM, BN, false, NW, WGN, WGM, S>(a, acc, smem, m0, n0, skip, tid, wm, wn, g, r16);
 }
 
 // ------------------------------------------------------------------------ weight gradient
@@ -2620,6 +2847,39 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
       launch_nt<128, 64, 2>(a, tapaligned, true, st);
     }
     return launch_status("fs2_conv_gemm(bf16)");
+  }
+  // tap-register halo kernel (conv_gemm_tapreg): 4-wave 128 x 64 tiles at 3 blocks per CU when
+  // they fill at least one round of the CUs (decoder k=9 forward and data gradient, encoder k=9
+  // forward, PostNet 512 -> 512; smaller grids keep the halo kernels' split-K / 64-row paths).
+  // Alone, decoder k=9 forward: 89.7 us vs 94.4 (128 x 128, 2 blocks per CU) and 97.7 (8-wave
+  // 256 x 128, one block per CU): independent blocks overlap one another's barrier / DMA phases
+  const int trk = g_tune[FS2_TUNE_TAPREG];
+  if (trk >= 0 && !voc && tapaligned && (taps == 5 || taps == 9) && pad >= 0 && pad < taps) {
+    const int cu = cu_count();
+    const int64_t t8 = (rows / 256) * ((c_out + 127) / 128), t4 = (rows / 128) * ((c_out + 63) / 64);
+    const bool ok8 = seq_len % 256 == 0, ok4 = seq_len % 128 == 0;
+    int pick = 0;
+    if (trk == 2) pick = ok8 ? 8 : 0;
+    else if (trk == 1) pick = ok4 ? 4 : 0;
+    else if (trk == 3) pick = ok4 ? 3 : 0;
+    else if (ok4 && t4 >= 3 * cu) pick = 4;
+    if (pick) {
+      a.tiles_m = (int)(rows / (pick == 8 ? 256 : 128));
+      a.tiles_n = (int)((c_out + (pick == 4 ? 63 : 127)) / (pick == 4 ? 64 : 128));
+      a.group = halo_group(a.tiles_n);
+      const unsigned grid = (unsigned)(a.tiles_m * a.tiles_n);
+      if (pick == 8) {
+        if (taps == 9) conv_gemm_tapreg<256, 128, 4, 2, 4, 9, 4, 1><<<grid, 512, 0, st>>>(a);
+        else conv_gemm_tapreg<256, 128, 4, 2, 4, 5, 4, 1><<<grid, 512, 0, st>>>(a);
+      } else if (pick == 3) {  // 4-wave 128 x 128 tiles, 2 blocks per CU
+        if (taps == 9) conv_gemm_tapreg<128, 128, 2, 2, 4, 9, 2, 2><<<grid, 256, 0, st>>>(a);
+        else conv_gemm_tapreg<128, 128, 2, 2, 4, 5, 2, 2><<<grid, 256, 0, st>>>(a);
+      } else {
+        if (taps == 9) conv_gemm_tapreg<128, 64, 2, 2, 4, 9, 2, 3><<<grid, 256, 0, st>>>(a);
+        else conv_gemm_tapreg<128, 64, 2, 2, 4, 5, 2, 3><<<grid, 256, 0, st>>>(a);
+      }
+      return launch_status("fs2_conv_gemm(bf16)");
+    }
   }
   // halo kernel (tile sizes as the tap-major choice below: 128x128 / 128x64 / 64x64 by grid;
   // FS2_TUNE_NT_HALO = 2 forces 128 x 128).  Every row tile must lie inside one utterance.

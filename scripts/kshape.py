@@ -9,8 +9,9 @@ summary averages unlike launches -- and prints total ms/step, launches/step and 
 duration of each group.  `--stats` also writes the per-kernel-name summary (the same columns
 as rocprofv3's `kernel_stats.csv`: Name, Calls, TotalDurationNs, AverageNs, Percentage).
 
-Lines tagged `conv_k9` are the launch set bench.py's `roofline` names (the k=9 halo
-implicit-GEMM convolutions: decoder + encoder FFN forward and data gradient).
+Lines tagged `conv_k9` are the tap-register k=9 convolutions (conv_gemm_tapreg: decoder FFN
+forward and data gradient, encoder forward) of the launch set bench.py's `roofline` names (the
+encoder's split-K data gradient runs on conv_gemm_halo).
 """
 import csv
 import sqlite3
@@ -53,7 +54,7 @@ def main():
           f"({len(rows) / steps:.0f} launches/step)")
     print(f"{'ms/step':>8} {'n/step':>6} {'avg us':>8}  {'wgs':>6}  kernel")
     for (name, wgs), v in sorted(groups.items(), key=lambda kv: -sum(kv[1]))[:top]:
-        tag = "  conv_k9" if "conv_gemm_halo<" in name and name.rstrip(")").endswith("9>") else ""
+        tag = "  conv_k9" if "conv_gemm_tapreg<" in name and ", 9, " in name else ""
         print(f"{sum(v) / 1e6 / steps:8.3f} {len(v) / steps:6.1f} {sum(v) / len(v) / 1e3:8.1f}  "
               f"{wgs:6d}  {name[:100]}{tag}")
     if stats_out:

@@ -735,6 +735,7 @@ def test_conv_gemm_bf16_halo(B, T, cin, cout, k):
     lens = torch.tensor([T - (7 * u) % T for u in range(B)], device=DEV)
     lens[-1] = 1
     try:
+        K.lib.fs2_set_tuning(19, -1)  # FS2_TUNE_TAPREG off: these are the halo kernels' checks
         K.lib.fs2_set_tuning(6, -1)  # FS2_TUNE_NT_HALO off: tap-major kernel
         y_tm = K.conv_gemm(x, wf, B * T, T, cin, cout, k, pad, bias=b)
         for mode in (0, 2, 5, 6, 7):  # 5-7: the 8-wave (one block per CU) variants
@@ -776,6 +777,62 @@ def test_conv_gemm_bf16_halo(B, T, cin, cout, k):
                 assert torch.isfinite(y1).all() and torch.isfinite(d1).all()
     finally:
         K.lib.fs2_set_tuning(6, 0)
+        K.lib.fs2_set_tuning(19, 0)
+
+
+@pytest.mark.parametrize("B,T,cin,cout,k,mode", [
+    (4, 512, 256, 1024, 9, 2), (4, 512, 256, 1024, 9, 1), (6, 512, 1024, 256, 9, 1),
+    (2, 256, 512, 512, 5, 2), (3, 128, 512, 512, 5, 1), (3, 128, 256, 320, 9, 1),
+    (2, 256, 256, 200, 9, 2)])
+def test_conv_gemm_bf16_tapreg(B, T, cin, cout, k, mode):
+    """The tap-register halo kernel (FS2_TUNE_TAPREG = 1: 4-wave 128 x 64 tiles, 2: 8-wave
+    256 x 128 tiles) against fp32 math on the same bf16 data, forward (bias + ReLU) and data
+    gradient (+ residual), and bitwise against the halo kernels (knob -1): the same MFMAs per
+    output in the same (channel block, tap, k-half) order.  With lens only the valid rows are
+    compared: a wave whose 64-row band lies past the length computes nothing (epilogue of 0),
+    the halo kernel skips at 16-row granularity."""
+    pad = (k - 1) // 2
+    x = bf(rnd(B * T, cin, seed=61))
+    w = bf(rnd(cout, cin, k, scale=1 / math.sqrt(cin * k), seed=62)).float()
+    b = rnd(cout, seed=63)
+    wf = torch.empty(cout * cin * k, device=DEV, dtype=torch.bfloat16)
+    wb = torch.empty(cout * cin * k, device=DEV, dtype=torch.bfloat16)
+    K.weight_prep(w, cout, cin, k, wf, wb)
+    lens = torch.tensor([T - (11 * u) % T for u in range(B)], device=DEV)
+    lens[-1] = 1
+    valid = (torch.arange(T, device=DEV)[None] < lens[:, None]).reshape(-1)
+    dy = bf(rnd(B * T, cout, seed=64))
+    aux = rnd(B * T, cin, seed=65)
+    M = B * T
+
+    def run(v):
+        K.lib.fs2_set_tuning(19, v)
+        K.lib.fs2_set_tuning(8, -1)  # halo reference unsplit (a split sums in another order)
+        try:
+            return (K.conv_gemm(x, wf, M, T, cin, cout, k, pad, bias=b, flags=K.EPI_RELU),
+                    K.conv_gemm(x, wf, M, T, cin, cout, k, pad, bias=b, flags=K.EPI_RELU,
+                                out_dtype=torch.bfloat16, lens=lens),
+                    K.conv_gemm(dy, wb, M, T, cout, cin, k, pad, flags=K.EPI_ADD_AUX, aux=aux),
+                    K.conv_gemm(dy, wb, M, T, cout, cin, k, pad, flags=K.EPI_ADD_AUX, aux=aux,
+                                lens=lens))
+        finally:
+            K.lib.fs2_set_tuning(19, 0)
+            K.lib.fs2_set_tuning(8, 0)
+    t, h = run(mode), run(-1)
+    close(t[0], F.relu(ref_conv(x.float(), w, b, B, T, pad)), 1e-5)
+    xm = x.float() * valid[:, None]
+    close(t[1].float()[valid], F.relu(ref_conv(xm, w, b, B, T, pad))[valid], 8e-3)
+    xr = x.float().clone().requires_grad_()
+    ref_conv(xr, w, b, B, T, pad).backward(dy.float())
+    close(t[2], xr.grad + aux, 1e-5)
+    if cout % 64 == 0:  # the data gradient runs on the halo kernels (zero rows past the length)
+        xr2 = xm.clone().requires_grad_()
+        ref_conv(xr2, w, b, B, T, pad).backward(dy.float() * valid[:, None])
+        close(t[3][valid], (xr2.grad + aux)[valid], 1e-5)
+    for a_, b_ in zip(t, h):
+        assert torch.isfinite(a_.float()).all()
+    assert torch.equal(t[0], h[0]) and torch.equal(t[2], h[2])
+    assert torch.equal(t[1][valid], h[1][valid]) and torch.equal(t[3][valid], h[3][valid])
 
 
 @pytest.mark.parametrize("B,T,cin,cout,k,flags", [

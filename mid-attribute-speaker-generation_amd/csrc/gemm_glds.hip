@@ -2861,12 +2861,22 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
     int pick = 0;
     if (trk == 2) pick = ok8 ? 8 : 0;
     else if (trk == 1) pick = ok4 ? 4 : 0;
-    else if (trk == 3) pick = ok4 ? 3 : 0;
+    else if (trk >= 3 && trk <= 5) pick = ok4 ? trk : 0;  // A/B variants below
     else if (ok4 && t4 >= 3 * cu) pick = 4;
     if (pick) {
       a.tiles_m = (int)(rows / (pick == 8 ? 256 : 128));
-      a.tiles_n = (int)((c_out + (pick == 4 ? 63 : 127)) / (pick == 4 ? 64 : 128));
-      a.group = halo_group(a.tiles_n);
+      const bool n64 = pick != 8 && pick != 3;
+      a.tiles_n = (int)((c_out + (n64 ? 63 : 127)) / (n64 ? 64 : 128));
+      // tile group: the n-tiles whose weight slice (~1.25 MB) an XCD's resident blocks share in
+      // its 4 MB L2 while they walk the m-tiles (all 16 n-tiles of the decoder k=9 forward, a
+      // 4.7 MB weight, re-fetched it past L2: 187 MB per launch; groups of 4: 92 -> 85 us)
+      if (g_tune[FS2_TUNE_NT_GROUP] > 0) {
+        a.group = halo_group(a.tiles_n);
+      } else {
+        const int64_t slice = (int64_t)(n64 ? 64 : 128) * K * 2;
+        int gr = (int)(((int64_t)5 << 18) / slice);
+        a.group = gr < 1 ? 1 : gr > a.tiles_n ? a.tiles_n : gr;
+      }
       const unsigned grid = (unsigned)(a.tiles_m * a.tiles_n);
       if (pick == 8) {
         if (taps == 9) conv_gemm_tapreg<256, 128, 4, 2, 4, 9, 4, 1><<<grid, 512, 0, st>>>(a);
@@ -2874,6 +2884,12 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
       } else if (pick == 3) {  // 4-wave 128 x 128 tiles, 2 blocks per CU
         if (taps == 9) conv_gemm_tapreg<128, 128, 2, 2, 4, 9, 2, 2><<<grid, 256, 0, st>>>(a);
         else conv_gemm_tapreg<128, 128, 2, 2, 4, 5, 2, 2><<<grid, 256, 0, st>>>(a);
+      } else if (pick == 5) {  // 3-slot weight ring (no LDS drain at the barrier), 2 per CU
+        if (taps == 9) conv_gemm_tapreg<128, 64, 2, 2, 4, 9, 3, 2><<<grid, 256, 0, st>>>(a);
+        else conv_gemm_tapreg<128, 64, 2, 2, 4, 5, 3, 2><<<grid, 256, 0, st>>>(a);
+      } else if (trk == 4) {  // 4-slot ring (tiles two taps ahead), 2 per CU
+        if (taps == 9) conv_gemm_tapreg<128, 64, 2, 2, 4, 9, 4, 2><<<grid, 256, 0, st>>>(a);
+        else conv_gemm_tapreg<128, 64, 2, 2, 4, 5, 4, 2><<<grid, 256, 0, st>>>(a);
       } else {
         if (taps == 9) conv_gemm_tapreg<128, 64, 2, 2, 4, 9, 2, 3><<<grid, 256, 0, st>>>(a);
         else conv_gemm_tapreg<128, 64, 2, 2, 4, 5, 2, 3><<<grid, 256, 0, st>>>(a);

@@ -69,6 +69,8 @@ def ab(spec, reps, only):
         valid = (torch.arange(T, device=dev)[None] < lens[:, None]).reshape(-1)
         x = (torch.randn(M, cin, device=dev) * valid[:, None]).to(bf)
         dy = (torch.randn(M, cout, device=dev) * valid[:, None]).to(bf)
+        if os.environ.get("NOLENS"):  # every row valid (no padding skips)
+            lens = None
         w = torch.randn(cout, cin, k, device=dev) / math.sqrt(cin * k)
         wf = torch.empty(cout * cin * k, device=dev, dtype=bf)
         wb = torch.empty_like(wf)

@@ -414,6 +414,16 @@ static int wgrad_splits(int64_t rows, int64_t c_in, int64_t c_out, int taps) {
     if (s > rows / 512) s = rows / 512;
     return (int)(s < 1 ? 1 : s);
   }
+  if ((taps == 3 || taps == 5 || taps == 9) && c_in % 64 == 0 && c_out % 64 == 0 &&
+      g_tune[FS2_TUNE_WGRAD_HALO] == 2) {
+    // conv_wgrad_halo with two k-groups per block (512 threads, one block per CU): about 256
+    // blocks of 64 x 64 tiles, each split at least 8 k-tiles of 64 rows
+    const int64_t t = (c_out / 64) * (c_in / 64);
+    int64_t s = (256 + t - 1) / t;
+    if (s > rows / 512) s = rows / 512;
+    if (s > 64) s = 64;
+    return (int)(s < 1 ? 1 : s);
+  }
   const int64_t Kp = (int64_t)taps * c_in;
   const int bt = wgrad_tile(rows, c_in, c_out, taps);
   const int64_t tiles = ((c_out + bt - 1) / bt) * ((Kp + bt - 1) / bt);

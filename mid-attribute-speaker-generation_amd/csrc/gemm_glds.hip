@@ -2191,20 +2191,26 @@ __global__ __launch_bounds__(256, 2) void wgrad_k1_q(WgradGlds a) {
 // 26 instead of 40 fragment reads per wave and k-tile; the next tap's x fragment is read
 // under the current tap's MFMAs.  Each wave also carries the bias gradient of its 16 o rows
 // (one extra MFMA per k-step, evenly spread).  WS = 0: the 32 x 32 wave quarters of round 1.
-template <int TAPS, int WS>
-__global__ __launch_bounds__(256, 2) void conv_wgrad_halo(WgradGlds a) {
-  constexpr int BO = 64, BC = 64, BK = 64, STAGES = 2;
+template <int TAPS, int WS, int KG = 1>
+__global__ __launch_bounds__(256 * KG, KG == 1 ? 2 : 1) void conv_wgrad_halo(WgradGlds a) {
+  static_assert(KG == 1 || (KG == 2 && WS == 1), "k-groups: the 64 (o) x 16 (c) wave tiles");
+  constexpr int BO = 64, BC = 64, BK = 64, STAGES = 2, NTH = 256 * KG;
   constexpr int HX = 8;                      // halo rows allocated (taps <= 9)
   constexpr int A_E = BK * BO;               // dy image
   constexpr int X_E = (BK + HX) * BC;        // x halo image
   constexpr int STAGE_E = A_E + X_E;
   constexpr int MAXKT = 1024;
-  __shared__ __attribute__((aligned(1024))) u16 smem[STAGES * STAGE_E + MAXKT + 64];
-  short* ktl = reinterpret_cast<short*>(smem + STAGES * STAGE_E);
-  int* wcnt = reinterpret_cast<int*>(smem + STAGES * STAGE_E + MAXKT);
+  __shared__ __attribute__((aligned(1024))) u16 smem[KG * STAGES * STAGE_E + MAXKT + 64];
+  short* ktl = reinterpret_cast<short*>(smem + KG * STAGES * STAGE_E);
+  int* wcnt = reinterpret_cast<int*>(smem + KG * STAGES * STAGE_E + MAXKT);
 
   const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // KG = 2: waves 4 g .. 4 g + 3 form k-group g, which takes every other 64-row k-tile of the
+  // split into its own LDS stages; the groups' partial tiles are summed (group 0 + group 1) at
+  // the end, so a split covers twice the rows of a 4-wave block (half the fp32 slabs)
+  const int wave_all = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int grp = wave_all >> 2, wave = wave_all & 3;
+  u16* const gsm = smem + grp * STAGES * STAGE_E;
   const int wm = wave >> 1, wn = wave & 1;
   const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3, r16 = lane & 15;
 
@@ -2223,7 +2229,7 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_halo(WgradGlds a) {
   int nk = nk_all;
   if (use_list) {  // ordered list of k-tiles holding a real row (as conv_wgrad_tn_glds)
     int total = 0;
-    for (int cc0 = 0; cc0 < nk_all; cc0 += 256) {
+    for (int cc0 = 0; cc0 < nk_all; cc0 += NTH) {
       const int kt = cc0 + tid;
       bool v = false;
       if (kt < nk_all) {
@@ -2231,14 +2237,14 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_halo(WgradGlds a) {
         v = !rows_all_padding(a.lens, a.T, k0, k0 + BK < r_end ? k0 + BK : r_end);
       }
       const uint64_t mask = __ballot(v);
-      if (lane == 0) wcnt[wave] = __popcll(mask);
+      if (lane == 0) wcnt[wave_all] = __popcll(mask);
       __syncthreads();
       int before = total;
-      for (int w = 0; w < wave; ++w) before += wcnt[w];
+      for (int w = 0; w < wave_all; ++w) before += wcnt[w];
       const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
       if (v) ktl[before + below] = (short)kt;
-      for (int w = 0; w < 4; ++w) total += wcnt[w];
+      for (int w = 0; w < 4 * KG; ++w) total += wcnt[w];
       __syncthreads();
     }
     nk = total;
@@ -2249,7 +2255,7 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_halo(WgradGlds a) {
   const int lrow = lane >> 3, lch = lane & 7;
   const int HR = BK + a.taps - 1, HP = (HR + 7) / 8;  // x halo rows / 8-row pieces
   auto issue = [&](int kt, int stage) {
-    u16* As = smem + stage * STAGE_E;
+    u16* As = gsm + stage * STAGE_E;
     u16* Xs = As + A_E;
     const int tile = use_list ? (int)ktl[kt] : kt;
     const int64_t k0 = r_begin + (int64_t)tile * BK;
@@ -2310,7 +2316,7 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_halo(WgradGlds a) {
     return __builtin_bit_cast(bf16x8g, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
   };
   auto compute = [&](int stage) {
-    const u16* As = smem + stage * STAGE_E;
+    const u16* As = gsm + stage * STAGE_E;
     const u16* Xs = As + A_E;
     if constexpr (WS == 1) {
 #pragma unroll
@@ -2370,7 +2376,63 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_halo(WgradGlds a) {
     }
   };
 
-  kloop<STAGES, 5>(nk, issue, compute);  // per-wave DMA count varies (<= 5): kloop waits vmcnt(0)-style
+  if constexpr (KG == 1) {
+    kloop<STAGES, 5>(nk, issue, compute);  // per-wave DMA count varies (<= 5): kloop waits vmcnt(0)-style
+  } else {
+    // kloop's two-stage schedule with both groups in step: iteration it holds k-tile
+    // KG it + grp of each group (one barrier per iteration for the whole block)
+    const int nit = (nk + KG - 1) / KG;
+    if (grp < nk) issue(grp, 0);
+    for (int it = 0; it < nit; ++it) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if ((it + 1) * KG + grp < nk) issue((it + 1) * KG + grp, (it + 1) & 1);
+      if (it * KG + grp < nk) compute(it & 1);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    // group 1's partial tile (and bias partial) into group 0's, 3 taps per LDS round (fixed
+    // order: group 0 + group 1)
+    float* xb = reinterpret_cast<float*>(smem);
+    constexpr int TC = 3;
+#pragma unroll
+    for (int j0 = 0; j0 < TAPS; j0 += TC) {
+      if (grp == 1) {
+#pragma unroll
+        for (int jc = 0; jc < TC; ++jc)
+          if (j0 + jc < TAPS) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                xb[(((wave * TC + jc) * 4 + i) * 4 + r) * 64 + lane] = acc[j0 + jc][i][0][r];
+          }
+        if (j0 == 0) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) xb[(4 * TC * 16 + wave * 4 + r) * 64 + lane] = accb[0][r];
+        }
+      }
+      __syncthreads();
+      if (grp == 0) {
+#pragma unroll
+        for (int jc = 0; jc < TC; ++jc)
+          if (j0 + jc < TAPS) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                acc[j0 + jc][i][0][r] += xb[(((wave * TC + jc) * 4 + i) * 4 + r) * 64 + lane];
+          }
+        if (j0 == 0) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) accb[0][r] += xb[(4 * TC * 16 + wave * 4 + r) * 64 + lane];
+        }
+      }
+      __syncthreads();
+    }
+    if (grp == 1) return;
+  }
 
   if (do_bias && r16 == 0) {
 #pragma unroll
@@ -2575,8 +2637,10 @@ int conv_wgrad_glds_launch(const void* dy, int64_t ldy, const void* x, int64_t l
     a.tiles_k = (int)(c_in / 64);
     const unsigned hgrid = (unsigned)(a.tiles_o * a.tiles_k * splits);
     const bool quarters = g_tune[FS2_TUNE_WGRAD_HALO] == 1;  // round-1 wave tiles (A/B)
-#define FS2_WH(T) (quarters ? conv_wgrad_halo<T, 0><<<hgrid, 256, 0, st>>>(a) \
-                            : conv_wgrad_halo<T, 1><<<hgrid, 256, 0, st>>>(a))
+    const bool kg2 = g_tune[FS2_TUNE_WGRAD_HALO] == 2;       // two k-groups per block
+#define FS2_WH(T) (kg2 ? conv_wgrad_halo<T, 1, 2><<<hgrid, 512, 0, st>>>(a)        \
+                       : quarters ? conv_wgrad_halo<T, 0><<<hgrid, 256, 0, st>>>(a) \
+                                  : conv_wgrad_halo<T, 1><<<hgrid, 256, 0, st>>>(a))
     if (taps == 9) FS2_WH(9);
     else if (taps == 5) FS2_WH(5);
     else FS2_WH(3);

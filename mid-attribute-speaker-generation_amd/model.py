@@ -114,6 +114,10 @@ def sinusoid_table(n_position, d_hid):
 # FS2_SERIAL_WGRAD_TAPS="9" (A/B): weight gradients of these kernel widths run on the main
 # stream, serially after the data gradient, instead of concurrently on the side stream
 _SERIAL_TAPS = frozenset(int(t) for t in os.environ.get("FS2_SERIAL_WGRAD_TAPS", "").split(",") if t)
+# FS2_WGRAD_AFTER_DGRAD: 1 = a Conv1d's (taps > 1) side-stream weight gradient is issued after
+# its own data gradient, so the two do not share the CUs (the data gradient then runs alone and
+# the weight gradient beside the lighter ops that follow it); 0 = issued before it (concurrent)
+WGRAD_AFTER_DGRAD = os.environ.get("FS2_WGRAD_AFTER_DGRAD", "0") == "1"
 
 
 class StepCtx:
@@ -366,10 +370,14 @@ class FFTBlock(nn.Module):
         ctx.wgrad(dy2_c, h, _g(w2.weight), M, T, w2.c_in, d, w2.k, w2.padding, lens=lens)
         dh = K.conv_gemm(dy2_c, w2._w_bwd, M, T, d, w2.c_in, w2.k, w2.padding,
                          flags=K.EPI_RELU_MASK_AUX, aux=h, out_dtype=cdt, lens=lens)
-        ctx.wgrad(dh, x1_c, _g(w1.weight), M, T, d, w1.c_out, w1.k, w1.padding, db=_g(w1.bias),
-                  lens=lens)
+        if not WGRAD_AFTER_DGRAD:
+            ctx.wgrad(dh, x1_c, _g(w1.weight), M, T, d, w1.c_out, w1.k, w1.padding,
+                      db=_g(w1.bias), lens=lens)
         K.conv_gemm(dh, w1._w_bwd, M, T, w1.c_out, d, w1.k, w1.padding, flags=K.EPI_ADD_AUX,
                     aux=dx1, out=dx1, lens=lens)
+        if WGRAD_AFTER_DGRAD:
+            ctx.wgrad(dh, x1_c, _g(w1.weight), M, T, d, w1.c_out, w1.k, w1.padding,
+                      db=_g(w1.bias), lens=lens)
         # LN1 -> fc -> attention -> QKV
         dx = torch.empty((M, d), dtype=torch.float32, device=x_c.device)
         dy1, dy1_t = K.ln_bwd(xh1, rs1, ln1.weight, ln1.bias, _g(ln1.weight), _g(ln1.bias),
@@ -613,13 +621,17 @@ class PostNet(nn.Module):
             dz, dz_t = K.bn_bwd(d, z, mean, rstd, bn.weight, bn.bias, _g(bn.weight), _g(bn.bias),
                                 i < n - 1, p, ctx.seed, self.site + i, copy=ctx.copy)
             dz_c = _t(dz, dz_t)
-            ctx.wgrad(dz_c, a_c, _g(conv.weight), M, T, conv.c_in, conv.c_out, conv.k,
-                         conv.padding, db=_g(conv.bias))
+            if not WGRAD_AFTER_DGRAD:
+                ctx.wgrad(dz_c, a_c, _g(conv.weight), M, T, conv.c_in, conv.c_out, conv.k,
+                          conv.padding, db=_g(conv.bias))
             if i > 0:
                 d = K.conv_gemm(dz_c, conv._w_bwd, M, T, conv.c_out, conv.c_in, conv.k, conv.padding)
             else:
                 K.conv_gemm(dz_c, conv._w_bwd, M, T, conv.c_out, conv.c_in, conv.k, conv.padding,
                             flags=K.EPI_ADD_AUX, aux=dx_acc, out=dx_acc)
+            if WGRAD_AFTER_DGRAD:
+                ctx.wgrad(dz_c, a_c, _g(conv.weight), M, T, conv.c_in, conv.c_out, conv.k,
+                          conv.padding, db=_g(conv.bias))
 
 
 # ----------------------------------------------------------------------------- GMM head

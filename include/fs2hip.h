@@ -270,7 +270,8 @@ int fs2_weight_prep_batch(int dtype, const int64_t* jobs, int n_jobs, int64_t n_
  *                          half of rows is past the utterance length (lens given)
  *   FS2_TUNE_NT_TILE       tap-major fwd/dX kernel (k = 1 projections, odd shapes): 0 = tile
  *                          by grid size, 1 / 2 / 3 = force 128x128 / 128x64 / 64x64
- *   FS2_TUNE_LN_TILE       fs2_conv_gemm_ln row tile: 0 = 64 x 256 (default), 1 = 128 x 256
+ *   FS2_TUNE_LN_TILE       fs2_conv_gemm_ln(_bwd) row tile: 0 = 64 x 256 (default), 1 = 128 x 256,
+ *                          2 = 64 x 256 with one LDS stage (k = 1, C_in % 64 == 0)
  *   FS2_TUNE_WGRAD_K1      k = 1 weight gradient: 0 = 64 x 64 tiles with the 128-row k-tiles
  *                          split over 4 waves (default), 1 = 128 x 128 tiles of 8 waves
  *                          (both: buffer-descriptor staging), -1 = the tap-major kernel;

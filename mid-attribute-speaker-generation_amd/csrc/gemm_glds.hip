@@ -2811,6 +2811,10 @@ int conv_gemm_ln_glds_launch(const void* x, int64_t ldx, const void* wk, int64_t
     return launch_status("fs2_conv_gemm_ln");
   }
   const bool k1 = tapaligned && taps == 1 && g_tune[FS2_TUNE_NT_K1] >= 0;
+  if (g_tune[FS2_TUNE_LN_TILE] == 2 && k1) {  // one LDS stage (40 KB): 3-4 blocks per CU
+    conv_gemm_nt_glds<64, 256, 1, true, false, true><<<grid, 256, 0, st>>>(a);
+    return launch_status("fs2_conv_gemm_ln");
+  }
   if (wide) {
     if (tapaligned) conv_gemm_nt_glds<128, 256, 2, true, false><<<grid, 256, 0, st>>>(a);
     else conv_gemm_nt_glds<128, 256, 2, false, false><<<grid, 256, 0, st>>>(a);
@@ -2853,7 +2857,9 @@ int conv_gemm_lnbwd_glds_launch(const void* x, int64_t ldx, const void* wk, int6
   a.tiles_m = (int)((rows + 63) / 64);
   a.tiles_n = 1;
   const unsigned grid = (unsigned)a.tiles_m;
-  if (taps == 1 && c_in % 64 == 0 && g_tune[FS2_TUNE_PERSIST] > 0 && a.tiles_m >= 2 * cu_count())
+  if (taps == 1 && c_in % 64 == 0 && g_tune[FS2_TUNE_LN_TILE] == 2 && g_tune[FS2_TUNE_NT_K1] >= 0)
+    conv_gemm_nt_glds<64, 256, 1, true, false, true><<<grid, 256, 0, st>>>(a);
+  else if (taps == 1 && c_in % 64 == 0 && g_tune[FS2_TUNE_PERSIST] > 0 && a.tiles_m >= 2 * cu_count())
     launch_persist<64, 256, 2>(a, st);
   else if (c_in % 64 == 0 && taps == 1 && g_tune[FS2_TUNE_NT_K1] >= 0)
     conv_gemm_nt_glds<64, 256, 2, true, false, true><<<grid, 256, 0, st>>>(a);

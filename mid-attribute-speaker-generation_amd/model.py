@@ -974,7 +974,28 @@ class FastSpeech2(nn.Module):
             # FS2_SIDE_PRIORITY: stream priority of the weight-gradient stream (torch's scale:
             # lower = higher priority; the main chain runs on the current stream)
             prio = int(os.environ.get("FS2_SIDE_PRIORITY", "0"))
-            self._side = torch.cuda.Stream(device=self.encoder.position_enc.device, priority=prio)
+            dev = self.encoder.position_enc.device
+            frac = float(os.environ.get("FS2_SIDE_CUMASK", "0") or 0)
+            if 0 < frac < 1:
+                # A/B: the weight-gradient stream restricted to a fraction of the CUs (a hash
+                # spreads the mask over every XCD whatever the bit -> CU numbering); meant with
+                # FS2_MAIN_PRIORITY, which moves the main chain off the legacy default stream
+                import ctypes
+                n = torch.cuda.get_device_properties(dev).multi_processor_count
+                bits = [(i * 37) % 64 < frac * 64 for i in range(n)]
+                words = (ctypes.c_uint32 * ((n + 31) // 32))()
+                for i, b in enumerate(bits):
+                    if b:
+                        words[i // 32] |= 1 << (i % 32)
+                hip = ctypes.CDLL("libamdhip64.so")
+                s = ctypes.c_void_p()
+                rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(s), ctypes.c_uint32(len(words)),
+                                                      words)
+                if rc != 0:
+                    raise RuntimeError(f"hipExtStreamCreateWithCUMask failed ({rc})")
+                self._side = torch.cuda.ExternalStream(s.value, device=dev)
+            else:
+                self._side = torch.cuda.Stream(device=dev, priority=prio)
         return self._side
 
     def join_side(self):

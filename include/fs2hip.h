@@ -287,10 +287,13 @@ int fs2_weight_prep_batch(int dtype, const int64_t* jobs, int n_jobs, int64_t n_
  *   FS2_TUNE_WGRAD_FUSE    k = 1 weight gradient (FS2_TUNE_WGRAD_K1 = 0): 0 = split slabs summed
  *                          by a reduce launch (default), 1 = the last split to finish a tile sums
  *                          them in split order inside the kernel (no reduce launch)
- *   FS2_TUNE_TAPREG        fwd/dX Conv1d taps 5 / 9 (C_in % 64 == 0): 0 = the tap-register halo
- *                          kernel where its grid fills the chip (default), -1 = off (the halo
- *                          kernels above), 1 = force its 4-wave 128 x 64 tiles, 2 = force its
- *                          8-wave 256 x 128 tiles (when T allows)
+ *   FS2_TUNE_TAPREG        fwd/dX Conv1d taps 5 / 9 (C_in % 64 == 0, c_out % 128 == 0): 0 = the
+ *                          tap-register halo kernel where its grid fills the chip (default:
+ *                          4-wave 128 x 64 tiles at 3 blocks per CU, 128 x 128 at 2 for
+ *                          c_out <= 256), -1 = off (the halo kernels above), 1 = force the
+ *                          128 x 64 tiles, 2 = force 8-wave 256 x 128 tiles (when T allows),
+ *                          3 = force 128 x 128, 4 / 5 = 128 x 64 at 2 blocks per CU with a
+ *                          4- / 3-slot weight ring, 7 = 128 x 128 also for c_out <= 512 (A/B)
  * Process-wide; query workspace sizes after setting.                                 */
 enum { FS2_TUNE_GEMM_STAGES = 0, FS2_TUNE_WGRAD_STAGES = 1, FS2_TUNE_WGRAD_TILE = 2,
        FS2_TUNE_WGRAD_SPLITS = 3, FS2_TUNE_LEGACY_GEMM = 4, FS2_TUNE_NT_GROUP = 5,

@@ -2919,10 +2919,13 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
     return launch_status("fs2_conv_gemm(bf16)");
   }
   // tap-register halo kernel (conv_gemm_tapreg): 4-wave 128 x 64 tiles at 3 blocks per CU when
-  // they fill at least one round of the CUs (decoder k=9 forward and data gradient, encoder k=9
-  // forward, PostNet 512 -> 512; smaller grids keep the halo kernels' split-K / 64-row paths).
-  // Alone, decoder k=9 forward: 89.7 us vs 94.4 (128 x 128, 2 blocks per CU) and 97.7 (8-wave
-  // 256 x 128, one block per CU): independent blocks overlap one another's barrier / DMA phases
+  // they fill at least one round of the CUs (decoder k=9 forward, encoder k=9 forward, PostNet
+  // 512 -> 512; smaller grids keep the halo kernels' split-K / 64-row paths).  Alone, decoder
+  // k=9 forward: 89.7 us vs 94.4 (128 x 128, 2 blocks per CU) and 97.7 (8-wave 256 x 128, one
+  // block per CU): independent blocks overlap one another's barrier / DMA phases.  Narrow
+  // outputs (c_out <= 256: the decoder k=9 data gradient, which runs beside the side stream's
+  // k=9 weight gradient) take the 128 x 128 tiles at 2 blocks per CU: slower alone (109 vs
+  // 87 us) but the dgrad||wgrad pair is 181 vs 191 us and the step 7.40 vs 7.55 ms
   const int trk = g_tune[FS2_TUNE_TAPREG];
   if (trk >= 0 && !voc && tapaligned && (taps == 5 || taps == 9) && pad >= 0 && pad < taps) {
     const int cu = cu_count();
@@ -2932,6 +2935,8 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
     if (trk == 2) pick = ok8 ? 8 : 0;
     else if (trk == 1) pick = ok4 ? 4 : 0;
     else if (trk >= 3 && trk <= 5) pick = ok4 ? trk : 0;  // A/B variants below
+    else if (trk == 7 && ok4 && c_out <= 512 && t4 >= 3 * cu) pick = 3;  // A/B
+    else if (ok4 && c_out <= 256 && t4 >= 3 * cu) pick = 3;
     else if (ok4 && t4 >= 3 * cu) pick = 4;
     if (pick) {
       a.tiles_m = (int)(rows / (pick == 8 ? 256 : 128));

@@ -783,10 +783,12 @@ def test_conv_gemm_bf16_halo(B, T, cin, cout, k):
 @pytest.mark.parametrize("B,T,cin,cout,k,mode", [
     (4, 512, 256, 1024, 9, 2), (4, 512, 256, 1024, 9, 1), (6, 512, 1024, 256, 9, 1),
     (2, 256, 512, 512, 5, 2), (3, 128, 512, 512, 5, 1), (3, 128, 256, 320, 9, 1),
-    (2, 256, 256, 200, 9, 2)])
+    (2, 256, 256, 200, 9, 2), (6, 512, 1024, 256, 9, 0), (4, 512, 256, 1024, 9, 3),
+    (3, 128, 512, 512, 5, 3)])
 def test_conv_gemm_bf16_tapreg(B, T, cin, cout, k, mode):
-    """The tap-register halo kernel (FS2_TUNE_TAPREG = 1: 4-wave 128 x 64 tiles, 2: 8-wave
-    256 x 128 tiles) against fp32 math on the same bf16 data, forward (bias + ReLU) and data
+    """The tap-register halo kernel (FS2_TUNE_TAPREG = 0: automatic, 1: 4-wave 128 x 64 tiles,
+    2: 8-wave 256 x 128 tiles, 3: 4-wave 128 x 128 tiles at two blocks per CU) against fp32 math
+    on the same bf16 data, forward (bias + ReLU) and data
     gradient (+ residual), and bitwise against the halo kernels (knob -1): the same MFMAs per
     output in the same (channel block, tap, k-half) order.  With lens only the valid rows are
     compared: a wave whose 64-row band lies past the length computes nothing (epilogue of 0),

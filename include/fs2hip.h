@@ -250,7 +250,8 @@ int fs2_weight_prep_batch(int dtype, const int64_t* jobs, int n_jobs, int64_t n_
  *   FS2_TUNE_WGRAD_HALO    weight gradient of Conv1d taps 3/5/9: 0 = halo kernel, each wave
  *                          64 (o) x 16 (c) for all taps (default), 1 = halo kernel with the
  *                          round-1 32 x 32 wave quarters, 2 = 8-wave blocks of two k-groups
- *                          (half the row splits and fp32 slabs), -1 = tap-major kernel
+ *                          (half the row splits and fp32 slabs), 3 = three LDS stages (two
+ *                          k-tiles in flight), -1 = tap-major kernel
  *   FS2_TUNE_HALO_SPLITK   64x64 halo fwd/dX on an under-filled grid (long-K encoder data
  *                          gradient): 0 = automatic channel-block split (128x64 tiles when
  *                          T % 128 == 0), -1 = off, -2 = 64x64 tiles only, n = n splits

@@ -1262,8 +1262,8 @@ FS2_DEV void static_for(Fn&& fn) {
 // fragment F[i + j], where F[f] = rows f + S m of the band's halo (f < S + taps - 1).  The
 // S + taps - 1 halo fragments of a channel block are each read from LDS once and held in a
 // rolling register window (tap j uses F[j .. j + S - 1]: one new fragment per tap and k-half);
-// the k=9 decoder forward (64 x 64 per wave) reads 24 + 72 fragments per 288 MFMAs, the halo
-// kernel's 128 x 32 wave tile 180.  Same MFMAs per output in the same (channel block, tap, k-half) order as the halo
+// per 64-channel block a 64 x 32 wave tile (S = 4, k = 9) reads 24 halo + 36 weight fragments
+// for 144 MFMAs (0.42 per MFMA), the halo kernel's 128 x 32 wave tile 0.63.  Same MFMAs per output in the same (channel block, tap, k-half) order as the halo
 // kernels: bitwise equal where both compute.
 // LDS halo image: halo row h sits at position (h mod S) * RS + h / S, so every F[f] reads 16
 // consecutive positions (chunk swizzle c ^ (h / S & 7): conflict-free ds_read_b128); the LDS-DMA
@@ -2191,10 +2191,11 @@ __global__ __launch_bounds__(256, 2) void wgrad_k1_q(WgradGlds a) {
 // 26 instead of 40 fragment reads per wave and k-tile; the next tap's x fragment is read
 // under the current tap's MFMAs.  Each wave also carries the bias gradient of its 16 o rows
 // (one extra MFMA per k-step, evenly spread).  WS = 0: the 32 x 32 wave quarters of round 1.
-template <int TAPS, int WS, int KG = 1>
+template <int TAPS, int WS, int KG = 1, int ST = 2>
 __global__ __launch_bounds__(256 * KG, KG == 1 ? 2 : 1) void conv_wgrad_halo(WgradGlds a) {
   static_assert(KG == 1 || (KG == 2 && WS == 1), "k-groups: the 64 (o) x 16 (c) wave tiles");
-  constexpr int BO = 64, BC = 64, BK = 64, STAGES = 2, NTH = 256 * KG;
+  static_assert(ST == 2 || (ST == 3 && KG == 1), "three stages: one k-group");
+  constexpr int BO = 64, BC = 64, BK = 64, STAGES = ST, NTH = 256 * KG;
   constexpr int HX = 8;                      // halo rows allocated (taps <= 9)
   constexpr int A_E = BK * BO;               // dy image
   constexpr int X_E = (BK + HX) * BC;        // x halo image
@@ -2376,7 +2377,24 @@ __global__ __launch_bounds__(256 * KG, KG == 1 ? 2 : 1) void conv_wgrad_halo(Wgr
     }
   };
 
-  if constexpr (KG == 1) {
+  if constexpr (KG == 1 && ST == 3) {
+    // three stages, two k-tiles in flight: the wait before tile kt leaves this wave's pieces
+    // of tile kt + 1 outstanding (2 dy pieces + its 2 or 3 x-halo pieces: counted per wave)
+    int mine = 2;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) mine += wave + 4 * i < HP ? 1 : 0;
+    if (nk > 0) issue(0, 0);
+    if (nk > 1) issue(1, 1);
+    for (int kt = 0; kt < nk; ++kt) {
+      vm_wait_n(kt + 1 < nk ? mine : 0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (kt + 2 < nk) issue(kt + 2, (kt + 2) % 3);
+      compute(kt % 3);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  } else if constexpr (KG == 1) {
     kloop<STAGES, 5>(nk, issue, compute);  // per-wave DMA count varies (<= 5): kloop waits vmcnt(0)-style
   } else {
     // kloop's two-stage schedule with both groups in step: iteration it holds k-tile
@@ -2638,9 +2656,11 @@ int conv_wgrad_glds_launch(const void* dy, int64_t ldy, const void* x, int64_t l
     const unsigned hgrid = (unsigned)(a.tiles_o * a.tiles_k * splits);
     const bool quarters = g_tune[FS2_TUNE_WGRAD_HALO] == 1;  // round-1 wave tiles (A/B)
     const bool kg2 = g_tune[FS2_TUNE_WGRAD_HALO] == 2;       // two k-groups per block
-#define FS2_WH(T) (kg2 ? conv_wgrad_halo<T, 1, 2><<<hgrid, 512, 0, st>>>(a)        \
-                       : quarters ? conv_wgrad_halo<T, 0><<<hgrid, 256, 0, st>>>(a) \
-                                  : conv_wgrad_halo<T, 1><<<hgrid, 256, 0, st>>>(a))
+    const bool st3 = g_tune[FS2_TUNE_WGRAD_HALO] == 3;       // three LDS stages
+#define FS2_WH(T) (kg2 ? conv_wgrad_halo<T, 1, 2><<<hgrid, 512, 0, st>>>(a)              \
+                       : st3 ? conv_wgrad_halo<T, 1, 1, 3><<<hgrid, 256, 0, st>>>(a)      \
+                             : quarters ? conv_wgrad_halo<T, 0><<<hgrid, 256, 0, st>>>(a) \
+                                        : conv_wgrad_halo<T, 1><<<hgrid, 256, 0, st>>>(a))
     if (taps == 9) FS2_WH(9);
     else if (taps == 5) FS2_WH(5);
     else FS2_WH(3);

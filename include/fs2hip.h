@@ -288,7 +288,7 @@ int fs2_weight_prep_batch(int dtype, const int64_t* jobs, int n_jobs, int64_t n_
  *   FS2_TUNE_WGRAD_FUSE    k = 1 weight gradient (FS2_TUNE_WGRAD_K1 = 0): 0 = split slabs summed
  *                          by a reduce launch (default), 1 = the last split to finish a tile sums
  *                          them in split order inside the kernel (no reduce launch)
- *   FS2_TUNE_TAPREG        fwd/dX Conv1d taps 5 / 9 (C_in % 64 == 0, c_out % 128 == 0): 0 = the
+ *   FS2_TUNE_TAPREG        fwd/dX Conv1d taps 5 / 9 (C_in % 64 == 0, T % 128 == 0): 0 = the
  *                          tap-register halo kernel where its grid fills the chip (default:
  *                          4-wave 128 x 64 tiles at 3 blocks per CU, 128 x 128 at 2 for
  *                          c_out <= 256), -1 = off (the halo kernels above), 1 = force the

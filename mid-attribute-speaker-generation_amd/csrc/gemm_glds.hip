@@ -2949,7 +2949,7 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
   const int trk = g_tune[FS2_TUNE_TAPREG];
   if (trk >= 0 && !voc && tapaligned && (taps == 5 || taps == 9) && pad >= 0 && pad < taps) {
     const int cu = cu_count();
-    const int64_t t8 = (rows / 256) * ((c_out + 127) / 128), t4 = (rows / 128) * ((c_out + 63) / 64);
+    const int64_t t4 = (rows / 128) * ((c_out + 63) / 64);
     const bool ok8 = seq_len % 256 == 0, ok4 = seq_len % 128 == 0;
     int pick = 0;
     if (trk == 2) pick = ok8 ? 8 : 0;

@@ -446,13 +446,13 @@ def cpu_baseline(batch_np, steps=3):
 
 
 # ----------------------------------------------------------------------------- main
-def build_trainer(M, TR, dtype, dev, rank, graph=False):
+def build_trainer(M, TR, dtype, dev, rank, graph=False, data_parallel=None):
     pp, mc, tc, path = PKG.config.load_configs("JVS-VCTK")
     cdt = {"f32": torch.float32, "bf16": torch.bfloat16}[dtype]
     model = M.FastSpeech2(pp, mc, path, device=dev, compute_dtype=cdt)
     model.train()
     model.seed(1234 + rank)
-    return model, TR.Trainer(model, pp, mc, tc, graph=graph), tc
+    return model, TR.Trainer(model, pp, mc, tc, graph=graph, data_parallel=data_parallel), tc
 
 
 def launch_check(world, rank):
@@ -523,12 +523,22 @@ def main():
     if os.environ.get("FS2_MAIN_PRIORITY"):  # A/B: the step's main chain on a prioritised stream
         main_stream = torch.cuda.Stream(dev, priority=int(os.environ["FS2_MAIN_PRIORITY"]))
         torch.cuda.set_stream(main_stream)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+    # FS2_DP1=1 (A/B): at N = 1, run the step through the data-parallel path on a one-rank
+    # RCCL group (global denominators, bucketed all-reduce on the communication stream) to
+    # price that machinery without the interconnect
+    dp1 = world == 1 and os.environ.get("FS2_DP1") == "1"
+    if world > 1 or dp1:
+        if dp1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29533")
+            dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
-    use_graph = world == 1 and args.graph
+    use_graph = world == 1 and args.graph and not dp1
     model, trainer, tc = build_trainer(M, TR, args.dtype, dev, rank,
-                                       graph=use_graph and not args.use_clf)
+                                       graph=use_graph and not args.use_clf,
+                                       data_parallel=True if dp1 else None)
     if args.use_clf:
         import random
         G = importlib.import_module("mid-attribute-speaker-generation_amd.ge2e")
@@ -634,7 +644,8 @@ def main():
                           "padded_frames_per_rank_step": padded_local,
                           "parallelism": f"dp{world}",
                           "use_clf": bool(args.use_clf),
-                          "execution": "hip-graph replay" if use_graph else "eager"},
+                          "execution": "hip-graph replay" if use_graph else "eager",
+                          **({"data_parallel": "one-rank RCCL group (FS2_DP1)"} if dp1 else {})},
                "roofline": roof, "step_roofline": step_roof}
 
     # decoder FFT block fwd + bwd, 3 extra steps (rank 0's figures; every rank runs them so
@@ -714,7 +725,7 @@ def main():
             out["cpu_baseline"] = None
         out["final_loss"] = round(loss_now, 5)
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
     return 0
 

@@ -163,10 +163,14 @@ class Trainer:
     quantity the kernels read (dropout key, LR, Adam bias corrections, BN counters) lives in
     device memory, so a replay is exactly an eager step; the returned tensors are the graph's
     static outputs (overwritten by the next replay).  A batch of another shape re-captures.
+
+    ``data_parallel`` (default: world size > 1) selects the data-parallel step -- global loss
+    denominators, bucketed gradient all-reduce on the communication stream; forcing it on a
+    one-rank group runs that code path on one GPU (tests/test_dp.py).
     """
 
     def __init__(self, model, preprocess_config, model_config, train_config, current_step=0,
-                 process_group=None, bucket_bytes=32 << 20, graph=False):
+                 process_group=None, bucket_bytes=32 << 20, graph=False, data_parallel=None):
         self.model = model
         self.graph_mode = bool(graph)
         self._graph = None
@@ -187,8 +191,11 @@ class Trainer:
                           "(HIP-graph replay captures whole optimiser steps only)", stacklevel=2)
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
+        self.dp = self.world > 1 if data_parallel is None else bool(data_parallel)
+        if self.dp and not dist.is_initialized():
+            raise ValueError("data_parallel needs an initialised process group")
         self.buckets = None
-        if self.world > 1:
+        if self.dp:
             arena = model.arena()
             with torch.no_grad():  # identical initial weights on every rank
                 dist.broadcast(arena.flat, src=0, group=process_group)
@@ -241,13 +248,13 @@ class Trainer:
         self.batch_step += 1
         acc = dict(grad_acc_step=self.grad_acc, update=update)
         if clf is not None:
-            if self.world > 1:
+            if self.dp:
                 raise NotImplementedError("use_clf with data parallelism")
             return train_step(self.model, self.opt, self.Loss, self.eLoss, batch, self.clip,
                               clf=clf, clf_args=clf_args, **acc)
-        if self.graph_mode and self.world == 1 and self.grad_acc == 1:
+        if self.graph_mode and not self.dp and self.grad_acc == 1:
             return self._graph_step(batch)
-        if self.world > 1:
+        if self.dp:
             glob = self._global_denominators(batch)
             self.Loss.denoms = glob[0:2]
             self.eLoss.denom = glob[2:3]

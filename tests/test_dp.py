@@ -218,3 +218,55 @@ def test_data_parallel_trainer_nccl_matches_emulation():
     with tempfile.TemporaryDirectory() as out:
         mp.spawn(_dp_worker, args=(2, _port(), out, "nccl"), nprocs=2, join=True)
         _check_dp(out)
+
+
+def _nccl_one_rank_worker(rank, port, out):
+    """One rank on a one-member RCCL group with the data-parallel step forced on, against a
+    plain Trainer on the same GPU and batches."""
+    import sys
+    sys.path.insert(0, REPO)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    pkg = importlib.import_module("mid-attribute-speaker-generation_amd")
+    M = importlib.import_module("mid-attribute-speaker-generation_amd.model")
+    tr = importlib.import_module("mid-attribute-speaker-generation_amd.train")
+    pp, mc, tc, path = pkg.config.load_configs("JVS-VCTK")
+    res = {}
+    for dp in (True, False):
+        model = M.FastSpeech2(pp, mc, path, device=dev)
+        pkg.seeded.load_seeded_(model)
+        model.dropout = False
+        model.train()
+        t = tr.Trainer(model, pp, mc, tc, data_parallel=dp)
+        if dp:
+            assert t.buckets is not None and t.buckets.comm is not None
+            t.buckets.log = []
+        losses = []
+        for s in range(2):
+            losses.append([float(x) for x in t.step(_shard(pkg, 0, dev, s))[0]])
+        torch.cuda.synchronize()
+        res[dp] = {"loss": losses, "w": model.arena().flat.cpu(),
+                   "log": list(t.buckets.log) if dp else None}
+    torch.save(res, f"{out}/nccl1.pt")
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_data_parallel_rccl_one_rank_matches_plain_step():
+    """The RCCL code path on the one-GPU pool: a one-member "nccl" group with
+    Trainer(data_parallel=True) -- rank-0 weight broadcast, device-side global denominators
+    all-reduced, every gradient bucket all-reduced asynchronously from the communication stream
+    against events of the compute streams, joined before the clip -- over 2 optimiser steps
+    equals the plain single-process step (losses and weights to fp32 rounding)."""
+    with tempfile.TemporaryDirectory() as out:
+        mp.spawn(_nccl_one_rank_worker, args=(_port(), out), nprocs=1, join=True)
+        r = torch.load(f"{out}/nccl1.pt")
+    dp, plain = r[True], r[False]
+    assert sorted(set(dp["log"])) == list(range(max(dp["log"]) + 1))  # every bucket went out
+    for a_, b_ in zip(dp["loss"], plain["loss"]):
+        for x, y in zip(a_, b_):
+            assert abs(x - y) <= 1e-5 * max(abs(y), 1e-6), (a_, b_)
+    w, wp = dp["w"], plain["w"]
+    assert (w - wp).abs().max().item() <= 1e-6 * wp.abs().max().item()

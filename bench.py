@@ -531,9 +531,9 @@ def main():
         if dp1:
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             os.environ.setdefault("MASTER_PORT", "29533")
-            dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+            TR.init_data_parallel(dev, rank=0, world_size=1)
         else:
-            dist.init_process_group("nccl", device_id=dev)
+            TR.init_data_parallel(dev)
 
     use_graph = world == 1 and args.graph and not dp1
     model, trainer, tc = build_trainer(M, TR, args.dtype, dev, rank,

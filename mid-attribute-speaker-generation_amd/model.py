@@ -264,6 +264,34 @@ class PositionwiseFeedForward(nn.Module):
         self.layer_norm = LayerNorm(d_in)
 
 
+# Weight-gradient streams created ahead of the communicator, per device index: see
+# reserve_streams.
+_RESERVED_SIDE = {}
+
+
+def reserve_streams(device):
+    """Give the step's two compute streams hardware queues of their own; call it before
+    anything else creates streams on ``device`` -- in particular before
+    ``dist.init_process_group(..., device_id=...)``, whose RCCL communicator creates streams.
+
+    HIP maps streams onto at most ``GPU_MAX_HW_QUEUES`` hardware queues per priority (4 on
+    the MI355X boxes): the first streams created get fresh queues, later ones share the
+    least-used queue, ties broken arbitrarily.  Two streams on one queue run in order, so the
+    weight-gradient stream sharing the legacy stream's queue serialises the step: the data-
+    parallel step on a one-rank group lost 1.9 ms/step (9.3 vs 7.4 ms) in 3 of 4 runs that
+    way (profiles/r3_ab_experiments.txt).  This launches on the legacy stream (its queue is
+    created on first use) and creates the weight-gradient stream next, so both get fresh
+    queues; FastSpeech2.side_stream() then hands out the reserved stream.
+    """
+    dev = torch.device(device)
+    idx = torch.cuda.current_device() if dev.index is None else dev.index
+    if idx not in _RESERVED_SIDE:
+        torch.zeros(1, device=dev).add_(1)  # first use of the legacy stream: its queue
+        _RESERVED_SIDE[idx] = torch.cuda.Stream(device=dev)
+        torch.cuda.synchronize(dev)
+    return _RESERVED_SIDE[idx]
+
+
 def _flat_view(t, n):
     """A 1-D view of ``n`` elements starting at ``t``'s first element (same storage)."""
     return t.detach().as_strided((n,), (1,), t.storage_offset())
@@ -976,10 +1004,11 @@ class FastSpeech2(nn.Module):
             prio = int(os.environ.get("FS2_SIDE_PRIORITY", "0"))
             dev = self.encoder.position_enc.device
             frac = float(os.environ.get("FS2_SIDE_CUMASK", "0") or 0)
-            if 0 < frac < 1:
+            if 0 < frac <= 1:
                 # A/B: the weight-gradient stream restricted to a fraction of the CUs (a hash
                 # spreads the mask over every XCD whatever the bit -> CU numbering); meant with
-                # FS2_MAIN_PRIORITY, which moves the main chain off the legacy default stream
+                # FS2_MAIN_PRIORITY, which moves the main chain off the legacy default stream.
+                # 1 = every CU: a CU-masked stream always gets a hardware queue of its own
                 import ctypes
                 n = torch.cuda.get_device_properties(dev).multi_processor_count
                 bits = [(i * 37) % 64 < frac * 64 for i in range(n)]
@@ -994,6 +1023,8 @@ class FastSpeech2(nn.Module):
                 if rc != 0:
                     raise RuntimeError(f"hipExtStreamCreateWithCUMask failed ({rc})")
                 self._side = torch.cuda.ExternalStream(s.value, device=dev)
+            elif prio == 0 and dev.index in _RESERVED_SIDE:
+                self._side = _RESERVED_SIDE[dev.index]
             else:
                 self._side = torch.cuda.Stream(device=dev, priority=prio)
         return self._side

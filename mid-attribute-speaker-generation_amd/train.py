@@ -80,6 +80,19 @@ def train_step(model, optimizer, Loss, eLoss, batch, grad_clip_thresh=1.0, grad_
     return losses, eloss, gnorm, output
 
 
+def init_data_parallel(device, **kwargs):
+    """``dist.init_process_group("nccl", ...)`` for the data-parallel step on ``device``.
+
+    Reserves the step's compute streams first (model.reserve_streams: the RCCL communicator
+    creates streams of its own at init) and puts the collectives on a high-priority stream,
+    whose hardware queues are a pool apart from the compute streams'.  Extra keyword arguments
+    go to ``init_process_group`` (rank, world_size, ...)."""
+    from .model import reserve_streams
+    reserve_streams(device)
+    opts = dist.ProcessGroupNCCL.Options(is_high_priority_stream=True)
+    dist.init_process_group("nccl", device_id=device, pg_options=opts, **kwargs)
+
+
 class GradBuckets:
     """Bucketed, backward-overlapped all-reduce of the arena's flat gradient buffer."""
 
@@ -106,7 +119,10 @@ class GradBuckets:
         # producers of the gradients besides the current stream (the weight-gradient side
         # stream): a callable returning the streams, each waited for by event at a launch
         self.producers = None
-        self.comm = torch.cuda.Stream(device=arena.grad.device) if arena.grad.is_cuda else None
+        # high priority: its own pool of hardware queues, so the event waits it carries never
+        # sit in a compute stream's queue (model.reserve_streams)
+        self.comm = (torch.cuda.Stream(device=arena.grad.device, priority=-1)
+                     if arena.grad.is_cuda else None)
         self.log = None  # optional list: bucket launches are appended (tests)
         del index
         self.reset()

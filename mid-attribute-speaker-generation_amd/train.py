@@ -18,6 +18,7 @@ Data parallel: one process per GPU, batch sharded by utterance.
   stream ever waits for a bucket (only the clip at the end of the step waits for them all).
 * BatchNorm statistics stay per rank (DataParallel's per-replica semantics).
 """
+import os
 import warnings
 
 import torch
@@ -84,12 +85,16 @@ def init_data_parallel(device, **kwargs):
     """``dist.init_process_group("nccl", ...)`` for the data-parallel step on ``device``.
 
     Reserves the step's compute streams first (model.reserve_streams: the RCCL communicator
-    creates streams of its own at init) and puts the collectives on a high-priority stream,
-    whose hardware queues are a pool apart from the compute streams'.  Extra keyword arguments
-    go to ``init_process_group`` (rank, world_size, ...)."""
+    creates streams of its own at init), so the legacy stream, the weight-gradient stream and
+    then ProcessGroupNCCL's collective stream take the first hardware queues.  Normal priority:
+    a high-priority stream in the process made every kernel ~2x slower (21 vs 7.5 ms/step,
+    profiles/r3_ab_experiments.txt).  Extra keyword arguments go to ``init_process_group``
+    (rank, world_size, ...)."""
     from .model import reserve_streams
-    reserve_streams(device)
-    opts = dist.ProcessGroupNCCL.Options(is_high_priority_stream=True)
+    if os.environ.get("FS2_DP_RESERVE", "1") == "1":  # A/B knob
+        reserve_streams(device)
+    opts = dist.ProcessGroupNCCL.Options(
+        is_high_priority_stream=os.environ.get("FS2_DP_PG_HIPRIO", "0") == "1")  # A/B knob
     dist.init_process_group("nccl", device_id=device, pg_options=opts, **kwargs)
 
 
@@ -117,12 +122,18 @@ class GradBuckets:
                                 arena.offsets[last] + arena.params[last].numel()))
         self.sizes = [len(idxs) for idxs in buckets]
         # producers of the gradients besides the current stream (the weight-gradient side
-        # stream): a callable returning the streams, each waited for by event at a launch
+        # stream): a callable returning the streams
         self.producers = None
-        # high priority: its own pool of hardware queues, so the event waits it carries never
-        # sit in a compute stream's queue (model.reserve_streams)
-        self.comm = (torch.cuda.Stream(device=arena.grad.device, priority=-1)
-                     if arena.grad.is_cuda else None)
+        # where a bucket's all-reduce is issued from: the last producer stream (the side
+        # stream, which trails the main chain), after it waits on an event of the current
+        # stream.  A separate communication stream would need a hardware queue of its own,
+        # and HIP shares 4 per priority among every stream of the process (high-priority
+        # streams push the process past the queues the scheduler maps at once: 2.8x slower
+        # steps, profiles/r3_ab_experiments.txt).  FS2_DP_COMM_STREAM=1: separate stream (A/B)
+        self.comm = None
+        if arena.grad.is_cuda and os.environ.get("FS2_DP_COMM_STREAM") == "1":
+            self.comm = torch.cuda.Stream(device=arena.grad.device,
+                                          priority=int(os.environ.get("FS2_DP_COMM_PRIORITY", "0")))
         self.log = None  # optional list: bucket launches are appended (tests)
         del index
         self.reset()
@@ -136,19 +147,23 @@ class GradBuckets:
         s, e = self.ranges[b]
         if self.log is not None:
             self.log.append(b)
-        if self.comm is None:
+        cur = torch.cuda.current_stream() if self.arena.grad.is_cuda else None
+        prods = [st for st in (self.producers() if self.producers else ()) if st is not None]
+        if cur is None or (self.comm is None and not prods):
             self.works.append(dist.all_reduce(self.arena.grad[s:e], group=self.group,
                                               async_op=True))
             return
         # the bucket's gradients are complete in stream order on the current stream and on
-        # the producer streams: the communication stream waits on an event of each (the
-        # compute streams themselves never wait for the collective)
-        for st in [torch.cuda.current_stream()] + list(self.producers() if self.producers else ()):
-            if st is not None:
+        # the producer streams: the issuing stream waits on an event of each of the others
+        # (the main chain never waits for the collective or for the side stream here)
+        issue = self.comm if self.comm is not None else prods[-1]
+        for st in [cur] + prods:
+            if st is not issue:
                 ev = torch.cuda.Event()
                 ev.record(st)
-                self.comm.wait_event(ev)
-        with torch.cuda.stream(self.comm):
+                issue.wait_event(ev)
+        self._issue = issue
+        with torch.cuda.stream(issue):
             self.works.append(dist.all_reduce(self.arena.grad[s:e], group=self.group,
                                               async_op=True))
 
@@ -165,8 +180,9 @@ class GradBuckets:
             self.next += 1
         for w in self.works:
             w.wait()  # stream-ordered: the clip/Adam kernels queue behind the collectives
-        if self.comm is not None:
-            torch.cuda.current_stream().wait_stream(self.comm)
+        if getattr(self, "_issue", None) is not None:
+            torch.cuda.current_stream().wait_stream(self._issue)
+            self._issue = None
         self.reset()
 
 

@@ -243,7 +243,7 @@ def _nccl_one_rank_worker(rank, port, out):
         model.train()
         t = tr.Trainer(model, pp, mc, tc, data_parallel=dp)
         if dp:
-            assert t.buckets is not None and t.buckets.comm is not None
+            assert t.buckets is not None
             t.buckets.log = []
         losses = []
         for s in range(2):
@@ -259,7 +259,7 @@ def _nccl_one_rank_worker(rank, port, out):
 def test_data_parallel_rccl_one_rank_matches_plain_step():
     """The RCCL code path on the one-GPU pool: a one-member "nccl" group with
     Trainer(data_parallel=True) -- rank-0 weight broadcast, device-side global denominators
-    all-reduced, every gradient bucket all-reduced asynchronously from the communication stream
+    all-reduced, every gradient bucket all-reduced asynchronously from the weight-gradient stream
     against events of the compute streams, joined before the clip -- over 2 optimiser steps
     equals the plain single-process step (losses and weights to fp32 rounding)."""
     with tempfile.TemporaryDirectory() as out:

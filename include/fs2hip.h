@@ -316,6 +316,18 @@ int fs2_conv_wgrad(int dtype, const void* dy, int64_t ldy, const void* x, int64_
                    float* db, int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out, int taps,
                    int pad, const int64_t* lens, float* ws, int64_t ws_bytes, void* stream);
 
+/* Several k = 1 weight gradients over the same rows in one launch (+ one split reduce):
+ * for each job j of `jobs` (HOST memory, n_jobs <= 4 rows of 8 int64:
+ * {dy, ldy, x, ldx, dw, db, c_in, c_out}, pointers as integers, db may be 0)
+ *   dw_j[o, c] += sum_r dy_j[r, o] * x_j[r, c],   db_j[o] += sum_r dy_j[r, o].
+ * The FFT block's QKV, fc and w_2 weight gradients (SubLayers.py:39-55,88) run as one grid;
+ * lens (optional): 64-row k-tiles made only of padding rows are skipped.  Fixed reduction
+ * order (bitwise reproducible).  ws_bytes >= fs2_conv_wgrad_k1_multi_ws_bytes(...).           */
+int64_t fs2_conv_wgrad_k1_multi_ws_bytes(const int64_t* jobs, int n_jobs, int64_t rows);
+int fs2_conv_wgrad_k1_multi(int dtype, const int64_t* jobs, int n_jobs, int64_t rows,
+                            int64_t seq_len, const int64_t* lens, float* ws, int64_t ws_bytes,
+                            void* stream);
+
 /* Column sums (bias / LayerNorm-affine / BatchNorm gradients):
  *   out[c] (+)= sum_r x[r, c]   in a fixed order (partials in ws, then in-order sum).   */
 int64_t fs2_colsum_ws_bytes(int64_t rows, int64_t cols);

@@ -86,6 +86,12 @@ int conv_wgrad_glds_launch(const void* dy, int64_t ldy, const void* x, int64_t l
                            float* db, int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out,
                            int taps, int pad, const int64_t* lens, int splits, int tile, float* ws,
                            unsigned* ctr, hipStream_t st);
+int conv_wgrad_band_launch(const void* dy, int64_t ldy, const void* x, int64_t ldx, float* dw,
+                           float* db, int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out,
+                           int taps, int pad, const int64_t* lens, hipStream_t st);
+int64_t wgrad_k1_multi_ws_floats(const int64_t* jobs, int n, int64_t rows);
+int wgrad_k1_multi_launch(const int64_t* jobs, int n, int64_t rows, int64_t seq_len,
+                          const int64_t* lens, float* ws, hipStream_t st);
 int conv_wgrad_bf16_launch(const void* dy, int64_t ldy, const void* x, int64_t ldx, float* slab,
                            int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out, int taps,
                            int pad, int splits, hipStream_t st);

@@ -414,16 +414,6 @@ static int wgrad_splits(int64_t rows, int64_t c_in, int64_t c_out, int taps) {
     if (s > rows / 512) s = rows / 512;
     return (int)(s < 1 ? 1 : s);
   }
-  if ((taps == 3 || taps == 5 || taps == 9) && c_in % 64 == 0 && c_out % 64 == 0 &&
-      g_tune[FS2_TUNE_WGRAD_HALO] == 2) {
-    // conv_wgrad_halo with two k-groups per block (512 threads, one block per CU): about 256
-    // blocks of 64 x 64 tiles, each split at least 8 k-tiles of 64 rows
-    const int64_t t = (c_out / 64) * (c_in / 64);
-    int64_t s = (256 + t - 1) / t;
-    if (s > rows / 512) s = rows / 512;
-    if (s > 64) s = 64;
-    return (int)(s < 1 ? 1 : s);
-  }
   const int64_t Kp = (int64_t)taps * c_in;
   const int bt = wgrad_tile(rows, c_in, c_out, taps);
   const int64_t tiles = ((c_out + bt - 1) / bt) * ((Kp + bt - 1) / bt);
@@ -619,6 +609,35 @@ int fs2_conv_wgrad(int dtype, const void* dy, int64_t ldy, const void* x, int64_
   wgrad_reduce<<<blocks, 256, 0, st>>>(ws, S, (int)c_out, (int)c_in, taps, dw);
   if (db) return colsum_launch((const float*)dy, ldy, rows, c_out, db, 1, ws + slab_floats, st);
   return launch_status("fs2_conv_wgrad");
+}
+
+int64_t fs2_conv_wgrad_k1_multi_ws_bytes(const int64_t* jobs, int n_jobs, int64_t rows) {
+  int64_t b = wgrad_k1_multi_ws_floats(jobs, n_jobs, rows) * 4;
+  for (int j = 0; j < n_jobs; ++j) {  // the fp32 path runs the jobs one by one
+    const int64_t w = fs2_conv_wgrad_ws_bytes(rows, jobs[8 * j + 6], jobs[8 * j + 7], 1);
+    b = w > b ? w : b;
+  }
+  return b;
+}
+
+int fs2_conv_wgrad_k1_multi(int dtype, const int64_t* jobs, int n_jobs, int64_t rows,
+                            int64_t seq_len, const int64_t* lens, float* ws, int64_t ws_bytes,
+                            void* stream) {
+  FS2_CHECK_ARG(jobs && n_jobs >= 1 && n_jobs <= 4, "fs2_conv_wgrad_k1_multi: 1..4 jobs");
+  FS2_CHECK_ARG(ws_bytes >= fs2_conv_wgrad_k1_multi_ws_bytes(jobs, n_jobs, rows),
+                "fs2_conv_wgrad_k1_multi: workspace too small");
+  FS2_CHECK_ARG(seq_len > 0 && rows % seq_len == 0, "fs2_conv_wgrad_k1_multi: rows must be batch x seq_len");
+  if (rows == 0) return FS2_OK;
+  if (dtype == FS2_BF16 && !g_tune[FS2_TUNE_LEGACY_GEMM])
+    return wgrad_k1_multi_launch(jobs, n_jobs, rows, seq_len, lens, ws, as_stream(stream));
+  for (int j = 0; j < n_jobs; ++j) {
+    const int64_t* r = jobs + 8 * j;
+    const int rc = fs2_conv_wgrad(dtype, (const void*)r[0], r[1], (const void*)r[2], r[3],
+                                  (float*)r[4], (float*)r[5], rows, seq_len, r[6], r[7], 1, 0, lens,
+                                  ws, ws_bytes, stream);
+    if (rc) return rc;
+  }
+  return FS2_OK;
 }
 
 int64_t fs2_colsum_ws_bytes(int64_t rows, int64_t cols) {

@@ -2175,44 +2175,30 @@ __global__ __launch_bounds__(256, 2) void wgrad_k1_q(WgradGlds a) {
 }
 
 // Halo weight gradient for Conv1d with 2 <= taps <= 9 (C_in, C_out multiples of 64, T a
-// multiple of 64): a block owns a 64 (o) x 64 (c) tile for ALL taps.  Per 64-row k-tile it
-// stages the dy tile (64 x 64) and the x rows of the tile plus the tap halo
-// (64 + taps - 1 rows, zero outside the utterance) ONCE, and tap j reads the x image at row
-// offset j: the tap-major kernel above re-stages both operands for every (tap, channel)
-// column tile, i.e. taps x more staging per FLOP.  dy fragments are read once per k-step
-// and reused by every tap.  Both images are [rows][64] bf16 (128-B rows) filled by LDS-DMA
-// with the chunk swizzle ((R >> 1) & 3) << 1 and read with ds_read_b64_tr_b16 (rows
-// {4g+q} u {16+4g+q} of a 32-row step; a row offset j keeps the pair in one swizzle class).
-// Output: the same split-K slab layout (and bias slab) as conv_wgrad_tn_glds.
-//
-// WS = 1 (default): each wave owns 64 (o) x 16 (c) of the block tile for all taps instead of
-// a 32 x 32 quarter: the dy fragments (4 per k-step) are read once and reused by every tap,
-// and a tap costs ONE shifted x fragment for 4 MFMAs (the 32 x 32 quarter needs two for 4),
-// 26 instead of 40 fragment reads per wave and k-tile; the next tap's x fragment is read
-// under the current tap's MFMAs.  Each wave also carries the bias gradient of its 16 o rows
-// (one extra MFMA per k-step, evenly spread).  WS = 0: the 32 x 32 wave quarters of round 1.
-template <int TAPS, int WS, int KG = 1, int ST = 2>
-__global__ __launch_bounds__(256 * KG, KG == 1 ? 2 : 1) void conv_wgrad_halo(WgradGlds a) {
-  static_assert(KG == 1 || (KG == 2 && WS == 1), "k-groups: the 64 (o) x 16 (c) wave tiles");
-  static_assert(ST == 2 || (ST == 3 && KG == 1), "three stages: one k-group");
-  constexpr int BO = 64, BC = 64, BK = 64, STAGES = ST, NTH = 256 * KG;
+// multiple of 64), the split-K path for grids that conv_wgrad_band (wgrad.hip) cannot fill:
+// a block owns a 64 (o) x 64 (c) tile for ALL taps.  Per 64-row k-tile it stages the dy tile
+// (64 x 64) and the x rows of the tile plus the tap halo (64 + taps - 1 rows, zero outside the
+// utterance) ONCE, and tap j reads the x image at row offset j.  Both images are [rows][64]
+// bf16 (128-B rows) filled by LDS-DMA with the chunk swizzle ((R >> 1) & 3) << 1 and read with
+// ds_read_b64_tr_b16 (rows {4g+q} u {16+4g+q} of a 32-row step).  Each wave owns 64 (o) x 16
+// (c) for all taps: the dy fragments (4 per k-step) are read once and reused by every tap, a
+// tap costs ONE shifted x fragment for 4 MFMAs, and the next taps' x fragments are read under
+// the current tap's MFMAs.  Each wave also carries the bias gradient of its 16 o rows.
+// Output: the split-K slab layout (and bias slab) of conv_wgrad_tn_glds.
+template <int TAPS>
+__global__ __launch_bounds__(256, 2) void conv_wgrad_halo(WgradGlds a) {
+  constexpr int BO = 64, BC = 64, BK = 64, STAGES = 2;
   constexpr int HX = 8;                      // halo rows allocated (taps <= 9)
   constexpr int A_E = BK * BO;               // dy image
   constexpr int X_E = (BK + HX) * BC;        // x halo image
   constexpr int STAGE_E = A_E + X_E;
   constexpr int MAXKT = 1024;
-  __shared__ __attribute__((aligned(1024))) u16 smem[KG * STAGES * STAGE_E + MAXKT + 64];
-  short* ktl = reinterpret_cast<short*>(smem + KG * STAGES * STAGE_E);
-  int* wcnt = reinterpret_cast<int*>(smem + KG * STAGES * STAGE_E + MAXKT);
+  __shared__ __attribute__((aligned(1024))) u16 smem[STAGES * STAGE_E + MAXKT + 64];
+  short* ktl = reinterpret_cast<short*>(smem + STAGES * STAGE_E);
+  int* wcnt = reinterpret_cast<int*>(smem + STAGES * STAGE_E + MAXKT);
 
   const int tid = threadIdx.x, lane = tid & 63;
-  // KG = 2: waves 4 g .. 4 g + 3 form k-group g, which takes every other 64-row k-tile of the
-  // split into its own LDS stages; the groups' partial tiles are summed (group 0 + group 1) at
-  // the end, so a split covers twice the rows of a 4-wave block (half the fp32 slabs)
-  const int wave_all = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int grp = wave_all >> 2, wave = wave_all & 3;
-  u16* const gsm = smem + grp * STAGES * STAGE_E;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3, r16 = lane & 15;
 
   const int per_split = a.tiles_o * a.tiles_k;  // tiles_k = C_in / 64 here
@@ -2230,7 +2216,7 @@ __global__ __launch_bounds__(256 * KG, KG == 1 ? 2 : 1) void conv_wgrad_halo(Wgr
   int nk = nk_all;
   if (use_list) {  // ordered list of k-tiles holding a real row (as conv_wgrad_tn_glds)
     int total = 0;
-    for (int cc0 = 0; cc0 < nk_all; cc0 += NTH) {
+    for (int cc0 = 0; cc0 < nk_all; cc0 += 256) {
       const int kt = cc0 + tid;
       bool v = false;
       if (kt < nk_all) {
@@ -2238,14 +2224,14 @@ __global__ __launch_bounds__(256 * KG, KG == 1 ? 2 : 1) void conv_wgrad_halo(Wgr
         v = !rows_all_padding(a.lens, a.T, k0, k0 + BK < r_end ? k0 + BK : r_end);
       }
       const uint64_t mask = __ballot(v);
-      if (lane == 0) wcnt[wave_all] = __popcll(mask);
+      if (lane == 0) wcnt[wave] = __popcll(mask);
       __syncthreads();
       int before = total;
-      for (int w = 0; w < wave_all; ++w) before += wcnt[w];
+      for (int w = 0; w < wave; ++w) before += wcnt[w];
       const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
       if (v) ktl[before + below] = (short)kt;
-      for (int w = 0; w < 4 * KG; ++w) total += wcnt[w];
+      for (int w = 0; w < 4; ++w) total += wcnt[w];
       __syncthreads();
     }
     nk = total;
@@ -2256,7 +2242,7 @@ __global__ __launch_bounds__(256 * KG, KG == 1 ? 2 : 1) void conv_wgrad_halo(Wgr
   const int lrow = lane >> 3, lch = lane & 7;
   const int HR = BK + a.taps - 1, HP = (HR + 7) / 8;  // x halo rows / 8-row pieces
   auto issue = [&](int kt, int stage) {
-    u16* As = gsm + stage * STAGE_E;
+    u16* As = smem + stage * STAGE_E;
     u16* Xs = As + A_E;
     const int tile = use_list ? (int)ktl[kt] : kt;
     const int64_t k0 = r_begin + (int64_t)tile * BK;
@@ -2283,32 +2269,19 @@ __global__ __launch_bounds__(256 * KG, KG == 1 ? 2 : 1) void conv_wgrad_halo(Wgr
     }
   };
 
-  constexpr int NA = WS ? 4 : 2, NB = WS ? 1 : 2;  // A (o) / B (c) fragments per wave
-  f32x4 acc[TAPS][NA][NB], accb[2];
+  f32x4 acc[TAPS][4], accb = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int j = 0; j < TAPS; ++j)
 #pragma unroll
-    for (int i = 0; i < NA; ++i)
-#pragma unroll
-      for (int jj = 0; jj < NB; ++jj) acc[j][i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
-  accb[0] = accb[1] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const bool do_bias = a.bslab != nullptr && tc == 0 && (WS || wn == 0);  // wave-uniform
+    for (int i = 0; i < 4; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool do_bias = a.bslab != nullptr && tc == 0;  // block-uniform
   bf16x8g ones;
 #pragma unroll
   for (int e = 0; e < 8; ++e) ones[e] = (__bf16)1.0f;
 
-  // transposed fragment: 16 columns at col0, rows rb + {4g+q} and rb + {16+4g+q}
+  // transposed fragment (asm reads, see ds_tr16; the caller waits with lgkm_wait): 16 columns
+  // at col0, rows rb + {4g+q} and rb + {16+4g+q}
   auto tr_frag = [&](const u16* img, int rb, int col0) -> bf16x8g {
-    const int R = rb + 4 * g + q;
-    const int lc = (col0 >> 3) + (p >> 1);
-    const int off = R * 64 + ((lc ^ swz(R)) << 3) + ((p & 1) << 2);
-    const s16x4g lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4g*)(img + off));
-    const s16x4g hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4g*)(img + off + 16 * 64));
-    return __builtin_bit_cast(bf16x8g, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-  };
-  // the same fragment by two asm reads (see ds_tr16: the builtin made every read wait for the
-  // next k-tile's DMA); the caller waits with lgkm_wait before use
-  auto tr_frag_asm = [&](const u16* img, int rb, int col0) -> bf16x8g {
     const int R = rb + 4 * g + q;
     const int lc = (col0 >> 3) + (p >> 1);
     const int off = R * 64 + ((lc ^ swz(R)) << 3) + ((p & 1) << 2);
@@ -2317,164 +2290,57 @@ __global__ __launch_bounds__(256 * KG, KG == 1 ? 2 : 1) void conv_wgrad_halo(Wgr
     return __builtin_bit_cast(bf16x8g, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
   };
   auto compute = [&](int stage) {
-    const u16* As = gsm + stage * STAGE_E;
+    const u16* As = smem + stage * STAGE_E;
     const u16* Xs = As + A_E;
-    if constexpr (WS == 1) {
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        // x fragments two taps ahead in a ring of three: tap j's MFMAs wait only for the reads
-        // up to its fragment (the LDS latency exceeds one tap's 4 MFMAs)
-        bf16x8g fa[4], fb[3];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) fa[i] = tr_frag_asm(As, ks * 32, i * 16);
-        fb[0] = tr_frag_asm(Xs, ks * 32, wave * 16);
-        if (TAPS > 1) fb[1] = tr_frag_asm(Xs, ks * 32 + 1, wave * 16);
-#pragma unroll
-        for (int j = 0; j < TAPS; ++j) {
-          if (j + 2 < TAPS) {
-            fb[(j + 2) % 3] = tr_frag_asm(Xs, ks * 32 + j + 2, wave * 16);
-            lgkm_wait<4>();  // all but the x fragments of taps j + 1, j + 2 landed
-          } else if (j + 1 < TAPS) {
-            lgkm_wait<2>();
-          } else {
-            lgkm_wait<0>();
-          }
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            acc[j][i][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j % 3], acc[j][i][0],
-                                                                   0, 0, 0);
-        }
-        if (do_bias) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            if (i == wave)
-              accb[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], ones, accb[0], 0, 0, 0);
-        }
-      }
-      return;
-    }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      bf16x8g fa[2];
+      // x fragments two taps ahead in a ring of three: tap j's MFMAs wait only for the reads
+      // up to its fragment (the LDS latency exceeds one tap's 4 MFMAs)
+      bf16x8g fa[4], fb[3];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) fa[i] = tr_frag(As, ks * 32, wm * 32 + i * 16);
-      if (do_bias) {
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-          accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], ones, accb[i], 0, 0, 0);
-      }
+      for (int i = 0; i < 4; ++i) fa[i] = tr_frag(As, ks * 32, i * 16);
+      fb[0] = tr_frag(Xs, ks * 32, wave * 16);
+      if (TAPS > 1) fb[1] = tr_frag(Xs, ks * 32 + 1, wave * 16);
 #pragma unroll
       for (int j = 0; j < TAPS; ++j) {
-        bf16x8g fb[2];
+        if (j + 2 < TAPS) {
+          fb[(j + 2) % 3] = tr_frag(Xs, ks * 32 + j + 2, wave * 16);
+          lgkm_wait<4>();  // all but the x fragments of taps j + 1, j + 2 landed
+        } else if (j + 1 < TAPS) {
+          lgkm_wait<2>();
+        } else {
+          lgkm_wait<0>();
+        }
 #pragma unroll
-        for (int jj = 0; jj < 2; ++jj) fb[jj] = tr_frag(Xs, ks * 32 + j, wn * 32 + jj * 16);
+        for (int i = 0; i < 4; ++i)
+          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j % 3], acc[j][i], 0, 0, 0);
+      }
+      if (do_bias) {
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int jj = 0; jj < 2; ++jj)
-            acc[j][i][jj % NB] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[jj], acc[j][i][jj % NB], 0, 0, 0);
+        for (int i = 0; i < 4; ++i)
+          if (i == wave) accb = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], ones, accb, 0, 0, 0);
       }
     }
   };
 
-  if constexpr (KG == 1 && ST == 3) {
-    // three stages, two k-tiles in flight: the wait before tile kt leaves this wave's pieces
-    // of tile kt + 1 outstanding (2 dy pieces + its 2 or 3 x-halo pieces: counted per wave)
-    int mine = 2;
-#pragma unroll
-    for (int i = 0; i < 3; ++i) mine += wave + 4 * i < HP ? 1 : 0;
-    if (nk > 0) issue(0, 0);
-    if (nk > 1) issue(1, 1);
-    for (int kt = 0; kt < nk; ++kt) {
-      vm_wait_n(kt + 1 < nk ? mine : 0);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      if (kt + 2 < nk) issue(kt + 2, (kt + 2) % 3);
-      compute(kt % 3);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-  } else if constexpr (KG == 1) {
-    kloop<STAGES, 5>(nk, issue, compute);  // per-wave DMA count varies (<= 5): kloop waits vmcnt(0)-style
-  } else {
-    // kloop's two-stage schedule with both groups in step: iteration it holds k-tile
-    // KG it + grp of each group (one barrier per iteration for the whole block)
-    const int nit = (nk + KG - 1) / KG;
-    if (grp < nk) issue(grp, 0);
-    for (int it = 0; it < nit; ++it) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      if ((it + 1) * KG + grp < nk) issue((it + 1) * KG + grp, (it + 1) & 1);
-      if (it * KG + grp < nk) compute(it & 1);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    // group 1's partial tile (and bias partial) into group 0's, 3 taps per LDS round (fixed
-    // order: group 0 + group 1)
-    float* xb = reinterpret_cast<float*>(smem);
-    constexpr int TC = 3;
-#pragma unroll
-    for (int j0 = 0; j0 < TAPS; j0 += TC) {
-      if (grp == 1) {
-#pragma unroll
-        for (int jc = 0; jc < TC; ++jc)
-          if (j0 + jc < TAPS) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-              for (int r = 0; r < 4; ++r)
-                xb[(((wave * TC + jc) * 4 + i) * 4 + r) * 64 + lane] = acc[j0 + jc][i][0][r];
-          }
-        if (j0 == 0) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) xb[(4 * TC * 16 + wave * 4 + r) * 64 + lane] = accb[0][r];
-        }
-      }
-      __syncthreads();
-      if (grp == 0) {
-#pragma unroll
-        for (int jc = 0; jc < TC; ++jc)
-          if (j0 + jc < TAPS) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-              for (int r = 0; r < 4; ++r)
-                acc[j0 + jc][i][0][r] += xb[(((wave * TC + jc) * 4 + i) * 4 + r) * 64 + lane];
-          }
-        if (j0 == 0) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) accb[0][r] += xb[(4 * TC * 16 + wave * 4 + r) * 64 + lane];
-        }
-      }
-      __syncthreads();
-    }
-    if (grp == 1) return;
-  }
+  kloop<STAGES, 5>(nk, issue, compute);  // per-wave DMA count varies (<= 5): vmcnt(0)-style
 
   if (do_bias && r16 == 0) {
 #pragma unroll
-    for (int i = 0; i < (WS ? 1 : 2); ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int o = o0 + (WS ? wave * 16 : wm * 32 + i * 16) + 4 * g + r;
-        a.bslab[(int64_t)z * a.Cout + o] = accb[i][r];
-      }
+    for (int r = 0; r < 4; ++r) a.bslab[(int64_t)z * a.Cout + o0 + wave * 16 + 4 * g + r] = accb[r];
   }
   // slab[z][o][j*Cin + c]: 16 consecutive c per row group (64-B runs)
   float* slab = a.slab + (int64_t)z * a.Cout * a.Kp;
 #pragma unroll
   for (int j = 0; j < TAPS; ++j)
 #pragma unroll
-    for (int i = 0; i < NA; ++i)
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int jj = 0; jj < NB; ++jj)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int o = o0 + (WS ? i * 16 : wm * 32 + i * 16) + 4 * g + r;
-          const int c = c0 + (WS ? wave * 16 : wn * 32 + jj * 16) + r16;
-          slab[(int64_t)o * a.Kp + (int64_t)j * a.Cin + c] = acc[j][i][jj][r];
-        }
+      for (int r = 0; r < 4; ++r) {
+        const int o = o0 + i * 16 + 4 * g + r;
+        const int c = c0 + wave * 16 + r16;
+        slab[(int64_t)o * a.Kp + (int64_t)j * a.Cin + c] = acc[j][i][r];
+      }
 }
 
 // dw[o][c][j] (+)= sum_z slab[z][o][j*Cin + c]; db[o] += sum_z bslab[z][o].  Split order is
@@ -2647,6 +2513,12 @@ int conv_wgrad_glds_launch(const void* dy, int64_t ldy, const void* x, int64_t l
                                                                      (int)c_out, total, dw, db);
     return launch_status("fs2_conv_wgrad(bf16)");
   }
+  if (taps > 1 && g_tune[FS2_TUNE_WGRAD_HALO] == 0) {
+    // no split slabs where the output tiles fill the chip (conv_wgrad_band, wgrad.hip)
+    const int rc = conv_wgrad_band_launch(dy, ldy, x, ldx, dw, db, rows, seq_len, c_in, c_out,
+                                          taps, pad, lens, st);
+    if (rc != -1) return rc;
+  }
   const bool halo = taps >= 2 && taps <= 9 && (taps == 3 || taps == 5 || taps == 9) &&
                     c_in % 64 == 0 && c_out % 64 == 0 && seq_len % 64 == 0 &&
                     g_tune[FS2_TUNE_WGRAD_HALO] >= 0;
@@ -2654,17 +2526,9 @@ int conv_wgrad_glds_launch(const void* dy, int64_t ldy, const void* x, int64_t l
     a.tiles_o = (int)(c_out / 64);
     a.tiles_k = (int)(c_in / 64);
     const unsigned hgrid = (unsigned)(a.tiles_o * a.tiles_k * splits);
-    const bool quarters = g_tune[FS2_TUNE_WGRAD_HALO] == 1;  // round-1 wave tiles (A/B)
-    const bool kg2 = g_tune[FS2_TUNE_WGRAD_HALO] == 2;       // two k-groups per block
-    const bool st3 = g_tune[FS2_TUNE_WGRAD_HALO] == 3;       // three LDS stages
-#define FS2_WH(T) (kg2 ? conv_wgrad_halo<T, 1, 2><<<hgrid, 512, 0, st>>>(a)              \
-                       : st3 ? conv_wgrad_halo<T, 1, 1, 3><<<hgrid, 256, 0, st>>>(a)      \
-                             : quarters ? conv_wgrad_halo<T, 0><<<hgrid, 256, 0, st>>>(a) \
-                                        : conv_wgrad_halo<T, 1><<<hgrid, 256, 0, st>>>(a))
-    if (taps == 9) FS2_WH(9);
-    else if (taps == 5) FS2_WH(5);
-    else FS2_WH(3);
-#undef FS2_WH
+    if (taps == 9) conv_wgrad_halo<9><<<hgrid, 256, 0, st>>>(a);
+    else if (taps == 5) conv_wgrad_halo<5><<<hgrid, 256, 0, st>>>(a);
+    else conv_wgrad_halo<3><<<hgrid, 256, 0, st>>>(a);
   }
   const unsigned grid = (unsigned)(a.tiles_o * a.tiles_k * splits);
   const int stages = g_tune[FS2_TUNE_WGRAD_STAGES] >= 1 && g_tune[FS2_TUNE_WGRAD_STAGES] <= 4

@@ -1,0 +1,764 @@
+// Conv1d weight gradient without split-K slabs: conv_wgrad_band.
+//
+//   dw[o, c, j] += sum_r dy[r, o] * x[r + j - pad, c]        (taps 3 / 5 / 9)
+//   db[o]       += sum_r dy[r, o]
+//
+// Replaces the weight half of ConvolutionBackward for the FFT-block Conv1d FFN
+// (transformer/SubLayers.py:85-93), the PostNet convs (transformer/Layers.py:129-137) and the
+// variance-predictor convs (model/modules.py:209-250).
+//
+// The product is a tall reduction: 24,576 rows against a 1,024 x 2,304 output for the decoder
+// FFN.  The round-3 kernel split the rows over 8 blocks per output tile and round-tripped eight
+// fp32 slabs (72 MB written, 81 MB read back by a reduce launch, for a 9.4 MB result).  Here
+// one block owns a 32 (o) x 32 (c) x taps output tile for ALL rows, so the grid is the output
+// tiles (256 blocks for the decoder / encoder FFN and the PostNet 512 x 512 convs) and no slab
+// exists: the four waves of a block each take every fourth band of rows, hold the whole tile
+// in registers (taps x 2 x 2 fragments of v_mfma_f32_16x16x32_bf16), and are summed in a fixed
+// order through LDS at the end ((w0 + w2) + (w1 + w3): bitwise reproducible), then added
+// straight into dw / db.
+//
+// Bands.  A band is 32 S consecutive rows inside one utterance (T % 32 S == 0).  Its step s
+// (s < S) is the 32-deep MFMA reduction over the rows s + S m (m = 0..31), so tap j of step s
+// needs the input rows s + j + S m of the band's halo: halo fragment F[s + j], where F[f] are
+// the halo rows f + S m (f < S + taps - 1).  Each halo fragment is read from LDS ONCE and feeds
+// every (s, j) with s + j = f -- the tap-register idea of conv_gemm_tapreg applied to the
+// reduction dimension (rows may be paired with MFMA k-slots in any order, as long as dy and x
+// use the same one).  The dy image stores band row h at position (h mod S) * 32 + h / S and the
+// x image halo row h at (h mod S) * RS + h / S, so every fragment is 32 consecutive positions.
+// Positions are 64-B rows (32 bf16 columns); the 32-B halves swap at (P >> 2) & 1, which makes
+// the ds_read_b64_tr_b16 fragment reads conflict-free at any starting position.
+//
+// Each wave stages its own bands through its own ST-slot LDS ring by LDS-DMA and waits only for
+// its own loads (counted vmcnt): there is no barrier in the main loop.  Rows past an
+// utterance's length (lens given) are staged from the zero line, and bands made only of them
+// are not visited.  The bias gradient rides on the dy fragments of the blocks of the first c
+// tile (an MFMA against a ones fragment).
+#include "common.hpp"
+
+namespace fs2 {
+
+typedef unsigned short u16;
+typedef __bf16 bf16x8w __attribute__((ext_vector_type(8)));
+typedef short s16x4w __attribute__((ext_vector_type(4)));
+
+static __device__ __attribute__((aligned(128))) uint4 g_wb_zero[8];  // zero source line
+
+struct WgradBand {
+  const u16* dy;
+  int64_t ldy;
+  const u16* x;
+  int64_t ldx;
+  float* dw;
+  float* db;
+  int64_t M, T;
+  int Cin, Cout, pad;
+  int tiles_o, tiles_c;
+  const int64_t* lens;
+};
+
+namespace {
+
+FS2_DEV void wb_glds16(const void* src, u16* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+
+// ds_read_b64_tr_b16 as inline asm (invisible to the compiler's wait-count pass, which would
+// otherwise make every read wait for all LDS-DMA in flight); waited for with wb_lgkm<N>
+FS2_DEV s16x4w wb_tr16(const u16* p) {
+  s16x4w r;
+  const uint32_t a = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) u16*)p;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(a));
+  return r;
+}
+template <int N>
+FS2_DEV void wb_lgkm() {
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+template <int N>
+FS2_DEV void wb_vm(int ahead) {  // at most `ahead` bands of N LDS-DMA instructions in flight
+  if (ahead <= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+  else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * N) : "memory");
+}
+
+}  // namespace
+
+template <int TAPS, int S, int ST>
+__global__ __launch_bounds__(256, 2) void conv_wgrad_band(WgradBand a) {
+  constexpr int BO = 32, BC = 32, W = 4, BR = 32 * S;
+  constexpr int HR = BR + TAPS - 1, RS = (HR + S - 1) / S, NF = S + TAPS - 1;
+  constexpr int DPOS = BR, XPOS = (S * RS + 15) / 16 * 16;  // image positions (64 B each)
+  constexpr int NQD = DPOS / 16, NQX = XPOS / 16, NQ = NQD + NQX;  // LDS-DMA per band
+  constexpr int STAGE_E = (DPOS + XPOS) * 32;                     // bf16 per ring slot
+  constexpr int RING_B = W * ST * STAGE_E * 2;
+  constexpr int QLD = BC * TAPS + 4;  // fp32 row stride of a dW-layout partial tile
+  constexpr int RED_B = 2 * BO * QLD * 4 + 2 * 2 * 64 * 16;  // two partial tiles + bias
+  static_assert(TAPS * 16 * 64 <= BO * QLD, "native partial fits a region");
+  constexpr int SMEM_B = RING_B > RED_B ? RING_B : RED_B;
+  constexpr int MAXB = 1024;
+  constexpr int LOOK = 2;  // halo fragments read ahead of their MFMAs
+  static_assert(NQ <= 31, "vmcnt bookkeeping");
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[SMEM_B + 2 * MAXB + 64];
+  short* blist = reinterpret_cast<short*>(smem + SMEM_B);
+  int* wcnt = reinterpret_cast<int*>(smem + SMEM_B + 2 * MAXB);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3, r16 = lane & 15;
+
+  // output tile: XCD-contiguous runs, c fastest (an XCD's blocks share their dy columns in L2)
+  const int nwg = a.tiles_o * a.tiles_c;
+  const int orig = blockIdx.x, xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int to = wg / a.tiles_c, tc = wg - to * a.tiles_c;
+  const int o0 = to * BO, c0 = tc * BC;
+
+  // bands holding a real row, in row order (wave ballots + prefix popcounts)
+  const int nbu = (int)(a.T / BR);
+  const int nb_all = (int)(a.M / BR);
+  const bool use_list = a.lens != nullptr && nb_all <= MAXB;
+  int nb = nb_all;
+  if (use_list) {
+    int total = 0;
+    for (int k0 = 0; k0 < nb_all; k0 += 256) {
+      const int k = k0 + tid;
+      bool v = false;
+      if (k < nb_all) {
+        const int b = k / nbu;
+        v = (int64_t)(k - b * nbu) * BR < a.lens[b];
+      }
+      const uint64_t mask = __ballot(v);
+      if (lane == 0) wcnt[wave] = __popcll(mask);
+      __syncthreads();
+      int before = total;
+      for (int w = 0; w < wave; ++w) before += wcnt[w];
+      const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
+      if (v) blist[before + below] = (short)k;
+      for (int w = 0; w < W; ++w) total += wcnt[w];
+      __syncthreads();
+    }
+    nb = total;
+  }
+  const int nbw = nb > wave ? (nb - wave + W - 1) / W : 0;  // this wave: bands wave + W i
+
+  // the 32-B halves of position P swap at (P >> 2) & 1 (16-B chunk index ^ 2)
+  auto swz = [](int P) { return ((P >> 2) & 1) << 1; };
+  const u16* zero = reinterpret_cast<const u16*>(g_wb_zero);
+  const int lpos = lane >> 2, lch = lane & 3;
+
+  auto issue = [&](int i, int slot) {
+    const int k = __builtin_amdgcn_readfirstlane(use_list ? (int)blist[wave + W * i] : wave + W * i);
+    const int b = k / nbu, t0 = (k - b * nbu) * BR;
+    const int64_t u0 = (int64_t)b * a.T;
+    int len = (int)a.T;
+    if (a.lens) {
+      const int64_t l = a.lens[b];
+      len = l < a.T ? (int)l : (int)a.T;
+    }
+    u16* Ds = reinterpret_cast<u16*>(smem) + (wave * ST + slot) * STAGE_E;
+    u16* Xs = Ds + DPOS * 32;
+#pragma unroll
+    for (int qi = 0; qi < NQD; ++qi) {
+      const int P = qi * 16 + lpos;
+      const int h = (P & 31) * S + (P >> 5);
+      const int col = o0 + ((lch ^ swz(P)) << 3);
+      const int t = t0 + h;
+      const u16* src = (t < len && col < a.Cout) ? a.dy + (u0 + t) * a.ldy + col : zero;
+      wb_glds16(src, Ds + qi * 16 * 32);
+    }
+#pragma unroll
+    for (int qi = 0; qi < NQX; ++qi) {
+      const int P = qi * 16 + lpos;
+      const int h = (P % RS) * S + P / RS;
+      const int col = c0 + ((lch ^ swz(P)) << 3);
+      const int t = t0 - a.pad + h;
+      const bool ok = P < S * RS && h < HR && t >= 0 && t < (int)a.T && col < a.Cin;
+      const u16* src = ok ? a.x + (u0 + t) * a.ldx + col : zero;
+      wb_glds16(src, Xs + qi * 16 * 32);
+    }
+  };
+
+  f32x4 acc[TAPS][2][2], accb[2];
+#pragma unroll
+  for (int j = 0; j < TAPS; ++j)
+#pragma unroll
+    for (int io = 0; io < 2; ++io)
+#pragma unroll
+      for (int ic = 0; ic < 2; ++ic) acc[j][io][ic] = f32x4{0.f, 0.f, 0.f, 0.f};
+  accb[0] = accb[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool do_bias = a.db != nullptr && tc == 0;  // block-uniform
+  bf16x8w ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = (__bf16)1.0f;
+
+  // fragment of 32 positions from pb, 16 columns at col0: positions pb + {4g+q} and + 16
+  auto frag = [&](const u16* img, int pb, int col0) -> bf16x8w {
+    const int lc = (col0 >> 3) + (p >> 1);
+    const int R0 = pb + 4 * g + q, R1 = R0 + 16;
+    const s16x4w lo = wb_tr16(img + R0 * 32 + ((lc ^ swz(R0)) << 3) + ((p & 1) << 2));
+    const s16x4w hi = wb_tr16(img + R1 * 32 + ((lc ^ swz(R1)) << 3) + ((p & 1) << 2));
+    return __builtin_bit_cast(bf16x8w, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+  };
+
+  auto compute = [&](int slot) {
+    const u16* Ds = reinterpret_cast<const u16*>(smem) + (wave * ST + slot) * STAGE_E;
+    const u16* Xs = Ds + DPOS * 32;
+    bf16x8w A[S][2], F[LOOK + 1][2];
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+#pragma unroll
+      for (int io = 0; io < 2; ++io) A[s][io] = frag(Ds, s * 32, io * 16);
+#pragma unroll
+    for (int f = 0; f < LOOK && f < NF; ++f)
+#pragma unroll
+      for (int ic = 0; ic < 2; ++ic) F[f][ic] = frag(Xs, (f % S) * RS + f / S, ic * 16);
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      if (f + LOOK < NF) {
+#pragma unroll
+        for (int ic = 0; ic < 2; ++ic)
+          F[(f + LOOK) % (LOOK + 1)][ic] = frag(Xs, ((f + LOOK) % S) * RS + (f + LOOK) / S, ic * 16);
+      }
+      // wait for the reads up to F[f]: the younger ones (F[f + 1 .. f + LOOK]) may stay in flight
+      const int younger = (NF - 1 - f < LOOK ? NF - 1 - f : LOOK) * 4;
+      if (younger >= 8) wb_lgkm<8>();
+      else if (younger == 4) wb_lgkm<4>();
+      else wb_lgkm<0>();
+      const bf16x8w* Ff = F[f % (LOOK + 1)];
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        const int j = f - s;
+        if (j < 0 || j >= TAPS) continue;
+#pragma unroll
+        for (int io = 0; io < 2; ++io)
+#pragma unroll
+          for (int ic = 0; ic < 2; ++ic)
+            acc[j][io][ic] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[s][io], Ff[ic], acc[j][io][ic],
+                                                                     0, 0, 0);
+        if (j == 0 && do_bias) {
+#pragma unroll
+          for (int io = 0; io < 2; ++io)
+            accb[io] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[s][io], ones, accb[io], 0, 0, 0);
+        }
+      }
+    }
+  };
+
+  for (int i = 0; i < ST - 1 && i < nbw; ++i) issue(i, i);
+  for (int i = 0; i < nbw; ++i) {
+    const int ahead = nbw - 1 - i < ST - 2 ? nbw - 1 - i : ST - 2;
+    wb_vm<NQ>(ahead);
+    if (i + ST - 1 < nbw) issue(i + ST - 1, (i + ST - 1) % ST);
+    compute(i % ST);
+  }
+
+  // fixed-order cross-wave sum: wave w (< 2) adds wave w + 2's partial, both write their sums
+  // in the dw layout ([o][c][j], row stride QLD), every thread adds the two and dw / db
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  float* Q = reinterpret_cast<float*>(smem);
+  f32x4* QB = reinterpret_cast<f32x4*>(Q + 2 * BO * QLD);  // [2][2 io][64 lanes]
+  const int reg = wave & 1;  // partial region of this wave pair
+  if (wave >= 2) {
+    f32x4* dst = reinterpret_cast<f32x4*>(Q + reg * BO * QLD);
+#pragma unroll
+    for (int j = 0; j < TAPS; ++j)
+#pragma unroll
+      for (int io = 0; io < 2; ++io)
+#pragma unroll
+        for (int ic = 0; ic < 2; ++ic) dst[((j * 2 + io) * 2 + ic) * 64 + lane] = acc[j][io][ic];
+    if (do_bias) {
+      QB[(reg * 2 + 0) * 64 + lane] = accb[0];
+      QB[(reg * 2 + 1) * 64 + lane] = accb[1];
+    }
+  }
+  __syncthreads();
+  if (wave < 2) {
+    const f32x4* src = reinterpret_cast<const f32x4*>(Q + reg * BO * QLD);
+#pragma unroll
+    for (int j = 0; j < TAPS; ++j)
+#pragma unroll
+      for (int io = 0; io < 2; ++io)
+#pragma unroll
+        for (int ic = 0; ic < 2; ++ic) acc[j][io][ic] += src[((j * 2 + io) * 2 + ic) * 64 + lane];
+    if (do_bias) {
+      accb[0] += QB[(reg * 2 + 0) * 64 + lane];
+      accb[1] += QB[(reg * 2 + 1) * 64 + lane];
+    }
+  }
+  __syncthreads();
+  if (wave < 2) {
+    float* dst = Q + reg * BO * QLD;
+#pragma unroll
+    for (int j = 0; j < TAPS; ++j)
+#pragma unroll
+      for (int io = 0; io < 2; ++io)
+#pragma unroll
+        for (int ic = 0; ic < 2; ++ic)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            dst[(io * 16 + 4 * g + r) * QLD + (ic * 16 + r16) * TAPS + j] = acc[j][io][ic][r];
+    if (do_bias && r16 == 0) {
+#pragma unroll
+      for (int io = 0; io < 2; ++io)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) QB[(reg * 2 + io) * 64 + 4 * g + r][0] = accb[io][r];
+    }
+  }
+  __syncthreads();
+  {
+    constexpr int V = BC * TAPS / 4;  // f32x4 per output row of the tile
+    const int64_t Kp = (int64_t)a.Cin * TAPS;
+    const int ncol = (a.Cin - c0 < BC ? a.Cin - c0 : BC) * TAPS;  // valid floats per row
+    for (int e = tid; e < BO * V; e += 256) {
+      const int o = e / V, v4 = e - o * V;
+      if (o0 + o >= a.Cout || 4 * v4 >= ncol) continue;
+      const f32x4 s = ld4(Q + o * QLD + 4 * v4) + ld4(Q + BO * QLD + o * QLD + 4 * v4);
+      float* d = a.dw + (int64_t)(o0 + o) * Kp + (int64_t)c0 * TAPS + 4 * v4;
+      st4(d, ld4(d) + s);
+    }
+    if (do_bias && tid < BO && o0 + tid < a.Cout) {
+      const int io = tid >> 4, gg = (tid & 15) >> 2, r = tid & 3;
+      const float b = QB[(0 * 2 + io) * 64 + 4 * gg + r][0] + QB[(1 * 2 + io) * 64 + 4 * gg + r][0];
+      a.db[o0 + tid] += b;
+    }
+  }
+}
+
+// -1: not eligible (the caller uses the split-K kernels)
+int conv_wgrad_band_launch(const void* dy, int64_t ldy, const void* x, int64_t ldx, float* dw,
+                           float* db, int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out,
+                           int taps, int pad, const int64_t* lens, hipStream_t st) {
+  const int S = 2, BR = 32 * S;
+  if (!(taps == 3 || taps == 5 || taps == 9)) return -1;
+  if (pad < 0 || pad > taps - 1) return -1;
+  if (c_in % 8 || c_out % 8 || ldx % 8 || ldy % 8 || ((uintptr_t)dy & 15) || ((uintptr_t)x & 15))
+    return -1;
+  if (seq_len % BR || rows % seq_len || rows / BR > (1 << 15)) return -1;
+  if (c_in < 32 || c_out < 32) return -1;
+  const int to = (int)((c_out + 31) / 32), tc = (int)((c_in + 31) / 32);
+  if (to * tc < 128) return -1;  // under-filled grid: split-K kernels
+  // f32x4 read-modify-writes of dw: rows of c_in * taps floats, tile columns 32 * taps
+  if (((uintptr_t)dw & 15) || (c_in * taps) % 4) return -1;
+  WgradBand a{(const u16*)dy, ldy, (const u16*)x, ldx, dw, db, rows, seq_len, (int)c_in,
+              (int)c_out, pad, to, tc, lens};
+  const unsigned grid = (unsigned)(to * tc);
+  if (taps == 9) conv_wgrad_band<9, 2, 2><<<grid, 256, 0, st>>>(a);
+  else if (taps == 5) conv_wgrad_band<5, 2, 2><<<grid, 256, 0, st>>>(a);
+  else conv_wgrad_band<3, 2, 2><<<grid, 256, 0, st>>>(a);
+  return launch_status("fs2_conv_wgrad(bf16, band)");
+}
+
+
+// ---------------------------------------------------------------- grouped k = 1 weight gradient
+// wgrad_k1_multi: the k = 1 weight gradients of one FFT block -- QKV (768 x 256 + bias), fc
+// (256 x 256) and w_2 (256 x 1024) at the decoder shapes, transformer/SubLayers.py:39-55,88 --
+// in ONE launch.  Their products are tall reductions (24,576 rows, 0.2 MFLOP per output), so
+// they run split-K: a 128 (o) x 128 (c) output tile over a range of rows per block, fp32
+// partial tiles into split slabs, summed in split order by ONE reduce launch.  Grouping the
+// three GEMMs puts 32 output tiles into the grid instead of 4-16, so the same 256 blocks need 8
+// row splits instead of 21-64: a third of the slab bytes, long row loops (48 k-tiles) that
+// amortise the prologue / epilogue, and 2 launches per block instead of 6.
+// Block: 8 waves; wave w owns the 64 x 64 quadrant w & 3 over rows 32 (w >> 2) .. + 31 of each
+// 64-row k-tile (the two row halves of a quadrant are summed through LDS at the end).  The
+// k-tiles (dy [64 rows][128 o] and x [64 rows][128 c], 256-B rows, LDS-DMA through buffer
+// descriptors) run through a 4-slot ring with three tiles in flight (counted vmcnt, one raw
+// barrier per tile).  Transposed fragments (ds_read_b64_tr_b16) with the chunk swizzle
+// (R & 7) << 1: a 32-lane read hits 16 distinct bank slots.  The bias gradient rides on the dy
+// fragments of the blocks of the first c tile (an MFMA against a ones fragment).
+struct K1Job {
+  const u16* dy;
+  int64_t ldy;
+  const u16* x;
+  int64_t ldx;
+  float* dw;
+  float* db;
+  float* slab;   // [splits][Cout][Cin]
+  float* bslab;  // [splits][Cout] (db != NULL)
+  int64_t rps;   // rows per split (multiple of 64)
+  int Cin, Cout, tiles_o, tiles_c, splits, begin;  // begin: the job's first block
+};
+constexpr int K1_MAXJ = 4;
+struct K1Multi {
+  K1Job job[K1_MAXJ];
+  int n, nblocks;
+  int64_t M, T;
+  const int64_t* lens;
+};
+
+namespace {
+FS2_DEV bool wb_rows_all_padding(const int64_t* lens, int64_t T, int64_t r0, int64_t r1) {
+  int64_t s = r0 / T;
+  if (r0 - s * T < lens[s]) return false;
+  for (++s; s * T < r1; ++s)
+    if (lens[s] > 0) return false;
+  return true;
+}
+}  // namespace
+
+__global__ __launch_bounds__(512, 1) void wgrad_k1_multi(K1Multi m) {
+  constexpr int BO = 128, BC = 128, BK = 64, NT = 512, STAGES = 4;
+  constexpr int IMG = BK * 128;     // one operand image: [64 rows][128] bf16 (256-B rows)
+  constexpr int STAGE_E = 2 * IMG;  // dy image then x image (32 KB)
+  constexpr int EPI_LD = 64 + 4;    // fp32 epilogue rows of a 64 x 64 quadrant
+  constexpr int EPI_B = (4 * 64 * EPI_LD + 4 * 64) * 4;
+  constexpr int SMEM_B = STAGES * STAGE_E * 2 > EPI_B ? STAGES * STAGE_E * 2 : EPI_B;
+  constexpr int MAXKT = 1024;
+  __shared__ __attribute__((aligned(1024))) u16 smem[SMEM_B / 2 + MAXKT + 64];
+  short* ktl = reinterpret_cast<short*>(smem + SMEM_B / 2);
+  int* wcnt = reinterpret_cast<int*>(smem + SMEM_B / 2 + MAXKT);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int quad = wave & 3, half = wave >> 2;
+  const int qo = (quad >> 1) * 64, qc = (quad & 1) * 64;
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3, r16 = lane & 15;
+
+  // XCD-contiguous block runs; a job's blocks are split-major, tiles fastest (an XCD's blocks
+  // share the rows of dy and x)
+  const int nwg = m.nblocks;
+  const int orig = blockIdx.x, xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  int jb = 0;
+#pragma unroll
+  for (int j = 1; j < K1_MAXJ; ++j)
+    if (j < m.n && wg >= m.job[j].begin) jb = j;
+  const K1Job J = m.job[jb];
+  const int local = wg - J.begin, tiles = J.tiles_o * J.tiles_c;
+  const int z = local / tiles, tile = local - z * tiles;
+  const int to = tile / J.tiles_c, tc = tile - to * J.tiles_c;
+  const int o0 = to * BO, c0 = tc * BC;
+  const int64_t r_begin = (int64_t)z * J.rps;
+  int64_t r_end = r_begin + J.rps;
+  if (r_end > m.M) r_end = m.M;
+  const int nk_all = r_end > r_begin ? (int)((r_end - r_begin + BK - 1) / BK) : 0;
+  // ordered list of the split's k-tiles holding a real row
+  const bool use_list = m.lens != nullptr && nk_all <= MAXKT;
+  int nk = nk_all;
+  if (use_list) {
+    int total = 0;
+    for (int cc0 = 0; cc0 < nk_all; cc0 += NT) {
+      const int kt = cc0 + tid;
+      bool v = false;
+      if (kt < nk_all) {
+        const int64_t k0 = r_begin + (int64_t)kt * BK;
+        v = !wb_rows_all_padding(m.lens, m.T, k0, k0 + BK < r_end ? k0 + BK : r_end);
+      }
+      const uint64_t mask = __ballot(v);
+      if (lane == 0) wcnt[wave] = __popcll(mask);
+      __syncthreads();
+      int before = total;
+      for (int w = 0; w < wave; ++w) before += wcnt[w];
+      const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
+      if (v) ktl[before + below] = (short)kt;
+      for (int w = 0; w < 8; ++w) total += wcnt[w];
+      __syncthreads();
+    }
+    nk = total;
+  }
+
+  // staging: a wave-instruction fills 4 image rows x 256 B; image row R = (2 wave + i) * 4 +
+  // lane / 16 (i < 2), physical 16-B chunk lane & 15 holding logical chunk (lane & 15) ^ swz(R).
+  // Buffer descriptors over the split's rows (the k-tile advance rides in the scalar offset);
+  // chunks past the channel count and rows past the split's end select an out-of-range voffset.
+  auto swz = [](int R) { return (R & 7) << 1; };
+  const auto dy_rs = buf_rsrc(J.dy + r_begin * J.ldy, (r_end - r_begin) * J.ldy * 2);
+  const auto x_rs = buf_rsrc(J.x + r_begin * J.ldx, (r_end - r_begin) * J.ldx * 2);
+  int Rl[2];
+  uint32_t a_vo[2], b_vo[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int R = (wave * 2 + i) * 4 + (lane >> 4);
+    const int lc = (lane & 15) ^ swz(R);
+    Rl[i] = R;
+    a_vo[i] = o0 + lc * 8 < J.Cout ? (uint32_t)((R * J.ldy + o0 + lc * 8) * 2) : kOOB;
+    b_vo[i] = c0 + lc * 8 < J.Cin ? (uint32_t)((R * J.ldx + c0 + lc * 8) * 2) : kOOB;
+  }
+  const int rows = (int)(r_end - r_begin);
+  auto issue = [&](int kt, int stage) {
+    u16* As = smem + stage * STAGE_E;
+    u16* Bs = As + IMG;
+    const int tl = __builtin_amdgcn_readfirstlane(use_list ? (int)ktl[kt] : kt);
+    const int lim = rows - tl * BK;  // rows of this k-tile inside the split
+    const uint32_t sa = (uint32_t)(tl * BK * J.ldy * 2), sb = (uint32_t)(tl * BK * J.ldx * 2);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const bool ok = Rl[i] < lim;
+      glds16_buf(dy_rs, As + (wave * 2 + i) * 4 * 128, ok ? a_vo[i] : kOOB, sa);
+      glds16_buf(x_rs, Bs + (wave * 2 + i) * 4 * 128, ok ? b_vo[i] : kOOB, sb);
+    }
+  };
+
+  f32x4 acc[4][4], accb[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    accb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const bool do_bias = J.db != nullptr && tc == 0 && (quad & 1) == 0;  // wave-uniform
+  bf16x8w ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = (__bf16)1.0f;
+  const int rbase = half * 32 + 4 * g + q, sw = swz(rbase);
+  auto tr = [&](const u16* img, int col0, int hi) -> s16x4w {
+    const int lc = (col0 >> 3) + (p >> 1);
+    return wb_tr16(img + (rbase + 16 * hi) * 128 + ((lc ^ sw) << 3) + ((p & 1) << 2));
+  };
+  auto cat = [](s16x4w lo, s16x4w hi) {
+    return __builtin_bit_cast(bf16x8w, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+  };
+  auto compute = [&](int stage) {
+    const u16* As = smem + stage * STAGE_E;
+    const u16* Bs = As + IMG;
+    s16x4w ra[4][2], rb[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      ra[i][0] = tr(As, qo + i * 16, 0);
+      ra[i][1] = tr(As, qo + i * 16, 1);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      rb[j][0] = tr(Bs, qc + j * 16, 0);
+      rb[j][1] = tr(Bs, qc + j * 16, 1);
+    }
+    bf16x8w fa[4];
+    // c fragment j's MFMAs wait only for the reads up to it (4-bit counter: the 16th read
+    // issues once the first has retired, so 6 - 2 j younger reads remain in flight)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (j == 0) wb_lgkm<6>();
+      else if (j == 1) wb_lgkm<4>();
+      else if (j == 2) wb_lgkm<2>();
+      else wb_lgkm<0>();
+      if (j == 0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fa[i] = cat(ra[i][0], ra[i][1]);
+      }
+      const bf16x8w fb = cat(rb[j][0], rb[j][1]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb, acc[i][j], 0, 0, 0);
+    }
+    if (do_bias) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], ones, accb[i], 0, 0, 0);
+    }
+  };
+
+  // ring: STAGES - 1 tiles issued ahead; per tile a counted vmcnt (this tile landed, the later
+  // ones stay in flight), one raw barrier (every wave's pieces landed AND every wave finished the
+  // previous tile, whose slot the refill overwrites), refill, MFMAs
+  for (int t = 0; t < STAGES - 1 && t < nk; ++t) issue(t, t);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int ahead = nk - 1 - kt < STAGES - 2 ? nk - 1 - kt : STAGES - 2;
+    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
+    compute(kt % STAGES);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+
+  // the two row halves of each quadrant through LDS: half 1 writes, half 0 adds and stores
+  float* Cs = reinterpret_cast<float*>(smem);
+  float* Bp = Cs + 4 * 64 * EPI_LD;
+  if (half == 1) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          Cs[(quad * 64 + i * 16 + 4 * g + r) * EPI_LD + j * 16 + r16] = acc[i][j][r];
+    if (do_bias && r16 == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Bp[quad * 64 + i * 16 + 4 * g + r] = accb[i][r];
+    }
+  }
+  __syncthreads();
+  if (half == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          Cs[(quad * 64 + i * 16 + 4 * g + r) * EPI_LD + j * 16 + r16] += acc[i][j][r];
+    if (do_bias && r16 == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Bp[quad * 64 + i * 16 + 4 * g + r] += accb[i][r];
+    }
+  }
+  __syncthreads();
+  {
+    // 128 x 128 outputs, 32 per thread: row o = tid / 4, 32 consecutive c; quadrant rows
+    const int o = tid >> 2, cc = (tid & 3) * 32;
+    const int qd = (o >> 6) * 2 + (cc >> 6), ro = o & 63, co = cc & 63;
+    float* slab = J.slab + (int64_t)z * J.Cout * J.Cin;
+    if (o0 + o < J.Cout) {
+#pragma unroll
+      for (int v = 0; v < 8; ++v) {
+        const f32x4 t = *reinterpret_cast<const f32x4*>(Cs + (qd * 64 + ro) * EPI_LD + co + 4 * v);
+        if (c0 + cc + 4 * v < J.Cin)
+          *reinterpret_cast<f32x4*>(slab + (int64_t)(o0 + o) * J.Cin + c0 + cc + 4 * v) = t;
+      }
+    }
+    if (J.db != nullptr && tc == 0 && tid < BO && o0 + tid < J.Cout)
+      J.bslab[(int64_t)z * J.Cout + o0 + tid] = Bp[((tid >> 6) * 2) * 64 + (tid & 63)];
+  }
+}
+
+// dw_j += sum_z slab_j[z] (f32x4 units), db_j += sum_z bslab_j[z]: the splits in order (fixed:
+// bitwise reproducible), eight split loads in flight per thread
+struct K1Red {
+  const float* slab[K1_MAXJ];
+  const float* bslab[K1_MAXJ];
+  float* dw[K1_MAXJ];
+  float* db[K1_MAXJ];
+  int64_t u_begin[K1_MAXJ + 1];  // f32x4 units of the weight gradients, per job
+  int64_t b_begin[K1_MAXJ + 1];  // bias outputs, per job (after every weight unit)
+  int splits[K1_MAXJ];
+  int n;
+};
+__global__ __launch_bounds__(256) void wgrad_k1_multi_reduce(K1Red r) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e < r.u_begin[r.n]) {
+    int j = 0;
+#pragma unroll
+    for (int k = 1; k < K1_MAXJ; ++k)
+      if (k < r.n && e >= r.u_begin[k]) j = k;
+    const int64_t i4 = (e - r.u_begin[j]) * 4, total = (r.u_begin[j + 1] - r.u_begin[j]) * 4;
+    const float* s = r.slab[j] + i4;
+    const int S = r.splits[j];
+    f32x4 acc = ld4(s);
+    int zz = 1;
+    for (; zz + 7 < S; zz += 8) {
+      f32x4 v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = ld4(s + (int64_t)(zz + k) * total);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc += v[k];
+    }
+    for (; zz < S; ++zz) acc += ld4(s + (int64_t)zz * total);
+    float* d = r.dw[j] + i4;
+    st4(d, ld4(d) + acc);
+    return;
+  }
+  const int64_t eb = e - r.u_begin[r.n];
+  if (eb >= r.b_begin[r.n]) return;
+  int j = 0;
+#pragma unroll
+  for (int k = 1; k < K1_MAXJ; ++k)
+    if (k < r.n && eb >= r.b_begin[k]) j = k;
+  const int64_t o = eb - r.b_begin[j], cout = r.b_begin[j + 1] - r.b_begin[j];
+  float acc = 0.f;
+  for (int zz = 0; zz < r.splits[j]; ++zz) acc += r.bslab[j][(int64_t)zz * cout + o];
+  r.db[j][o] += acc;
+}
+
+// jobs: host int64 rows {dy, ldy, x, ldx, dw, db, c_in, c_out}; splits chosen so that the grid
+// is about 256 blocks of 128 x 128 tiles
+static int k1_multi_splits(int64_t tiles_total, int64_t rows) {
+  int64_t s = (256 + tiles_total / 2) / tiles_total;
+  if (s > rows / 256) s = rows / 256;  // >= 4 k-tiles per split
+  return (int)(s < 1 ? 1 : s);
+}
+
+int64_t wgrad_k1_multi_ws_floats(const int64_t* jobs, int n, int64_t rows) {
+  int64_t tiles = 0;
+  for (int j = 0; j < n; ++j) {
+    const int64_t cin = jobs[8 * j + 6], cout = jobs[8 * j + 7];
+    tiles += ((cout + 127) / 128) * ((cin + 127) / 128);
+  }
+  const int S = k1_multi_splits(tiles > 0 ? tiles : 1, rows);
+  int64_t f = 0;
+  for (int j = 0; j < n; ++j) {
+    const int64_t cin = jobs[8 * j + 6], cout = jobs[8 * j + 7];
+    f += S * cout * cin + (jobs[8 * j + 5] ? S * cout : 0);
+    f = (f + 3) / 4 * 4;
+  }
+  return f;
+}
+
+int wgrad_k1_multi_launch(const int64_t* jobs, int n, int64_t rows, int64_t seq_len,
+                          const int64_t* lens, float* ws, hipStream_t st) {
+  FS2_CHECK_ARG(n >= 1 && n <= K1_MAXJ, "fs2_conv_wgrad_k1_multi: 1..%d jobs", K1_MAXJ);
+  int64_t tiles = 0;
+  for (int j = 0; j < n; ++j) {
+    const int64_t* r = jobs + 8 * j;
+    FS2_CHECK_ARG(r[6] % 8 == 0 && r[7] % 8 == 0 && r[1] % 8 == 0 && r[3] % 8 == 0 &&
+                      (r[0] & 15) == 0 && (r[2] & 15) == 0 && (r[4] & 15) == 0,
+                  "fs2_conv_wgrad_k1_multi: channel counts / strides must be multiples of 8, "
+                  "operands 16-B aligned");
+    tiles += ((r[7] + 127) / 128) * ((r[6] + 127) / 128);
+  }
+  const int S = k1_multi_splits(tiles, rows);
+  int64_t rps = (rows + S - 1) / S;
+  rps = (rps + 63) / 64 * 64;
+  for (int j = 0; j < n; ++j) {
+    const int64_t ld = jobs[8 * j + 1] > jobs[8 * j + 3] ? jobs[8 * j + 1] : jobs[8 * j + 3];
+    FS2_CHECK_ARG((rps + 64) * ld * 2 < ((int64_t)1 << 31),
+                  "fs2_conv_wgrad_k1_multi: a row split exceeds 32-bit buffer offsets");
+  }
+  K1Multi m{};
+  K1Red red{};
+  m.n = red.n = n;
+  m.M = rows;
+  m.T = seq_len;
+  m.lens = lens;
+  int begin = 0;
+  int64_t f = 0, ub = 0, bb = 0;
+  for (int j = 0; j < n; ++j) {
+    const int64_t* r = jobs + 8 * j;
+    K1Job& J = m.job[j];
+    J.dy = (const u16*)r[0];
+    J.ldy = r[1];
+    J.x = (const u16*)r[2];
+    J.ldx = r[3];
+    J.dw = (float*)r[4];
+    J.db = (float*)r[5];
+    J.Cin = (int)r[6];
+    J.Cout = (int)r[7];
+    J.tiles_o = (J.Cout + 127) / 128;
+    J.tiles_c = (J.Cin + 127) / 128;
+    J.splits = S;
+    J.rps = rps;
+    J.begin = begin;
+    begin += J.tiles_o * J.tiles_c * S;
+    J.slab = ws + f;
+    f += (int64_t)S * J.Cout * J.Cin;
+    J.bslab = J.db ? ws + f : nullptr;
+    if (J.db) f += (int64_t)S * J.Cout;
+    f = (f + 3) / 4 * 4;
+    red.slab[j] = J.slab;
+    red.bslab[j] = J.bslab;
+    red.dw[j] = J.dw;
+    red.db[j] = J.db;
+    red.splits[j] = S;
+    red.u_begin[j] = ub;
+    ub += (int64_t)J.Cout * J.Cin / 4;
+    red.b_begin[j] = bb;
+    bb += J.db ? J.Cout : 0;
+  }
+  red.u_begin[n] = ub;
+  red.b_begin[n] = bb;
+  m.nblocks = begin;
+  wgrad_k1_multi<<<(unsigned)begin, 512, 0, st>>>(m);
+  wgrad_k1_multi_reduce<<<(unsigned)((ub + bb + 255) / 256), 256, 0, st>>>(red);
+  return launch_status("fs2_conv_wgrad_k1_multi");
+}
+
+}  // namespace fs2

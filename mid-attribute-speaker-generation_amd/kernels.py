@@ -232,6 +232,38 @@ def conv_wgrad(dy, x, dw, rows, seq_len, c_in, c_out, taps, pad, db=None, ws_buf
                        stream() if on_stream is None else on_stream)
 
 
+def _k1_jobs(jobs):
+    """ctypes int64 table {dy, ldy, x, ldx, dw, db, c_in, c_out} per job (host memory)."""
+    arr = (ctypes.c_int64 * (8 * len(jobs)))()
+    for j, (dy, x, dw, db, c_in, c_out) in enumerate(jobs):
+        _dev(dy, x, dw, db)
+        if dy.dtype != x.dtype:
+            raise RuntimeError(f"conv_wgrad_k1_multi operand dtypes differ: {dy.dtype} vs {x.dtype}")
+        arr[8 * j:8 * j + 8] = [dy.data_ptr(), c_out, x.data_ptr(), c_in, dw.data_ptr(),
+                                0 if db is None else db.data_ptr(), c_in, c_out]
+    return arr
+
+
+def conv_wgrad_k1_multi_ws_bytes(jobs, rows):
+    return lib.fs2_conv_wgrad_k1_multi_ws_bytes(_k1_jobs(jobs), len(jobs), rows)
+
+
+def conv_wgrad_k1_multi(jobs, rows, seq_len, lens=None, ws_buf=None, on_stream=None):
+    """Several k = 1 weight gradients over the same rows in one grouped launch:
+    jobs = [(dy, x, dw, db_or_None, c_in, c_out), ...] (at most 4); dw (+)= dy^T x, db (+)=
+    column sums of dy.  ``ws_buf``: caller-owned fp32 workspace."""
+    arr = _k1_jobs(jobs)
+    n = lib.fs2_conv_wgrad_k1_multi_ws_bytes(arr, len(jobs), rows)
+    if ws_buf is not None:
+        if ws_buf.numel() * 4 < n:
+            raise RuntimeError("conv_wgrad_k1_multi: workspace too small")
+        w, n = ws_buf, ws_buf.numel() * 4
+    else:
+        w = ws(n, jobs[0][0].device)
+    lib.fs2_conv_wgrad_k1_multi(code(jobs[0][0].dtype), arr, len(jobs), rows, seq_len, ptr(lens),
+                                ptr(w), n, stream() if on_stream is None else on_stream)
+
+
 def colsum(x, rows, cols, out, accumulate=True):
     _dev(x, out)
     n = lib.fs2_colsum_ws_bytes(rows, cols)

@@ -133,35 +133,66 @@ class StepCtx:
         self.side = None  # stream for the weight-gradient GEMMs (off the critical path)
         self.ws_cache = None  # dict holding the side stream's shared split-K workspace
         self.keep = []  # operands read by side-stream work, released at the next join
+        self.k1 = None  # held-back grouped k = 1 weight gradients: (key, jobs, lens)
 
     def p(self, p):
         return float(p) if self.drop else 0.0
 
-    def wgrad(self, dy, x, dw, rows, seq_len, c_in, c_out, taps, pad, db=None, lens=None):
-        """Weight (+bias) gradient GEMM.  Nothing in the backward waits for it, so with a
-        side stream it runs concurrently with the data-gradient chain on the main stream
-        (the small GEMMs of a block fill the GPU together); ``join`` orders it back."""
-        if self.side is None or taps in _SERIAL_TAPS:
-            return K.conv_wgrad(dy, x, dw, rows, seq_len, c_in, c_out, taps, pad, db=db,
-                                lens=lens)
+    def _side_ws(self, need, device):
         # one workspace for every side-stream weight gradient (they run in stream order);
         # allocated on the main stream and only grown outside graph capture, so nothing is
         # allocated on the side stream (a captured graph owns only main-stream allocations)
-        need = K.lib.fs2_conv_wgrad_ws_bytes(rows, c_in, c_out, taps) // 4 + 1
+        need = need // 4 + 1
         ws = self.ws_cache.get("wgrad")
         if ws is None or ws.numel() < need:
             if torch.cuda.is_current_stream_capturing():
                 raise RuntimeError("weight-gradient workspace must be sized before capture")
             K.lib.fs2_stream_wait(K.stream(), self.side.cuda_stream)  # old buffer drained
-            ws = self.ws_cache["wgrad"] = torch.empty(need, dtype=torch.float32, device=dy.device)
+            ws = self.ws_cache["wgrad"] = torch.empty(need, dtype=torch.float32, device=device)
+        return ws
+
+    def wgrad(self, dy, x, dw, rows, seq_len, c_in, c_out, taps, pad, db=None, lens=None,
+              group=False):
+        """Weight (+bias) gradient GEMM.  Nothing in the backward waits for it, so with a
+        side stream it runs concurrently with the data-gradient chain on the main stream
+        (the small GEMMs of a block fill the GPU together); ``join`` orders it back.
+        ``group`` (k = 1 only): held back and issued with the other grouped k = 1 weight
+        gradients of the same rows as ONE grouped launch at ``flush`` (fs2_conv_wgrad_k1_multi)."""
+        if group and taps == 1:
+            key = (rows, seq_len, None if lens is None else lens.data_ptr())
+            if self.k1 and (self.k1[0] != key or len(self.k1[1]) == 4):
+                self.flush()
+            if not self.k1:
+                self.k1 = (key, [], lens)
+            self.k1[1].append((dy, x, dw, db, c_in, c_out))
+            return
+        if self.side is None or taps in _SERIAL_TAPS:
+            return K.conv_wgrad(dy, x, dw, rows, seq_len, c_in, c_out, taps, pad, db=db,
+                                lens=lens)
+        ws = self._side_ws(K.lib.fs2_conv_wgrad_ws_bytes(rows, c_in, c_out, taps), dy.device)
         side = self.side.cuda_stream
         K.lib.fs2_stream_wait(side, K.stream())
         K.conv_wgrad(dy, x, dw, rows, seq_len, c_in, c_out, taps, pad, db=db, ws_buf=ws,
                      on_stream=side, lens=lens)
         self.keep.append((dy, x))  # not freed (reusable by the main stream) before the join
 
+    def flush(self):
+        """Issue the held-back grouped k = 1 weight gradients (one launch + one reduce)."""
+        if not self.k1:
+            return
+        (rows, seq_len, _), jobs, lens = self.k1
+        self.k1 = None
+        if self.side is None:
+            return K.conv_wgrad_k1_multi(jobs, rows, seq_len, lens=lens)
+        ws = self._side_ws(K.conv_wgrad_k1_multi_ws_bytes(jobs, rows), jobs[0][0].device)
+        side = self.side.cuda_stream
+        K.lib.fs2_stream_wait(side, K.stream())
+        K.conv_wgrad_k1_multi(jobs, rows, seq_len, lens=lens, ws_buf=ws, on_stream=side)
+        self.keep.extend((j[0], j[1]) for j in jobs)
+
     def join(self):
         """Make the current stream wait for every weight-gradient GEMM issued so far."""
+        self.flush()
         if self.side is not None:
             K.lib.fs2_stream_wait(K.stream(), self.side.cuda_stream)
             self.keep.clear()
@@ -172,6 +203,9 @@ class StepCtx:
             self.hook(params)
 
 
+# the FFT block's three k = 1 weight gradients (w_2, fc, QKV) as one grouped launch at the end
+# of its backward (fs2_conv_wgrad_k1_multi); FS2_GROUP_K1=0: one launch each (A/B)
+GROUP_K1 = os.environ.get("FS2_GROUP_K1", "1") != "0"
 # bf16 path: FFT-block post-LayerNorms fused into the fc / w_2 GEMM epilogues (fs2_conv_gemm_ln)
 FUSE_LN = os.environ.get("FS2_FUSE_LN", "1") != "0"  # step-level A/B switch
 FUSE_LN_MIN_ROWS = 16384
@@ -395,7 +429,8 @@ class FFTBlock(nn.Module):
                                   site_in=self.site + 1, dres=dx1, dres_add=False, copy=ctx.copy,
                                   dbias_in=_g(w2.bias))
         dy2_c = _t(dy2, dy2_t)
-        ctx.wgrad(dy2_c, h, _g(w2.weight), M, T, w2.c_in, d, w2.k, w2.padding, lens=lens)
+        ctx.wgrad(dy2_c, h, _g(w2.weight), M, T, w2.c_in, d, w2.k, w2.padding, lens=lens,
+                  group=GROUP_K1)
         dh = K.conv_gemm(dy2_c, w2._w_bwd, M, T, d, w2.c_in, w2.k, w2.padding,
                          flags=K.EPI_RELU_MASK_AUX, aux=h, out_dtype=cdt, lens=lens)
         if not WGRAD_AFTER_DGRAD:
@@ -414,10 +449,12 @@ class FFTBlock(nn.Module):
                               dbias_in=_g(a.fc.bias))
         dy1_c = _t(dy1, dy1_t)
         hd = a.n_head * a.d_k
-        ctx.wgrad(dy1_c, o, _g(a.fc.weight), M, T, hd, d, 1, 0, lens=lens)
+        ctx.wgrad(dy1_c, o, _g(a.fc.weight), M, T, hd, d, 1, 0, lens=lens, group=GROUP_K1)
         do = K.conv_gemm(dy1_c, a.fc._w_bwd, M, T, d, hd, 1, 0, out_dtype=cdt, lens=lens)
         dqkv = K.attn_bwd(qkv, o, do, lse, lens, B, T, a.n_head, a.d_k, 1.0 / math.sqrt(a.d_k))
-        ctx.wgrad(dqkv, x_c, self._qkv_gw, M, T, d, n3, 1, 0, db=self._qkv_gb, lens=lens)
+        ctx.wgrad(dqkv, x_c, self._qkv_gw, M, T, d, n3, 1, 0, db=self._qkv_gb, lens=lens,
+                  group=GROUP_K1)
+        ctx.flush()
         if prev is not None:
             pb, ps = prev
             pf = pb.pos_ffn

@@ -984,11 +984,14 @@ def test_convT_as_phase_conv():
 
 @pytest.mark.parametrize("B,T,cin,cout,k", [(6, 512, 256, 1024, 9), (4, 128, 256, 256, 3),
                                             (3, 256, 512, 512, 5), (48, 128, 256, 1024, 9),
-                                            (2, 64, 1024, 256, 9)])
+                                            (2, 64, 1024, 256, 9), (3, 64, 200, 1024, 9),
+                                            (2, 128, 256, 1000, 5), (3, 128, 256, 1024, 3)])
 def test_conv_wgrad_halo(B, T, cin, cout, k):
-    """The all-taps halo weight gradient (taps 3/5/9, T % 64 == 0) against fp32 autograd on
-    the same bf16 data and against the tap-major kernel, with the fused bias gradient and
-    the padding k-tile skip."""
+    """The Conv1d (taps 3/5/9) weight gradient with its fused bias gradient against fp32
+    autograd on the same bf16 data: FS2_TUNE_WGRAD_HALO 0 = the slab-free band kernel where the
+    32 x 32 output tiles fill the chip (else the split-K halo kernel), 1 = the split-K halo
+    kernel (C_in % 64 == 0, else tap-major), -1 = the tap-major kernel.  Partial o / c tiles,
+    determinism, accumulation into dw, and the padding-band skip under lens."""
     pad = (k - 1) // 2
     x = bf(rnd(B * T, cin, seed=71))
     dy = bf(rnd(B * T, cout, seed=72))
@@ -1002,14 +1005,19 @@ def test_conv_wgrad_halo(B, T, cin, cout, k):
             dw, db = torch.zeros_like(w), torch.zeros(cout, device=DEV)
             K.conv_wgrad(dy, x, dw, B * T, T, cin, cout, k, pad, db=db)
             out[mode] = (dw, db)
+            close(dw, wr.grad, 1e-5)
+            close(db, dy.float().sum(0), 1e-5)
     finally:
         K.lib.fs2_set_tuning(7, 0)
-    close(out[0][0], wr.grad, 1e-5)
-    close(out[0][1], dy.float().sum(0), 1e-5)
-    close(out[0][0], out[-1][0], 1e-5)
-    # the two halo wave layouts run the same MFMAs on the same fragments: bitwise equal
-    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
-    # lens: zero dy rows past each length, skipped k-tiles change nothing (bitwise)
+    # fixed reduction order: a second run is bitwise equal; dw / db accumulate
+    dw2, db2 = out[0][0].clone(), out[0][1].clone()
+    K.conv_wgrad(dy, x, dw2, B * T, T, cin, cout, k, pad, db=db2)
+    dw3, db3 = torch.zeros_like(w), torch.zeros(cout, device=DEV)
+    K.conv_wgrad(dy, x, dw3, B * T, T, cin, cout, k, pad, db=db3)
+    assert torch.equal(dw3, out[0][0]) and torch.equal(db3, out[0][1])
+    close(dw2, 2 * wr.grad, 1e-5)
+    close(db2, 2 * dy.float().sum(0), 1e-5)
+    # lens: zero dy rows past each length; the all-padding bands / k-tiles are skipped
     lens = torch.tensor([T - (13 * u) % T for u in range(B)], device=DEV)
     padr = (torch.arange(T, device=DEV)[None] >= lens[:, None]).reshape(-1)
     dyz = dy * (~padr)[:, None]
@@ -1017,4 +1025,48 @@ def test_conv_wgrad_halo(B, T, cin, cout, k):
     dw1, db1 = torch.zeros_like(w), torch.zeros(cout, device=DEV)
     K.conv_wgrad(dyz, x, dw0, B * T, T, cin, cout, k, pad, db=db0)
     K.conv_wgrad(dyz, x, dw1, B * T, T, cin, cout, k, pad, db=db1, lens=lens)
-    assert torch.equal(dw0, dw1) and torch.equal(db0, db1)
+    close(dw1, dw0, 1e-6)
+    close(db1, db0, 1e-6)
+
+
+@pytest.mark.parametrize("B,T,lens_on", [(48, 512, True), (48, 128, False), (3, 64, True),
+                                         (2, 128, False)])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+def test_wgrad_k1_multi(B, T, lens_on, dt):
+    """The grouped k = 1 weight gradient (the FFT block's QKV + bias, fc and w_2 products in one
+    launch: wgrad_k1_multi + one split reduce) against fp32 references on the same data, with
+    accumulation into dw / db, a partial 128-wide tile (80 outputs), determinism, and the
+    padding k-tile skip under lens."""
+    M = B * T
+    shapes = [(256, 768, True), (256, 256, False), (1024, 256, False), (256, 80, True)]
+    lens = None
+    valid = torch.ones(M, dtype=torch.bool, device=DEV)
+    if lens_on:
+        lens = torch.tensor([T - (37 * u) % T for u in range(B)], device=DEV)
+        valid = (torch.arange(T, device=DEV)[None] < lens[:, None]).reshape(-1)
+    jobs, refs = [], []
+    for i, (cin, cout, bias) in enumerate(shapes):
+        x = rnd(M, cin, seed=90 + i).to(dt)
+        dy = (rnd(M, cout, seed=95 + i) * valid[:, None]).to(dt)
+        dw = rnd(cout, cin, scale=0.1, seed=99 + i)
+        db = rnd(cout, scale=0.1, seed=103 + i) if bias else None
+        refs.append((dw + dy.float().t() @ x.float(), None if db is None else db + dy.float().sum(0)))
+        jobs.append((dy, x, dw, db, cin, cout))
+    snap = [(j[2].clone(), None if j[3] is None else j[3].clone()) for j in jobs]
+    K.conv_wgrad_k1_multi(jobs, M, T, lens=lens)
+    tol = 1e-5 if dt == torch.bfloat16 else 1e-4
+    for (dy, x, dw, db, cin, cout), (rw, rb) in zip(jobs, refs):
+        close(dw, rw, tol)
+        if db is not None:
+            close(db, rb, tol)
+    # a second run from the same starting point is bitwise equal
+    first = [(j[2].clone(), None if j[3] is None else j[3].clone()) for j in jobs]
+    for j, (w0, b0) in zip(jobs, snap):
+        j[2].copy_(w0)
+        if j[3] is not None:
+            j[3].copy_(b0)
+    K.conv_wgrad_k1_multi(jobs, M, T, lens=lens)
+    for j, (w1, b1) in zip(jobs, first):
+        assert torch.equal(j[2], w1)
+        if j[3] is not None:
+            assert torch.equal(j[3], b1)

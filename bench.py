@@ -108,7 +108,8 @@ class ClassTimer:
         self.rec = []                  # (class, start, end, flop)
         self._streams = {}
         self._pool, self._next = [], 0  # events created up front (creation is host-expensive)
-        self._orig = {n: getattr(K, n) for n in ("conv_gemm", "conv_wgrad", "attn_fwd", "attn_bwd")}
+        self._orig = {n: getattr(K, n) for n in ("conv_gemm", "conv_wgrad", "conv_wgrad_k1_multi",
+                                                 "attn_fwd", "attn_bwd")}
 
     def reset(self, mode, n_events):
         self.mode, self.rec, self._next = mode, [], 0
@@ -154,6 +155,12 @@ class ClassTimer:
             return T._timed(f"wgrad_k{taps}", 2.0 * r * c_out * c_in * taps, kw.get("on_stream"),
                             o["conv_wgrad"], dy, x, dw, rows, seq_len, c_in, c_out, taps, pad, **kw)
 
+        def conv_wgrad_k1_multi(jobs, rows, seq_len, **kw):  # grouped k = 1 weight gradients
+            r = T._rows(rows, seq_len, kw.get("lens"))
+            fl = sum(2.0 * r * j[4] * j[5] for j in jobs)
+            return T._timed("wgrad_k1", fl, kw.get("on_stream"), o["conv_wgrad_k1_multi"], jobs,
+                            rows, seq_len, **kw)
+
         def attn_fwd(qkv, lens, batch, seq_len, heads, d_head, scale):
             fl = 4.0 * heads * d_head * T.sq_by_T.get(seq_len, batch * seq_len * seq_len)
             return T._timed("attention_fwd", fl, None, o["attn_fwd"], qkv, lens, batch, seq_len,
@@ -165,6 +172,7 @@ class ClassTimer:
                             batch, seq_len, heads, d_head, scale)
 
         self.K.conv_gemm, self.K.conv_wgrad = conv_gemm, conv_wgrad
+        self.K.conv_wgrad_k1_multi = conv_wgrad_k1_multi
         self.K.attn_fwd, self.K.attn_bwd = attn_fwd, attn_bwd
 
     def table(self, steps, peak):
@@ -255,7 +263,7 @@ class OpTimer:
     main-stream chain as in every step."""
 
     FNS = ("conv_gemm", "conv_gemm_ln", "conv_gemm_ln_bwd", "attn_fwd", "attn_bwd", "ln_fwd",
-           "ln_bwd", "conv_wgrad")
+           "ln_bwd", "conv_wgrad", "conv_wgrad_k1_multi")
     FWD = {(256, 768, 1): "qkv", (256, 256, 1): "fc", (256, 1024, 9): "w1_k9",
            (1024, 256, 1): "w2"}
     BWD = {(256, 1024, 1): "w2_dgrad", (1024, 256, 9): "w1_k9_dgrad", (256, 256, 1): "fc_dgrad",
@@ -285,6 +293,11 @@ class OpTimer:
             return "attention_bwd", 10.0 * a[7] * a[8] * self.sq_by_T.get(a[6], a[5] * a[6] * a[6])
         if name in ("ln_fwd", "ln_bwd"):
             return name, 0.0
+        if name == "conv_wgrad_k1_multi":  # (jobs, rows, seq_len): w_2 + fc + QKV, one launch
+            jobs, rows, T = a[0], a[1], a[2]
+            r = self.valid_by_T.get(T, rows) if kw.get("lens") is not None else rows
+            names = "+".join(self.WGRAD.get((j[4], j[5], 1), "k1").replace("_wgrad", "") for j in jobs)
+            return f"{names}_wgrad(grouped)", sum(2.0 * r * j[4] * j[5] for j in jobs)
         rows, T, c_in, c_out, taps = a[2], a[3], a[4], a[5], a[6]
         if name == "conv_wgrad":
             rows, T, c_in, c_out, taps = a[3], a[4], a[5], a[6], a[7]
@@ -520,11 +533,8 @@ def main():
         K.lib.fs2_set_tuning(int(knob), int(val))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if os.environ.get("FS2_MAIN_PRIORITY"):  # A/B: the step's main chain on a prioritised stream
-        main_stream = torch.cuda.Stream(dev, priority=int(os.environ["FS2_MAIN_PRIORITY"]))
-        torch.cuda.set_stream(main_stream)
     # FS2_DP1=1 (A/B): at N = 1, run the step through the data-parallel path on a one-rank
-    # RCCL group (global denominators, bucketed all-reduce on the communication stream) to
+    # RCCL group (global denominators, bucketed all-reduce from the weight-gradient stream) to
     # price that machinery without the interconnect
     dp1 = world == 1 and os.environ.get("FS2_DP1") == "1"
     if world > 1 or dp1:

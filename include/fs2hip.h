@@ -235,23 +235,21 @@ int fs2_weight_prep_tile_channels(int dtype);
 int fs2_weight_prep_batch(int dtype, const int64_t* jobs, int n_jobs, int64_t n_tiles,
                           void* stream);
 
-/* Kernel-selection knobs for benchmarking (0 = automatic choice, the default):
- *   FS2_TUNE_GEMM_STAGES   fwd/dX LDS stages (1 or 2)
- *   FS2_TUNE_WGRAD_STAGES  weight-gradient LDS stages (1 or 2)
- *   FS2_TUNE_WGRAD_TILE    weight-gradient tile width (64 or 128)
- *   FS2_TUNE_WGRAD_SPLITS  weight-gradient row splits (1..64)
- *   FS2_TUNE_LEGACY_GEMM   1 = the register-staged bf16 kernels of round 1
+/* Kernel-selection knobs for benchmarking (0 = automatic choice, the default).  Variants that
+ * measured slower or neutral were removed in round 4 (their A/B records stay in profiles/):
+ *   FS2_TUNE_GEMM_STAGES   fwd/dX LDS stages (1..4) of the tap-major kernel
+ *   FS2_TUNE_WGRAD_STAGES  weight-gradient LDS stages (1..4) of the tap-major wgrad kernel
+ *   FS2_TUNE_WGRAD_TILE    weight-gradient tile width (64 or 128) of the tap-major wgrad kernel
+ *   FS2_TUNE_WGRAD_SPLITS  weight-gradient row splits (1..64) of the split-K wgrad kernels
+ *   FS2_TUNE_LEGACY_GEMM   1 = the register-staged bf16 kernels of round 1 (A/B against round 1)
  *   FS2_TUNE_NT_GROUP      fwd/dX n-tiles per L2 tile group
- *   FS2_TUNE_NT_HALO       fwd/dX Conv1d (taps > 1) halo kernel: 0 = automatic (default),
- *                          -1 = off (tap-major kernel), 1 = 4-wave tiles only, 2 = force
- *                          128-wide tiles, 3 = single-buffered weight tile, 4 = 3-slot ring,
- *                          5 / 6 / 7 = 8-wave 256x128 3-slot / 128x128 3-slot / 256x128 2-slot,
- *                          9 = round-2's rule (8-wave 256x128 also for C_in = 512; A/B only)
- *   FS2_TUNE_WGRAD_HALO    weight gradient of Conv1d taps 3/5/9: 0 = halo kernel, each wave
- *                          64 (o) x 16 (c) for all taps (default), 1 = halo kernel with the
- *                          round-1 32 x 32 wave quarters, 2 = 8-wave blocks of two k-groups
- *                          (half the row splits and fp32 slabs), 3 = three LDS stages (two
- *                          k-tiles in flight), -1 = tap-major kernel
+ *   FS2_TUNE_NT_HALO       fwd/dX Conv1d (taps > 1) halo kernel: 0 = automatic (8-wave 256 x 128
+ *                          tiles for the wide c_in <= 256 forward shapes, else 4-wave tiles by
+ *                          grid size), 1 = 4-wave tiles only, 2 = force 128-wide 4-wave tiles,
+ *                          -1 = off (tap-major kernel)
+ *   FS2_TUNE_WGRAD_HALO    weight gradient of Conv1d taps 3/5/9: 0 = the slab-free band kernel
+ *                          where its 32 x 32 output tiles fill the chip, else the split-K halo
+ *                          kernel (default), 1 = the split-K halo kernel, -1 = tap-major kernel
  *   FS2_TUNE_HALO_SPLITK   64x64 halo fwd/dX on an under-filled grid (long-K encoder data
  *                          gradient): 0 = automatic channel-block split (128x64 tiles when
  *                          T % 128 == 0), -1 = off, -2 = 64x64 tiles only, n = n splits
@@ -260,49 +258,29 @@ int fs2_weight_prep_batch(int dtype, const int64_t* jobs, int n_jobs, int64_t n_
  *                          at two workgroups per CU in dK/dV (automatic), -1 = one group
  *                          everywhere, 1 = as 0 with the one-workgroup-per-CU dK/dV build,
  *                          2 = two groups in dK/dV too, 3 = dK/dV at three workgroups per CU
- *   FS2_TUNE_HALO_DB       halo fwd/dX kernel, 2-slot weight ring: 0 = one halo stage, loaded
- *                          at each channel block (default), 1 = double-buffered halo stage
- *                          (the next channel block's rows in flight; A/B within run noise)
- *   FS2_TUNE_HALO_PIPE     halo fwd/dX kernel, 2-slot weight ring: 0 = fragment-pipelined
- *                          loop (default: the next step's LDS fragments are read under the
- *                          current step's second MFMA half; one barrier per step, mid-step),
- *                          -1 = the loop that reads all of a step's fragments after its barrier,
- *                          2 = pipelined without the half-width body for waves whose second
- *                          half of rows is past the utterance length (lens given)
  *   FS2_TUNE_NT_TILE       tap-major fwd/dX kernel (k = 1 projections, odd shapes): 0 = tile
  *                          by grid size, 1 / 2 / 3 = force 128x128 / 128x64 / 64x64
- *   FS2_TUNE_LN_TILE       fs2_conv_gemm_ln(_bwd) row tile: 0 = 64 x 256 (default), 1 = 128 x 256,
- *                          2 = 64 x 256 with one LDS stage (k = 1, C_in % 64 == 0)
+ *   FS2_TUNE_LN_TILE       fs2_conv_gemm_ln(_bwd) row tile: 0 = 64 x 256 (default), 1 = 128 x 256
  *   FS2_TUNE_WGRAD_K1      k = 1 weight gradient: 0 = 64 x 64 tiles with the 128-row k-tiles
  *                          split over 4 waves (default), 1 = 128 x 128 tiles of 8 waves
  *                          (both: buffer-descriptor staging), -1 = the tap-major kernel;
  *                          -2 = also the round-2 split reduce for taps > 1 (A/B)
- *   FS2_TUNE_PERSIST       k = 1 projections (fs2_conv_gemm, _ln, _ln_bwd) on grids of >= 2
- *                          tiles per CU: 1 = persistent GEMM (ring across tiles), 0 = per-tile
- *                          launch grid (default)
  *   FS2_TUNE_NT_K1         k = 1 projections on the tap-major kernel: 0 = buffer-descriptor
  *                          staging build (default), -1 = the general tap-walking build (A/B)
  *   FS2_TUNE_ATTN_DMA      bf16 attention at T >= 256: 0 = K / V (Q / dO) tiles by LDS-DMA into
  *                          a 2-slot ring, exp2-folded softmax (default), 1 = 3-slot forward ring
  *                          at one workgroup per CU, -1 = the register-staged kernels (A/B)
- *   FS2_TUNE_WGRAD_FUSE    k = 1 weight gradient (FS2_TUNE_WGRAD_K1 = 0): 0 = split slabs summed
- *                          by a reduce launch (default), 1 = the last split to finish a tile sums
- *                          them in split order inside the kernel (no reduce launch)
- *   FS2_TUNE_TAPREG        fwd/dX Conv1d taps 5 / 9 (C_in % 64 == 0, T % 128 == 0): 0 = the
- *                          tap-register halo kernel where its grid fills the chip (default:
- *                          4-wave 128 x 64 tiles at 3 blocks per CU, 128 x 128 at 2 for
+ *   FS2_TUNE_TAPREG        fwd/dX Conv1d taps 5 / 9 (C_in % 64 == 0, T and rows % 128 == 0):
+ *                          0 = the tap-register halo kernel where its grid fills the chip
+ *                          (default: 4-wave 128 x 64 tiles at 3 blocks per CU, 128 x 128 at 2 for
  *                          c_out <= 256), -1 = off (the halo kernels above), 1 = force the
- *                          128 x 64 tiles, 2 = force 8-wave 256 x 128 tiles (when T allows),
- *                          3 = force 128 x 128, 4 / 5 = 128 x 64 at 2 blocks per CU with a
- *                          4- / 3-slot weight ring, 7 = 128 x 128 also for c_out <= 512 (A/B)
+ *                          128 x 64 tiles, 3 = force 128 x 128
  * Process-wide; query workspace sizes after setting.                                 */
 enum { FS2_TUNE_GEMM_STAGES = 0, FS2_TUNE_WGRAD_STAGES = 1, FS2_TUNE_WGRAD_TILE = 2,
        FS2_TUNE_WGRAD_SPLITS = 3, FS2_TUNE_LEGACY_GEMM = 4, FS2_TUNE_NT_GROUP = 5,
        FS2_TUNE_NT_HALO = 6, FS2_TUNE_WGRAD_HALO = 7, FS2_TUNE_HALO_SPLITK = 8,
-       FS2_TUNE_ATTN = 9, FS2_TUNE_HALO_DB = 10, FS2_TUNE_HALO_PIPE = 11, FS2_TUNE_NT_TILE = 12,
-       FS2_TUNE_LN_TILE = 13, FS2_TUNE_WGRAD_K1 = 14, FS2_TUNE_PERSIST = 15,
-       FS2_TUNE_NT_K1 = 16, FS2_TUNE_ATTN_DMA = 17,
-       FS2_TUNE_WGRAD_FUSE = 18, FS2_TUNE_TAPREG = 19, FS2_TUNE_COUNT = 20 };
+       FS2_TUNE_ATTN = 9, FS2_TUNE_NT_TILE = 10, FS2_TUNE_LN_TILE = 11, FS2_TUNE_WGRAD_K1 = 12,
+       FS2_TUNE_NT_K1 = 13, FS2_TUNE_ATTN_DMA = 14, FS2_TUNE_TAPREG = 15, FS2_TUNE_COUNT = 16 };
 int fs2_set_tuning(int knob, int value);
 
 /* Weight (and optionally bias) gradient, accumulated into the fp32 master-gradient layout:

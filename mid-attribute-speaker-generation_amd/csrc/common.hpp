@@ -85,7 +85,7 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
 int conv_wgrad_glds_launch(const void* dy, int64_t ldy, const void* x, int64_t ldx, float* dw,
                            float* db, int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out,
                            int taps, int pad, const int64_t* lens, int splits, int tile, float* ws,
-                           unsigned* ctr, hipStream_t st);
+                           hipStream_t st);
 int conv_wgrad_band_launch(const void* dy, int64_t ldy, const void* x, int64_t ldx, float* dw,
                            float* db, int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out,
                            int taps, int pad, const int64_t* lens, hipStream_t st);

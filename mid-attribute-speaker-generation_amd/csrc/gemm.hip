@@ -547,18 +547,12 @@ int fs2_conv_weight_prep(int dtype, const float* w, int64_t c_out, int64_t c_in,
   return launch_status("fs2_conv_weight_prep");
 }
 
-// workspace: split slabs [S][c_out][taps c_in], bias partials, then one arrival counter per
-// 64 x 64 output tile (the in-kernel split reduce of wgrad_k1_q)
-static int64_t wgrad_ctr_offset(int64_t rows, int64_t c_in, int64_t c_out, int taps) {
+// workspace: split slabs [S][c_out][taps c_in], then the bias partials
+int64_t fs2_conv_wgrad_ws_bytes(int64_t rows, int64_t c_in, int64_t c_out, int taps) {
   const int64_t S = wgrad_splits(rows, c_in, c_out, taps);
   const int64_t bias_part = S * c_out > ((rows + CS_ROWS - 1) / CS_ROWS) * c_out
                                 ? S * c_out : ((rows + CS_ROWS - 1) / CS_ROWS) * c_out;
-  return S * c_out * taps * c_in + bias_part;  // floats
-}
-
-int64_t fs2_conv_wgrad_ws_bytes(int64_t rows, int64_t c_in, int64_t c_out, int taps) {
-  const int64_t ctrs = ((c_out + 63) / 64) * ((taps * c_in + 63) / 64);
-  return (wgrad_ctr_offset(rows, c_in, c_out, taps) + ctrs) * 4;
+  return (S * c_out * taps * c_in + bias_part) * 4;
 }
 
 int fs2_conv_wgrad(int dtype, const void* dy, int64_t ldy, const void* x, int64_t ldx, float* dw,
@@ -573,8 +567,6 @@ int fs2_conv_wgrad(int dtype, const void* dy, int64_t ldy, const void* x, int64_
     if (!g_tune[FS2_TUNE_LEGACY_GEMM])
       return conv_wgrad_glds_launch(dy, ldy, x, ldx, dw, db, rows, seq_len, c_in, c_out, taps, pad,
                                     lens, S, wgrad_tile(rows, c_in, c_out, taps), ws,
-                                    reinterpret_cast<unsigned*>(
-                                        ws + wgrad_ctr_offset(rows, c_in, c_out, taps)),
                                     as_stream(stream));
     int rc = conv_wgrad_bf16_launch(dy, ldy, x, ldx, ws, rows, seq_len, c_in, c_out, taps, pad, S,
                                     as_stream(stream));

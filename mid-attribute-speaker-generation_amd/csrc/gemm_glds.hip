@@ -56,8 +56,6 @@ struct GldsArgs {
   u16* y2;              // FS2_EPI_Y2 bf16 output (ld = N)
   float alpha2;
   int kz;               // halo kernel: channel-block splits (0/1 = none; see halo_splitk_reduce)
-  int halo_db;          // halo kernel, BST == 2: double-buffered halo stage (FS2_TUNE_HALO_DB)
-  int no_trim;          // halo kernel, pipelined loop: no half-width body (FS2_TUNE_HALO_PIPE 2)
   float* slab;          // kz > 1: [kz][M][N] fp32 partial products
   // LayerNorm epilogue (fs2_conv_gemm_ln; 256-wide tiles hold whole rows): ln_out != NULL
   const float* ln_res;
@@ -170,9 +168,8 @@ FS2_DEV void kloop(int nk, Issue&& issue, Compute&& compute) {
 }
 
 // Workgroup barrier of the epilogues: LDS writes retired (lgkmcnt(0)), then a raw s_barrier.
-// __syncthreads() would also wait vmcnt(0), draining any LDS-DMA still in flight -- in the
-// persistent GEMM that is the next tile's k-steps; at the end of the other kernels no DMA is
-// in flight and the two are the same.  (The epilogues share no global memory between threads.)
+// __syncthreads() would also wait vmcnt(0); at the end of the kernels no DMA is in flight and
+// the two are the same.  (The epilogues share no global memory between threads.)
 FS2_DEV void epi_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -694,161 +691,19 @@ __global__ __launch_bounds__(256) void conv_gemm_nt_glds(GldsArgs a) {
   nt_epilogue<BM, BN, VOC>(a, acc, smem, m0, n0, skip, tid, wm, wn, g, r16);
 }
 
-// ------------------------------------------------------------------------ persistent k = 1 GEMM
-// gemm_nt_persist: the tap-major kernel's tiles and epilogues for the Linear / 1x1 Conv1d
-// projections (taps = 1, K % 64 == 0), persistent: one workgroup per CU slot walks a list of
-// tiles, and its LDS-DMA ring of STAGES k-tile slots runs across tile boundaries -- the next
-// tile's first k-steps are in flight while the current tile's epilogue (through its own LDS
-// region, raw barriers that leave the DMA pending) stores.  The short-K projections (K = 256:
-// four k-steps) were bound by that per-tile chain of load latency -> MFMA -> store, not by
-// bytes or MFMAs (profiles/r2_hipblaslt_vs_ours.txt).  Each XCD takes a contiguous range of
-// tiles, n fastest (a row band's A tile is re-read by the n-tiles from its XCD's L2); with
-// lens the m-tiles are interleaved as in conv_gemm_nt_glds and all-padding tiles run no
-// k-steps (epilogue only).
-template <int BM, int BN, int STAGES>
-__global__ __launch_bounds__(256, 1) void gemm_nt_persist(GldsArgs a) {
-  constexpr int BK = 64;
-  constexpr int AW = BM / 32, BW = BN / 32;  // glds per wave per k-step
-  constexpr int MI = BM / 32, NI = BN / 32;
-  constexpr int STAGE_E = (BM + BN) * BK;
-  constexpr int EPI_LD = BN + 4;
-  // epilogue region: the fp32 half tile (+ nt_epilogue_lnbwd's reduction rows on 64 x 256 tiles)
-  constexpr int EPI_E = (BM / 2) * EPI_LD * 2 + (BM == 64 && BN == 256 ? 3 * 8 * 64 * 8 : 0);
-  __shared__ __attribute__((aligned(1024))) u16 smem[STAGES * STAGE_E + EPI_E];
-  u16* epi = smem + STAGES * STAGE_E;
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
-  const int g = lane >> 4, r16 = lane & 15;
-
-  // this workgroup's tiles: XCD x = blockIdx % 8 owns tiles [T x / 8, T (x + 1) / 8), its
-  // workgroups take every gx-th of them
-  const int T = a.tiles_m * a.tiles_n, G = gridDim.x;
-  const int xcd = blockIdx.x & 7, jx = blockIdx.x >> 3, gx = (G - xcd + 7) >> 3;
-  const int t_beg = (int)((int64_t)T * xcd / 8) + jx, t_end = (int)((int64_t)T * (xcd + 1) / 8);
-  const int nk = a.K / BK;
-  auto tile_of = [&](int t, int64_t& m0, int& n0) {
-    const int tm = m_interleave(t / a.tiles_n, a.tiles_m, a.lens != nullptr);
-    m0 = (int64_t)tm * BM;
-    n0 = (t % a.tiles_n) * BN;
-  };
-  auto steps_of = [&](int t) {  // k-steps of tile t (0: all rows padding)
-    int64_t m0;
-    int n0;
-    tile_of(t, m0, n0);
-    const bool skip = a.lens && rows_all_padding(a.lens, a.T, m0, m0 + BM < a.M ? m0 + BM : a.M);
-    return skip ? 0 : nk;
-  };
-
-  // per-lane staging: A row R = (wave AW + i) * 8 + lane / 8 (logical chunk (lane & 7) ^
-  // ((R >> 1) & 7)), B row likewise
-  const int lrow = lane >> 3;
-  int a_lc[AW], b_lc[BW];
-#pragma unroll
-  for (int i = 0; i < AW; ++i) a_lc[i] = (lane & 7) ^ ((((wave * AW + i) * 8 + lrow) >> 1) & 7);
-#pragma unroll
-  for (int i = 0; i < BW; ++i) b_lc[i] = (lane & 7) ^ ((((wave * BW + i) * 8 + lrow) >> 1) & 7);
-  const u16* zero = reinterpret_cast<const u16*>(g_zero_line);
-  auto issue = [&](int t, int kt, int slot) {
-    int64_t m0;
-    int n0;
-    tile_of(t, m0, n0);
-    u16* As = smem + slot * STAGE_E;
-    u16* Bs = As + BM * BK;
-    const int k0 = kt * BK;
-#pragma unroll
-    for (int i = 0; i < AW; ++i) {
-      const int64_t m = m0 + (wave * AW + i) * 8 + lrow;
-      glds16(m < a.M ? a.x + m * a.ldx + k0 + a_lc[i] * 8 : zero, As + (wave * AW + i) * 8 * BK);
-    }
-#pragma unroll
-    for (int i = 0; i < BW; ++i) {
-      const int n = n0 + (wave * BW + i) * 8 + lrow;
-      glds16(n < a.N ? a.w + (int64_t)n * a.K + k0 + b_lc[i] * 8 : zero, Bs + (wave * BW + i) * 8 * BK);
-    }
-  };
-
-  f32x4 acc[MI][NI];
-  const int sw = (r16 >> 1) & 7;
-  const int fo0 = r16 * BK + ((0 * 4 + g) ^ sw) * 8;
-  const int fo1 = r16 * BK + ((1 * 4 + g) ^ sw) * 8;
-  auto compute = [&](int slot) {
-    const u16* As = smem + slot * STAGE_E + wm * (BM / 2) * BK;
-    const u16* Bs = smem + slot * STAGE_E + BM * BK + wn * (BN / 2) * BK;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int fo = ks ? fo1 : fo0;
-      bf16x8g fa[MI], fb[NI];
-#pragma unroll
-      for (int i = 0; i < MI; ++i) fa[i] = *reinterpret_cast<const bf16x8g*>(As + i * 16 * BK + fo);
-#pragma unroll
-      for (int j = 0; j < NI; ++j) fb[j] = *reinterpret_cast<const bf16x8g*>(Bs + j * 16 * BK + fo);
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < NI; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-    }
-  };
-
-  // issue cursor (tile it, k-step ik) over the flattened (tile, k-step) stream; `ahead` steps
-  // issued beyond the one being consumed
-  int it = t_beg, ik = 0;
-  while (it < t_end && steps_of(it) == 0) it += gx;
-  auto advance = [&]() {
-    if (++ik == nk) {
-      ik = 0;
-      do it += gx; while (it < t_end && steps_of(it) == 0);
-    }
-  };
-  int issued = 0, consumed = 0;
-  for (int d = 0; d < STAGES - 1 && it < t_end; ++d) {
-    issue(it, ik, issued % STAGES);
-    ++issued;
-    advance();
-  }
-  for (int t = t_beg; t < t_end; t += gx) {
-    int64_t m0;
-    int n0;
-    tile_of(t, m0, n0);
-    const int ns = steps_of(t);
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-      for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int kt = 0; kt < ns; ++kt) {
-      // step `consumed` landed: at most (issued - consumed - 1) younger steps stay in flight
-      const int ahead = issued - consumed - 1;
-      vm_wait_tiles<AW + BW>(ahead < STAGES - 2 ? ahead : STAGES - 2);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      if (it < t_end) {  // refill the slot consumed last step (every wave is past its reads)
-        issue(it, ik, issued % STAGES);
-        ++issued;
-        advance();
-      }
-      compute(consumed % STAGES);
-      ++consumed;
-    }
-    nt_epilogue<BM, BN, false>(a, acc, epi, m0, n0, ns == 0, tid, wm, wn, g, r16);
-  }
-}
-
 // ------------------------------------------------------------------------ halo variant
 // Conv1d with taps > 1, Cin % 64 == 0 and T % BM == 0 (every row tile lies inside one
 // utterance).  The reduction runs channel-block-major: for each 64-channel block the
 // BM + taps - 1 input rows of the tile and its tap halo (zero outside the utterance) are
 // staged in LDS ONCE, and tap j reads them at row offset j -- only the weight tile is
-// re-staged per tap.  Against the tap-major kernel above this removes (taps-1)/taps of the
-// A-operand LDS-DMA traffic: the k=9 FFN conv moves 18 KB instead of 32 KB per 64-deep step
-// of a 128 x 128 tile, and that traffic, not the MFMA, bounds the tap-major kernel
-// (per-CU vector-memory rate; profiles/).  LDS rows are swizzled chunk c -> c ^ (row & 7),
+// re-staged per tap, through a 2-slot ring.  Against the tap-major kernel above this removes
+// (taps-1)/taps of the A-operand LDS-DMA traffic: the k=9 FFN conv moves 18 KB instead of
+// 32 KB per 64-deep step of a 128 x 128 tile.  LDS rows are swizzled chunk c -> c ^ (row & 7),
 // which keeps the 16-row fragment reads conflict-free at every row offset.
 template <int BM, int BN, int BST, int HX, bool VOC, int NWAVE = 4, bool PIPE = false>
-__global__ __launch_bounds__(NWAVE * 64, NWAVE == 8 ? 1 : BST == 1 ? 4 : (HX > 16 || BST > 2) ? 2 : 3)
+__global__ __launch_bounds__(NWAVE * 64, NWAVE == 8 ? 1 : HX > 16 ? 2 : 3)
 void conv_gemm_halo(GldsArgs a) {
-  static_assert(!PIPE || BST == 2, "the fragment-pipelined loop runs on the 2-slot weight ring");
+  static_assert(BST == 2, "the 2-slot weight ring (1- and 3-slot rings measured slower, profiles/r2_ab_experiments.txt)");
   // NWAVE = 4: 2 x 2 waves; NWAVE = 8: 2 (rows) x 4 (columns) waves, one block per CU
   const int dil = VOC ? a.dil : 1;
   constexpr int BK = 64;
@@ -894,7 +749,6 @@ void conv_gemm_halo(GldsArgs a) {
   const int ncb_all = a.Cin / 64, cb0 = z * ncb_all / kz, cb1 = (z + 1) * ncb_all / kz;
 
   const int lrow = lane >> 3;
-  const u16* zero = reinterpret_cast<const u16*>(g_zero_line);
   const int HR = BM + (a.taps - 1) * dil, HP = (HR + 7) / 8;
   const int64_t u0 = (m0 / a.T) * a.T;
   // input rows past the utterance's length are zero in the FFT blocks (Layers.py:25,28) and in
@@ -906,7 +760,7 @@ void conv_gemm_halo(GldsArgs a) {
   // it are staged as zeros; outputs past it are masked downstream of the FFT / variance-
   // predictor convs -- the only lens users of this kernel)
   int mi_act = MI;
-  if (!VOC && a.lens && !a.no_trim) {
+  if (!VOC && a.lens) {
     const int64_t nv = u1 - (m0 + wm * (BM / 2));
     mi_act = nv <= 0 ? 0 : nv >= BM / 2 ? MI : (int)((nv + 15) / 16);
   }
@@ -1005,19 +859,7 @@ void conv_gemm_halo(GldsArgs a) {
   };
   if (!skip) {
     const int ncb = cb1 - cb0;
-    if constexpr (BST == 1) {
-      for (int cb = 0; cb < ncb; ++cb) {
-        for (int j = 0; j < a.taps; ++j) {
-          if (j == 0) issue_a(cb, 0);
-          issue_b(cb, j, 0);
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          __builtin_amdgcn_s_barrier();
-          compute(j, 0, 0);
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          __builtin_amdgcn_s_barrier();
-        }
-      }
-    } else if constexpr (PIPE) {
+    if constexpr (PIPE) {    } else if constexpr (PIPE) {
       // Fragment-pipelined 2-slot loop.  Step s = (cb, j) reads weight slot s & 1 and halo slot
       // cb & 1 as two k-halves held in two register sets: set 1 (s, ks 1) is read while set 0's
       // MFMAs issue; then ONE barrier, after which set 0 is refilled with step s + 1's first
@@ -1096,35 +938,6 @@ void conv_gemm_halo(GldsArgs a) {
       else pipe_loop(std::integral_constant<int, MI>{});
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
-    } else if (BST == 2 && a.halo_db) {
-      // Step s = (cb, j) reads halo slot cb & 1 and weight slot s & 1.  Issue order per step
-      // (after the barrier): weight tile s + 1, then -- at j == 0 -- the halo of channel block
-      // cb + 1 into the other halo slot (free: block cb - 1's last reads finished before this
-      // step's barrier).  Loads complete in issue order, so waiting for weight tile s also
-      // covers every halo issued before it; only at j == 1 is the just-issued halo allowed to
-      // stay in flight (vmcnt = this wave's halo pieces), giving it a full step to land.
-      const int S = ncb * a.taps;
-      issue_a(0, 0);
-      issue_b(0, 0, 0);
-      int cb = 0, j = 0;
-      for (int s = 0; s < S; ++s) {
-        if (j == 1 && cb + 1 < ncb) vm_wait_n(qa);
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        if (s + 1 < S) {
-          const int cbn = j + 1 == a.taps ? cb + 1 : cb, jn = j + 1 == a.taps ? 0 : j + 1;
-          issue_b(cbn, jn, (s + 1) & 1);
-        }
-        if (j == 0 && cb + 1 < ncb) issue_a(cb + 1, (cb + 1) & 1);
-        compute(j, s & 1, cb & 1);
-        if (++j == a.taps) {
-          j = 0;
-          ++cb;
-        }
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
     } else {
       // weight-tile ring of BST slots, BST-1 tiles ahead: step s = (cb, j) reads slot s % BST
       // while tiles s+1 .. s+BST-1 are in flight.  At a channel-block boundary the single
@@ -1139,8 +952,6 @@ void conv_gemm_halo(GldsArgs a) {
           __builtin_amdgcn_s_barrier();
           issue_a(cb, 0);
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        } else if (BST == 3 && s + 1 < S) {
-          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(BW) : "memory");  // tile s+1 may fly
         } else {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
@@ -1483,11 +1294,6 @@ struct WgradGlds {
   int64_t rows_per_split;
   int tiles_o, tiles_k, splits;
   const int64_t* lens;  // optional: 64-row k-tiles made only of padding rows are skipped
-  // in-kernel split reduce (wgrad_k1_q, FS2_TUNE_WGRAD_FUSE = 1): per-tile arrival counters
-  // (zeroed before the launch) and the gradients the last arriving split accumulates into
-  unsigned* ctr;
-  float* dw;
-  float* db;
 };
 
 typedef short s16x4g __attribute__((ext_vector_type(4)));
@@ -2141,37 +1947,6 @@ __global__ __launch_bounds__(256, 2) void wgrad_k1_q(WgradGlds a) {
       a.bslab[(int64_t)z * a.Cout + o0 + tid] =
           ((Bp[tid] + Bp[BO + tid]) + Bp[2 * BO + tid]) + Bp[3 * BO + tid];
   }
-  if (a.ctr) {
-    // the tile's last split to arrive sums the splits' partial tiles in split order (a fixed
-    // order whatever the arrival order: deterministic) into dw / db -- no separate reduce pass
-    __shared__ int last;
-    __threadfence();  // this block's partials visible device-wide before its arrival
-    __syncthreads();
-    if (tid == 0) last = atomicAdd(a.ctr + to * a.tiles_k + tc, 1u) == (unsigned)(a.splits - 1);
-    __syncthreads();
-    if (last) {
-      __threadfence();
-      const int o = tid >> 2, cc = (tid & 3) * 16;
-      const int64_t zs = (int64_t)a.Cout * a.Kp;
-      if (o0 + o < a.Cout) {
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
-          const int c = c0 + cc + 4 * v;
-          if (c >= a.Cin) continue;
-          const float* p = a.slab + (int64_t)(o0 + o) * a.Kp + c;
-          f32x4 t = ld4(p);
-          for (int zz = 1; zz < a.splits; ++zz) t += ld4(p + zz * zs);
-          float* d = a.dw + (int64_t)(o0 + o) * a.Cin + c;
-          st4(d, ld4(d) + t);
-        }
-      }
-      if (do_bias && tid < BO && o0 + tid < a.Cout) {
-        float b = a.bslab[o0 + tid];
-        for (int zz = 1; zz < a.splits; ++zz) b += a.bslab[(int64_t)zz * a.Cout + o0 + tid];
-        a.db[o0 + tid] += b;
-      }
-    }
-  }
 }
 
 // Halo weight gradient for Conv1d with 2 <= taps <= 9 (C_in, C_out multiples of 64, T a
@@ -2466,7 +2241,7 @@ __global__ __launch_bounds__(256) void wgrad_reduce_rows(const float* __restrict
 int conv_wgrad_glds_launch(const void* dy, int64_t ldy, const void* x, int64_t ldx, float* dw,
                            float* db, int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out,
                            int taps, int pad, const int64_t* lens, int splits, int tile, float* ws,
-                           unsigned* ctr, hipStream_t st) {
+                           hipStream_t st) {
   FS2_CHECK_ARG(c_in % 8 == 0 && c_out % 8 == 0 && ldx % 8 == 0 && ldy % 8 == 0 &&
                     ((uintptr_t)dy & 15) == 0 && ((uintptr_t)x & 15) == 0,
                 "fs2_conv_wgrad(bf16): channel counts / strides must be multiples of 8, operands 16-B aligned");
@@ -2487,15 +2262,6 @@ int conv_wgrad_glds_launch(const void* dy, int64_t ldy, const void* x, int64_t l
     a.tiles_o = (int)((c_out + 63) / 64);
     a.tiles_k = (int)((c_in + 63) / 64);
     const unsigned g1 = (unsigned)(a.tiles_o * a.tiles_k * splits);
-    if (g_tune[FS2_TUNE_WGRAD_FUSE] == 1 && ctr) {  // last-arriving split reduces in-kernel
-      if (hipMemsetAsync(ctr, 0, sizeof(unsigned) * a.tiles_o * a.tiles_k, st) != hipSuccess)
-        return launch_status("fs2_conv_wgrad(bf16)");
-      a.ctr = ctr;
-      a.dw = dw;
-      a.db = db;
-      wgrad_k1_q<2><<<g1, 256, 0, st>>>(a);
-      return launch_status("fs2_conv_wgrad(bf16)");
-    }
     wgrad_k1_q<2><<<g1, 256, 0, st>>>(a);
     const int64_t total = c_out * c_in;
     wgrad_reduce_k1<<<(unsigned)((total / 4 + 63) / 64), 256, 0, st>>>(ws, bslab, splits,
@@ -2577,13 +2343,6 @@ static int cu_count() {
       n = 256;
   }
   return n;
-}
-
-// gemm_nt_persist launch: one workgroup per CU (at most one per tile)
-template <int BM, int BN, int S>
-static void launch_persist(GldsArgs a, hipStream_t st) {
-  const int T = a.tiles_m * a.tiles_n, n = cu_count();
-  gemm_nt_persist<BM, BN, S><<<(unsigned)(T < n ? T : n), 256, 0, st>>>(a);
 }
 
 template <int BM, int BN, int S>
@@ -2689,16 +2448,7 @@ int conv_gemm_ln_glds_launch(const void* x, int64_t ldx, const void* wk, int64_t
   a.tiles_n = 1;
   const unsigned grid = (unsigned)a.tiles_m;
   const bool tapaligned = c_in % 64 == 0;
-  if (!wide && taps == 1 && tapaligned && g_tune[FS2_TUNE_PERSIST] > 0 &&
-      a.tiles_m >= 2 * cu_count()) {
-    launch_persist<64, 256, 2>(a, st);
-    return launch_status("fs2_conv_gemm_ln");
-  }
   const bool k1 = tapaligned && taps == 1 && g_tune[FS2_TUNE_NT_K1] >= 0;
-  if (g_tune[FS2_TUNE_LN_TILE] == 2 && k1) {  // one LDS stage (40 KB): 3-4 blocks per CU
-    conv_gemm_nt_glds<64, 256, 1, true, false, true><<<grid, 256, 0, st>>>(a);
-    return launch_status("fs2_conv_gemm_ln");
-  }
   if (wide) {
     if (tapaligned) conv_gemm_nt_glds<128, 256, 2, true, false><<<grid, 256, 0, st>>>(a);
     else conv_gemm_nt_glds<128, 256, 2, false, false><<<grid, 256, 0, st>>>(a);
@@ -2741,11 +2491,7 @@ int conv_gemm_lnbwd_glds_launch(const void* x, int64_t ldx, const void* wk, int6
   a.tiles_m = (int)((rows + 63) / 64);
   a.tiles_n = 1;
   const unsigned grid = (unsigned)a.tiles_m;
-  if (taps == 1 && c_in % 64 == 0 && g_tune[FS2_TUNE_LN_TILE] == 2 && g_tune[FS2_TUNE_NT_K1] >= 0)
-    conv_gemm_nt_glds<64, 256, 1, true, false, true><<<grid, 256, 0, st>>>(a);
-  else if (taps == 1 && c_in % 64 == 0 && g_tune[FS2_TUNE_PERSIST] > 0 && a.tiles_m >= 2 * cu_count())
-    launch_persist<64, 256, 2>(a, st);
-  else if (c_in % 64 == 0 && taps == 1 && g_tune[FS2_TUNE_NT_K1] >= 0)
+  if (c_in % 64 == 0 && taps == 1 && g_tune[FS2_TUNE_NT_K1] >= 0)
     conv_gemm_nt_glds<64, 256, 2, true, false, true><<<grid, 256, 0, st>>>(a);
   else if (c_in % 64 == 0) conv_gemm_nt_glds<64, 256, 2, true, false><<<grid, 256, 0, st>>>(a);
   else conv_gemm_nt_glds<64, 256, 2, false, false><<<grid, 256, 0, st>>>(a);
@@ -2771,9 +2517,6 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
   GldsArgs a{(const u16*)x, ldx, (const u16*)wk, y, ldy, rows, seq_len, (int)c_in, (int)c_out,
              taps, pad, K, bias, flags, aux, ld_aux, 0, 0, vec, 1, lens,
              ve.dil, ve.alpha, ve.scale, (u16*)ve.y2, ve.alpha2};
-  a.halo_db = g_tune[FS2_TUNE_HALO_DB] > 0 ? 1 : 0;
-  a.no_trim = g_tune[FS2_TUNE_HALO_PIPE] == 2 ? 1 : 0;
-  const bool pipe = g_tune[FS2_TUNE_HALO_PIPE] >= 0;  // step A/B: 8.46 -> 8.39 ms
   const bool tapaligned = c_in % 64 == 0;
   const bool voc = ve.dil != 1 || (flags & (FS2_EPI_LRELU | FS2_EPI_ACC_Y | FS2_EPI_Y2)) || !y;
   const int64_t big = ((rows + 127) / 128) * ((c_out + 127) / 128);
@@ -2814,17 +2557,15 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
   if (trk >= 0 && !voc && tapaligned && (taps == 5 || taps == 9) && pad >= 0 && pad < taps) {
     const int cu = cu_count();
     const int64_t t4 = (rows / 128) * ((c_out + 63) / 64);
-    const bool ok8 = seq_len % 256 == 0, ok4 = seq_len % 128 == 0;
+    const bool ok4 = seq_len % 128 == 0 && rows % 128 == 0 && rows % seq_len == 0;
     int pick = 0;
-    if (trk == 2) pick = ok8 ? 8 : 0;
-    else if (trk == 1) pick = ok4 ? 4 : 0;
-    else if (trk >= 3 && trk <= 5) pick = ok4 ? trk : 0;  // A/B variants below
-    else if (trk == 7 && ok4 && c_out <= 512 && t4 >= 3 * cu) pick = 3;  // A/B
+    if (trk == 1) pick = ok4 ? 4 : 0;                  // force 128 x 64
+    else if (trk == 3) pick = ok4 ? 3 : 0;             // force 128 x 128
     else if (ok4 && c_out <= 256 && t4 >= 3 * cu) pick = 3;
     else if (ok4 && t4 >= 3 * cu) pick = 4;
     if (pick) {
-      a.tiles_m = (int)(rows / (pick == 8 ? 256 : 128));
-      const bool n64 = pick != 8 && pick != 3;
+      a.tiles_m = (int)(rows / 128);
+      const bool n64 = pick == 4;
       a.tiles_n = (int)((c_out + (n64 ? 63 : 127)) / (n64 ? 64 : 128));
       // tile group: the n-tiles whose weight slice (~1.25 MB) an XCD's resident blocks share in
       // its 4 MB L2 while they walk the m-tiles (all 16 n-tiles of the decoder k=9 forward, a
@@ -2837,18 +2578,9 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
         a.group = gr < 1 ? 1 : gr > a.tiles_n ? a.tiles_n : gr;
       }
       const unsigned grid = (unsigned)(a.tiles_m * a.tiles_n);
-      if (pick == 8) {
-        if (taps == 9) conv_gemm_tapreg<256, 128, 4, 2, 4, 9, 4, 1><<<grid, 512, 0, st>>>(a);
-        else conv_gemm_tapreg<256, 128, 4, 2, 4, 5, 4, 1><<<grid, 512, 0, st>>>(a);
-      } else if (pick == 3) {  // 4-wave 128 x 128 tiles, 2 blocks per CU
+      if (pick == 3) {  // 4-wave 128 x 128 tiles, 2 blocks per CU
         if (taps == 9) conv_gemm_tapreg<128, 128, 2, 2, 4, 9, 2, 2><<<grid, 256, 0, st>>>(a);
         else conv_gemm_tapreg<128, 128, 2, 2, 4, 5, 2, 2><<<grid, 256, 0, st>>>(a);
-      } else if (pick == 5) {  // 3-slot weight ring (no LDS drain at the barrier), 2 per CU
-        if (taps == 9) conv_gemm_tapreg<128, 64, 2, 2, 4, 9, 3, 2><<<grid, 256, 0, st>>>(a);
-        else conv_gemm_tapreg<128, 64, 2, 2, 4, 5, 3, 2><<<grid, 256, 0, st>>>(a);
-      } else if (trk == 4) {  // 4-slot ring (tiles two taps ahead), 2 per CU
-        if (taps == 9) conv_gemm_tapreg<128, 64, 2, 2, 4, 9, 4, 2><<<grid, 256, 0, st>>>(a);
-        else conv_gemm_tapreg<128, 64, 2, 2, 4, 5, 4, 2><<<grid, 256, 0, st>>>(a);
       } else {
         if (taps == 9) conv_gemm_tapreg<128, 64, 2, 2, 4, 9, 2, 3><<<grid, 256, 0, st>>>(a);
         else conv_gemm_tapreg<128, 64, 2, 2, 4, 5, 2, 3><<<grid, 256, 0, st>>>(a);
@@ -2863,28 +2595,19 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
   // utterances a multiple of 64 rows only (the vocoder's 64-rows-per-frame stage over an odd
   // frame count): 64-row tiles keep the halo kernel (the tap-major one re-stages A per tap)
   if (halo_bm == 128 && seq_len % 128 != 0 && seq_len % 64 == 0) halo_bm = 64;
-  // 8-wave variants (FS2_TUNE_NT_HALO 5 / 6 / 7: 256x128 3-slot / 128x128 3-slot / 256x128
-  // 2-slot), one block per CU with the weight prefetch in flight across the barrier
-  // Default for the wide forward shapes (c_in <= 256, >= 512 128x128 tiles, T % 256 == 0: the
-  // decoder FFN k=9 forward): 256 x 128 two-slot, 8 waves (k=9 decoder forward 114 -> 102 us
-  // alone, scripts/halo_check.py).  FS2_TUNE_NT_HALO 1 disables it.
-  int h8 = g_tune[FS2_TUNE_NT_HALO];
-  // (C_in 512 -- the PostNet convs, forward and data gradient -- run faster on the 4-wave
-  // 128 x 128 tiles: 78 -> 73 us and 84 -> 77 us alone; the 8-wave tile's 384-block grid is
-  // 1.5 rounds of the CUs there)
-  if (h8 == 9) h8 = big >= 512 && c_in <= 512 ? 7 : 0;  // the earlier rule (A/B only)
-  else if (h8 == 0 && big >= 512 && c_in <= 256) h8 = 7;
-  if ((h8 == 5 || h8 == 6 || h8 == 7) && taps > 1 && (taps - 1) * ve.dil <= 16 && tapaligned &&
-      !voc && seq_len % (h8 == 6 ? 128 : 256) == 0) {
-    const int bm = h8 == 6 ? 128 : 256;
-    a.tiles_m = (int)((rows + bm - 1) / bm);
+  // 8-wave 256 x 128 halo tiles, one block per CU with the weight prefetch in flight across the
+  // barrier, for the wide forward shapes (c_in <= 256, >= 512 128x128 tiles, T % 256 == 0) that
+  // the tap-register kernel does not take (k=9 decoder forward 114 -> 102 us alone,
+  // scripts/halo_check.py; FS2_TUNE_NT_HALO 1 disables it).  C_in 512 (the PostNet convs) ran
+  // faster on the 4-wave 128 x 128 tiles (78 -> 73 / 84 -> 77 us: the 8-wave grid of 384 blocks
+  // is 1.5 rounds of the CUs there).  Deeper rings and 128 x 128 8-wave tiles measured slower.
+  if (g_tune[FS2_TUNE_NT_HALO] == 0 && big >= 512 && c_in <= 256 && taps > 1 &&
+      (taps - 1) * ve.dil <= 16 && tapaligned && !voc && seq_len % 256 == 0) {
+    a.tiles_m = (int)((rows + 255) / 256);
     a.tiles_n = (int)((c_out + 127) / 128);
     a.group = halo_group(a.tiles_n);
     const unsigned grid = (unsigned)(a.tiles_m * a.tiles_n);
-    if (h8 == 5) conv_gemm_halo<256, 128, 3, 16, false, 8><<<grid, 512, 0, st>>>(a);
-    else if (h8 == 6) conv_gemm_halo<128, 128, 3, 16, false, 8><<<grid, 512, 0, st>>>(a);
-    else if (pipe) conv_gemm_halo<256, 128, 2, 16, false, 8, true><<<grid, 512, 0, st>>>(a);
-    else conv_gemm_halo<256, 128, 2, 16, false, 8><<<grid, 512, 0, st>>>(a);
+    conv_gemm_halo<256, 128, 2, 16, false, 8, true><<<grid, 512, 0, st>>>(a);
     return launch_status("fs2_conv_gemm(bf16)");
   }
   if (taps > 1 && (taps - 1) * ve.dil <= 64 && tapaligned && seq_len % halo_bm == 0 &&
@@ -2896,29 +2619,11 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
     // HX: halo rows beyond the tile, 16 (taps <= 17 undilated: the FFT/PostNet/VP convs) or
     // 64 (dilated vocoder convs; the larger A image leaves 2 blocks per CU)
     const bool hx64 = (taps - 1) * ve.dil > 16;
-#define FS2_HALO(BM_, BN_, BST_)                                                    \
-  if (hx64) conv_gemm_halo<BM_, BN_, 2, 64, true><<<grid, 256, 0, st>>>(a);        \
-  else if (voc) conv_gemm_halo<BM_, BN_, 2, 16, true><<<grid, 256, 0, st>>>(a);    \
-  else conv_gemm_halo<BM_, BN_, BST_, 16, false><<<grid, 256, 0, st>>>(a);
 #define FS2_HALO2(BM_, BN_)                                                                  \
   if (hx64) conv_gemm_halo<BM_, BN_, 2, 64, true><<<grid, 256, 0, st>>>(a);                  \
   else if (voc) conv_gemm_halo<BM_, BN_, 2, 16, true><<<grid, 256, 0, st>>>(a);              \
-  else if (pipe) conv_gemm_halo<BM_, BN_, 2, 16, false, 4, true><<<grid, 256, 0, st>>>(a);   \
-  else conv_gemm_halo<BM_, BN_, 2, 16, false><<<grid, 256, 0, st>>>(a);
-    if (g_tune[FS2_TUNE_NT_HALO] == 3) {  // single-buffered weight tile (A/B experiments)
-      if (halo_wide && halo_bm == 128) { FS2_HALO(128, 128, 1) }
-      else if (halo_wide) { FS2_HALO(64, 128, 1) }
-      else if (halo_bm == 128) { FS2_HALO(128, 64, 1) }
-      else { FS2_HALO(64, 64, 1) }
-    } else if (g_tune[FS2_TUNE_NT_HALO] == 4) {  // 3-slot weight ring, 2 tiles ahead
-      if (halo_wide && halo_bm == 128) { FS2_HALO(128, 128, 3) }
-      else if (halo_wide) { FS2_HALO(64, 128, 3) }
-      else if (halo_bm == 128) { FS2_HALO(128, 64, 3) }
-      else { FS2_HALO(64, 64, 3) }
-    } else {
-      // (a third ring slot measured faster alone for the k=9 data gradients, 71 -> 65 us, but
-      // 1.7-2x slower inside the step, where the weight-gradient stream shares the CUs and
-      // the lower occupancy (2 blocks/CU) cannot absorb it: knob 4 keeps it for experiments)
+  else conv_gemm_halo<BM_, BN_, 2, 16, false, 4, true><<<grid, 256, 0, st>>>(a);
+    {
       if (halo_wide && halo_bm == 128) {
         const int kz = g_tune[FS2_TUNE_HALO_SPLITK] > 0 ? halo_splitk(a, grid, voc, hx64, st) : 1;
         if (kz > 1) {  // forced split of 128x128 tiles (experiments)
@@ -2936,8 +2641,7 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
         const int kz = g_tune[FS2_TUNE_HALO_SPLITK] > 0 ? halo_splitk(a, grid, voc, hx64, st) : 1;
         if (kz > 1) {
           a.kz = kz;
-          if (pipe) conv_gemm_halo<128, 64, 2, 16, false, 4, true><<<grid * kz, 256, 0, st>>>(a);
-          else conv_gemm_halo<128, 64, 2, 16, false><<<grid * kz, 256, 0, st>>>(a);
+          conv_gemm_halo<128, 64, 2, 16, false, 4, true><<<grid * kz, 256, 0, st>>>(a);
           const int64_t n8 = rows * (c_out / 8);
           halo_splitk_reduce<128><<<(unsigned)((n8 + 255) / 256 < 2048 ? (n8 + 255) / 256 : 2048),
                                     256, 0, st>>>(a);
@@ -2955,15 +2659,13 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
         const int kz = kz2 > 1 ? 1 : halo_splitk(a, grid, voc, hx64, st);
         if (kz2 > 1) {
           a2.kz = kz2;
-          if (pipe) conv_gemm_halo<128, 64, 2, 16, false, 4, true><<<grid2 * kz2, 256, 0, st>>>(a2);
-          else conv_gemm_halo<128, 64, 2, 16, false><<<grid2 * kz2, 256, 0, st>>>(a2);
+          conv_gemm_halo<128, 64, 2, 16, false, 4, true><<<grid2 * kz2, 256, 0, st>>>(a2);
           const int64_t n8 = rows * (c_out / 8);
           halo_splitk_reduce<128><<<(unsigned)((n8 + 255) / 256 < 2048 ? (n8 + 255) / 256 : 2048),
                                     256, 0, st>>>(a2);
         } else if (kz > 1) {
           a.kz = kz;
-          if (pipe) conv_gemm_halo<64, 64, 2, 16, false, 4, true><<<grid * kz, 256, 0, st>>>(a);
-          else conv_gemm_halo<64, 64, 2, 16, false><<<grid * kz, 256, 0, st>>>(a);
+          conv_gemm_halo<64, 64, 2, 16, false, 4, true><<<grid * kz, 256, 0, st>>>(a);
           const int64_t n8 = rows * (c_out / 8);
           halo_splitk_reduce<64><<<(unsigned)((n8 + 255) / 256 < 2048 ? (n8 + 255) / 256 : 2048),
                                    256, 0, st>>>(a);
@@ -2972,14 +2674,7 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
         }
       }
     }
-#undef FS2_HALO
 #undef FS2_HALO2
-  } else if (taps == 1 && !voc && tapaligned && g_tune[FS2_TUNE_PERSIST] > 0 &&
-             big >= 2 * cu_count()) {
-    // persistent projection GEMM (gemm_nt_persist): 128 x 128 tiles, 3-slot ring across tiles
-    a.tiles_m = (int)((rows + 127) / 128);
-    a.tiles_n = (int)((c_out + 127) / 128);
-    launch_persist<128, 128, 3>(a, st);
   } else if ((big >= 512 && g_tune[FS2_TUNE_NT_TILE] == 0) || g_tune[FS2_TUNE_NT_TILE] == 1) {
     a.tiles_m = (int)((rows + 127) / 128);
     a.tiles_n = (int)((c_out + 127) / 128);

@@ -299,8 +299,9 @@ class PositionwiseFeedForward(nn.Module):
 
 
 # Weight-gradient streams created ahead of the communicator, per device index: see
-# reserve_streams.
+# reserve_streams.  _RESERVED_BEFORE_PG[index]: no process group existed at the reservation.
 _RESERVED_SIDE = {}
+_RESERVED_BEFORE_PG = {}
 
 
 def reserve_streams(device):
@@ -320,10 +321,33 @@ def reserve_streams(device):
     dev = torch.device(device)
     idx = torch.cuda.current_device() if dev.index is None else dev.index
     if idx not in _RESERVED_SIDE:
+        import torch.distributed as dist
+        _RESERVED_BEFORE_PG[idx] = not (dist.is_available() and dist.is_initialized())
         torch.zeros(1, device=dev).add_(1)  # first use of the legacy stream: its queue
         _RESERVED_SIDE[idx] = torch.cuda.Stream(device=dev)
         torch.cuda.synchronize(dev)
     return _RESERVED_SIDE[idx]
+
+
+def stream_reservation_problem(device):
+    """None if ``device``'s compute streams were reserved (reserve_streams) before any process
+    group existed, else what went wrong -- the data-parallel step then risks sharing one hardware
+    queue between the two compute streams (+25 % step time, silently; profiles/r3_ab_experiments.txt).
+    The reservation mitigates the collision (fresh queues for the first streams); it cannot
+    prove which queue a stream landed on."""
+    dev = torch.device(device)
+    if dev.type != "cuda":
+        return None
+    idx = torch.cuda.current_device() if dev.index is None else dev.index
+    if idx not in _RESERVED_SIDE:
+        return (f"cuda:{idx}: the weight-gradient stream was not reserved; call "
+                "train.init_data_parallel(device, ...) (or model.reserve_streams(device) before "
+                "dist.init_process_group) so the RCCL communicator's streams do not take the "
+                "compute streams' hardware queues")
+    if not _RESERVED_BEFORE_PG.get(idx, False):
+        return (f"cuda:{idx}: the weight-gradient stream was reserved after the process group "
+                "was created; the communicator's streams may already share its hardware queue")
+    return None
 
 
 def _flat_view(t, n):
@@ -1036,34 +1060,8 @@ class FastSpeech2(nn.Module):
         if not self.overlap_wgrad:
             return None
         if self._side is None:
-            # FS2_SIDE_PRIORITY: stream priority of the weight-gradient stream (torch's scale:
-            # lower = higher priority; the main chain runs on the current stream)
-            prio = int(os.environ.get("FS2_SIDE_PRIORITY", "0"))
             dev = self.encoder.position_enc.device
-            frac = float(os.environ.get("FS2_SIDE_CUMASK", "0") or 0)
-            if 0 < frac <= 1:
-                # A/B: the weight-gradient stream restricted to a fraction of the CUs (a hash
-                # spreads the mask over every XCD whatever the bit -> CU numbering); meant with
-                # FS2_MAIN_PRIORITY, which moves the main chain off the legacy default stream.
-                # 1 = every CU: a CU-masked stream always gets a hardware queue of its own
-                import ctypes
-                n = torch.cuda.get_device_properties(dev).multi_processor_count
-                bits = [(i * 37) % 64 < frac * 64 for i in range(n)]
-                words = (ctypes.c_uint32 * ((n + 31) // 32))()
-                for i, b in enumerate(bits):
-                    if b:
-                        words[i // 32] |= 1 << (i % 32)
-                hip = ctypes.CDLL("libamdhip64.so")
-                s = ctypes.c_void_p()
-                rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(s), ctypes.c_uint32(len(words)),
-                                                      words)
-                if rc != 0:
-                    raise RuntimeError(f"hipExtStreamCreateWithCUMask failed ({rc})")
-                self._side = torch.cuda.ExternalStream(s.value, device=dev)
-            elif prio == 0 and dev.index in _RESERVED_SIDE:
-                self._side = _RESERVED_SIDE[dev.index]
-            else:
-                self._side = torch.cuda.Stream(device=dev, priority=prio)
+            self._side = _RESERVED_SIDE.get(dev.index) or torch.cuda.Stream(device=dev)
         return self._side
 
     def join_side(self):

@@ -13,9 +13,9 @@ Data parallel: one process per GPU, batch sharded by utterance.
   buffer.  The buffer is laid out in reverse backward order, every block's backward reports
   its parameters as final (``StepCtx.notify``), and a bucket's all-reduce is launched as soon
   as all of its parameters are final, so communication overlaps the rest of the backward.
-  Each all-reduce runs on a communication stream that waits on events recorded on the main
-  compute stream and on the weight-gradient side stream at launch time: neither compute
-  stream ever waits for a bucket (only the clip at the end of the step waits for them all).
+  Each all-reduce is issued from the weight-gradient side stream after it waits on an event
+  recorded on the main compute stream at launch time: the main chain never waits for a
+  bucket (only the clip at the end of the step waits for them all).
 * BatchNorm statistics stay per rank (DataParallel's per-replica semantics).
 """
 import os
@@ -91,11 +91,8 @@ def init_data_parallel(device, **kwargs):
     profiles/r3_ab_experiments.txt).  Extra keyword arguments go to ``init_process_group``
     (rank, world_size, ...)."""
     from .model import reserve_streams
-    if os.environ.get("FS2_DP_RESERVE", "1") == "1":  # A/B knob
-        reserve_streams(device)
-    opts = dist.ProcessGroupNCCL.Options(
-        is_high_priority_stream=os.environ.get("FS2_DP_PG_HIPRIO", "0") == "1")  # A/B knob
-    dist.init_process_group("nccl", device_id=device, pg_options=opts, **kwargs)
+    reserve_streams(device)
+    dist.init_process_group("nccl", device_id=device, **kwargs)
 
 
 class GradBuckets:
@@ -122,18 +119,13 @@ class GradBuckets:
                                 arena.offsets[last] + arena.params[last].numel()))
         self.sizes = [len(idxs) for idxs in buckets]
         # producers of the gradients besides the current stream (the weight-gradient side
-        # stream): a callable returning the streams
+        # stream): a callable returning the streams.  A bucket's all-reduce is issued from the
+        # last producer stream (the side stream, which trails the main chain), after it waits
+        # on an event of the current stream.  A separate communication stream would need a
+        # hardware queue of its own, and HIP shares 4 per priority among every stream of the
+        # process (profiles/r3_ab_experiments.txt: separate / high-priority communication
+        # streams measured 1.04-2.8x slower steps)
         self.producers = None
-        # where a bucket's all-reduce is issued from: the last producer stream (the side
-        # stream, which trails the main chain), after it waits on an event of the current
-        # stream.  A separate communication stream would need a hardware queue of its own,
-        # and HIP shares 4 per priority among every stream of the process (high-priority
-        # streams push the process past the queues the scheduler maps at once: 2.8x slower
-        # steps, profiles/r3_ab_experiments.txt).  FS2_DP_COMM_STREAM=1: separate stream (A/B)
-        self.comm = None
-        if arena.grad.is_cuda and os.environ.get("FS2_DP_COMM_STREAM") == "1":
-            self.comm = torch.cuda.Stream(device=arena.grad.device,
-                                          priority=int(os.environ.get("FS2_DP_COMM_PRIORITY", "0")))
         self.log = None  # optional list: bucket launches are appended (tests)
         del index
         self.reset()
@@ -149,14 +141,14 @@ class GradBuckets:
             self.log.append(b)
         cur = torch.cuda.current_stream() if self.arena.grad.is_cuda else None
         prods = [st for st in (self.producers() if self.producers else ()) if st is not None]
-        if cur is None or (self.comm is None and not prods):
+        if cur is None or not prods:
             self.works.append(dist.all_reduce(self.arena.grad[s:e], group=self.group,
                                               async_op=True))
             return
         # the bucket's gradients are complete in stream order on the current stream and on
         # the producer streams: the issuing stream waits on an event of each of the others
         # (the main chain never waits for the collective or for the side stream here)
-        issue = self.comm if self.comm is not None else prods[-1]
+        issue = prods[-1]
         for st in [cur] + prods:
             if st is not issue:
                 ev = torch.cuda.Event()
@@ -197,8 +189,10 @@ class Trainer:
     static outputs (overwritten by the next replay).  A batch of another shape re-captures.
 
     ``data_parallel`` (default: world size > 1) selects the data-parallel step -- global loss
-    denominators, bucketed gradient all-reduce on the communication stream; forcing it on a
-    one-rank group runs that code path on one GPU (tests/test_dp.py).
+    denominators, bucketed gradient all-reduce from the weight-gradient stream; forcing it on a
+    one-rank group runs that code path on one GPU (tests/test_dp.py).  On the GPU it warns
+    (raises with FS2_DP_STRICT=1) when the device's compute streams were not reserved before
+    the process group existed (train.init_data_parallel does both in the right order).
     """
 
     def __init__(self, model, preprocess_config, model_config, train_config, current_step=0,
@@ -228,6 +222,12 @@ class Trainer:
             raise ValueError("data_parallel needs an initialised process group")
         self.buckets = None
         if self.dp:
+            from .model import stream_reservation_problem
+            problem = stream_reservation_problem(model.encoder.position_enc.device)
+            if problem is not None:
+                if os.environ.get("FS2_DP_STRICT") == "1":
+                    raise RuntimeError(problem)
+                warnings.warn(problem, RuntimeWarning, stacklevel=2)
             arena = model.arena()
             with torch.no_grad():  # identical initial weights on every rank
                 dist.broadcast(arena.flat, src=0, group=process_group)

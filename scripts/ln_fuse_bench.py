@@ -49,9 +49,9 @@ for name, T, cin, cnt in (("dec fc+ln1", 512, 256, 6), ("dec w2+ln2", 512, 1024,
 
     row = [timeit(two)]
     for tile in (0, 1):
-        K.lib.fs2_set_tuning(13, tile)
+        K.lib.fs2_set_tuning(11, tile)
         row.append(timeit(lambda: K.conv_gemm_ln(x, wf, M, T, cin, d, 1, 0, g, bt, bias=b, res=res, **kw)))
-        K.lib.fs2_set_tuning(13, 0)
+        K.lib.fs2_set_tuning(11, 0)
     for i, t in enumerate(row):
         tot[i] = tot.get(i, 0.0) + cnt * t
     print(f"{name:12s} gemm+ln_fwd {row[0]:6.1f} us   fused 64x256 {row[1]:6.1f} us   "

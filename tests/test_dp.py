@@ -272,3 +272,69 @@ def test_data_parallel_rccl_one_rank_matches_plain_step():
             assert abs(x - y) <= 1e-5 * max(abs(y), 1e-6), (a_, b_)
     w, wp = dp["w"], plain["w"]
     assert (w - wp).abs().max().item() <= 1e-6 * wp.abs().max().item()
+
+
+def test_stream_reservation_check_host_logic():
+    """stream_reservation_problem (the check Trainer(data_parallel=True) runs): no complaint on
+    CPU devices; a CUDA device whose weight-gradient stream was never reserved, or reserved only
+    after the process group existed, is reported; reserved before it, accepted.  The module's
+    bookkeeping is driven directly (no GPU call)."""
+    M = importlib.import_module("mid-attribute-speaker-generation_amd.model")
+    assert M.stream_reservation_problem("cpu") is None
+    saved = dict(M._RESERVED_SIDE), dict(M._RESERVED_BEFORE_PG)
+    try:
+        M._RESERVED_SIDE.pop(7, None)
+        M._RESERVED_BEFORE_PG.pop(7, None)
+        msg = M.stream_reservation_problem(torch.device("cuda", 7))
+        assert msg is not None and "not reserved" in msg and "init_data_parallel" in msg
+        M._RESERVED_SIDE[7] = object()
+        M._RESERVED_BEFORE_PG[7] = False
+        msg = M.stream_reservation_problem(torch.device("cuda", 7))
+        assert msg is not None and "after the process group" in msg
+        M._RESERVED_BEFORE_PG[7] = True
+        assert M.stream_reservation_problem(torch.device("cuda", 7)) is None
+    finally:
+        M._RESERVED_SIDE.clear()
+        M._RESERVED_SIDE.update(saved[0])
+        M._RESERVED_BEFORE_PG.clear()
+        M._RESERVED_BEFORE_PG.update(saved[1])
+
+
+def _unreserved_worker(rank, port, out):
+    """A one-member RCCL group created with dist.init_process_group directly (the reference's
+    call, train.py:67-68), no stream reservation: Trainer(data_parallel=True) must warn, and
+    raise under FS2_DP_STRICT=1."""
+    import sys
+    import warnings
+    sys.path.insert(0, REPO)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    pkg = importlib.import_module("mid-attribute-speaker-generation_amd")
+    M = importlib.import_module("mid-attribute-speaker-generation_amd.model")
+    tr = importlib.import_module("mid-attribute-speaker-generation_amd.train")
+    pp, mc, tc, path = pkg.config.load_configs("JVS-VCTK")
+    model = M.FastSpeech2(pp, mc, path, device=dev)
+    res = {}
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        tr.Trainer(model, pp, mc, tc, data_parallel=True)
+    res["warned"] = [str(x.message) for x in w if issubclass(x.category, RuntimeWarning)]
+    os.environ["FS2_DP_STRICT"] = "1"
+    try:
+        tr.Trainer(model, pp, mc, tc, data_parallel=True)
+        res["raised"] = None
+    except RuntimeError as e:
+        res["raised"] = str(e)
+    torch.save(res, f"{out}/unres.pt")
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_data_parallel_warns_without_stream_reservation():
+    with tempfile.TemporaryDirectory() as out:
+        mp.spawn(_unreserved_worker, args=(_port(), out), nprocs=1, join=True)
+        r = torch.load(f"{out}/unres.pt")
+    assert any("not reserved" in m for m in r["warned"]), r
+    assert r["raised"] is not None and "not reserved" in r["raised"], r

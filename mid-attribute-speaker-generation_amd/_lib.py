@@ -55,6 +55,7 @@ class KernelError(RuntimeError):
 class _Lib:
     def __init__(self):
         self._dll = None
+        self._missing = frozenset()
         self._sigs = parse_header()
 
     def load(self):
@@ -65,12 +66,19 @@ class _Lib:
                     "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)")
             dll = ctypes.CDLL(LIB_PATH)
             override = bool(os.environ.get("FS2HIP_LIB"))
+            missing = []
             for name, (res, args) in self._sigs.items():
                 if override and not hasattr(dll, name):
-                    continue  # an older library selected for an A/B run: only its own entry points
+                    missing.append(name)  # an older library selected for an A/B run
+                    continue
                 fn = getattr(dll, name)
                 fn.restype = res
                 fn.argtypes = args
+            if missing:
+                import warnings
+                warnings.warn(f"FS2HIP_LIB={LIB_PATH} lacks {len(missing)} entry points of "
+                              f"{HEADER}: {', '.join(sorted(missing))}", RuntimeWarning, stacklevel=2)
+            self._missing = frozenset(missing)
             self._dll = dll
         return self._dll
 
@@ -81,6 +89,9 @@ class _Lib:
         if not name.startswith("fs2_"):
             raise AttributeError(name)
         dll = self.load()
+        if name in self._missing:
+            raise KernelError(f"{name} is not in FS2HIP_LIB={LIB_PATH} (a library built before it "
+                              "was added to include/fs2hip.h)")
         fn = getattr(dll, name)
         if fn.restype is ctypes.c_int and name not in ("fs2_abi_version", "fs2_weight_prep_tile_channels",
                                                         "fs2_resblock1_supported"):

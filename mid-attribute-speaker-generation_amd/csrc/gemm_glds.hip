@@ -859,7 +859,7 @@ void conv_gemm_halo(GldsArgs a) {
   };
   if (!skip) {
     const int ncb = cb1 - cb0;
-    if constexpr (PIPE) {    } else if constexpr (PIPE) {
+    if constexpr (PIPE) {
       // Fragment-pipelined 2-slot loop.  Step s = (cb, j) reads weight slot s & 1 and halo slot
       // cb & 1 as two k-halves held in two register sets: set 1 (s, ks 1) is read while set 0's
       // MFMAs issue; then ONE barrier, after which set 0 is refilled with step s + 1's first

@@ -316,7 +316,11 @@ def reserve_streams(device):
     parallel step on a one-rank group lost 1.9 ms/step (9.3 vs 7.4 ms) in 3 of 4 runs that
     way (profiles/r3_ab_experiments.txt).  This launches on the legacy stream (its queue is
     created on first use) and creates the weight-gradient stream next, so both get fresh
-    queues; FastSpeech2.side_stream() then hands out the reserved stream.
+    queues; FastSpeech2.side_stream() then hands out the reserved stream.  It mitigates the
+    collision rather than removing it: HIP exposes no way to pin a stream to a queue, and a
+    one-rank DP run still measured 8.16 ms once against 7.53 plain (r3_ab_experiments.txt).
+    Trainer(data_parallel=True) warns when the reservation did not precede the process group
+    (stream_reservation_problem).
     """
     dev = torch.device(device)
     idx = torch.cuda.current_device() if dev.index is None else dev.index

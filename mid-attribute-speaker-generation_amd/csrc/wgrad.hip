@@ -80,26 +80,27 @@ template <int N>
 FS2_DEV void wb_vm(int ahead) {  // at most `ahead` bands of N LDS-DMA instructions in flight
   if (ahead <= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-  else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * N) : "memory");
+  else if (ahead == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * N) : "memory");
+  else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * N) : "memory");
 }
 
 }  // namespace
 
-template <int TAPS, int S, int ST>
-__global__ __launch_bounds__(256, 2) void conv_wgrad_band(WgradBand a) {
-  constexpr int BO = 32, BC = 32, W = 4, BR = 32 * S;
+template <int TAPS, int S, int ST, int W>
+__global__ __launch_bounds__(64 * W, W == 8 ? 1 : 2) void conv_wgrad_band(WgradBand a) {
+  constexpr int BO = 32, BC = 32, BR = 32 * S, NT = 64 * W;
   constexpr int HR = BR + TAPS - 1, RS = (HR + S - 1) / S, NF = S + TAPS - 1;
   constexpr int DPOS = BR, XPOS = (S * RS + 15) / 16 * 16;  // image positions (64 B each)
   constexpr int NQD = DPOS / 16, NQX = XPOS / 16, NQ = NQD + NQX;  // LDS-DMA per band
   constexpr int STAGE_E = (DPOS + XPOS) * 32;                     // bf16 per ring slot
   constexpr int RING_B = W * ST * STAGE_E * 2;
   constexpr int QLD = BC * TAPS + 4;  // fp32 row stride of a dW-layout partial tile
-  constexpr int RED_B = 2 * BO * QLD * 4 + 2 * 2 * 64 * 16;  // two partial tiles + bias
+  constexpr int RED_B = (W / 2) * (BO * QLD * 4 + 2 * 64 * 16);  // W / 2 partial tiles + bias
   static_assert(TAPS * 16 * 64 <= BO * QLD, "native partial fits a region");
   constexpr int SMEM_B = RING_B > RED_B ? RING_B : RED_B;
   constexpr int MAXB = 1024;
   constexpr int LOOK = 2;  // halo fragments read ahead of their MFMAs
-  static_assert(NQ <= 31, "vmcnt bookkeeping");
+  static_assert(NQ * (ST - 2 > 0 ? ST - 2 : 1) <= 63 && ST <= 5, "vmcnt bookkeeping");
   __shared__ __attribute__((aligned(1024))) unsigned char smem[SMEM_B + 2 * MAXB + 64];
   short* blist = reinterpret_cast<short*>(smem + SMEM_B);
   int* wcnt = reinterpret_cast<int*>(smem + SMEM_B + 2 * MAXB);
@@ -122,7 +123,7 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_band(WgradBand a) {
   int nb = nb_all;
   if (use_list) {
     int total = 0;
-    for (int k0 = 0; k0 < nb_all; k0 += 256) {
+    for (int k0 = 0; k0 < nb_all; k0 += NT) {
       const int k = k0 + tid;
       bool v = false;
       if (k < nb_all) {
@@ -255,43 +256,47 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_band(WgradBand a) {
     compute(i % ST);
   }
 
-  // fixed-order cross-wave sum: wave w (< 2) adds wave w + 2's partial, both write their sums
-  // in the dw layout ([o][c][j], row stride QLD), every thread adds the two and dw / db
+  // fixed-order cross-wave sum, a tree through LDS: waves [h, 2h) write their partials, waves
+  // [0, h) add them (h = W/2, ..., 2), so wave 0 holds (p0 + p4) + (p2 + p6) and wave 1 the
+  // odd pairs (W = 8); both write their sums in the dw layout ([o][c][j], row stride QLD) and
+  // every thread adds the two into dw / db
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   float* Q = reinterpret_cast<float*>(smem);
-  f32x4* QB = reinterpret_cast<f32x4*>(Q + 2 * BO * QLD);  // [2][2 io][64 lanes]
-  const int reg = wave & 1;  // partial region of this wave pair
-  if (wave >= 2) {
-    f32x4* dst = reinterpret_cast<f32x4*>(Q + reg * BO * QLD);
+  f32x4* QB = reinterpret_cast<f32x4*>(Q + (W / 2) * BO * QLD);  // [W / 2][2 io][64 lanes]
 #pragma unroll
-    for (int j = 0; j < TAPS; ++j)
+  for (int h = W / 2; h >= 2; h /= 2) {
+    if (wave >= h && wave < 2 * h) {
+      f32x4* dst = reinterpret_cast<f32x4*>(Q + (wave - h) * BO * QLD);
 #pragma unroll
-      for (int io = 0; io < 2; ++io)
+      for (int j = 0; j < TAPS; ++j)
 #pragma unroll
-        for (int ic = 0; ic < 2; ++ic) dst[((j * 2 + io) * 2 + ic) * 64 + lane] = acc[j][io][ic];
-    if (do_bias) {
-      QB[(reg * 2 + 0) * 64 + lane] = accb[0];
-      QB[(reg * 2 + 1) * 64 + lane] = accb[1];
+        for (int io = 0; io < 2; ++io)
+#pragma unroll
+          for (int ic = 0; ic < 2; ++ic) dst[((j * 2 + io) * 2 + ic) * 64 + lane] = acc[j][io][ic];
+      if (do_bias) {
+        QB[((wave - h) * 2 + 0) * 64 + lane] = accb[0];
+        QB[((wave - h) * 2 + 1) * 64 + lane] = accb[1];
+      }
     }
-  }
-  __syncthreads();
-  if (wave < 2) {
-    const f32x4* src = reinterpret_cast<const f32x4*>(Q + reg * BO * QLD);
+    __syncthreads();
+    if (wave < h) {
+      const f32x4* src = reinterpret_cast<const f32x4*>(Q + wave * BO * QLD);
 #pragma unroll
-    for (int j = 0; j < TAPS; ++j)
+      for (int j = 0; j < TAPS; ++j)
 #pragma unroll
-      for (int io = 0; io < 2; ++io)
+        for (int io = 0; io < 2; ++io)
 #pragma unroll
-        for (int ic = 0; ic < 2; ++ic) acc[j][io][ic] += src[((j * 2 + io) * 2 + ic) * 64 + lane];
-    if (do_bias) {
-      accb[0] += QB[(reg * 2 + 0) * 64 + lane];
-      accb[1] += QB[(reg * 2 + 1) * 64 + lane];
+          for (int ic = 0; ic < 2; ++ic) acc[j][io][ic] += src[((j * 2 + io) * 2 + ic) * 64 + lane];
+      if (do_bias) {
+        accb[0] += QB[(wave * 2 + 0) * 64 + lane];
+        accb[1] += QB[(wave * 2 + 1) * 64 + lane];
+      }
     }
+    __syncthreads();
   }
-  __syncthreads();
   if (wave < 2) {
-    float* dst = Q + reg * BO * QLD;
+    float* dst = Q + wave * BO * QLD;
 #pragma unroll
     for (int j = 0; j < TAPS; ++j)
 #pragma unroll
@@ -305,7 +310,7 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_band(WgradBand a) {
 #pragma unroll
       for (int io = 0; io < 2; ++io)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) QB[(reg * 2 + io) * 64 + 4 * g + r][0] = accb[io][r];
+        for (int r = 0; r < 4; ++r) QB[(wave * 2 + io) * 64 + 4 * g + r][0] = accb[io][r];
     }
   }
   __syncthreads();
@@ -313,7 +318,7 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_band(WgradBand a) {
     constexpr int V = BC * TAPS / 4;  // f32x4 per output row of the tile
     const int64_t Kp = (int64_t)a.Cin * TAPS;
     const int ncol = (a.Cin - c0 < BC ? a.Cin - c0 : BC) * TAPS;  // valid floats per row
-    for (int e = tid; e < BO * V; e += 256) {
+    for (int e = tid; e < BO * V; e += NT) {
       const int o = e / V, v4 = e - o * V;
       if (o0 + o >= a.Cout || 4 * v4 >= ncol) continue;
       const f32x4 s = ld4(Q + o * QLD + 4 * v4) + ld4(Q + BO * QLD + o * QLD + 4 * v4);
@@ -346,9 +351,17 @@ int conv_wgrad_band_launch(const void* dy, int64_t ldy, const void* x, int64_t l
   WgradBand a{(const u16*)dy, ldy, (const u16*)x, ldx, dw, db, rows, seq_len, (int)c_in,
               (int)c_out, pad, to, tc, lens};
   const unsigned grid = (unsigned)(to * tc);
-  if (taps == 9) conv_wgrad_band<9, 2, 2><<<grid, 256, 0, st>>>(a);
-  else if (taps == 5) conv_wgrad_band<5, 2, 2><<<grid, 256, 0, st>>>(a);
-  else conv_wgrad_band<3, 2, 2><<<grid, 256, 0, st>>>(a);
+  // variant (A/B, FS2_TUNE_WGRAD_BAND): 0 = 8 waves x 2-slot rings, 1 = 4 waves x 4-slot rings,
+  // 2 = 4 waves x 2-slot rings
+  const int v = g_tune[FS2_TUNE_WGRAD_BAND];
+#define FS2_WB(T_)                                                         \
+  if (v == 1) conv_wgrad_band<T_, 2, 4, 4><<<grid, 256, 0, st>>>(a);       \
+  else if (v == 2) conv_wgrad_band<T_, 2, 2, 4><<<grid, 256, 0, st>>>(a);  \
+  else conv_wgrad_band<T_, 2, 2, 8><<<grid, 512, 0, st>>>(a);
+  if (taps == 9) { FS2_WB(9) }
+  else if (taps == 5) { FS2_WB(5) }
+  else { FS2_WB(3) }
+#undef FS2_WB
   return launch_status("fs2_conv_wgrad(bf16, band)");
 }
 

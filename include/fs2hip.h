@@ -275,15 +275,17 @@ int fs2_weight_prep_batch(int dtype, const int64_t* jobs, int n_jobs, int64_t n_
  *                          (default: 4-wave 128 x 64 tiles at 3 blocks per CU, 128 x 128 at 2 for
  *                          c_out <= 256), -1 = off (the halo kernels above), 1 = force the
  *                          128 x 64 tiles, 3 = force 128 x 128
- *   FS2_TUNE_WGRAD_BAND    band weight gradient: 0 = 8 waves per block with 2-slot rings
- *                          (default), 1 = 4 waves with 4-slot rings, 2 = 4 waves, 2-slot
+ *   FS2_TUNE_WGRAD_BAND    band weight gradient: 0 = 4 waves per block with 2-slot rings
+ *                          (default), 1 = 4 waves with 4-slot rings, 2 = 8 waves, 2-slot
+ *   FS2_TUNE_ATTN_XCD      LDS-DMA attention kernels: 0 = the blocks of one (utterance, head) on
+ *                          one XCD (K / V reuse in its L2; default), -1 = the launch grid's order
  * Process-wide; query workspace sizes after setting.                                 */
 enum { FS2_TUNE_GEMM_STAGES = 0, FS2_TUNE_WGRAD_STAGES = 1, FS2_TUNE_WGRAD_TILE = 2,
        FS2_TUNE_WGRAD_SPLITS = 3, FS2_TUNE_LEGACY_GEMM = 4, FS2_TUNE_NT_GROUP = 5,
        FS2_TUNE_NT_HALO = 6, FS2_TUNE_WGRAD_HALO = 7, FS2_TUNE_HALO_SPLITK = 8,
        FS2_TUNE_ATTN = 9, FS2_TUNE_NT_TILE = 10, FS2_TUNE_LN_TILE = 11, FS2_TUNE_WGRAD_K1 = 12,
        FS2_TUNE_NT_K1 = 13, FS2_TUNE_ATTN_DMA = 14, FS2_TUNE_TAPREG = 15,
-       FS2_TUNE_WGRAD_BAND = 16, FS2_TUNE_COUNT = 17 };
+       FS2_TUNE_WGRAD_BAND = 16, FS2_TUNE_ATTN_XCD = 17, FS2_TUNE_COUNT = 18 };
 int fs2_set_tuning(int knob, int value);
 
 /* Weight (and optionally bias) gradient, accumulated into the fp32 master-gradient layout:

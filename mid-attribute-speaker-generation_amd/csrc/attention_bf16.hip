@@ -860,20 +860,39 @@ FS2_DEV void tile_loop(int nt, Issue&& issue, Full&& full, Last&& last) {
 }
 }  // namespace
 
+// (query / key block, bh) of this workgroup.  xg != 0: the blocks of one (utterance, head) are
+// dealt to one XCD -- blocks b and b + 8 share an XCD under round-robin dispatch (speed only,
+// never correctness) -- so its K / V (Q / dO) tiles are fetched into one L2, while the (b, h)
+// pairs still go round-robin over the XCDs (a length mix on each).  Needs gridDim.y % 8 == 0.
+namespace {
+FS2_DEV void attn_block(int xg, int& blk, int& bh) {
+  blk = blockIdx.x;
+  bh = blockIdx.y;
+  if (xg) {
+    const int nx = gridDim.x, lin = blockIdx.y * nx + blockIdx.x;
+    const int slot = lin >> 3, grp = slot / nx;
+    bh = (lin & 7) + 8 * grp;
+    blk = slot - grp * nx;
+  }
+}
+}  // namespace
+
 // forward: 4 waves x 32 queries (two 16-row groups per wave), K / V tiles by LDS-DMA
 template <int STAGES>
 __global__ __launch_bounds__(256, STAGES == 2 ? 2 : 1) void attn_fwd_dma(
     const u16* __restrict__ qkv, u16* __restrict__ o, float* __restrict__ lse,
-    const int64_t* __restrict__ lens, int T, int H, float scale) {
+    const int64_t* __restrict__ lens, int T, int H, float scale, int xg) {
   constexpr int NW = 4, NT = 256, QBLK = 128;
   __shared__ __attribute__((aligned(1024))) u16 smem[STAGES * 2 * IMG];
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, r16 = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int q4 = r16 >> 2, p4 = r16 & 3;
-  const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
+  int blk, bh;
+  attn_block(xg, blk, bh);
+  const int b = bh / H, h = bh - b * H;
   const int L = (int)min(lens[b], (int64_t)T);
   const int64_t ld = 3LL * H * DH, ldo = (int64_t)H * DH;
-  const int q0 = blockIdx.x * QBLK;
+  const int q0 = blk * QBLK;
   const u16* base = qkv + (int64_t)b * T * ld;
   u16* obase = o + (int64_t)b * T * ldo + h * DH;
 
@@ -989,16 +1008,18 @@ __global__ __launch_bounds__(256, STAGES == 2 ? 2 : 1) void attn_fwd_dma(
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_dma(
     const u16* __restrict__ qkv, const u16* __restrict__ o, const u16* __restrict__ d_o,
     const float* __restrict__ lse, float* __restrict__ delta, u16* __restrict__ d_qkv,
-    const int64_t* __restrict__ lens, int T, int H, float scale) {
+    const int64_t* __restrict__ lens, int T, int H, float scale, int xg) {
   constexpr int NW = 4, NT = 256, QBLK = 128, STAGES = 2;
   __shared__ __attribute__((aligned(1024))) u16 smem[STAGES * 2 * IMG];
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, r16 = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int q4 = r16 >> 2, p4 = r16 & 3;
-  const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
+  int blk, bh;
+  attn_block(xg, blk, bh);
+  const int b = bh / H, h = bh - b * H;
   const int L = (int)min(lens[b], (int64_t)T);
   const int64_t ld = 3LL * H * DH, ldo = (int64_t)H * DH;
-  const int q0 = blockIdx.x * QBLK;
+  const int q0 = blk * QBLK;
   const u16* base = qkv + (int64_t)b * T * ld;
   u16* dbase = d_qkv + (int64_t)b * T * ld + h * DH;
 
@@ -1107,17 +1128,19 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_dma(
 __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_dma(
     const u16* __restrict__ qkv, const u16* __restrict__ d_o, const float* __restrict__ lse,
     const float* __restrict__ delta, u16* __restrict__ d_qkv, const int64_t* __restrict__ lens,
-    int T, int H, float scale) {
+    int T, int H, float scale, int xg) {
   constexpr int NW = 4, STAGES = 2;
   constexpr int SLOT_E = 2 * IMG + 2 * QB * 2;  // Q image, dO image, lse[64], delta[64] (fp32)
   __shared__ __attribute__((aligned(1024))) u16 smem[STAGES * SLOT_E];
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, r16 = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int q4 = r16 >> 2, p4 = r16 & 3;
-  const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
+  int blk, bh;
+  attn_block(xg, blk, bh);
+  const int b = bh / H, h = bh - b * H;
   const int L = (int)min(lens[b], (int64_t)T);
   const int64_t ld = 3LL * H * DH, ldo = (int64_t)H * DH;
-  const int k0 = blockIdx.x * QB;
+  const int k0 = blk * QB;
   const u16* base = qkv + (int64_t)b * T * ld;
   u16* dk_base = d_qkv + (int64_t)b * T * ld + (int64_t)H * DH + h * DH;
   u16* dv_base = d_qkv + (int64_t)b * T * ld + 2LL * H * DH + h * DH;
@@ -1217,10 +1240,11 @@ int attn_fwd_bf16_launch(const void* qkv, void* o, float* lse, const int64_t* le
   const int dma = g_tune[FS2_TUNE_ATTN_DMA];
   if (seq_len >= 256 && g_tune[FS2_TUNE_ATTN] >= 0 && dma >= 0) {
     dim3 grid((unsigned)((seq_len + 127) / 128), (unsigned)(batch * heads));
+    const int xg = g_tune[FS2_TUNE_ATTN_XCD] >= 0 && (batch * heads) % 8 == 0;
     if (dma == 1)
-      attn_fwd_dma<3><<<grid, 256, 0, st>>>((const u16*)qkv, (u16*)o, lse, lens, (int)seq_len, heads, scale);
+      attn_fwd_dma<3><<<grid, 256, 0, st>>>((const u16*)qkv, (u16*)o, lse, lens, (int)seq_len, heads, scale, xg);
     else
-      attn_fwd_dma<2><<<grid, 256, 0, st>>>((const u16*)qkv, (u16*)o, lse, lens, (int)seq_len, heads, scale);
+      attn_fwd_dma<2><<<grid, 256, 0, st>>>((const u16*)qkv, (u16*)o, lse, lens, (int)seq_len, heads, scale, xg);
   } else if (seq_len >= 256 && g_tune[FS2_TUNE_ATTN] >= 0) {
     dim3 grid((unsigned)((seq_len + 127) / 128), (unsigned)(batch * heads));
     attn_fwd_bf16<4><<<grid, 256, 0, st>>>((const u16*)qkv, (u16*)o, lse, lens, (int)seq_len, heads, scale);
@@ -1238,9 +1262,10 @@ int attn_bwd_bf16_launch(const void* qkv, const void* o, const void* d_o, const 
   dim3 grid1((unsigned)((seq_len + QB - 1) / QB), (unsigned)(batch * heads));
   dim3 grid2((unsigned)((seq_len + 127) / 128), (unsigned)(batch * heads));
   const bool dma = seq_len >= 256 && g_tune[FS2_TUNE_ATTN_DMA] >= 0 && (tune == 0 || tune == 1);
+  const int xg = g_tune[FS2_TUNE_ATTN_XCD] >= 0 && (batch * heads) % 8 == 0;
   if (dma) {  // dQ with delta fused, LDS-DMA staged
     attn_bwd_dq_dma<<<grid2, 256, 0, st>>>((const u16*)qkv, (const u16*)o, (const u16*)d_o, lse, ws,
-                                           (u16*)d_qkv, lens, (int)seq_len, heads, scale);
+                                           (u16*)d_qkv, lens, (int)seq_len, heads, scale, xg);
   } else if (seq_len >= 256 && tune >= 0) {  // dQ with delta fused
     attn_bwd_dq_bf16<4><<<grid2, 256, 0, st>>>((const u16*)qkv, (const u16*)o, (const u16*)d_o, lse, ws,
                                                (u16*)d_qkv, lens, (int)seq_len, heads, scale);
@@ -1256,7 +1281,7 @@ int attn_bwd_bf16_launch(const void* qkv, const void* o, const void* d_o, const 
   // workgroup per CU (384 workgroups = 1.5 rounds of the CUs)
   if (dma && tune == 0)
     attn_bwd_dkdv_dma<<<grid1, 256, 0, st>>>((const u16*)qkv, (const u16*)d_o, lse, ws, (u16*)d_qkv,
-                                             lens, (int)seq_len, heads, scale);
+                                             lens, (int)seq_len, heads, scale, xg);
   else if (seq_len >= 256 && tune == 2)
     attn_bwd_dkdv_bf16<4><<<grid2, 256, 0, st>>>((const u16*)qkv, (const u16*)d_o, lse, ws, (u16*)d_qkv,
                                                  lens, (int)seq_len, heads, scale);

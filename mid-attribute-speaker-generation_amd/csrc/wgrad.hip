@@ -351,13 +351,15 @@ int conv_wgrad_band_launch(const void* dy, int64_t ldy, const void* x, int64_t l
   WgradBand a{(const u16*)dy, ldy, (const u16*)x, ldx, dw, db, rows, seq_len, (int)c_in,
               (int)c_out, pad, to, tc, lens};
   const unsigned grid = (unsigned)(to * tc);
-  // variant (A/B, FS2_TUNE_WGRAD_BAND): 0 = 8 waves x 2-slot rings, 1 = 4 waves x 4-slot rings,
-  // 2 = 4 waves x 2-slot rings
+  // variant (FS2_TUNE_WGRAD_BAND): 0 = 4 waves x 2-slot rings (default), 1 = 4 waves x 4-slot
+  // rings, 2 = 8 waves x 2-slot rings.  Alone the 8-wave blocks are the fastest (decoder k=9
+  // 98 vs 133 us), but their 160 KB of LDS per CU starve the main-stream kernels they run
+  // beside: step 7.61 vs 7.07 ms (profiles/r4_ab_experiments.txt)
   const int v = g_tune[FS2_TUNE_WGRAD_BAND];
 #define FS2_WB(T_)                                                         \
   if (v == 1) conv_wgrad_band<T_, 2, 4, 4><<<grid, 256, 0, st>>>(a);       \
-  else if (v == 2) conv_wgrad_band<T_, 2, 2, 4><<<grid, 256, 0, st>>>(a);  \
-  else conv_wgrad_band<T_, 2, 2, 8><<<grid, 512, 0, st>>>(a);
+  else if (v == 2) conv_wgrad_band<T_, 2, 2, 8><<<grid, 512, 0, st>>>(a);  \
+  else conv_wgrad_band<T_, 2, 2, 4><<<grid, 256, 0, st>>>(a);
   if (taps == 9) { FS2_WB(9) }
   else if (taps == 5) { FS2_WB(5) }
   else { FS2_WB(3) }

@@ -261,10 +261,8 @@ int fs2_weight_prep_batch(int dtype, const int64_t* jobs, int n_jobs, int64_t n_
  *   FS2_TUNE_NT_TILE       tap-major fwd/dX kernel (k = 1 projections, odd shapes): 0 = tile
  *                          by grid size, 1 / 2 / 3 = force 128x128 / 128x64 / 64x64
  *   FS2_TUNE_LN_TILE       fs2_conv_gemm_ln(_bwd) row tile: 0 = 64 x 256 (default), 1 = 128 x 256
- *   FS2_TUNE_WGRAD_K1      k = 1 weight gradient: 0 = 64 x 64 tiles with the 128-row k-tiles
- *                          split over 4 waves (default), 1 = 128 x 128 tiles of 8 waves
- *                          (both: buffer-descriptor staging), -1 = the tap-major kernel;
- *                          -2 = also the round-2 split reduce for taps > 1 (A/B)
+ *   FS2_TUNE_WGRAD_K1      k = 1 weight gradient: 0 = the grouped split-K kernel of
+ *                          fs2_conv_wgrad_k1_multi with one job (default), -1 = the tap-major kernel
  *   FS2_TUNE_NT_K1         k = 1 projections on the tap-major kernel: 0 = buffer-descriptor
  *                          staging build (default), -1 = the general tap-walking build (A/B)
  *   FS2_TUNE_ATTN_DMA      bf16 attention at T >= 256: 0 = K / V (Q / dO) tiles by LDS-DMA into
@@ -276,16 +274,19 @@ int fs2_weight_prep_batch(int dtype, const int64_t* jobs, int n_jobs, int64_t n_
  *                          c_out <= 256), -1 = off (the halo kernels above), 1 = force the
  *                          128 x 64 tiles, 3 = force 128 x 128
  *   FS2_TUNE_WGRAD_BAND    band weight gradient: 0 = 4 waves per block with 2-slot rings
- *                          (default), 1 = 4 waves with 4-slot rings, 2 = 8 waves, 2-slot
+ *                          (default), 1 = 4 waves with 4-slot rings, 2 = 8 waves, 2-slot,
+ *                          3 = default blocks but only on grids of >= 128 tiles (round-4 rule)
  *   FS2_TUNE_ATTN_XCD      LDS-DMA attention kernels: 0 = the blocks of one (utterance, head) on
  *                          one XCD (K / V reuse in its L2; default), -1 = the launch grid's order
+ *   FS2_TUNE_WGRAD_K1M_STAGES  grouped k = 1 weight gradient LDS ring: 0 = 4 slots, 2 / 3 slots
  * Process-wide; query workspace sizes after setting.                                 */
 enum { FS2_TUNE_GEMM_STAGES = 0, FS2_TUNE_WGRAD_STAGES = 1, FS2_TUNE_WGRAD_TILE = 2,
        FS2_TUNE_WGRAD_SPLITS = 3, FS2_TUNE_LEGACY_GEMM = 4, FS2_TUNE_NT_GROUP = 5,
        FS2_TUNE_NT_HALO = 6, FS2_TUNE_WGRAD_HALO = 7, FS2_TUNE_HALO_SPLITK = 8,
        FS2_TUNE_ATTN = 9, FS2_TUNE_NT_TILE = 10, FS2_TUNE_LN_TILE = 11, FS2_TUNE_WGRAD_K1 = 12,
        FS2_TUNE_NT_K1 = 13, FS2_TUNE_ATTN_DMA = 14, FS2_TUNE_TAPREG = 15,
-       FS2_TUNE_WGRAD_BAND = 16, FS2_TUNE_ATTN_XCD = 17, FS2_TUNE_COUNT = 18 };
+       FS2_TUNE_WGRAD_BAND = 16, FS2_TUNE_ATTN_XCD = 17, FS2_TUNE_WGRAD_K1M_STAGES = 18,
+       FS2_TUNE_COUNT = 19 };
 int fs2_set_tuning(int knob, int value);
 
 /* Weight (and optionally bias) gradient, accumulated into the fp32 master-gradient layout:

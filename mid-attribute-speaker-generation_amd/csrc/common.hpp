@@ -12,14 +12,13 @@
 
 #define FS2_DEV __device__ __forceinline__
 
+
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 namespace fs2 {
 
 extern int g_tune[FS2_TUNE_COUNT];  // fs2_set_tuning knobs (abi.hip)
-// k = 1 weight gradients on wgrad_k1_glds (and its split rule) unless FS2_TUNE_WGRAD_K1 = -1
-inline bool k1_split_rule() { return g_tune[FS2_TUNE_WGRAD_K1] >= 0; }
 
 // ------------------------------------------------------------------ error reporting
 void set_error(const char* fmt, ...);

@@ -398,22 +398,6 @@ static int wgrad_splits(int64_t rows, int64_t c_in, int64_t c_out, int taps) {
     const int s = g_tune[FS2_TUNE_WGRAD_SPLITS];
     return s < 1 ? 1 : s > 64 ? 64 : s;
   }
-  if (taps == 1 && g_tune[FS2_TUNE_WGRAD_K1] == 0) {
-    // wgrad_k1_q: 64 x 64 tiles at two blocks per CU -- about 512 blocks, each split at least
-    // 8 k-tiles of 128 rows
-    const int64_t t1 = ((c_out + 63) / 64) * ((c_in + 63) / 64);
-    int64_t s = (512 + t1 / 2) / t1;
-    if (s > rows / 1024) s = rows / 1024;
-    return (int)(s < 1 ? 1 : s);
-  }
-  if (taps == 1 && k1_split_rule()) {
-    // wgrad_k1_glds (FS2_TUNE_WGRAD_K1 = 1): 128 x 128 tiles at one block per CU -- about 256 blocks, each split at
-    // least 8 k-tiles of 64 rows
-    const int64_t t1 = ((c_out + 127) / 128) * ((c_in + 127) / 128);
-    int64_t s = (256 + t1 / 2) / t1;
-    if (s > rows / 512) s = rows / 512;
-    return (int)(s < 1 ? 1 : s);
-  }
   const int64_t Kp = (int64_t)taps * c_in;
   const int bt = wgrad_tile(rows, c_in, c_out, taps);
   const int64_t tiles = ((c_out + bt - 1) / bt) * ((Kp + bt - 1) / bt);
@@ -552,7 +536,13 @@ int64_t fs2_conv_wgrad_ws_bytes(int64_t rows, int64_t c_in, int64_t c_out, int t
   const int64_t S = wgrad_splits(rows, c_in, c_out, taps);
   const int64_t bias_part = S * c_out > ((rows + CS_ROWS - 1) / CS_ROWS) * c_out
                                 ? S * c_out : ((rows + CS_ROWS - 1) / CS_ROWS) * c_out;
-  return (S * c_out * taps * c_in + bias_part) * 4;
+  int64_t b = (S * c_out * taps * c_in + bias_part) * 4;
+  if (taps == 1) {  // bf16 k = 1: the grouped kernel with one job (wgrad.hip)
+    const int64_t job[8] = {0, c_out, 0, c_in, 0, 1, c_in, c_out};
+    const int64_t m = wgrad_k1_multi_ws_floats(job, 1, rows) * 4;
+    b = m > b ? m : b;
+  }
+  return b;
 }
 
 int fs2_conv_wgrad(int dtype, const void* dy, int64_t ldy, const void* x, int64_t ldx, float* dw,
@@ -564,6 +554,15 @@ int fs2_conv_wgrad(int dtype, const void* dy, int64_t ldy, const void* x, int64_
                   "fs2_conv_wgrad: workspace too small");
     if (rows == 0) return FS2_OK;
     const int S = wgrad_splits(rows, c_in, c_out, taps);
+    if (taps == 1 && !g_tune[FS2_TUNE_LEGACY_GEMM] && g_tune[FS2_TUNE_WGRAD_K1] == 0) {
+      // k = 1: the grouped split-K kernel with one job (128 x 128 tiles, one reduce)
+      const int64_t job[8] = {(int64_t)dy, ldy, (int64_t)x, ldx, (int64_t)dw, (int64_t)db, c_in, c_out};
+      FS2_CHECK_ARG(c_in % 8 == 0 && c_out % 8 == 0 && ldx % 8 == 0 && ldy % 8 == 0 &&
+                        ((uintptr_t)dy & 15) == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)dw & 15) == 0,
+                    "fs2_conv_wgrad(bf16, k = 1): channel counts / strides must be multiples of 8, "
+                    "operands and dw 16-B aligned");
+      return wgrad_k1_multi_launch(job, 1, rows, seq_len, lens, ws, as_stream(stream));
+    }
     if (!g_tune[FS2_TUNE_LEGACY_GEMM])
       return conv_wgrad_glds_launch(dy, ldy, x, ldx, dw, db, rows, seq_len, c_in, c_out, taps, pad,
                                     lens, S, wgrad_tile(rows, c_in, c_out, taps), ws,

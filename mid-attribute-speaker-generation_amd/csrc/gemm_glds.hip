@@ -1536,419 +1536,6 @@ __global__ __launch_bounds__(256) void conv_wgrad_tn_glds(WgradGlds a) {
   }
 }
 
-// k = 1 weight gradient (Linear / 1x1 Conv1d), FS2_TUNE_WGRAD_K1 = 1 (measured 13 % slower per
-// step than wgrad_k1_q below, profiles/r3_ab_experiments.txt): a 128 (o) x 128 (c) output tile
-// per block of 8 waves.  Wave w owns the 64 x 64 quadrant w & 3 over rows 32 (w >> 2) .. +31 of each 64-row
-// k-tile, and the two row halves of a quadrant are summed through LDS at the end.  The k-tiles
-// (dy [64 rows][128 o] and x [64 rows][128 c], 256-B rows, LDS-DMA) run through a 4-slot ring
-// with three tiles in flight (counted vmcnt, raw barrier: 96 KB in flight per CU).  Against
-// conv_wgrad_tn_glds (64 x 64 tiles of 2 x 2 waves of 32 x 32, one tile in flight): a quarter of
-// the L2 -> LDS operand traffic per FLOP (each staged row feeds 128 x 128 outputs), every
-// transposed fragment read feeds 4 MFMAs instead of 2, and the load latency is covered -- that
-// kernel measured MFMA-busy 0.09 at the decoder QKV shape, 39 % of its wave cycles waiting on the
-// next tile's DMA (profiles/r3_wgrad_pmc.txt).  Same split-K slab layout (slab[z][o][c], bias
-// slab[z][o]) and wgrad_reduce_k1.  The bias gradient rides on the dy fragments of the blocks
-// of the first c tile (an MFMA against a ones fragment).
-__global__ __launch_bounds__(512, 1) void wgrad_k1_glds(WgradGlds a) {
-  constexpr int BO = 128, BC = 128, BK = 64, NT = 512, STAGES = 4;
-  constexpr int IMG = BK * 128;          // one operand image: [64 rows][128] bf16 (256-B rows)
-  constexpr int STAGE_E = 2 * IMG;       // dy image then x image (32 KB)
-  constexpr int EPI_LD = 64 + 4;         // fp32 epilogue rows of a 64 x 64 quadrant
-  constexpr int EPI_B = (4 * 64 * EPI_LD + 4 * 64) * 4;
-  constexpr int SMEM_B = STAGES * STAGE_E * 2 > EPI_B ? STAGES * STAGE_E * 2 : EPI_B;
-  constexpr int MAXKT = 1024;
-  __shared__ __attribute__((aligned(1024))) u16 smem[SMEM_B / 2 + MAXKT + 64];
-  short* ktl = reinterpret_cast<short*>(smem + SMEM_B / 2);
-  int* wcnt = reinterpret_cast<int*>(smem + SMEM_B / 2 + MAXKT);
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int quad = wave & 3, half = wave >> 2;
-  const int qo = (quad >> 1) * 64, qc = (quad & 1) * 64;
-  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3, r16 = lane & 15;
-
-  const int per_split = a.tiles_o * a.tiles_k;
-  const int nwg = per_split * a.splits;
-  const int orig = blockIdx.x, xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
-  const int z = wg / per_split, rem = wg - z * per_split;
-  const int tc = rem % a.tiles_k, to = rem / a.tiles_k;
-  const int o0 = to * BO, c0 = tc * BC;
-  const int64_t r_begin = (int64_t)z * a.rows_per_split;
-  int64_t r_end = r_begin + a.rows_per_split;
-  if (r_end > a.M) r_end = a.M;
-  const int nk_all = r_end > r_begin ? (int)((r_end - r_begin + BK - 1) / BK) : 0;
-  // ordered list of the split's k-tiles holding a real row (as conv_wgrad_tn_glds)
-  const bool use_list = a.lens != nullptr && nk_all <= MAXKT;
-  int nk = nk_all;
-  if (use_list) {
-    int total = 0;
-    for (int cc0 = 0; cc0 < nk_all; cc0 += NT) {
-      const int kt = cc0 + tid;
-      bool v = false;
-      if (kt < nk_all) {
-        const int64_t k0 = r_begin + (int64_t)kt * BK;
-        v = !rows_all_padding(a.lens, a.T, k0, k0 + BK < r_end ? k0 + BK : r_end);
-      }
-      const uint64_t mask = __ballot(v);
-      if (lane == 0) wcnt[wave] = __popcll(mask);
-      __syncthreads();
-      int before = total;
-      for (int w = 0; w < wave; ++w) before += wcnt[w];
-      const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
-                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
-      if (v) ktl[before + below] = (short)kt;
-      for (int w = 0; w < 8; ++w) total += wcnt[w];
-      __syncthreads();
-    }
-    nk = total;
-  }
-
-  // staging: a wave-instruction fills 4 image rows x 256 B; image row R = (2 wave + i) * 4 +
-  // lane / 16 (i < 2), physical 16-B chunk lane & 15 holding logical chunk (lane & 15) ^
-  // swz(R), swz(R) = (R & 7) << 1 (the BT = 128 swizzle of conv_wgrad_tn_glds: a 32-lane
-  // transposed read hits 16 distinct bank slots)
-  auto swz = [](int R) { return (R & 7) << 1; };
-  // buffer descriptors over the split's rows of dy and x (the k-tile advance rides in the scalar
-  // offset); a lane whose chunk lies past the channel count, or whose row lies past the split's
-  // end, selects an out-of-range voffset and stages zeros.  The row clip is the voffset select,
-  // not the record count, so it holds whether or not the range check sees the scalar offset.
-  const auto dy_rs = buf_rsrc(a.dy + r_begin * a.ldy, (r_end - r_begin) * a.ldy * 2);
-  const auto x_rs = buf_rsrc(a.x + r_begin * a.ldx, (r_end - r_begin) * a.ldx * 2);
-  int Rl[2];
-  uint32_t a_vo[2], b_vo[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int R = (wave * 2 + i) * 4 + (lane >> 4);
-    const int lc = (lane & 15) ^ swz(R);
-    Rl[i] = R;
-    a_vo[i] = o0 + lc * 8 < a.Cout ? (uint32_t)((R * a.ldy + o0 + lc * 8) * 2) : kOOB;
-    b_vo[i] = c0 + lc * 8 < a.Cin ? (uint32_t)((R * a.ldx + c0 + lc * 8) * 2) : kOOB;
-  }
-  const int rows = (int)(r_end - r_begin);
-  auto issue = [&](int kt, int stage) {
-    u16* As = smem + stage * STAGE_E;
-    u16* Bs = As + IMG;
-    const int tile = __builtin_amdgcn_readfirstlane(use_list ? (int)ktl[kt] : kt);
-    const int lim = rows - tile * BK;  // rows of this k-tile inside the split
-    const uint32_t sa = (uint32_t)(tile * BK * a.ldy * 2), sb = (uint32_t)(tile * BK * a.ldx * 2);
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const bool ok = Rl[i] < lim;
-      glds16_buf(dy_rs, As + (wave * 2 + i) * 4 * 128, ok ? a_vo[i] : kOOB, sa);
-      glds16_buf(x_rs, Bs + (wave * 2 + i) * 4 * 128, ok ? b_vo[i] : kOOB, sb);
-    }
-  };
-
-  f32x4 acc[4][4], accb[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    accb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-  // bias gradient: the waves of the c-half-0 quadrants of the first c tile (block-uniform tile
-  // test, wave-uniform quadrant test)
-  const bool do_bias = a.bslab != nullptr && tc == 0 && (quad & 1) == 0;
-  bf16x8g ones;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) ones[e] = (__bf16)1.0f;
-  // transposed fragment halves of this wave's 32 rows (asm reads, see ds_tr16)
-  const int rbase = half * 32 + 4 * g + q, sw = swz(rbase);
-  auto tr = [&](const u16* img, int col0, int hi) -> s16x4g {
-    const int lc = (col0 >> 3) + (p >> 1);
-    return ds_tr16(img + (rbase + 16 * hi) * 128 + ((lc ^ sw) << 3) + ((p & 1) << 2));
-  };
-  auto cat = [](s16x4g lo, s16x4g hi) {
-    return __builtin_bit_cast(bf16x8g, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-  };
-  auto compute = [&](int stage) {
-    const u16* As = smem + stage * STAGE_E;
-    const u16* Bs = As + IMG;
-    s16x4g ra[4][2], rb[4][2];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      ra[i][0] = tr(As, qo + i * 16, 0);
-      ra[i][1] = tr(As, qo + i * 16, 1);
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      rb[j][0] = tr(Bs, qc + j * 16, 0);
-      rb[j][1] = tr(Bs, qc + j * 16, 1);
-    }
-    bf16x8g fa[4];
-    // c fragment j's MFMAs wait only for the reads up to it (4-bit counter: the 16th read
-    // issues once the first has retired, so 6 - 2 j younger reads remain in flight)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if (j == 0) lgkm_wait<6>();
-      else if (j == 1) lgkm_wait<4>();
-      else if (j == 2) lgkm_wait<2>();
-      else lgkm_wait<0>();
-      if (j == 0) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) fa[i] = cat(ra[i][0], ra[i][1]);
-      }
-      const bf16x8g fb = cat(rb[j][0], rb[j][1]);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb, acc[i][j], 0, 0, 0);
-    }
-    if (do_bias) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], ones, accb[i], 0, 0, 0);
-    }
-  };
-
-  kloop<STAGES, 4>(nk, issue, compute);
-
-  // the two row halves of each quadrant through LDS: half 1 writes, half 0 adds and stores
-  float* Cs = reinterpret_cast<float*>(smem);
-  float* Bp = Cs + 4 * 64 * EPI_LD;
-  if (half == 1) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          Cs[(quad * 64 + i * 16 + 4 * g + r) * EPI_LD + j * 16 + r16] = acc[i][j][r];
-    if (do_bias && r16 == 0) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) Bp[quad * 64 + i * 16 + 4 * g + r] = accb[i][r];
-    }
-  }
-  __syncthreads();
-  if (half == 0) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          Cs[(quad * 64 + i * 16 + 4 * g + r) * EPI_LD + j * 16 + r16] += acc[i][j][r];
-    if (do_bias && r16 == 0) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) Bp[quad * 64 + i * 16 + 4 * g + r] += accb[i][r];
-    }
-  }
-  __syncthreads();
-  {
-    // 128 x 128 outputs, 32 per thread: row o = tid / 4, 32 consecutive c; quadrant rows
-    const int o = tid >> 2, cc = (tid & 3) * 32;
-    const int qd = (o >> 6) * 2 + (cc >> 6), ro = o & 63, co = cc & 63;
-    float* slab = a.slab + (int64_t)z * a.Cout * a.Kp;
-    if (o0 + o < a.Cout) {
-#pragma unroll
-      for (int v = 0; v < 8; ++v) {
-        const f32x4 t = *reinterpret_cast<const f32x4*>(Cs + (qd * 64 + ro) * EPI_LD + co + 4 * v);
-        if (c0 + cc + 4 * v < a.Cin)
-          *reinterpret_cast<f32x4*>(slab + (int64_t)(o0 + o) * a.Kp + c0 + cc + 4 * v) = t;
-      }
-    }
-    if (a.bslab != nullptr && tc == 0 && tid < BO && o0 + tid < a.Cout)
-      a.bslab[(int64_t)z * a.Cout + o0 + tid] = Bp[((tid >> 6) * 2) * 64 + (tid & 63)];
-  }
-}
-
-// wgrad_k1_q (FS2_TUNE_WGRAD_K1 = 0, default): 64 (o) x 64 (c) output tile per block with the
-// reduction rows split over the block's 4 waves: a k-tile is 128 rows, wave w multiplies rows
-// 32 w .. 32 w + 31 of it into its own 64 x 64 accumulators, and the four partial tiles are summed
-// in wave order through LDS at the end.  Against conv_wgrad_tn_glds (2 x 2 waves of 32 x 32 on
-// 64-row k-tiles) every transposed fragment read feeds 4 MFMAs instead of 2 and the per-k-tile
-// staging / address work is paid once per 128 rows: that kernel measured MFMA-busy 0.095 at the
-// decoder QKV shape (profiles/r3_wgrad_pmc.txt), issue-bound on its per-tile overhead.  Same
-// split-K slab layout (slab[z][o][c], bias slab[z][o]) and wgrad_reduce_k1.  The bias gradient
-// rides on the dy fragments of the blocks of the first c tile (an MFMA against a ones fragment).
-template <int STAGES>
-__global__ __launch_bounds__(256, 2) void wgrad_k1_q(WgradGlds a) {
-  constexpr int BO = 64, BC = 64, BK = 128, NT = 256;
-  constexpr int IMG = BK * 64;           // one operand image: [128 rows][64] bf16 (128-B rows)
-  constexpr int STAGE_E = 2 * IMG;       // dy image then x image
-  constexpr int EPI_LD = BC + 4;         // fp32 epilogue rows
-  constexpr int EPI_B = 4 * BO * EPI_LD * 4 + 4 * BO * 4;  // 4 partial tiles + 4 bias partials
-  constexpr int SMEM_B = STAGES * STAGE_E * 2 > EPI_B ? STAGES * STAGE_E * 2 : EPI_B;
-  constexpr int MAXKT = 1024;
-  __shared__ __attribute__((aligned(1024))) u16 smem[SMEM_B / 2 + MAXKT + 64];
-  short* ktl = reinterpret_cast<short*>(smem + SMEM_B / 2);
-  int* wcnt = reinterpret_cast<int*>(smem + SMEM_B / 2 + MAXKT);
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3, r16 = lane & 15;
-
-  const int per_split = a.tiles_o * a.tiles_k;
-  const int nwg = per_split * a.splits;
-  const int orig = blockIdx.x, xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
-  const int z = wg / per_split, rem = wg - z * per_split;
-  const int tc = rem % a.tiles_k, to = rem / a.tiles_k;
-  const int o0 = to * BO, c0 = tc * BC;
-  const int64_t r_begin = (int64_t)z * a.rows_per_split;
-  int64_t r_end = r_begin + a.rows_per_split;
-  if (r_end > a.M) r_end = a.M;
-  const int nk_all = r_end > r_begin ? (int)((r_end - r_begin + BK - 1) / BK) : 0;
-  // ordered list of the split's k-tiles holding a real row (as conv_wgrad_tn_glds)
-  const bool use_list = a.lens != nullptr && nk_all <= MAXKT;
-  int nk = nk_all;
-  if (use_list) {
-    int total = 0;
-    for (int cc0 = 0; cc0 < nk_all; cc0 += NT) {
-      const int kt = cc0 + tid;
-      bool v = false;
-      if (kt < nk_all) {
-        const int64_t k0 = r_begin + (int64_t)kt * BK;
-        v = !rows_all_padding(a.lens, a.T, k0, k0 + BK < r_end ? k0 + BK : r_end);
-      }
-      const uint64_t mask = __ballot(v);
-      if (lane == 0) wcnt[wave] = __popcll(mask);
-      __syncthreads();
-      int before = total;
-      for (int w = 0; w < wave; ++w) before += wcnt[w];
-      const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
-                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
-      if (v) ktl[before + below] = (short)kt;
-      for (int w = 0; w < 4; ++w) total += wcnt[w];
-      __syncthreads();
-    }
-    nk = total;
-  }
-
-  // staging: image row R = (4 wave + i) * 8 + lane / 8 (i < 4), physical 16-B chunk lane & 7
-  // holding logical chunk (lane & 7) ^ swz(R), swz(R) = ((R >> 1) & 3) << 1 (the BT = 64
-  // swizzle of conv_wgrad_tn_glds: a 32-lane transposed read hits 16 distinct bank slots)
-  auto swz = [](int R) { return ((R >> 1) & 3) << 1; };
-  // buffer descriptors over the split's rows (k-tile advance in the scalar offset); chunks past
-  // the channel count and rows past the split's end select an out-of-range voffset (zeros)
-  const auto dy_rs = buf_rsrc(a.dy + r_begin * a.ldy, (r_end - r_begin) * a.ldy * 2);
-  const auto x_rs = buf_rsrc(a.x + r_begin * a.ldx, (r_end - r_begin) * a.ldx * 2);
-  int Rl[4];
-  uint32_t a_vo[4], b_vo[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int R = (wave * 4 + i) * 8 + (lane >> 3);
-    const int lc = (lane & 7) ^ swz(R);
-    Rl[i] = R;
-    a_vo[i] = o0 + lc * 8 < a.Cout ? (uint32_t)((R * a.ldy + o0 + lc * 8) * 2) : kOOB;
-    b_vo[i] = c0 + lc * 8 < a.Cin ? (uint32_t)((R * a.ldx + c0 + lc * 8) * 2) : kOOB;
-  }
-  const int rows = (int)(r_end - r_begin);
-  auto issue = [&](int kt, int stage) {
-    u16* As = smem + stage * STAGE_E;
-    u16* Bs = As + IMG;
-    const int tile = __builtin_amdgcn_readfirstlane(use_list ? (int)ktl[kt] : kt);
-    const int lim = rows - tile * BK;
-    const uint32_t sa = (uint32_t)(tile * BK * a.ldy * 2), sb = (uint32_t)(tile * BK * a.ldx * 2);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const bool ok = Rl[i] < lim;
-      glds16_buf(dy_rs, As + (wave * 4 + i) * 8 * 64, ok ? a_vo[i] : kOOB, sa);
-      glds16_buf(x_rs, Bs + (wave * 4 + i) * 8 * 64, ok ? b_vo[i] : kOOB, sb);
-    }
-  };
-
-  f32x4 acc[4][4], accb[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    accb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-  const bool do_bias = a.bslab != nullptr && tc == 0;  // block-uniform
-  bf16x8g ones;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) ones[e] = (__bf16)1.0f;
-  // transposed fragment halves of this wave's 32 rows (asm reads, see ds_tr16)
-  const int rbase = wave * 32 + 4 * g + q, sw = swz(rbase);
-  auto tr = [&](const u16* img, int col0, int hi) -> s16x4g {
-    const int lc = (col0 >> 3) + (p >> 1);
-    return ds_tr16(img + (rbase + 16 * hi) * 64 + ((lc ^ sw) << 3) + ((p & 1) << 2));
-  };
-  auto cat = [](s16x4g lo, s16x4g hi) {
-    return __builtin_bit_cast(bf16x8g, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-  };
-  auto compute = [&](int stage) {
-    const u16* As = smem + stage * STAGE_E;
-    const u16* Bs = As + IMG;
-    s16x4g ra[4][2], rb[4][2];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      ra[i][0] = tr(As, i * 16, 0);
-      ra[i][1] = tr(As, i * 16, 1);
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      rb[j][0] = tr(Bs, j * 16, 0);
-      rb[j][1] = tr(Bs, j * 16, 1);
-    }
-    bf16x8g fa[4];
-    // the c fragment j's MFMAs wait only for the reads up to it (4-bit counter: the 16th read
-    // issues once the first has retired, so 6 - 2 j younger reads remain in flight)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if (j == 0) lgkm_wait<6>();
-      else if (j == 1) lgkm_wait<4>();
-      else if (j == 2) lgkm_wait<2>();
-      else lgkm_wait<0>();
-      if (j == 0) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) fa[i] = cat(ra[i][0], ra[i][1]);
-      }
-      const bf16x8g fb = cat(rb[j][0], rb[j][1]);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb, acc[i][j], 0, 0, 0);
-    }
-    if (do_bias) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], ones, accb[i], 0, 0, 0);
-    }
-  };
-
-  kloop<STAGES, 8>(nk, issue, compute);
-
-  // the four waves' partial tiles (and bias partials) through LDS, summed in wave order
-  float* Cs = reinterpret_cast<float*>(smem);
-  float* Bp = Cs + 4 * BO * EPI_LD;
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        Cs[(wave * BO + i * 16 + 4 * g + r) * EPI_LD + j * 16 + r16] = acc[i][j][r];
-  if (do_bias && r16 == 0) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) Bp[wave * BO + i * 16 + 4 * g + r] = accb[i][r];
-  }
-  __syncthreads();
-  {
-    const int o = tid >> 2, cc = (tid & 3) * 16;  // 16 consecutive c of row o per thread
-    float* slab = a.slab + (int64_t)z * a.Cout * a.Kp;
-    if (o0 + o < a.Cout) {
-#pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        f32x4 t = *reinterpret_cast<const f32x4*>(Cs + (0 * BO + o) * EPI_LD + cc + 4 * v);
-#pragma unroll
-        for (int w = 1; w < 4; ++w) t += *reinterpret_cast<const f32x4*>(Cs + (w * BO + o) * EPI_LD + cc + 4 * v);
-        if (c0 + cc + 4 * v < a.Cin)
-          *reinterpret_cast<f32x4*>(slab + (int64_t)(o0 + o) * a.Kp + c0 + cc + 4 * v) = t;
-      }
-    }
-    if (do_bias && tid < BO && o0 + tid < a.Cout)
-      a.bslab[(int64_t)z * a.Cout + o0 + tid] =
-          ((Bp[tid] + Bp[BO + tid]) + Bp[2 * BO + tid]) + Bp[3 * BO + tid];
-  }
-}
-
 // Halo weight gradient for Conv1d with 2 <= taps <= 9 (C_in, C_out multiples of 64, T a
 // multiple of 64), the split-K path for grids that conv_wgrad_band (wgrad.hip) cannot fill:
 // a block owns a 64 (o) x 64 (c) tile for ALL taps.  Per 64-row k-tile it stages the dy tile
@@ -2252,33 +1839,6 @@ int conv_wgrad_glds_launch(const void* dy, int64_t ldy, const void* x, int64_t l
   WgradGlds a{(const u16*)dy, ldy, (const u16*)x, ldx, ws, bslab, rows, seq_len, (int)c_in,
               (int)c_out, taps, pad, (int)Kp, rps, (int)((c_out + tile - 1) / tile),
               (int)((Kp + tile - 1) / tile), splits, lens};
-  // wgrad_k1_glds stages through buffer descriptors with 32-bit byte offsets within a split
-  const bool off32 = (rps + 128) * (ldx > ldy ? ldx : ldy) * 2 < ((int64_t)1 << 31);
-  if (taps == 1 && g_tune[FS2_TUNE_WGRAD_K1] == 0 && c_in % 8 == 0 && off32) {
-    // k = 1, 64 x 64 tiles with the 128-row k-tiles split over the 4 waves (wgrad_k1_q);
-    // rows_per_split in 128-row k-tiles
-    int64_t rps1 = (rows + splits - 1) / splits;
-    a.rows_per_split = (rps1 + 127) / 128 * 128;
-    a.tiles_o = (int)((c_out + 63) / 64);
-    a.tiles_k = (int)((c_in + 63) / 64);
-    const unsigned g1 = (unsigned)(a.tiles_o * a.tiles_k * splits);
-    wgrad_k1_q<2><<<g1, 256, 0, st>>>(a);
-    const int64_t total = c_out * c_in;
-    wgrad_reduce_k1<<<(unsigned)((total / 4 + 63) / 64), 256, 0, st>>>(ws, bslab, splits,
-                                                                     (int)c_out, total, dw, db);
-    return launch_status("fs2_conv_wgrad(bf16)");
-  }
-  if (taps == 1 && g_tune[FS2_TUNE_WGRAD_K1] == 1 && c_in % 8 == 0 && off32) {
-    // k = 1: 128 x 128 tiles of 8 waves (wgrad_k1_glds), splits in 64-row k-tiles
-    a.tiles_o = (int)((c_out + 127) / 128);
-    a.tiles_k = (int)((c_in + 127) / 128);
-    const unsigned g1 = (unsigned)(a.tiles_o * a.tiles_k * splits);
-    wgrad_k1_glds<<<g1, 512, 0, st>>>(a);
-    const int64_t total = c_out * c_in;
-    wgrad_reduce_k1<<<(unsigned)((total / 4 + 63) / 64), 256, 0, st>>>(ws, bslab, splits,
-                                                                     (int)c_out, total, dw, db);
-    return launch_status("fs2_conv_wgrad(bf16)");
-  }
   if (taps > 1 && g_tune[FS2_TUNE_WGRAD_HALO] == 0) {
     // no split slabs where the output tiles fill the chip (conv_wgrad_band, wgrad.hip)
     const int rc = conv_wgrad_band_launch(dy, ldy, x, ldx, dw, db, rows, seq_len, c_in, c_out,
@@ -2321,7 +1881,7 @@ int conv_wgrad_glds_launch(const void* dy, int64_t ldy, const void* x, int64_t l
     const int64_t total = c_out * c_in;  // multiple of 64 (both channel counts % 8 == 0)
     wgrad_reduce_k1<<<(unsigned)((total / 4 + 63) / 64), 256, 0, st>>>(ws, bslab, splits,
                                                                      (int)c_out, total, dw, db);
-  } else if (taps * c_in <= RROW_MAX && c_in % 4 == 0 && g_tune[FS2_TUNE_WGRAD_K1] != -2) {
+  } else if (taps * c_in <= RROW_MAX && c_in % 4 == 0) {
     wgrad_reduce_rows<<<(unsigned)c_out, 256, 0, st>>>(ws, bslab, splits, (int)c_out, (int)c_in,
                                                        taps, dw, db);
   } else {

@@ -345,7 +345,12 @@ int conv_wgrad_band_launch(const void* dy, int64_t ldy, const void* x, int64_t l
   if (seq_len % BR || rows % seq_len || rows / BR > (1 << 15)) return -1;
   if (c_in < 32 || c_out < 32) return -1;
   const int to = (int)((c_out + 31) / 32), tc = (int)((c_in + 31) / 32);
-  if (to * tc < 128) return -1;  // under-filled grid: split-K kernels
+  // grids under half the CUs keep the split-K kernels (the variance predictors' 256 x 256 k=3
+  // convs at T = 128: 64 tiles), unless those would be the tap-major kernel (C % 64 != 0: the
+  // PostNet's 80-channel convs, 48 tiles -- 26 vs 47 us alone, on 48 CUs)
+  const bool halo_ok = c_in % 64 == 0 && c_out % 64 == 0 && seq_len % 64 == 0;
+  const int min_tiles = g_tune[FS2_TUNE_WGRAD_BAND] == 3 ? 128 : halo_ok ? 128 : 32;
+  if (to * tc < min_tiles) return -1;
   // f32x4 read-modify-writes of dw: rows of c_in * taps floats, tile columns 32 * taps
   if (((uintptr_t)dw & 15) || (c_in * taps) % 4) return -1;
   WgradBand a{(const u16*)dy, ldy, (const u16*)x, ldx, dw, db, rows, seq_len, (int)c_in,
@@ -414,8 +419,9 @@ FS2_DEV bool wb_rows_all_padding(const int64_t* lens, int64_t T, int64_t r0, int
 }
 }  // namespace
 
+template <int STAGES>
 __global__ __launch_bounds__(512, 1) void wgrad_k1_multi(K1Multi m) {
-  constexpr int BO = 128, BC = 128, BK = 64, NT = 512, STAGES = 4;
+  constexpr int BO = 128, BC = 128, BK = 64, NT = 512;
   constexpr int IMG = BK * 128;     // one operand image: [64 rows][128] bf16 (256-B rows)
   constexpr int STAGE_E = 2 * IMG;  // dy image then x image (32 KB)
   constexpr int EPI_LD = 64 + 4;    // fp32 epilogue rows of a 64 x 64 quadrant
@@ -572,7 +578,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_k1_multi(K1Multi m) {
   for (int t = 0; t < STAGES - 1 && t < nk; ++t) issue(t, t);
   for (int kt = 0; kt < nk; ++kt) {
     const int ahead = nk - 1 - kt < STAGES - 2 ? nk - 1 - kt : STAGES - 2;
-    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    if (ahead >= 2 && STAGES >= 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -688,7 +694,7 @@ __global__ __launch_bounds__(256) void wgrad_k1_multi_reduce(K1Red r) {
 // is about 256 blocks of 128 x 128 tiles
 static int k1_multi_splits(int64_t tiles_total, int64_t rows) {
   int64_t s = (256 + tiles_total / 2) / tiles_total;
-  if (s > rows / 256) s = rows / 256;  // >= 4 k-tiles per split
+  if (s > rows / 512) s = rows / 512;  // >= 8 k-tiles per split (small products: fewer slabs)
   return (int)(s < 1 ? 1 : s);
 }
 
@@ -771,7 +777,11 @@ int wgrad_k1_multi_launch(const int64_t* jobs, int n, int64_t rows, int64_t seq_
   red.u_begin[n] = ub;
   red.b_begin[n] = bb;
   m.nblocks = begin;
-  wgrad_k1_multi<<<(unsigned)begin, 512, 0, st>>>(m);
+  // LDS ring depth (FS2_TUNE_WGRAD_K1M_STAGES, A/B): 0 = 4 slots (128 KB, three k-tiles in flight)
+  const int stg = g_tune[FS2_TUNE_WGRAD_K1M_STAGES];
+  if (stg == 2) wgrad_k1_multi<2><<<(unsigned)begin, 512, 0, st>>>(m);
+  else if (stg == 3) wgrad_k1_multi<3><<<(unsigned)begin, 512, 0, st>>>(m);
+  else wgrad_k1_multi<4><<<(unsigned)begin, 512, 0, st>>>(m);
   wgrad_k1_multi_reduce<<<(unsigned)((ub + bb + 255) / 256), 256, 0, st>>>(red);
   return launch_status("fs2_conv_wgrad_k1_multi");
 }

@@ -613,7 +613,12 @@ def test_conv_gemm_bf16_padding_tiles():
     d0 = K.conv_gemm(dy, wb, B * T, T, cout, cin, k, 4, flags=K.EPI_ADD_AUX, aux=aux)
     d1 = K.conv_gemm(dy, wb, B * T, T, cout, cin, k, 4, flags=K.EPI_ADD_AUX, aux=aux, lens=lens)
     assert torch.equal(d1[~tile_pad], d0[~tile_pad]) and torch.equal(d1[tile_pad], aux[tile_pad])
-    for tile in (64, 128):
+    # weight gradient: the split-K kernels (FS2_TUNE_WGRAD_HALO = 1, both tap-major tile widths)
+    # skip all-padding k-tiles at no change (bitwise); the band kernel (default) deals the bands
+    # that hold a real row over its waves in rank order, so skipping re-deals them: equal to
+    # fp32 rounding
+    for halo, tile in ((1, 64), (1, 128), (0, 0)):
+        K.lib.fs2_set_tuning(7, halo)
         K.lib.fs2_set_tuning(2, tile)
         try:
             dw0, db0 = torch.zeros_like(w), torch.zeros(cout, device=DEV)
@@ -622,7 +627,12 @@ def test_conv_gemm_bf16_padding_tiles():
             K.conv_wgrad(dy, x, dw1, B * T, T, cin, cout, k, 4, db=db1, lens=lens)
         finally:
             K.lib.fs2_set_tuning(2, 0)
-        assert torch.equal(dw0, dw1) and torch.equal(db0, db1)
+            K.lib.fs2_set_tuning(7, 0)
+        if halo:
+            assert torch.equal(dw0, dw1) and torch.equal(db0, db1)
+        else:
+            close(dw1, dw0, 1e-6)
+            close(db1, db0, 1e-6)
 
 
 @pytest.mark.parametrize("act,res", [(True, False), (False, True)])

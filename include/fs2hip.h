@@ -280,8 +280,9 @@ int fs2_weight_prep_batch(int dtype, const int64_t* jobs, int n_jobs, int64_t n_
  *   FS2_TUNE_ATTN_XCD      LDS-DMA attention kernels: 0 = the blocks of one (utterance, head) on
  *                          one XCD (K / V reuse in its L2; default), -1 = the launch grid's order
  *   FS2_TUNE_WGRAD_K1M_STAGES  grouped k = 1 weight gradient LDS ring: 0 = 4 slots, 2 / 3 slots
- *   FS2_TUNE_K1_BIG        k = 1 projections (fs2_conv_gemm): 1 = 8-wave 256 x 256 / 128 x 128
- *                          tiles (gemm_k1_big), 0 = the 4-wave tap-major kernel (default)
+ *   FS2_TUNE_K1_BIG        k = 1 projections (fs2_conv_gemm, C_in % 64 == 0): 0 = the 4-wave
+ *                          tap-major kernel (default); 8 waves (gemm_k1_big): 1 = 256 x 256 tiles
+ *                          for c_out >= 512 else 128 x 128, 2 = 128 x 128, 3 = 128 x 256
  * Process-wide; query workspace sizes after setting.                                 */
 enum { FS2_TUNE_GEMM_STAGES = 0, FS2_TUNE_WGRAD_STAGES = 1, FS2_TUNE_WGRAD_TILE = 2,
        FS2_TUNE_WGRAD_SPLITS = 3, FS2_TUNE_LEGACY_GEMM = 4, FS2_TUNE_NT_GROUP = 5,

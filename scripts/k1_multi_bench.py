@@ -2,7 +2,9 @@
 three fs2_conv_wgrad launches (+ their split reduces) against one fs2_conv_wgrad_k1_multi
 (grouped launch + one reduce), alone and beside a k = 9 data gradient on the main stream.
 
-    python scripts/k1_multi_bench.py [--reps 20]
+    python scripts/k1_multi_bench.py [--reps 20] [--probe]
+
+--probe: 10 grouped launches at the decoder shape only (for rocprofv3 --pmc passes).
 """
 import importlib
 import math
@@ -37,7 +39,8 @@ def timeit(fn, reps):
 
 def main():
     reps = int(sys.argv[sys.argv.index("--reps") + 1]) if "--reps" in sys.argv else 20
-    for T in (512, 128):
+    probe = "--probe" in sys.argv
+    for T in ((512,) if probe else (512, 128)):
         M = 48 * T
         lens = LENS[T]
         valid = (torch.arange(T, device=dev)[None] < lens[:, None]).reshape(-1)
@@ -59,6 +62,11 @@ def main():
         def grp():
             K.conv_wgrad_k1_multi(jobs, M, T, lens=lens, ws_buf=wsm)
 
+        if probe:
+            for _ in range(10):
+                grp()
+            torch.cuda.synchronize()
+            return
         t_s, t_g = [], []
         for _ in range(3):
             t_s.append(timeit(sep, reps))

@@ -370,7 +370,8 @@ def test_conv_gemm_bf16(B, T, cin, cout, k):
 def test_conv_gemm_k1_big(B, T, cin, cout):
     """8-wave projection GEMM (FS2_TUNE_K1_BIG 1 / 2 / 3: 256 x 256, 128 x 128, 128 x 256 tiles)
     bitwise equal to the 4-wave kernel (same k order per output), over ragged row counts,
-    utterance lengths (padding tiles) and the bias / ReLU-mask / residual-add epilogues."""
+    utterance lengths (padding tiles: valid rows) and the bias / ReLU-mask / residual-add
+    epilogues."""
     x = bf(rnd(B * T, cin, seed=11))
     w = bf(rnd(cout, cin, scale=1 / math.sqrt(cin), seed=12))
     b = rnd(cout, seed=13)
@@ -393,10 +394,13 @@ def test_conv_gemm_k1_big(B, T, cin, cout):
         K.lib.fs2_set_tuning(19, 0)
     close(runs[0][0], ref, 1e-5)
     close(runs[0][3], ref - b + auxf, 1e-5)
+    # with lens, rows of all-padding tiles are not computed: the tilings differ there, so the
+    # lens outputs are compared on the valid rows
+    live = (torch.arange(T, device=DEV)[None] < lens[:, None]).reshape(-1)
     for knob in (1, 2, 3):
-        for r0, r1 in zip(runs[0], runs[knob]):
+        for i, (r0, r1) in enumerate(zip(runs[0], runs[knob])):
             if r0 is not None:
-                assert torch.equal(r0, r1), knob
+                assert torch.equal(r0[live], r1[live]) if i in (1, 2) else torch.equal(r0, r1), (knob, i)
 
 
 @pytest.mark.parametrize("knob", [0, 1, -1, 2])  # FS2_TUNE_ATTN: kernel variants (fs2hip.h)

@@ -260,8 +260,7 @@ int fs2_weight_prep_batch(int dtype, const int64_t* jobs, int n_jobs, int64_t n_
  *                          2 = two groups in dK/dV too, 3 = dK/dV at three workgroups per CU
  *   FS2_TUNE_NT_TILE       tap-major fwd/dX kernel (k = 1 projections, odd shapes): 0 = tile
  *                          by grid size, 1 / 2 / 3 = force 128x128 / 128x64 / 64x64
- *   FS2_TUNE_LN_TILE       fs2_conv_gemm_ln(_bwd) row tile: 0 = 64 x 256 (default), 1 = 128 x 256,
- *                          2 = 128 x 256 on 8 waves (gemm_k1_big; forward, k = 1)
+ *   FS2_TUNE_LN_TILE       fs2_conv_gemm_ln(_bwd) row tile: 0 = 64 x 256 (default), 1 = 128 x 256
  *   FS2_TUNE_WGRAD_K1      k = 1 weight gradient: 0 = the grouped split-K kernel of
  *                          fs2_conv_wgrad_k1_multi with one job (default), -1 = the tap-major kernel
  *   FS2_TUNE_NT_K1         k = 1 projections on the tap-major kernel: 0 = buffer-descriptor
@@ -280,9 +279,6 @@ int fs2_weight_prep_batch(int dtype, const int64_t* jobs, int n_jobs, int64_t n_
  *   FS2_TUNE_ATTN_XCD      LDS-DMA attention kernels: 0 = the blocks of one (utterance, head) on
  *                          one XCD (K / V reuse in its L2; default), -1 = the launch grid's order
  *   FS2_TUNE_WGRAD_K1M_STAGES  grouped k = 1 weight gradient LDS ring: 0 = 4 slots, 2 / 3 slots
- *   FS2_TUNE_K1_BIG        k = 1 projections (fs2_conv_gemm, C_in % 64 == 0): 0 = the 4-wave
- *                          tap-major kernel (default); 8 waves (gemm_k1_big): 1 = 256 x 256 tiles
- *                          for c_out >= 512 else 128 x 128, 2 = 128 x 128, 3 = 128 x 256
  * Process-wide; query workspace sizes after setting.                                 */
 enum { FS2_TUNE_GEMM_STAGES = 0, FS2_TUNE_WGRAD_STAGES = 1, FS2_TUNE_WGRAD_TILE = 2,
        FS2_TUNE_WGRAD_SPLITS = 3, FS2_TUNE_LEGACY_GEMM = 4, FS2_TUNE_NT_GROUP = 5,
@@ -290,7 +286,7 @@ enum { FS2_TUNE_GEMM_STAGES = 0, FS2_TUNE_WGRAD_STAGES = 1, FS2_TUNE_WGRAD_TILE 
        FS2_TUNE_ATTN = 9, FS2_TUNE_NT_TILE = 10, FS2_TUNE_LN_TILE = 11, FS2_TUNE_WGRAD_K1 = 12,
        FS2_TUNE_NT_K1 = 13, FS2_TUNE_ATTN_DMA = 14, FS2_TUNE_TAPREG = 15,
        FS2_TUNE_WGRAD_BAND = 16, FS2_TUNE_ATTN_XCD = 17, FS2_TUNE_WGRAD_K1M_STAGES = 18,
-       FS2_TUNE_K1_BIG = 19, FS2_TUNE_COUNT = 20 };
+       FS2_TUNE_COUNT = 19 };
 int fs2_set_tuning(int knob, int value);
 
 /* Weight (and optionally bias) gradient, accumulated into the fp32 master-gradient layout:

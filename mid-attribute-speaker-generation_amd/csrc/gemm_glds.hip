@@ -691,99 +691,6 @@ __global__ __launch_bounds__(256) void conv_gemm_nt_glds(GldsArgs a) {
   nt_epilogue<BM, BN, VOC>(a, acc, smem, m0, n0, skip, tid, wm, wn, g, r16);
 }
 
-// ------------------------------------------------------------------------ 8-wave k = 1 GEMM
-// gemm_k1_big: the Linear / 1x1 Conv1d projections (taps = 1, K % 64 == 0) on BM x BN tiles of
-// WGM x WGN = 8 waves (2 per SIMD), STAGES-slot LDS-DMA ring with STAGES - 1 k-tiles in flight.
-// The 4-wave 128 x 128 tiles of conv_gemm_nt_glds re-stage each A row band once per 128 output
-// columns and keep one 32 KB k-tile in flight per block: at the K = 256 projections (four
-// k-tiles) every k-tile pays the global latency (PMC: MFMA busy 0.10, 44-50 % of the wave cycles
-// parked on the DMA wait; profiles/r4_linear_k1_pmc_*.txt).  256 x 256 tiles halve the L2 -> LDS
-// bytes per MFMA, and 128 KB of k-tiles are in flight per CU.  Staging (lane-linear [rows][64]
-// images, chunk swizzle c ^ ((R >> 1) & 7) on the source), fragments and epilogue (nt_epilogue,
-// whole-row LayerNorm for 256-wide tiles) as conv_gemm_nt_glds.
-template <int BM, int BN, int WGM, int WGN, int STAGES>
-__global__ __launch_bounds__(WGM * WGN * 64, 1) void gemm_k1_big(GldsArgs a) {
-  constexpr int NW = WGM * WGN, BK = 64;
-  constexpr int AW = BM / (8 * NW), BW = BN / (8 * NW);  // glds per wave per k-tile (8 rows each)
-  static_assert(BM % (8 * NW) == 0 && BN % (8 * NW) == 0 && WGM % 2 == 0, "staging");
-  constexpr int MI = BM / WGM / 16, NI = BN / WGN / 16;
-  constexpr int STAGE_E = (BM + BN) * BK;
-  constexpr int EPI_E = (BM / 2) * (BN + 4) * 2;
-  constexpr int SMEM_E = STAGES * STAGE_E > EPI_E ? STAGES * STAGE_E : EPI_E;
-  __shared__ __attribute__((aligned(1024))) u16 smem[SMEM_E];
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave / WGN, wn = wave % WGN;
-  const int g = lane >> 4, r16 = lane & 15;
-
-  // XCD-aware bijective renumbering; groups of `group` n-tiles, m-tiles within, n fastest
-  const int nwg = a.tiles_m * a.tiles_n;
-  const int orig = blockIdx.x, xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
-  const int gfull = a.tiles_m * a.group;
-  const int ng = wg / gfull, rem = wg - ng * gfull;
-  const int gsz = a.tiles_n - ng * a.group < a.group ? a.tiles_n - ng * a.group : a.group;
-  const int tm = m_interleave(rem / gsz, a.tiles_m, a.lens != nullptr);
-  const int tn = ng * a.group + (rem - (rem / gsz) * gsz);
-  const int64_t m0 = (int64_t)tm * BM;
-  const int n0 = tn * BN;
-  const bool skip = a.lens && rows_all_padding(a.lens, a.T, m0, m0 + BM < a.M ? m0 + BM : a.M);
-
-  const int lrow = lane >> 3;
-  const auto x_rs = buf_rsrc(a.x + m0 * a.ldx, (a.M - m0 < BM ? a.M - m0 : BM) * a.ldx * 2);
-  const auto w_rs = buf_rsrc(a.w + (int64_t)n0 * a.K, (int64_t)(a.N - n0 < BN ? a.N - n0 : BN) * a.K * 2);
-  uint32_t a_vo[AW], b_vo[BW];
-#pragma unroll
-  for (int i = 0; i < AW; ++i) {
-    const int R = (wave * AW + i) * 8 + lrow;
-    a_vo[i] = (uint32_t)(((int64_t)R * a.ldx + (((lane & 7) ^ ((R >> 1) & 7)) * 8)) * 2);
-  }
-#pragma unroll
-  for (int i = 0; i < BW; ++i) {
-    const int R = (wave * BW + i) * 8 + lrow;
-    b_vo[i] = (uint32_t)(((int64_t)R * a.K + (((lane & 7) ^ ((R >> 1) & 7)) * 8)) * 2);
-  }
-  auto issue = [&](int kt, int stage) {
-    u16* As = smem + stage * STAGE_E;
-    u16* Bs = As + BM * BK;
-    const uint32_t k0 = (uint32_t)(kt * BK * 2);
-#pragma unroll
-    for (int i = 0; i < AW; ++i) glds16_buf(x_rs, As + (wave * AW + i) * 8 * BK, a_vo[i], k0);
-#pragma unroll
-    for (int i = 0; i < BW; ++i) glds16_buf(w_rs, Bs + (wave * BW + i) * 8 * BK, b_vo[i], k0);
-  };
-
-  f32x4 acc[MI][NI];
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int sw = (r16 >> 1) & 7;
-  const int fo0 = r16 * BK + ((0 * 4 + g) ^ sw) * 8;
-  const int fo1 = r16 * BK + ((1 * 4 + g) ^ sw) * 8;
-  auto compute = [&](int stage) {
-    const u16* As = smem + stage * STAGE_E + wm * (BM / WGM) * BK;
-    const u16* Bs = smem + stage * STAGE_E + BM * BK + wn * (BN / WGN) * BK;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int fo = ks ? fo1 : fo0;
-      bf16x8g fa[MI], fb[NI];
-#pragma unroll
-      for (int i = 0; i < MI; ++i) fa[i] = *reinterpret_cast<const bf16x8g*>(As + i * 16 * BK + fo);
-#pragma unroll
-      for (int j = 0; j < NI; ++j) fb[j] = *reinterpret_cast<const bf16x8g*>(Bs + j * 16 * BK + fo);
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < NI; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-    }
-  };
-  if (!skip) kloop<STAGES, AW + BW>(a.K / BK, issue, compute);
-  nt_epilogue<BM, BN, false, NW, WGN, WGM>(a, acc, smem, m0, n0, skip, tid, wm, wn, g, r16);
-}
-
 // ------------------------------------------------------------------------ halo variant
 // Conv1d with taps > 1, Cin % 64 == 0 and T % BM == 0 (every row tile lies inside one
 // utterance).  The reduction runs channel-block-major: for each 64-channel block the
@@ -2095,17 +2002,14 @@ int conv_gemm_ln_glds_launch(const void* x, int64_t ldx, const void* wk, int64_t
   a.ln_seed = p_in > 0.f ? seed : nullptr;
   a.ln_site = site_in;
   a.ln_p = p_in;
-  const bool big8 = g_tune[FS2_TUNE_LN_TILE] == 2 && taps == 1 && c_in % 64 == 0;
-  const bool wide = g_tune[FS2_TUNE_LN_TILE] == 1 || big8;
+  const bool wide = g_tune[FS2_TUNE_LN_TILE] == 1;
   const int bm = wide ? 128 : 64;
   a.tiles_m = (int)((rows + bm - 1) / bm);
   a.tiles_n = 1;
   const unsigned grid = (unsigned)a.tiles_m;
   const bool tapaligned = c_in % 64 == 0;
   const bool k1 = tapaligned && taps == 1 && g_tune[FS2_TUNE_NT_K1] >= 0;
-  if (big8) {
-    gemm_k1_big<128, 256, 2, 4, 2><<<grid, 512, 0, st>>>(a);
-  } else if (wide) {
+  if (wide) {
     if (tapaligned) conv_gemm_nt_glds<128, 256, 2, true, false><<<grid, 256, 0, st>>>(a);
     else conv_gemm_nt_glds<128, 256, 2, false, false><<<grid, 256, 0, st>>>(a);
   } else {
@@ -2331,18 +2235,6 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
       }
     }
 #undef FS2_HALO2
-  } else if (taps == 1 && !voc && tapaligned && g_tune[FS2_TUNE_K1_BIG] > 0) {
-    // 8-wave projection GEMM (gemm_k1_big): 1 = 256 x 256 tiles for c_out >= 512, else
-    // 128 x 128; 2 = 128 x 128 everywhere; 3 = 128 x 256
-    const int kb = g_tune[FS2_TUNE_K1_BIG];
-    const int bm = kb == 1 && c_out >= 512 ? 256 : 128, bn = kb == 3 || bm == 256 ? 256 : 128;
-    a.tiles_m = (int)((rows + bm - 1) / bm);
-    a.tiles_n = (int)((c_out + bn - 1) / bn);
-    a.group = a.tiles_n;
-    const unsigned grid = (unsigned)(a.tiles_m * a.tiles_n);
-    if (bm == 256) gemm_k1_big<256, 256, 2, 4, 2><<<grid, 512, 0, st>>>(a);
-    else if (bn == 256) gemm_k1_big<128, 256, 2, 4, 2><<<grid, 512, 0, st>>>(a);
-    else gemm_k1_big<128, 128, 2, 4, 2><<<grid, 512, 0, st>>>(a);
   } else if ((big >= 512 && g_tune[FS2_TUNE_NT_TILE] == 0) || g_tune[FS2_TUNE_NT_TILE] == 1) {
     a.tiles_m = (int)((rows + 127) / 128);
     a.tiles_n = (int)((c_out + 127) / 128);

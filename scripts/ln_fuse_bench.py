@@ -48,12 +48,12 @@ for name, T, cin, cnt in (("dec fc+ln1", 512, 256, 6), ("dec w2+ln2", 512, 1024,
         K.ln_fwd(y, g, bt, res=res, seq_len=T, copy=bf, **kw)
 
     row = [timeit(two)]
-    for tile in (0, 1, 2):
+    for tile in (0, 1):
         K.lib.fs2_set_tuning(11, tile)
         row.append(timeit(lambda: K.conv_gemm_ln(x, wf, M, T, cin, d, 1, 0, g, bt, bias=b, res=res, **kw)))
         K.lib.fs2_set_tuning(11, 0)
     for i, t in enumerate(row):
         tot[i] = tot.get(i, 0.0) + cnt * t
     print(f"{name:12s} gemm+ln_fwd {row[0]:6.1f} us   fused 64x256 {row[1]:6.1f} us   "
-          f"fused 128x256 {row[2]:6.1f} us   8-wave 128x256 {row[3]:6.1f} us", flush=True)
-print(f"per step: two launches {tot[0]:.0f} us, fused 64x256 {tot[1]:.0f} us, 128x256 {tot[2]:.0f} us, 8-wave {tot[3]:.0f} us")
+          f"fused 128x256 {row[2]:6.1f} us", flush=True)
+print(f"per step: two launches {tot[0]:.0f} us, fused 64x256 {tot[1]:.0f} us, 128x256 {tot[2]:.0f} us")

@@ -365,44 +365,6 @@ def test_conv_gemm_bf16(B, T, cin, cout, k):
     close(db2, dy.float().sum(0) + 1, 1e-5)
 
 
-@pytest.mark.parametrize("B,T,cin,cout", [(4, 512, 256, 768), (3, 512, 1024, 256),
-                                          (5, 128, 256, 1024), (2, 200, 768, 256), (7, 33, 256, 80)])
-def test_conv_gemm_k1_big(B, T, cin, cout):
-    """8-wave projection GEMM (FS2_TUNE_K1_BIG 1 / 2 / 3: 256 x 256, 128 x 128, 128 x 256 tiles)
-    bitwise equal to the 4-wave kernel (same k order per output), over ragged row counts,
-    utterance lengths (padding tiles: valid rows) and the bias / ReLU-mask / residual-add
-    epilogues."""
-    x = bf(rnd(B * T, cin, seed=11))
-    w = bf(rnd(cout, cin, scale=1 / math.sqrt(cin), seed=12))
-    b = rnd(cout, seed=13)
-    lens = torch.tensor([max(1, T - 37 * i) for i in range(B)], device=DEV)
-    auxb = bf(rnd(B * T, cout, seed=14))
-    auxf = rnd(B * T, cout, seed=15)
-    ref = x.float() @ w.float().t() + b
-    runs = {}
-    try:
-        for knob in (0, 1, 2, 3):
-            K.lib.fs2_set_tuning(19, knob)  # FS2_TUNE_K1_BIG
-            y = K.conv_gemm(x, w, B * T, T, cin, cout, 1, 0, bias=b)
-            yl = K.conv_gemm(x, w, B * T, T, cin, cout, 1, 0, bias=b, out_dtype=torch.bfloat16, lens=lens)
-            ym = K.conv_gemm(x, w, B * T, T, cin, cout, 1, 0, flags=K.EPI_RELU_MASK_AUX, aux=auxb,
-                             out_dtype=torch.bfloat16, lens=lens) if cout % 8 == 0 else None
-            ya = auxf.clone()
-            K.conv_gemm(x, w, B * T, T, cin, cout, 1, 0, flags=K.EPI_ADD_AUX, aux=ya, out=ya)
-            runs[knob] = (y, yl, ym, ya)
-    finally:
-        K.lib.fs2_set_tuning(19, 0)
-    close(runs[0][0], ref, 1e-5)
-    close(runs[0][3], ref - b + auxf, 1e-5)
-    # with lens, rows of all-padding tiles are not computed: the tilings differ there, so the
-    # lens outputs are compared on the valid rows
-    live = (torch.arange(T, device=DEV)[None] < lens[:, None]).reshape(-1)
-    for knob in (1, 2, 3):
-        for i, (r0, r1) in enumerate(zip(runs[0], runs[knob])):
-            if r0 is not None:
-                assert torch.equal(r0[live], r1[live]) if i in (1, 2) else torch.equal(r0, r1), (knob, i)
-
-
 @pytest.mark.parametrize("knob", [0, 1, -1, 2])  # FS2_TUNE_ATTN: kernel variants (fs2hip.h)
 @pytest.mark.parametrize("B,T,lens", [(2, 64, [64, 40]), (3, 130, [130, 77, 1]),
                                       (2, 512, [512, 300]), (3, 300, [300, 129, 64])])
@@ -551,12 +513,11 @@ def test_conv_gemm_bf16_pipeline_depths(stages, B, T, cin, cout, k):
 @pytest.mark.parametrize("B,T,lens,cin,p,tile", [
     (3, 50, [50, 17, 1], 256, 0.0, 0), (2, 200, [200, 130], 1024, 0.2, 0),
     (4, 128, [128, 70, 33, 128], 256, 0.2, 1), (6, 512, [512, 300, 129, 128, 1, 400], 1024, 0.1, 0),
-    (5, 37, None, 256, 0.3, 1), (2, 64, [64, 9], 80, 0.1, 0), (4, 128, [128, 70, 33, 128], 256, 0.2, 2),
-    (6, 512, [512, 300, 129, 128, 1, 400], 1024, 0.1, 2), (5, 37, None, 256, 0.3, 2)])
+    (5, 37, None, 256, 0.3, 1), (2, 64, [64, 9], 80, 0.1, 0)])
 def test_conv_gemm_ln(B, T, lens, cin, p, tile):
     """fs2_conv_gemm_ln (GEMM + bias + dropout + residual + LayerNorm + row mask in one
     kernel) equals fs2_conv_gemm (fp32 y) -> fs2_ln_fwd bitwise: out, its bf16 copy, and
-    xhat / rstd on the rows the backward reads; every row tile (FS2_TUNE_LN_TILE 0 / 1 / 2)."""
+    xhat / rstd on the rows the backward reads; both row tiles (FS2_TUNE_LN_TILE)."""
     M, d = B * T, 256
     lt = None if lens is None else torch.tensor(lens, device=DEV)
     x = bf(rnd(M, cin, seed=51))

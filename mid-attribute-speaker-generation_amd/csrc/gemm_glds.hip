@@ -384,8 +384,46 @@ FS2_DEV void nt_epilogue(const GldsArgs& a, f32x4 (&acc)[BM / WM / 16][BN / WN /
   if (skip && (a.flags & FS2_EPI_SKIP_NOSTORE)) return;  // block-uniform
   float* Cs = reinterpret_cast<float*>(smem);
   const bool out_bf16 = a.flags & FS2_EPI_OUT_BF16, aux_bf16 = a.flags & FS2_EPI_AUX_BF16;
+  constexpr int TPR = BN / 8;            // threads per row
+  constexpr int RPP = NWAVE * 64 / TPR;  // rows per pass
+  constexpr int NP = (BM / 2) / RPP;     // passes per half
+  const int cc = (tid % TPR) * 8;
+  const int n = n0 + cc;
+  // The bias (the same 8 columns in every pass) and a half's aux rows are loaded BEFORE the
+  // half's LDS write: their latency then overlaps it.  Loaded inside each pass, they put a
+  // dependent global load between the pass's LDS read and its store, four passes in series
+  // (k = 1 QKV projection: 28.5 us with, 15.1 us without the epilogue; its LDS transpose
+  // alone costs 2.4 us and its stores alone 4.1 us; profiles/r4_ab_experiments.txt).
+  // (fp32 aux rows only where a half has at most two passes: four would cost 32 registers)
+  constexpr bool PF32 = NP <= 2;
+  const bool pf = !VOC && a.vec && n < a.N;
+  const bool pf_aux = pf && (a.flags & (FS2_EPI_ADD_AUX | FS2_EPI_RELU_MASK_AUX)) &&
+                      (aux_bf16 || PF32);
+  f32x4 bz0 = f32x4{0.f, 0.f, 0.f, 0.f}, bz1 = bz0;
+  if (pf && (a.flags & FS2_EPI_BIAS) && !skip) {
+    bz0 = *reinterpret_cast<const f32x4*>(a.bias + n);
+    bz1 = *reinterpret_cast<const f32x4*>(a.bias + n + 4);
+  }
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
+    uint4 araw[NP][PF32 ? 2 : 1];  // aux rows of this half: bf16 in [p][0], fp32 in [p][0..1]
+    if (pf_aux) {
+#pragma unroll
+      for (int p = 0; p < NP; ++p) {
+        const int64_t m = m0 + h * (BM / 2) + p * RPP + tid / TPR;
+#pragma unroll
+        for (int q = 0; q < (PF32 ? 2 : 1); ++q) araw[p][q] = uint4{0u, 0u, 0u, 0u};
+        if (m < a.M) {
+          if (aux_bf16) {
+            araw[p][0] = *reinterpret_cast<const uint4*>((const u16*)a.aux + m * a.ld_aux + n);
+          } else if constexpr (PF32) {
+            const uint4* ap = reinterpret_cast<const uint4*>((const float*)a.aux + m * a.ld_aux + n);
+            araw[p][0] = ap[0];
+            araw[p][1] = ap[1];
+          }
+        }
+      }
+    }
     if (wm / WPH == h) {
       const int rb = (wm % WPH) * WR;
 #pragma unroll
@@ -397,12 +435,8 @@ FS2_DEV void nt_epilogue(const GldsArgs& a, f32x4 (&acc)[BM / WM / 16][BN / WN /
             Cs[(rb + i * 16 + 4 * g + r) * EPI_LD + wn * (BN / WN) + j * 16 + r16] = acc[i][j][r];
     }
     epi_barrier();
-    constexpr int TPR = BN / 8;           // threads per row
-    constexpr int RPP = NWAVE * 64 / TPR; // rows per pass
-    const int cc = (tid % TPR) * 8;
-    const int n = n0 + cc;
 #pragma unroll
-    for (int p = 0; p < (BM / 2) / RPP; ++p) {
+    for (int p = 0; p < NP; ++p) {
       const int rr = p * RPP + tid / TPR;
       const int64_t m = m0 + h * (BM / 2) + rr;
       if (m >= a.M || n >= a.N) continue;
@@ -421,8 +455,8 @@ FS2_DEV void nt_epilogue(const GldsArgs& a, f32x4 (&acc)[BM / WM / 16][BN / WN /
       }
       if (a.vec) {
         if ((a.flags & FS2_EPI_BIAS) && !skip) {
-          const f32x4 b0 = *reinterpret_cast<const f32x4*>(a.bias + n);
-          const f32x4 b1 = *reinterpret_cast<const f32x4*>(a.bias + n + 4);
+          const f32x4 b0 = pf ? bz0 : *reinterpret_cast<const f32x4*>(a.bias + n);
+          const f32x4 b1 = pf ? bz1 : *reinterpret_cast<const f32x4*>(a.bias + n + 4);
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             v[e] += b0[e];
@@ -430,7 +464,23 @@ FS2_DEV void nt_epilogue(const GldsArgs& a, f32x4 (&acc)[BM / WM / 16][BN / WN /
           }
         }
         float av[8];
-        if (a.flags & (FS2_EPI_ADD_AUX | FS2_EPI_RELU_MASK_AUX)) {
+        if (pf_aux) {
+          if (aux_bf16) {
+            const uint4 raw = araw[p][0];
+            const uint32_t wv[4] = {raw.x, raw.y, raw.z, raw.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              av[2 * e] = __uint_as_float(wv[e] << 16);
+              av[2 * e + 1] = __uint_as_float(wv[e] & 0xffff0000u);
+            }
+          } else if constexpr (PF32) {
+            const uint4 r0 = araw[p][0], r1 = araw[p][1];
+            av[0] = __uint_as_float(r0.x); av[1] = __uint_as_float(r0.y);
+            av[2] = __uint_as_float(r0.z); av[3] = __uint_as_float(r0.w);
+            av[4] = __uint_as_float(r1.x); av[5] = __uint_as_float(r1.y);
+            av[6] = __uint_as_float(r1.z); av[7] = __uint_as_float(r1.w);
+          }
+        } else if (a.flags & (FS2_EPI_ADD_AUX | FS2_EPI_RELU_MASK_AUX)) {
           if (aux_bf16) {
             const uint4 raw = *reinterpret_cast<const uint4*>((const u16*)a.aux + m * a.ld_aux + n);
             const uint32_t wv[4] = {raw.x, raw.y, raw.z, raw.w};
@@ -534,8 +584,10 @@ FS2_DEV void nt_epilogue(const GldsArgs& a, f32x4 (&acc)[BM / WM / 16][BN / WN /
 // K1: taps == 1 and K % 64 == 0 (the Linear / 1x1 projections) -- A and B stage through buffer
 // descriptors based at the tile's first row: per-lane 32-bit offsets fixed over the k loop, the
 // k-step in the scalar offset, rows past M / N out of the descriptors' range (zeros).
+// (the K1 128 x 128 one-stage build, the projections' workhorse, is held to three blocks per CU)
 template <int BM, int BN, int STAGES, bool TAPALIGNED, bool VOC, bool K1 = false>
-__global__ __launch_bounds__(256) void conv_gemm_nt_glds(GldsArgs a) {
+__global__ __launch_bounds__(256, (K1 && BM == 128 && BN == 128 && STAGES == 1) ? 3 : 1) void
+conv_gemm_nt_glds(GldsArgs a) {
   static_assert(!K1 || (TAPALIGNED && !VOC), "K1: taps == 1, K % 64 == 0, no vocoder epilogue");
   const int dil = VOC ? a.dil : 1;
   constexpr int BK = 64;

@@ -344,7 +344,11 @@ int conv_wgrad_band_launch(const void* dy, int64_t ldy, const void* x, int64_t l
     return -1;
   if (seq_len % BR || rows % seq_len || rows / BR > (1 << 15)) return -1;
   if (c_in < 32 || c_out < 32) return -1;
-  if (g_tune[FS2_TUNE_WGRAD_BAND] == 4 && taps != 9 && c_in % 64 == 0 && c_out % 64 == 0) return -1;
+  // taps 3 / 5 with 64-multiple channels (PostNet 512, variance predictors) stay on the split-K
+  // halo kernel: step 6.91 vs 6.98 ms with the band kernel there (profiles/r4_ab_experiments.txt)
+  if (g_tune[FS2_TUNE_WGRAD_BAND] != 4 && taps != 9 && c_in % 64 == 0 && c_out % 64 == 0 &&
+      seq_len % 64 == 0)
+    return -1;
   const int to = (int)((c_out + 31) / 32), tc = (int)((c_in + 31) / 32);
   // grids under half the CUs keep the split-K kernels (the variance predictors' 256 x 256 k=3
   // convs at T = 128: 64 tiles), unless those would be the tap-major kernel (C % 64 != 0: the

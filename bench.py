@@ -375,6 +375,31 @@ def probe_conv(reps=10):
     torch.cuda.synchronize()
 
 
+def probe_wgrad(reps=10):
+    """The decoder-shaped launches of the k=9 weight-gradient class alone (dW1 += dh^T x1~ with
+    the fused bias gradient, lens as in the step), for the PMC passes of ``hbm_traffic``."""
+    K = importlib.import_module("mid-attribute-speaker-generation_amd.kernels")
+    syn = PKG.data.syn_batch(48, 128, seed=0)
+    M_, T_ = 48 * int(syn[8]), int(syn[8])
+    dev = torch.device("cuda", 0)
+    lens = torch.tensor(syn[7], device=dev)
+    valid = (torch.arange(T_, device=dev)[None] < lens[:, None]).reshape(-1, 1)
+    x = (torch.randn(M_, D, device=dev) * valid).to(torch.bfloat16)
+    dh = (torch.randn(M_, F, device=dev) * valid).to(torch.bfloat16)
+    dw = torch.zeros(F, D, KW, device=dev)
+    db = torch.zeros(F, device=dev)
+    for _ in range(reps):
+        K.conv_wgrad(dh, x, dw, M_, T_, D, F, KW, 4, db=db, lens=lens)
+    torch.cuda.synchronize()
+
+
+def probe_wgrad_alg_bytes(syn):
+    """Compulsory bytes of one k=9 weight-gradient launch: the valid rows of dh (V x 1024 bf16)
+    and of x (V x 256 bf16) read once, dW (1024 x 2304 fp32) read and written (accumulated)."""
+    V = int(np.sum(syn[7]))
+    return V * F * 2 + V * D * 2 + 2 * F * D * KW * 4
+
+
 def probe_alg_bytes(syn):
     """Compulsory bytes of the probe's two launches (mean per launch): forward reads the
     valid rows of x (V x 256 bf16) and the weight (1024 x 2304 bf16) once and writes every
@@ -387,8 +412,9 @@ def probe_alg_bytes(syn):
     return (fwd + dgr) // 2
 
 
-def hbm_traffic(timeout=300):
-    """Per-launch memory-side bytes of the probe's k=9 conv launches from rocprofv3 PMC
+def hbm_traffic(timeout=300, kind="conv"):
+    """Per-launch memory-side bytes of the probe's k=9 conv (kind "conv") or weight-gradient
+    (kind "wgrad") launches from rocprofv3 PMC
     counters: FETCH_SIZE and WRITE_SIZE (KiB) in separate passes (they do not fit one TCC
     pass), FETCH_SIZE doubled (gfx950 reports half the bytes of 16-B-per-lane streaming
     reads; MI355X_MICROARCH.md, HBM).  These count L2 misses, Infinity-Cache hits included."""
@@ -405,7 +431,7 @@ def hbm_traffic(timeout=300):
             d = os.path.join(tmp, ctr)
             cmd = ["timeout", "-s", "KILL", str(timeout), prof, "--pmc", ctr, "-d", d, "-o",
                    "probe", "--output-format", "csv", "--", sys.executable,
-                   os.path.abspath(__file__), "--probe-conv"]
+                   os.path.abspath(__file__), "--probe-" + kind]
             try:
                 r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout + 30)
             except subprocess.TimeoutExpired:
@@ -416,10 +442,16 @@ def hbm_traffic(timeout=300):
             vals = []
             for row in csv.DictReader(open(files[0])):
                 kn = row.get("Kernel_Name", "")
-                if ("conv_gemm_halo" in kn or "conv_gemm_tapreg" in kn) and row.get("Counter_Name") == ctr:
+                names = (("conv_gemm_halo", "conv_gemm_tapreg") if kind == "conv" else
+                         ("conv_wgrad_band", "conv_wgrad_halo", "wgrad_reduce"))
+                if any(n in kn for n in names) and row.get("Counter_Name") == ctr:
                     vals.append(float(row["Counter_Value"]))
             if not vals:
-                return None, f"{ctr}: no conv_gemm_halo / conv_gemm_tapreg dispatches"
+                return None, f"{ctr}: no {kind} dispatches"
+            # a split-K weight gradient is two launches (partials + reduce): bytes per pair
+            per_launch = 2 if kind == "wgrad" and any(
+                "wgrad_reduce" in row.get("Kernel_Name", "") for row in csv.DictReader(open(files[0]))) else 1
+            per[ctr] = float(np.mean(vals)) * per_launch
             per[ctr] = float(np.mean(vals))
     return (per["FETCH_SIZE"] * 2.0 + per["WRITE_SIZE"]) * 1024.0, per
 
@@ -501,8 +533,12 @@ def main():
                     help="BASELINE config 3: the --use_clf step (second forward with shuffled "
                          "speakers + GE2E language discriminator on 150-frame chunks)")
     ap.add_argument("--probe-conv", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--probe-wgrad", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.probe_wgrad:
+        probe_wgrad()
+        return
     if args.probe_conv:
         probe_conv()
         return 0
@@ -623,13 +659,18 @@ def main():
                                   "skip all-padding row tiles)",
                     "per_launch_flop": round(c["gflop_per_step"] * 1e9 / c["launches_per_step"]),
                     "avg_launch_ms": c["avg_launch_ms"]}
-            if dom == "conv_k9" and world == 1 and args.dtype == "bf16" and not args.no_traffic:
-                traffic, detail = hbm_traffic()
+            if dom in ("conv_k9", "wgrad_k9") and world == 1 and args.dtype == "bf16" and \
+                    not args.no_traffic:
+                kind = "conv" if dom == "conv_k9" else "wgrad"
+                traffic, detail = hbm_traffic(kind=kind)
                 if traffic is not None:
+                    syn0 = PKG.data.syn_batch(48, 128, seed=0)
                     roof["traffic"] = round(traffic)
-                    roof["traffic_unit"] = ("bytes/launch (FETCH_SIZE x2 + WRITE_SIZE, PMC) of the "
-                                            "class's decoder-shaped fwd + data-gradient launches")
-                    roof["traffic_algorithmic"] = probe_alg_bytes(PKG.data.syn_batch(48, 128, seed=0))
+                    roof["traffic_unit"] = (
+                        "bytes/launch (FETCH_SIZE x2 + WRITE_SIZE, PMC) of the class's decoder-shaped "
+                        + ("fwd + data-gradient launches" if kind == "conv" else "weight-gradient launches"))
+                    roof["traffic_algorithmic"] = (probe_alg_bytes(syn0) if kind == "conv"
+                                                   else probe_wgrad_alg_bytes(syn0))
                 else:
                     roof["traffic_note"] = detail
             roof["classes"] = classes

@@ -719,6 +719,32 @@ def test_conv_gemm_bf16_halo(B, T, cin, cout, k):
         K.lib.fs2_set_tuning(15, 0)
 
 
+@pytest.mark.parametrize("mode", [0, 1, 3])
+def test_conv_gemm_bf16_tapreg_ragged_rows(mode):
+    """A row count that is not a whole number of utterances (here not a multiple of the 128-row
+    tile either): the tap-register kernel is not eligible (rows % seq_len, rows % 128) and the
+    launch falls back to a kernel that computes every row -- rows past the matrix read as zero,
+    as in a reference whose input is zero there."""
+    B, T, cin, cout, k = 4, 512, 256, 1024, 9
+    M = B * T - 96
+    pad = (k - 1) // 2
+    xf = bf(rnd(B * T, cin, seed=81))
+    xf[M:] = 0
+    w = bf(rnd(cout, cin, k, scale=1 / math.sqrt(cin * k), seed=82)).float()
+    b = rnd(cout, seed=83)
+    wf = torch.empty(cout * cin * k, device=DEV, dtype=torch.bfloat16)
+    wb = torch.empty(cout * cin * k, device=DEV, dtype=torch.bfloat16)
+    K.weight_prep(w, cout, cin, k, wf, wb)
+    K.lib.fs2_set_tuning(15, mode)  # FS2_TUNE_TAPREG
+    try:
+        y = K.conv_gemm(xf[:M].contiguous(), wf, M, T, cin, cout, k, pad, bias=b, flags=K.EPI_RELU)
+    finally:
+        K.lib.fs2_set_tuning(15, 0)
+    ref = F.relu(ref_conv(xf.float(), w, b, B, T, pad))[:M]
+    assert y.shape == (M, cout) and torch.isfinite(y).all()
+    close(y, ref, 1e-5)
+
+
 @pytest.mark.parametrize("B,T,cin,cout,k,mode", [
     (4, 512, 256, 1024, 9, 0), (4, 512, 256, 1024, 9, 1), (6, 512, 1024, 256, 9, 1),
     (2, 256, 512, 512, 5, 3), (3, 128, 512, 512, 5, 1), (3, 128, 256, 320, 9, 1),

@@ -362,7 +362,8 @@ FS2_DEV void nt_epilogue_lnbwd(const GldsArgs& a, f32x4 (&acc)[BM / 32][256 / WN
 // half).  SROW > 0 (conv_gemm_tapreg): fragment i of a wave holds the rows i + SROW * m
 // (m = 0..15) of its band; the fragments are staged as usual and the store pass maps each
 // output row back to its (fragment, m) slot.
-template <int BM, int BN, bool VOC, int NWAVE = 4, int WN = 2, int WM = 2, int SROW = 0>
+template <int BM, int BN, bool VOC, int NWAVE = 4, int WN = 2, int WM = 2, int SROW = 0,
+          bool BF16D = false>
 FS2_DEV void nt_epilogue(const GldsArgs& a, f32x4 (&acc)[BM / WM / 16][BN / WN / 16], u16* smem,
                          int64_t m0, int n0, bool skip, int tid, int wm, int wn, int g, int r16) {
   constexpr int MI = BM / WM / 16, NI = BN / WN / 16;
@@ -382,6 +383,52 @@ FS2_DEV void nt_epilogue(const GldsArgs& a, f32x4 (&acc)[BM / WM / 16][BN / WN /
     }
   }
   if (skip && (a.flags & FS2_EPI_SKIP_NOSTORE)) return;  // block-uniform
+  if constexpr (BF16D && !VOC && SROW == 0) {
+    // bf16 output with a column-only epilogue (bias, ReLU): applied in the accumulator layout
+    // (the bias of a lane's column is one value per 16-column fragment), rounded to bf16 and
+    // written to LDS as ONE whole tile -- half the LDS bytes of the fp32 half-tile passes and a
+    // single barrier -- then stored as 16-B row vectors.  Same operations per element: bitwise
+    // equal to the fp32 path below.
+    constexpr int LDB = BN + 4;  // u16 row stride: 8 B pad
+    static_assert(BM * LDB <= (BM / 2) * (BN + 4) * 2, "bf16 tile fits the epilogue region");
+    if (a.vec && (a.flags & FS2_EPI_OUT_BF16) &&
+        !(a.flags & (FS2_EPI_ADD_AUX | FS2_EPI_RELU_MASK_AUX))) {
+      const bool relu = a.flags & FS2_EPI_RELU;
+      const bool bias = (a.flags & FS2_EPI_BIAS) && !skip;
+      float bj[NI];
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int col = n0 + wn * (BN / WN) + j * 16 + r16;
+        bj[j] = bias && col < a.N ? a.bias[col] : 0.f;
+      }
+      u16* Cb = smem;
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float v = acc[i][j][r];
+            if (bias) v += bj[j];
+            if (relu) v = fmaxf(v, 0.f);
+            Cb[(wm * WR + i * 16 + 4 * g + r) * LDB + wn * (BN / WN) + j * 16 + r16] = fbv(v);
+          }
+      epi_barrier();
+      constexpr int TPR = BN / 8, RPP = NWAVE * 64 / TPR;
+      const int cc = (tid % TPR) * 8;
+      const int n = n0 + cc;
+#pragma unroll
+      for (int p = 0; p < BM / RPP; ++p) {
+        const int rr = p * RPP + tid / TPR;
+        const int64_t m = m0 + rr;
+        if (m >= a.M || n >= a.N) continue;
+        *reinterpret_cast<uint4*>((u16*)a.y + m * a.ldy + n) =
+            *reinterpret_cast<const uint4*>(Cb + rr * LDB + cc);
+      }
+      epi_barrier();
+      return;
+    }
+  }
   float* Cs = reinterpret_cast<float*>(smem);
   const bool out_bf16 = a.flags & FS2_EPI_OUT_BF16, aux_bf16 = a.flags & FS2_EPI_AUX_BF16;
   constexpr int TPR = BN / 8;            // threads per row
@@ -740,7 +787,7 @@ conv_gemm_nt_glds(GldsArgs a) {
     else kloop<STAGES, AW + BW>(nk, issue, compute);
   }
 
-  nt_epilogue<BM, BN, VOC>(a, acc, smem, m0, n0, skip, tid, wm, wn, g, r16);
+  nt_epilogue<BM, BN, VOC, 4, 2, 2, 0, K1>(a, acc, smem, m0, n0, skip, tid, wm, wn, g, r16);
 }
 
 // ------------------------------------------------------------------------ halo variant

@@ -391,8 +391,24 @@ FS2_DEV void nt_epilogue(const GldsArgs& a, f32x4 (&acc)[BM / WM / 16][BN / WN /
     // equal to the fp32 path below.
     constexpr int LDB = BN + 4;  // u16 row stride: 8 B pad
     static_assert(BM * LDB <= (BM / 2) * (BN + 4) * 2, "bf16 tile fits the epilogue region");
-    if (a.vec && (a.flags & FS2_EPI_OUT_BF16) &&
-        !(a.flags & (FS2_EPI_ADD_AUX | FS2_EPI_RELU_MASK_AUX))) {
+    const bool rmask = (a.flags & FS2_EPI_RELU_MASK_AUX) && (a.flags & FS2_EPI_AUX_BF16);
+    if (a.vec && (a.flags & FS2_EPI_OUT_BF16) && !(a.flags & FS2_EPI_ADD_AUX) &&
+        (rmask || !(a.flags & FS2_EPI_RELU_MASK_AUX))) {
+      constexpr int TPR = BN / 8, RPP = NWAVE * 64 / TPR, NPB = BM / RPP, NPF = NPB / 2;
+      const int cc = (tid % TPR) * 8;
+      const int n = n0 + cc;
+      // ReLU mask (bf16 aux > 0): applied to the bf16 row vectors -- rounding 0 gives 0, so the
+      // mask commutes with the rounding.  The first half of the passes' aux rows is loaded
+      // before the LDS write, the second half one pass ahead of its use.
+      uint4 am[NPB];
+      if (rmask) {
+#pragma unroll
+        for (int p = 0; p < NPF; ++p) {
+          const int64_t m = m0 + p * RPP + tid / TPR;
+          am[p] = m < a.M && n < a.N ? *reinterpret_cast<const uint4*>((const u16*)a.aux + m * a.ld_aux + n)
+                                      : uint4{0u, 0u, 0u, 0u};
+        }
+      }
       const bool relu = a.flags & FS2_EPI_RELU;
       const bool bias = (a.flags & FS2_EPI_BIAS) && !skip;
       float bj[NI];
@@ -414,16 +430,29 @@ FS2_DEV void nt_epilogue(const GldsArgs& a, f32x4 (&acc)[BM / WM / 16][BN / WN /
             Cb[(wm * WR + i * 16 + 4 * g + r) * LDB + wn * (BN / WN) + j * 16 + r16] = fbv(v);
           }
       epi_barrier();
-      constexpr int TPR = BN / 8, RPP = NWAVE * 64 / TPR;
-      const int cc = (tid % TPR) * 8;
-      const int n = n0 + cc;
 #pragma unroll
-      for (int p = 0; p < BM / RPP; ++p) {
+      for (int p = 0; p < NPB; ++p) {
+        if (rmask && p + NPF < NPB) {
+          const int64_t m = m0 + (p + NPF) * RPP + tid / TPR;
+          am[p + NPF] = m < a.M && n < a.N
+                            ? *reinterpret_cast<const uint4*>((const u16*)a.aux + m * a.ld_aux + n)
+                            : uint4{0u, 0u, 0u, 0u};
+        }
         const int rr = p * RPP + tid / TPR;
         const int64_t m = m0 + rr;
         if (m >= a.M || n >= a.N) continue;
-        *reinterpret_cast<uint4*>((u16*)a.y + m * a.ldy + n) =
-            *reinterpret_cast<const uint4*>(Cb + rr * LDB + cc);
+        uint4 o = *reinterpret_cast<const uint4*>(Cb + rr * LDB + cc);
+        if (rmask) {  // keep each bf16 half where its aux half is > 0: sign clear, 0 < |x| <= inf
+          auto pos = [](uint32_t h) { return (h & 0x8000u) == 0 && (h & 0x7fffu) != 0 && (h & 0x7fffu) <= 0x7f80u; };
+          auto keep = [&](uint32_t y, uint32_t x) {
+            return y & ((pos(x & 0xffffu) ? 0x0000ffffu : 0u) | (pos(x >> 16) ? 0xffff0000u : 0u));
+          };
+          o.x = keep(o.x, am[p].x);
+          o.y = keep(o.y, am[p].y);
+          o.z = keep(o.z, am[p].z);
+          o.w = keep(o.w, am[p].w);
+        }
+        *reinterpret_cast<uint4*>((u16*)a.y + m * a.ldy + n) = o;
       }
       epi_barrier();
       return;

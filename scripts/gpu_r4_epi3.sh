@@ -1,4 +1,4 @@
-# bf16 whole-tile epilogue of the k=1 GEMMs: kernel tests, k=1 projections alone under ablib (HEAD) and the
+# bf16 whole-tile epilogue of the k=1 GEMMs (+ ReLU-mask): kernel tests, k=1 projections alone under ablib (HEAD) and the
 # working build, then step A/B (3 rounds)
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out/epi3
 o=gpurun_out/epi3

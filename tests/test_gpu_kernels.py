@@ -365,6 +365,44 @@ def test_conv_gemm_bf16(B, T, cin, cout, k):
     close(db2, dy.float().sum(0) + 1, 1e-5)
 
 
+@pytest.mark.parametrize("B,T,cin,cout", [(48, 512, 256, 768), (48, 512, 256, 1024), (7, 130, 256, 256),
+                                          (3, 50, 1024, 256)])
+def test_conv_gemm_k1_bf16_epilogue(B, T, cin, cout):
+    """The k = 1 GEMMs' bf16 whole-tile epilogue (bias / ReLU in the accumulator layout, ReLU
+    mask on the bf16 row vectors) bitwise against the general epilogue of the tap-walking build
+    (FS2_TUNE_NT_K1 = -1), with and without utterance lengths; aux values include zeros,
+    negative zeros, infinities and NaN (a NaN aux masks, as NaN > 0 is false)."""
+    x = bf(rnd(B * T, cin, seed=91))
+    w = bf(rnd(cout, cin, scale=1 / math.sqrt(cin), seed=92))
+    b = rnd(cout, seed=93)
+    aux = bf(rnd(B * T, cout, seed=94))
+    aux[::7, ::5] = 0.0
+    aux[::11, ::3] = -0.0
+    aux[5, :8] = float("inf")
+    aux[6, :8] = float("-inf")
+    aux[7, :8] = float("nan")
+    lens = torch.tensor([max(1, T - 37 * i) for i in range(B)], device=DEV)
+    res = {}
+    try:
+        for knob in (0, -1):
+            K.lib.fs2_set_tuning(13, knob)  # FS2_TUNE_NT_K1
+            res[knob] = [
+                K.conv_gemm(x, w, B * T, T, cin, cout, 1, 0, bias=b, out_dtype=torch.bfloat16),
+                K.conv_gemm(x, w, B * T, T, cin, cout, 1, 0, bias=b, flags=K.EPI_RELU,
+                            out_dtype=torch.bfloat16, lens=lens),
+                K.conv_gemm(x, w, B * T, T, cin, cout, 1, 0, out_dtype=torch.bfloat16),
+                K.conv_gemm(x, w, B * T, T, cin, cout, 1, 0, flags=K.EPI_RELU_MASK_AUX, aux=aux,
+                            out_dtype=torch.bfloat16),
+                K.conv_gemm(x, w, B * T, T, cin, cout, 1, 0, flags=K.EPI_RELU_MASK_AUX, aux=aux,
+                            out_dtype=torch.bfloat16, lens=lens)]
+    finally:
+        K.lib.fs2_set_tuning(13, 0)
+    for i, (r0, r1) in enumerate(zip(res[0], res[-1])):
+        assert torch.equal(r0, r1), i
+    ref = (x.float() @ w.float().t() + b).to(torch.bfloat16)
+    close(res[0][0].float(), ref.float(), 8e-3)
+
+
 @pytest.mark.parametrize("knob", [0, 1, -1, 2])  # FS2_TUNE_ATTN: kernel variants (fs2hip.h)
 @pytest.mark.parametrize("B,T,lens", [(2, 64, [64, 40]), (3, 130, [130, 77, 1]),
                                       (2, 512, [512, 300]), (3, 300, [300, 129, 64])])

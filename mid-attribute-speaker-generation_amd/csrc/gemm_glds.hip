@@ -383,7 +383,7 @@ FS2_DEV void nt_epilogue(const GldsArgs& a, f32x4 (&acc)[BM / WM / 16][BN / WN /
     }
   }
   if (skip && (a.flags & FS2_EPI_SKIP_NOSTORE)) return;  // block-uniform
-  if constexpr (BF16D && !VOC && SROW == 0) {
+  if constexpr (BF16D && !VOC) {
     // bf16 output with a column-only epilogue (bias, ReLU): applied in the accumulator layout
     // (the bias of a lane's column is one value per 16-column fragment), rounded to bf16 and
     // written to LDS as ONE whole tile -- half the LDS bytes of the fp32 half-tile passes and a
@@ -427,7 +427,12 @@ FS2_DEV void nt_epilogue(const GldsArgs& a, f32x4 (&acc)[BM / WM / 16][BN / WN /
             float v = acc[i][j][r];
             if (bias) v += bj[j];
             if (relu) v = fmaxf(v, 0.f);
-            Cb[(wm * WR + i * 16 + 4 * g + r) * LDB + wn * (BN / WN) + j * 16 + r16] = fbv(v);
+            // output row of accumulator (i, 4g + r): SROW > 0 (conv_gemm_tapreg) holds rows
+            // i % SROW + SROW * m of the wave's band i / SROW (see below)
+            const int row = SROW > 0 ? wm * WR + (i / (SROW > 0 ? SROW : 1)) * 16 * SROW +
+                                           i % (SROW > 0 ? SROW : 1) + SROW * (4 * g + r)
+                                     : wm * WR + i * 16 + 4 * g + r;
+            Cb[row * LDB + wn * (BN / WN) + j * 16 + r16] = fbv(v);
           }
       epi_barrier();
 #pragma unroll
@@ -1395,7 +1400,7 @@ __global__ __launch_bounds__(WGM * WGN * 64, MINB) void conv_gemm_tapreg(GldsArg
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
   }
-  nt_epilogue<BM, BN, false, NW, WGN, WGM, S>(a, acc, smem, m0, n0, skip, tid, wm, wn, g, r16);
+  nt_epilogue<BM, BN, false, NW, WGN, WGM, S, true>(a, acc, smem, m0, n0, skip, tid, wm, wn, g, r16);
 }
 
 // ------------------------------------------------------------------------ weight gradient

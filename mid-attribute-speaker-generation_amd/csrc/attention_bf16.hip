@@ -141,6 +141,28 @@ FS2_DEV void store4_bf16(u16* p, const f32x4& v) {
   w.y = (uint32_t)f2bf(v.z) | ((uint32_t)f2bf(v.w) << 16);
   *reinterpret_cast<uint2*>(p) = w;
 }
+
+// The values of output fragments 2d (columns 32d + 4g .. + 3 of the lane's row) and 2d + 1
+// (columns 32d + 16 + 4g .. + 3) stored as ONE 16-B vector per lane instead of two 8-B ones:
+// v_permlane16_swap exchanges them between the 16-lane rows g and g ^ 1 (same row of the
+// output), so even rows g store columns 32d + 4g .. + 7 and odd rows 32d + 16 + 4(g - 1) .. + 7.
+// Half the store instructions of an issue-bound store tail (the guide's T21, for 16-lane rows);
+// same bytes, same values.  p = the row's column 32d; both lanes of a pair must be active.
+FS2_DEV void store8x2_bf16(u16* p, const f32x4& a, const f32x4& b, int g) {
+  const uint32_t a0 = (uint32_t)f2bf(a.x) | ((uint32_t)f2bf(a.y) << 16);
+  const uint32_t a1 = (uint32_t)f2bf(a.z) | ((uint32_t)f2bf(a.w) << 16);
+  const uint32_t b0 = (uint32_t)f2bf(b.x) | ((uint32_t)f2bf(b.y) << 16);
+  const uint32_t b1 = (uint32_t)f2bf(b.z) | ((uint32_t)f2bf(b.w) << 16);
+  const auto s0 = __builtin_amdgcn_permlane16_swap(a0, b0, false, false);
+  const auto s1 = __builtin_amdgcn_permlane16_swap(a1, b1, false, false);
+  const bool odd = g & 1;
+  uint4 o;
+  o.x = odd ? s0[0] : a0;
+  o.y = odd ? s1[0] : a1;
+  o.z = odd ? b0 : s0[1];
+  o.w = odd ? b1 : s1[1];
+  *reinterpret_cast<uint4*>(p + 4 * g + (odd ? 12 : 0)) = o;
+}
 }  // namespace
 
 
@@ -997,8 +1019,8 @@ __global__ __launch_bounds__(256, STAGES == 2 ? 2 : 1) void attn_fwd_dma(
     if (q < T) {
       const float inv = 1.f / l_run[gq];
 #pragma unroll
-      for (int ds = 0; ds < 8; ++ds)
-        store4_bf16(obase + (int64_t)q * ldo + 16 * ds + 4 * g, oacc[gq][ds] * inv);
+      for (int d = 0; d < 4; ++d)
+        store8x2_bf16(obase + (int64_t)q * ldo + 32 * d, oacc[gq][2 * d] * inv, oacc[gq][2 * d + 1] * inv, g);
       if (g == 0) lse[(int64_t)bh * T + q] = (m_run[gq] + __log2f(l_run[gq])) * 0.6931471805599453f;
     }
   }
@@ -1118,8 +1140,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_dma(
     const int q = q0 + wave * 32 + gq * 16 + r16;
     if (q < T) {
 #pragma unroll
-      for (int ds = 0; ds < 8; ++ds)
-        store4_bf16(dbase + (int64_t)q * ld + 16 * ds + 4 * g, dq[gq][ds] * scale);
+      for (int d = 0; d < 4; ++d)
+        store8x2_bf16(dbase + (int64_t)q * ld + 32 * d, dq[gq][2 * d] * scale, dq[gq][2 * d + 1] * scale, g);
     }
   }
 }
@@ -1226,9 +1248,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_dma(
   }
   if (key < T) {
 #pragma unroll
-    for (int ds = 0; ds < 8; ++ds) {
-      store4_bf16(dk_base + (int64_t)key * ld + 16 * ds + 4 * g, dk[ds] * scale);
-      store4_bf16(dv_base + (int64_t)key * ld + 16 * ds + 4 * g, dv[ds]);
+    for (int d = 0; d < 4; ++d) {
+      store8x2_bf16(dk_base + (int64_t)key * ld + 32 * d, dk[2 * d] * scale, dk[2 * d + 1] * scale, g);
+      store8x2_bf16(dv_base + (int64_t)key * ld + 32 * d, dv[2 * d], dv[2 * d + 1], g);
     }
   }
 }

@@ -251,7 +251,8 @@ __global__ __launch_bounds__(256) void attn_fwd_bf16_g1(const u16* __restrict__ 
   if (q < T) {
     const float inv = 1.f / l_run;
 #pragma unroll
-    for (int ds = 0; ds < 8; ++ds) store4_bf16(obase + (int64_t)q * ldo + 16 * ds + 4 * g, oacc[ds] * inv);
+    for (int d = 0; d < 4; ++d)
+      store8x2_bf16(obase + (int64_t)q * ldo + 32 * d, oacc[2 * d] * inv, oacc[2 * d + 1] * inv, g);
     if (g == 0) lse[(int64_t)bh * T + q] = m_run + __logf(l_run);
   }
 }
@@ -345,7 +346,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_bf16_g1(const u16* __restrict
   }
   if (q < T) {
 #pragma unroll
-    for (int ds = 0; ds < 8; ++ds) store4_bf16(dbase + (int64_t)q * ld + 16 * ds + 4 * g, dq[ds] * scale);
+    for (int d = 0; d < 4; ++d)
+      store8x2_bf16(dbase + (int64_t)q * ld + 32 * d, dq[2 * d] * scale, dq[2 * d + 1] * scale, g);
   }
 }
 
@@ -438,9 +440,9 @@ __global__ __launch_bounds__(256, MINB) void attn_bwd_dkdv_bf16_g1(const u16* __
   }
   if (key < T) {
 #pragma unroll
-    for (int ds = 0; ds < 8; ++ds) {
-      store4_bf16(dk_base + (int64_t)key * ld + 16 * ds + 4 * g, dk[ds] * scale);
-      store4_bf16(dv_base + (int64_t)key * ld + 16 * ds + 4 * g, dv[ds]);
+    for (int d = 0; d < 4; ++d) {
+      store8x2_bf16(dk_base + (int64_t)key * ld + 32 * d, dk[2 * d] * scale, dk[2 * d + 1] * scale, g);
+      store8x2_bf16(dv_base + (int64_t)key * ld + 32 * d, dv[2 * d], dv[2 * d + 1], g);
     }
   }
 }

@@ -10,7 +10,7 @@ for i in 1 2; do
     echo "[${lib:-new}] $(grep -E 'decoder|encoder' $o/a.log | tr '\n' ' ')"
   done
 done
-for round in 1 2 3; do
+for round in 1 2; do
   for spec in "base|FS2HIP_LIB=ablib/libfs2hip_base.so" "new|FS2_X=0"; do
     label=${spec%%|*}; envs=${spec#*|}
     env $envs timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-traffic --no-f32 > $o/b.log 2>&1 || { tail -20 $o/b.log; exit 1; }

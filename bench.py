@@ -439,20 +439,23 @@ def hbm_traffic(timeout=300, kind="conv"):
             files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
             if r.returncode != 0 or not files:
                 return None, f"{ctr} pass failed (rc {r.returncode})"
-            vals = []
+            # per kernel kind: a split-K weight gradient is two launches (partials + the
+            # in-order reduce), so its bytes per call are the sum of the two kinds' means
+            kinds = ({"main": ("conv_gemm_halo", "conv_gemm_tapreg")} if kind == "conv" else
+                     {"main": ("conv_wgrad_band", "conv_wgrad_halo", "conv_wgrad_wide"),
+                      "reduce": ("wgrad_reduce", "wgrad_k1_multi_reduce")})
+            vals = {k: [] for k in kinds}
             for row in csv.DictReader(open(files[0])):
                 kn = row.get("Kernel_Name", "")
-                names = (("conv_gemm_halo", "conv_gemm_tapreg") if kind == "conv" else
-                         ("conv_wgrad_band", "conv_wgrad_halo", "wgrad_reduce"))
-                if any(n in kn for n in names) and row.get("Counter_Name") == ctr:
-                    vals.append(float(row["Counter_Value"]))
-            if not vals:
+                if row.get("Counter_Name") != ctr:
+                    continue
+                for k, names in kinds.items():
+                    if any(n in kn for n in names):
+                        vals[k].append(float(row["Counter_Value"]))
+                        break
+            if not vals["main"]:
                 return None, f"{ctr}: no {kind} dispatches"
-            # a split-K weight gradient is two launches (partials + reduce): bytes per pair
-            per_launch = 2 if kind == "wgrad" and any(
-                "wgrad_reduce" in row.get("Kernel_Name", "") for row in csv.DictReader(open(files[0]))) else 1
-            per[ctr] = float(np.mean(vals)) * per_launch
-            per[ctr] = float(np.mean(vals))
+            per[ctr] = float(sum(np.mean(v) for v in vals.values() if v))
     return (per["FETCH_SIZE"] * 2.0 + per["WRITE_SIZE"]) * 1024.0, per
 
 
@@ -526,6 +529,8 @@ def main():
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC passes")
     ap.add_argument("--no-f32", action="store_true", help="skip the fp32 companion measurement")
+    ap.add_argument("--per-kernel-issue", action="store_true",
+                    help="A/B: issue the FFT blocks kernel by kernel from Python (model.C_BLOCKS off)")
     ap.add_argument("--graph", action="store_true",
                     help="N=1: capture the step once into a HIP graph and replay it (measured "
                          "slower than eager here: replay serialises the weight-gradient stream)")
@@ -563,6 +568,8 @@ def main():
     M = importlib.import_module("mid-attribute-speaker-generation_amd.model")
     K = importlib.import_module("mid-attribute-speaker-generation_amd.kernels")
     TR = importlib.import_module("mid-attribute-speaker-generation_amd.train")
+    if args.per_kernel_issue:
+        M.C_BLOCKS = False
     # FS2_TUNE="knob=value,...": kernel-selection knobs (include/fs2hip.h) for A/B runs
     for kv in filter(None, os.environ.get("FS2_TUNE", "").split(",")):
         knob, val = kv.split("=")
@@ -614,16 +621,26 @@ def main():
     kw = (lambda: clf_kw()) if args.use_clf else (lambda: {})
     n_warm = max(args.warmup, 2 if use_graph else 0)  # graph: step 1 captures
     survey = 3 if (not args.no_roofline and not use_graph and n_warm >= 4) else 0
+    # The FFT blocks are issued from C (model.C_BLOCKS) in the measured steps; the per-class and
+    # per-op attributions need a Python-side event around every kernel, so their steps run the
+    # per-kernel host path: the same kernels in the same order (bitwise the same step,
+    # tests/test_gpu_parity.py::test_c_blocks_step_bitwise), only the host issue differs.
+    c_blocks = M.C_BLOCKS
     for i in range(n_warm):
         if survey and i == n_warm - survey:
+            M.C_BLOCKS = False
             timer.reset("all", 600 * survey)  # class survey: the last warm-up steps
         trainer.step(batch, **kw())
+    M.C_BLOCKS = c_blocks
     torch.cuda.synchronize()
     classes, dom = None, None
     if survey:
         classes = timer.table(survey, PEAK[args.dtype][0])
         dom = max(classes, key=lambda c: classes[c]["ms_per_step"])
-        timer.reset(dom, 200 * args.steps)  # timed region: the dominant class only
+        timer.mode = None
+        for _ in range(2):  # settle after the instrumented steps
+            trainer.step(batch, **kw())
+        torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
@@ -633,7 +650,18 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    timed = timer.table(args.steps, PEAK[args.dtype][0]) if dom else None
+    timed = None
+    if dom:
+        # the dominant class alone, its launches between HIP events, over as many further steps
+        # on the per-kernel host path
+        n_dom = min(args.steps, 10)
+        M.C_BLOCKS = False
+        timer.reset(dom, 200 * n_dom)
+        for _ in range(n_dom):
+            trainer.step(batch, **kw())
+        torch.cuda.synchronize()
+        timed = timer.table(n_dom, PEAK[args.dtype][0])
+        M.C_BLOCKS = c_blocks
     timer.mode = None
     t = torch.tensor([dt], device=dev, dtype=torch.float64)
     fr = torch.tensor([frames_local], device=dev, dtype=torch.float64)
@@ -654,7 +682,7 @@ def main():
                     "frac": c["frac"], "traffic": None,
                     "kernel": f"{dom}: the step's dominant launch set by in-step time "
                               f"({c['launches_per_step']} launches/step, {c['ms_per_step']} ms/step "
-                              "in the timed steps)",
+                              "in steps after the timed region, per-kernel host path)",
                     "flop_basis": "2 * valid frames * C_out * C_in * taps per launch (kernels "
                                   "skip all-padding row tiles)",
                     "per_launch_flop": round(c["gflop_per_step"] * 1e9 / c["launches_per_step"]),
@@ -676,7 +704,9 @@ def main():
             roof["classes"] = classes
             roof["classes_basis"] = ("every class timed in the last 3 warm-up steps (events on "
                                      "~170 launches make those steps host-bound); the dominant "
-                                     "class alone is timed over the timed steps")
+                                     "class alone over up to 10 steps after the timed region; "
+                                     "both on the per-kernel host path (model.C_BLOCKS off: the "
+                                     "same kernels, issued one by one from Python)")
         step_roof = {"gflop_padded": STEP_GFLOP_PADDED, "achieved": None, "frac": None}
         if args.batch == 48 and args.src_len == 128 and not args.use_clf:
             ach = STEP_GFLOP_PADDED / (ms_step / 1e3) / 1e3
@@ -696,6 +726,8 @@ def main():
                           "parallelism": f"dp{world}",
                           "use_clf": bool(args.use_clf),
                           "execution": "hip-graph replay" if use_graph else "eager",
+                          "host_issue": ("one C-ABI call per FFT block (fs2_fft_block_fwd / _bwd)"
+                                         if M.C_BLOCKS else "one C-ABI call per kernel"),
                           **({"data_parallel": "one-rank RCCL group (FS2_DP1)"} if dp1 else {})},
                "roofline": roof, "step_roofline": step_roof}
 
@@ -731,8 +763,10 @@ def main():
                      {T_m: float((mel ** 2).sum()), T_s: float((src ** 2).sum())})
         ot.install()
         bt.ops, bt.ev, bt.on = ot, [], True
+        M.C_BLOCKS = False  # every kernel call between events: the per-kernel host path
         for _ in range(3):
             trainer.step(batch)
+        M.C_BLOCKS = c_blocks
         bt.on, bt.ops = False, None
         for n, fn in ot._orig.items():
             setattr(K, n, fn)

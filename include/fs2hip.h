@@ -280,6 +280,10 @@ int fs2_weight_prep_batch(int dtype, const int64_t* jobs, int n_jobs, int64_t n_
  *   FS2_TUNE_ATTN_XCD      LDS-DMA attention kernels: 0 = the blocks of one (utterance, head) on
  *                          one XCD (K / V reuse in its L2; default), -1 = the launch grid's order
  *   FS2_TUNE_WGRAD_K1M_STAGES  grouped k = 1 weight gradient LDS ring: 0 = 4 slots, 2 / 3 slots
+ *   FS2_TUNE_WGRAD_WIDE    weight gradient of Conv1d taps 3/5/9 (T % 64 == 0) on the wide-tile
+ *                          kernel (64 x 64 x taps tiles, row splits to ~256 blocks): 0 = where a
+ *                          channel count is not a 64-multiple (default), 1 = wherever eligible,
+ *                          -1 = off (band / split-K halo kernels), n > 1 = everywhere, n splits
  * Process-wide; query workspace sizes after setting.                                 */
 enum { FS2_TUNE_GEMM_STAGES = 0, FS2_TUNE_WGRAD_STAGES = 1, FS2_TUNE_WGRAD_TILE = 2,
        FS2_TUNE_WGRAD_SPLITS = 3, FS2_TUNE_LEGACY_GEMM = 4, FS2_TUNE_NT_GROUP = 5,
@@ -287,14 +291,73 @@ enum { FS2_TUNE_GEMM_STAGES = 0, FS2_TUNE_WGRAD_STAGES = 1, FS2_TUNE_WGRAD_TILE 
        FS2_TUNE_ATTN = 9, FS2_TUNE_NT_TILE = 10, FS2_TUNE_LN_TILE = 11, FS2_TUNE_WGRAD_K1 = 12,
        FS2_TUNE_NT_K1 = 13, FS2_TUNE_ATTN_DMA = 14, FS2_TUNE_TAPREG = 15,
        FS2_TUNE_WGRAD_BAND = 16, FS2_TUNE_ATTN_XCD = 17, FS2_TUNE_WGRAD_K1M_STAGES = 18,
-       FS2_TUNE_COUNT = 19 };
+       FS2_TUNE_WGRAD_WIDE = 19, FS2_TUNE_COUNT = 20 };
 int fs2_set_tuning(int knob, int value);
+
+/* ---------------------------------------------------------------- one FFT block per call
+ * transformer/Layers.py:21-30 (FFTBlock.forward: MultiHeadAttention SubLayers.py:29-57, then
+ * PositionwiseFeedForward SubLayers.py:85-93, post-LN, padded rows masked) and its backward,
+ * bf16, issued from C: the same entry points in the same order as the per-kernel host path
+ * (model.FFTBlock.fwd / bwd), so the results are bitwise those.  `blk` is a host int64 table of
+ * FS2_FB_WORDS words (pointers as integers): geometry, the bf16 compute-layout weights
+ * (fs2_conv_weight_prep: QKV fused as one (3 h d_k, d) Linear), the fp32 biases / LayerNorm
+ * affines, and the fp32 gradient buffers they accumulate into.                               */
+enum { FS2_FB_D = 0, FS2_FB_HEADS, FS2_FB_DK, FS2_FB_DINNER, FS2_FB_TAPS, FS2_FB_PAD, FS2_FB_SITE,
+       FS2_FB_WQKV_F, FS2_FB_WQKV_B, FS2_FB_BQKV, FS2_FB_WFC_F, FS2_FB_WFC_B, FS2_FB_BFC,
+       FS2_FB_W1_F, FS2_FB_W1_B, FS2_FB_B1, FS2_FB_W2_F, FS2_FB_W2_B, FS2_FB_B2,
+       FS2_FB_LN1_G, FS2_FB_LN1_B, FS2_FB_LN2_G, FS2_FB_LN2_B,
+       FS2_FB_GQKV_W, FS2_FB_GQKV_B, FS2_FB_GFC_W, FS2_FB_GFC_B, FS2_FB_G1_W, FS2_FB_G1_B,
+       FS2_FB_G2_W, FS2_FB_G2_B, FS2_FB_GLN1_G, FS2_FB_GLN1_B, FS2_FB_GLN2_G, FS2_FB_GLN2_B,
+       FS2_FB_WORDS };
+enum { FS2_FA_X2 = 0, FS2_FA_X2_T = 1 };
+/* Forward: x (rows, d) fp32 residual stream and its bf16 copy x_t -> the activation region
+ * `act` (fs2_fft_block_act_bytes; saved for the backward) whose FS2_FA_X2 / FS2_FA_X2_T
+ * tensors (byte offsets: fs2_fft_block_act_offset) are the block output and its copy.
+ * fuse_ln: the post-LNs in the fc / w_2 GEMM epilogues (fs2_conv_gemm_ln).  p: dropout rate
+ * (0 = off), seed device int64[1].                                                          */
+int64_t fs2_fft_block_act_bytes(const int64_t* blk, int64_t rows, int64_t batch, int64_t seq_len,
+                                int fuse_ln);
+int64_t fs2_fft_block_act_offset(const int64_t* blk, int64_t rows, int64_t batch,
+                                 int64_t seq_len, int fuse_ln, int which);
+int fs2_fft_block_fwd(const int64_t* blk, const float* x, const void* x_t, void* act, int64_t rows,
+                      int64_t batch, int64_t seq_len, const int64_t* lens, float p,
+                      const uint64_t* seed, int fuse_ln, void* stream);
+/* Backward from dx2 (the output gradient) or from (carry_dy2_t, carry_dx1), the block's LN2
+ * backward already done by the following block.  dx (rows, d) fp32: the input gradient, or,
+ * with prev_blk (the block before this one, its act region), that block's LN2 backward runs in
+ * this block's QKV data-gradient epilogue (fs2_conv_gemm_ln_bwd) and writes prev_dy2_t (bf16)
+ * / prev_dx1 (fp32) -- its carry -- instead (dx is then scratch).  tmp: fs2_fft_block_tmp_bytes.
+ * The weight gradients run on side_stream (NULL: stream) with side_ws
+ * (>= fs2_fft_block_side_ws_bytes); act, tmp and the carry buffers are read there after the
+ * call returns: keep them until that stream is joined.                                      */
+int64_t fs2_fft_block_tmp_bytes(const int64_t* blk, int64_t rows, int64_t batch, int64_t seq_len);
+int64_t fs2_fft_block_side_ws_bytes(const int64_t* blk, int64_t rows);
+int fs2_fft_block_bwd(const int64_t* blk, void* act, const void* x_t, int fuse_ln, float p,
+                      const float* dx2, const void* carry_dy2_t, float* carry_dx1,
+                      const int64_t* prev_blk, void* prev_act, int prev_fuse_ln, float prev_p,
+                      void* tmp, float* dx, void* prev_dy2_t, float* prev_dx1, int64_t rows,
+                      int64_t batch, int64_t seq_len, const int64_t* lens, const uint64_t* seed,
+                      float* side_ws, int64_t side_ws_bytes, void* stream, void* side_stream);
+
+/* Stand-in for one gradient all-reduce of the data-parallel step, for pricing the collective
+ * schedule at N ranks on one GPU (train.CollectiveModel; not on the training path):
+ * `blocks` workgroups read and write back `bytes` of buf[0..n) (values unchanged), paced to
+ * last duration_ns -- a ring all-reduce's CU occupancy, HBM traffic and duration without the
+ * interconnect.  Replaces no reference code (the reference's only collective is
+ * nn.DataParallel, train.py:67-68). */
+int fs2_collective_standin(float* buf, int64_t n, int64_t bytes, int blocks, int64_t duration_ns,
+                           void* stream);
 
 /* Weight (and optionally bias) gradient, accumulated into the fp32 master-gradient layout:
  *   dw[o, c, j] += sum_r dy[r, o] * x[r + j - pad, c]
  *   db[o]       += sum_r dy[r, o]                          (db may be NULL)
- * Split-K over rows with per-split fp32 slabs in `ws` and an in-order reduction
- * (bitwise reproducible).  `ws_bytes` >= fs2_conv_wgrad_ws_bytes(...).
+ * bf16, taps 3 / 5 / 9, T % 64 == 0: 64 x 64 x taps output tiles shared by 8 waves, the rows
+ * split into ~256 / tiles ranges whose fp32 slabs in `ws` are summed in split order; other
+ * shapes: split-K slabs with an in-order reduction.  Bitwise reproducible for the same inputs
+ * AND the same lens: with lens, 64-row bands / k-tiles made only of rows past each length
+ * are skipped, which changes which split sums which rows (results then agree to fp32
+ * rounding with the lens-free call on zero padding rows, not bitwise).
+ * `ws_bytes` >= fs2_conv_wgrad_ws_bytes(...).
  * Replaces the weight/bias half of ConvolutionBackward / AddmmBackward.                */
 int64_t fs2_conv_wgrad_ws_bytes(int64_t rows, int64_t c_in, int64_t c_out, int taps);
 int fs2_conv_wgrad(int dtype, const void* dy, int64_t ldy, const void* x, int64_t ldx, float* dw,

@@ -85,9 +85,16 @@ int conv_wgrad_glds_launch(const void* dy, int64_t ldy, const void* x, int64_t l
                            float* db, int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out,
                            int taps, int pad, const int64_t* lens, int splits, int tile, float* ws,
                            hipStream_t st);
+// returned by a launcher whose kernel does not apply to the shape (the caller tries the next
+// one); distinct from every FS2_ERR_* status, so an argument error is never taken for it
+constexpr int kNotEligible = 1;
 int conv_wgrad_band_launch(const void* dy, int64_t ldy, const void* x, int64_t ldx, float* dw,
                            float* db, int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out,
                            int taps, int pad, const int64_t* lens, hipStream_t st);
+int conv_wgrad_wide_launch(const void* dy, int64_t ldy, const void* x, int64_t ldx, float* dw,
+                           float* db, int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out,
+                           int taps, int pad, const int64_t* lens, float* ws, hipStream_t st);
+int64_t conv_wgrad_wide_ws_floats(int64_t rows, int64_t c_in, int64_t c_out, int taps);
 int64_t wgrad_k1_multi_ws_floats(const int64_t* jobs, int n, int64_t rows);
 int wgrad_k1_multi_launch(const int64_t* jobs, int n, int64_t rows, int64_t seq_len,
                           const int64_t* lens, float* ws, hipStream_t st);

@@ -537,6 +537,8 @@ int64_t fs2_conv_wgrad_ws_bytes(int64_t rows, int64_t c_in, int64_t c_out, int t
   const int64_t bias_part = S * c_out > ((rows + CS_ROWS - 1) / CS_ROWS) * c_out
                                 ? S * c_out : ((rows + CS_ROWS - 1) / CS_ROWS) * c_out;
   int64_t b = (S * c_out * taps * c_in + bias_part) * 4;
+  const int64_t wide = conv_wgrad_wide_ws_floats(rows, c_in, c_out, taps) * 4;  // wgrad.hip
+  b = wide > b ? wide : b;
   if (taps == 1) {  // bf16 k = 1: the grouped kernel with one job (wgrad.hip)
     const int64_t job[8] = {0, c_out, 0, c_in, 0, 1, c_in, c_out};
     const int64_t m = wgrad_k1_multi_ws_floats(job, 1, rows) * 4;
@@ -561,6 +563,9 @@ int fs2_conv_wgrad(int dtype, const void* dy, int64_t ldy, const void* x, int64_
                         ((uintptr_t)dy & 15) == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)dw & 15) == 0,
                     "fs2_conv_wgrad(bf16, k = 1): channel counts / strides must be multiples of 8, "
                     "operands and dw 16-B aligned");
+      // the kernel reads lens[row / seq_len] to skip all-padding k-tiles
+      FS2_CHECK_ARG(lens == nullptr || (seq_len > 0 && rows % seq_len == 0),
+                    "fs2_conv_wgrad(bf16, k = 1): with lens, rows must be batch x seq_len");
       return wgrad_k1_multi_launch(job, 1, rows, seq_len, lens, ws, as_stream(stream));
     }
     if (!g_tune[FS2_TUNE_LEGACY_GEMM])

@@ -1973,10 +1973,16 @@ int conv_wgrad_glds_launch(const void* dy, int64_t ldy, const void* x, int64_t l
               (int)c_out, taps, pad, (int)Kp, rps, (int)((c_out + tile - 1) / tile),
               (int)((Kp + tile - 1) / tile), splits, lens};
   if (taps > 1 && g_tune[FS2_TUNE_WGRAD_HALO] == 0) {
+    // 64 x 64 x taps tiles shared by eight waves (conv_wgrad_wide, wgrad.hip)
+    const int rcw = conv_wgrad_wide_launch(dy, ldy, x, ldx, dw, db, rows, seq_len, c_in, c_out,
+                                           taps, pad, lens, ws, st);
+    if (rcw != kNotEligible) return rcw;
+  }
+  if (taps > 1 && g_tune[FS2_TUNE_WGRAD_HALO] == 0) {
     // no split slabs where the output tiles fill the chip (conv_wgrad_band, wgrad.hip)
     const int rc = conv_wgrad_band_launch(dy, ldy, x, ldx, dw, db, rows, seq_len, c_in, c_out,
                                           taps, pad, lens, st);
-    if (rc != -1) return rc;
+    if (rc != kNotEligible) return rc;
   }
   const bool halo = taps >= 2 && taps <= 9 && (taps == 3 || taps == 5 || taps == 9) &&
                     c_in % 64 == 0 && c_out % 64 == 0 && seq_len % 64 == 0 &&

@@ -33,6 +33,8 @@
 // utterance's length (lens given) are staged from the zero line, and bands made only of them
 // are not visited.  The bias gradient rides on the dy fragments of the blocks of the first c
 // tile (an MFMA against a ones fragment).
+#include <type_traits>
+
 #include "common.hpp"
 
 namespace fs2 {
@@ -333,31 +335,370 @@ __global__ __launch_bounds__(64 * W, W == 8 ? 1 : 2) void conv_wgrad_band(WgradB
   }
 }
 
-// -1: not eligible (the caller uses the split-K kernels)
+// ---------------------------------------------------------------- wide-tile weight gradient
+// conv_wgrad_wide: the same product on 64 (o) x 64 (c) x taps output tiles, the rows split Z
+// ways (Z ~ 256 / tiles) into fp32 slabs summed in split order by one reduce launch.
+//
+// Why: the band kernel's 32 x 32 tile re-streams every dy column block 8 times and every x column
+// block 32 times (684 MB through L2 -> LDS per decoder launch against 63 MB of operands), and
+// every one of its waves stages its own operands, so each SIMD's one wave pays 9 LDS-DMA
+// instructions and 48 transposed reads per 72 MFMAs with nothing to hide their latency.  A
+// 64 x 64 tile halves the staged bytes per MAC (dy 64 + x 72 positions of 128 B per 64-row band
+// for 64 x 64 x taps outputs), and the block's eight waves SHARE each staged band: wave (wo, wc)
+// owns o 32 wo .. + 31 x c 16 wc .. + 15 x all taps (18 accumulator fragments, ~120 VGPRs: two
+// waves per SIMD), the 17 LDS-DMA pieces of a band are spread over the waves, and one barrier
+// per band guards a ST-slot ring (17 KB per slot).  The tap-register reduction order of the
+// band kernel is kept: step s (s < 2) of a band reduces its rows s + 2 m, tap j of step s needs
+// halo fragment F[s + j], and each F[f] is read from LDS once for every (s, j) with s + j = f.
+// Per wave and band: 4 dy fragments + 10 x fragments (28 transposed reads) for 36 MFMAs.
+//
+// Rows: bands of 64 rows inside one utterance (T % 64 == 0); bands made only of rows past an
+// utterance's length (lens given) are not visited; split z takes the list's bands
+// [z nb / Z, (z + 1) nb / Z) in row order.  Within a block the sum runs over bands in order and
+// over the two steps of a band in order; the slabs are summed in split order: bitwise
+// reproducible for a given lens.  The bias gradient rides on the dy fragments of the waves with
+// wc == 0 in the blocks of the first c tile (MFMA against a ones fragment).  Z == 1 adds the
+// tile straight into dw / db.
+constexpr int WIDE_MAXB = 2048;  // bands (of 64 rows) listed in LDS when lens are given
+struct WgradWide {
+  const u16* dy;
+  int64_t ldy;
+  const u16* x;
+  int64_t ldx;
+  float* dw;
+  float* db;
+  float* slab;   // [Z][Cout][Cin taps] (Z > 1)
+  float* bslab;  // [Z][Cout] (Z > 1, db given)
+  int64_t M, T;
+  int Cin, Cout, pad;
+  int tiles_o, tiles_c, Z;
+  const int64_t* lens;
+};
+
+namespace {
+template <int N, typename Fn>
+FS2_DEV void ww_static_for(Fn&& fn) {
+  if constexpr (N > 0) {
+    ww_static_for<N - 1>(fn);
+    fn(std::integral_constant<int, N - 1>{});
+  }
+}
+// ds_read_b64_tr_b16 at a per-lane base + a compile-time byte offset (the instruction's
+// 16-bit immediate): every fragment address of the main loop is one of a few per-lane bases
+template <int OFF>
+FS2_DEV s16x4w ww_tr(uint32_t base) {
+  static_assert(OFF >= 0 && OFF < 65536, "ds offset field");
+  s16x4w r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(base), "n"(OFF));
+  return r;
+}
+}  // namespace
+
+template <int TAPS, int ST>
+__global__ __launch_bounds__(512, 4) void conv_wgrad_wide(WgradWide a) {
+  constexpr int BO = 64, BC = 64, S = 2, BR = 64, NT = 512;
+  constexpr int HR = BR + TAPS - 1, RS = (HR + 1) / 2, NF = S + TAPS - 1;
+  constexpr int PB = 128;                                // bytes per image position (64 bf16)
+  constexpr int DPOS = BR, XPOS = (2 * RS + 7) / 8 * 8;  // image positions
+  constexpr int NPD = DPOS / 8, NPX = XPOS / 8, NP = NPD + NPX;  // 1-KB LDS-DMA pieces per band
+  static_assert(NP > 8 && NP <= 24, "piece bookkeeping: 2 or 3 pieces per wave");
+  constexpr int STAGE_B = (DPOS + XPOS) * PB;
+  constexpr int RING_B = ST * STAGE_B;
+  static_assert(RING_B < 65536, "fragment offsets fit the ds immediate");
+  constexpr int QLD = BC * TAPS + 4;  // fp32 row stride of a 16-row epilogue slice
+  constexpr int EPI_B = 16 * QLD * 4 > 64 * 68 * 4 ? 16 * QLD * 4 : 64 * 68 * 4;
+  constexpr int SMEM_B = RING_B > EPI_B ? RING_B : EPI_B;
+  constexpr int MAXB = WIDE_MAXB;
+  constexpr int LOOK = 1;
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[SMEM_B + 4 * MAXB + 64];
+  short* blist = reinterpret_cast<short*>(smem + SMEM_B);          // band index
+  short* brem = reinterpret_cast<short*>(smem + SMEM_B + 2 * MAXB);  // its rows below the length
+  int* wcnt = reinterpret_cast<int*>(smem + SMEM_B + 4 * MAXB);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wo = wave >> 2, wc = wave & 3;
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3, r16 = lane & 15;
+
+  // block -> (split, o tile, c tile): XCD-contiguous runs, c fastest, then o, then split (an
+  // XCD's blocks share the rows of one split)
+  // (the bias gradient: Z * ceil(Cout / 64) further blocks after the tiles, see below)
+  const int nmain = a.tiles_o * a.tiles_c * a.Z;
+  const int nwg = nmain + (a.db != nullptr ? a.Z * a.tiles_o : 0);
+  const int orig = blockIdx.x, xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const bool bias_blk = wg >= nmain;  // block-uniform
+  const int wb = wg - nmain;
+  const int tc = bias_blk ? 0 : wg % a.tiles_c, t2 = bias_blk ? 0 : wg / a.tiles_c;
+  const int to = bias_blk ? wb % a.tiles_o : t2 % a.tiles_o;
+  const int z = bias_blk ? wb / a.tiles_o : t2 / a.tiles_o;
+  const int o0 = to * BO, c0 = tc * BC;
+
+  // bands holding a real row, in row order, with the count of their rows below the length
+  // (the launcher admits lens only with nb_all <= MAXB).  Kept in LDS: a global load of lens in
+  // the main loop would make the compiler wait vmcnt(0), draining the LDS-DMA ring every band.
+  const int nbu = (int)(a.T / BR);
+  const int nb_all = (int)(a.M / BR);
+  const bool use_list = a.lens != nullptr;
+  int nb = nb_all;
+  if (use_list) {
+    int total = 0;
+    for (int k0 = 0; k0 < nb_all; k0 += NT) {
+      const int k = k0 + tid;
+      bool v = false;
+      int rem = 0;
+      if (k < nb_all) {
+        const int b = k / nbu;
+        const int64_t r = a.lens[b] - (int64_t)(k - b * nbu) * BR;
+        v = r > 0;
+        rem = r < BR ? (int)r : BR;
+      }
+      const uint64_t mask = __ballot(v);
+      if (lane == 0) wcnt[wave] = __popcll(mask);
+      __syncthreads();
+      int before = total;
+      for (int w = 0; w < wave; ++w) before += wcnt[w];
+      const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
+      if (v) {
+        blist[before + below] = (short)k;
+        brem[before + below] = (short)rem;
+      }
+      for (int w = 0; w < 8; ++w) total += wcnt[w];
+      __syncthreads();
+    }
+    nb = total;
+  }
+  const int kb0 = (int)((int64_t)z * nb / a.Z), kb1 = (int)((int64_t)(z + 1) * nb / a.Z);
+  const int nbs = kb1 - kb0;
+
+  if (bias_blk) {
+    // db[o0 .. o0 + 63] over this split's bands: thread (row t / 8, 8 columns) loads one 16-B
+    // row piece per band (rows past the length skipped), then the 64 row partials of each
+    // column are summed in row order through LDS -- kept out of the tile blocks, whose MFMA
+    // bias accumulators would cost the registers that keep them at two waves per SIMD
+    const int rr = tid >> 3, cc = o0 + (tid & 7) * 8;
+    float sum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < nbs; ++i) {
+      const int kk = kb0 + i;
+      const int k = use_list ? (int)blist[kk] : kk;
+      const int rem = use_list ? (int)brem[kk] : BR;
+      const int b = k / nbu, t0 = (k - b * nbu) * BR;
+      if (rr < rem && cc < a.Cout) {
+        const uint4 v = *reinterpret_cast<const uint4*>(a.dy + ((int64_t)b * a.T + t0 + rr) * a.ldy + cc);
+        const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          sum[2 * e] += __uint_as_float(w4[e] << 16);
+          sum[2 * e + 1] += __uint_as_float(w4[e] & 0xffff0000u);
+        }
+      }
+    }
+    float* R = reinterpret_cast<float*>(smem);  // [64 rows][64 + 4 columns]
+#pragma unroll
+    for (int e = 0; e < 8; ++e) R[rr * 68 + (tid & 7) * 8 + e] = sum[e];
+    __syncthreads();
+    if (tid < BO && o0 + tid < a.Cout) {
+      float acc = 0.f;
+      for (int r = 0; r < 64; ++r) acc += R[r * 68 + tid];
+      if (a.Z == 1) a.db[o0 + tid] += acc;
+      else a.bslab[(int64_t)z * a.Cout + o0 + tid] = acc;
+    }
+    return;
+  }
+
+  // position P's 16-B chunks are XOR-swizzled by ((P >> 1) & 3) << 1: any 8 consecutive
+  // positions read as 16-column transposed fragments hit 64 distinct banks per half-wave
+  auto swz = [](int P) { return ((P >> 1) & 3) << 1; };
+  // LDS-DMA through buffer descriptors: dy from row 0, x from row -pad (the halo's first row);
+  // a band's rows ride in the scalar offset, each piece's lanes have a fixed voffset; rows
+  // outside the band's valid range select an out-of-range voffset (zeros)
+  const auto dy_rs = buf_rsrc(a.dy, a.M * a.ldy * 2);
+  const auto x_rs = buf_rsrc(a.x - (int64_t)a.pad * a.ldx, (a.M + a.pad) * a.ldx * 2);
+  const int npw = wave + 16 < NP ? 3 : 2;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) unsigned char*)smem;
+
+  auto issue = [&](int i, int slot) {
+    const int kk = kb0 + i;
+    const int k = __builtin_amdgcn_readfirstlane(use_list ? (int)blist[kk] : kk);
+    const int rem = __builtin_amdgcn_readfirstlane(use_list ? (int)brem[kk] : BR);
+    const int b = k / nbu, t0 = (k - b * nbu) * BR;
+    const int64_t r0 = (int64_t)b * a.T + t0;
+    unsigned char* St = smem + slot * STAGE_B;
+    // the pieces' per-lane rows / offsets are recomputed here (a few VALU) rather than held
+    // across the loop: an opaque copy of the lane id keeps the compiler from hoisting them
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const int lpos = ln >> 3, lch = ln & 7;
+#pragma unroll
+    for (int kp = 0; kp < 3; ++kp) {
+      if (kp == 2 && npw < 3) break;
+      const int pi = wave + 8 * kp;
+      if (pi < NPD) {
+        const int P = pi * 8 + lpos;
+        const int h = (P & 31) * 2 + (P >> 5);
+        const int col = o0 + ((lch ^ swz(P)) << 3);
+        const bool ok = col < a.Cout && h < rem;
+        glds16_buf(dy_rs, St + pi * 8 * PB, ok ? (uint32_t)((h * a.ldy + col) * 2) : kOOB,
+                   (uint32_t)(r0 * a.ldy * 2));
+      } else {
+        const int P = (pi - NPD) * 8 + lpos;
+        const int h = (P % RS) * 2 + P / RS;
+        const int col = c0 + ((lch ^ swz(P)) << 3);
+        const int t = t0 - a.pad + h;
+        const bool ok = pi < NP && P < 2 * RS && h < HR && col < a.Cin && t >= 0 && t < (int)a.T;
+        glds16_buf(x_rs, St + pi * 8 * PB, ok ? (uint32_t)((h * a.ldx + col) * 2) : kOOB,
+                   (uint32_t)(r0 * a.ldx * 2));
+      }
+    }
+  };
+  // wait until this wave's pieces of all but the `ahead` youngest issued bands have landed
+  auto vm = [&](int ahead) {
+    const int n = ahead * npw;
+    switch (n) {
+      case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+      case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+      case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+      case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+      case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+      default: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    }
+  };
+
+  f32x4 acc[2][TAPS];
+#pragma unroll
+  for (int io = 0; io < 2; ++io)
+#pragma unroll
+    for (int j = 0; j < TAPS; ++j) acc[io][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // per-lane fragment bases: a fragment of 32 positions from pb (rows pb + 4g + q and + 16) and
+  // 16 columns at col0 reads base(pb mod 8, col0) + (pb - pb mod 8) * PB (+ 16 PB): the swizzle
+  // of position pb + L depends on pb only through pb mod 8
+  const int L = 4 * g + q;
+  auto fbase = [&](int r, int col0, int img) -> uint32_t {
+    const int lc = (col0 >> 3) + (p >> 1);
+    return lds0 + (uint32_t)(img + (r + L) * PB + ((lc ^ swz(r + L)) << 4) + ((p & 1) << 3));
+  };
+  const uint32_t bA0 = fbase(0, wo * 32, 0), bA1 = fbase(0, wo * 32 + 16, 0);
+  uint32_t bF[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) bF[r] = fbase(r, wc * 16, DPOS * PB);
+
+  auto compute = [&](auto slot_c) {
+    constexpr int SO = decltype(slot_c)::value * STAGE_B;
+    auto cat = [](s16x4w lo, s16x4w hi) {
+      return __builtin_bit_cast(bf16x8w, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+    };
+    bf16x8w A[S][2], F[LOOK + 1];
+    ww_static_for<S>([&](auto sc) {
+      constexpr int s = decltype(sc)::value;
+      A[s][0] = cat(ww_tr<SO + s * 32 * PB>(bA0), ww_tr<SO + (s * 32 + 16) * PB>(bA0));
+      A[s][1] = cat(ww_tr<SO + s * 32 * PB>(bA1), ww_tr<SO + (s * 32 + 16) * PB>(bA1));
+    });
+    auto rdF = [&](auto fc) -> bf16x8w {
+      constexpr int f = decltype(fc)::value;
+      constexpr int pb = (f % S) * RS + f / S, r = pb & 7, off = SO + (pb - r) * PB;
+      return cat(ww_tr<off>(bF[r]), ww_tr<off + 16 * PB>(bF[r]));
+    };
+    ww_static_for<LOOK>([&](auto fc) { F[decltype(fc)::value] = rdF(fc); });
+    ww_static_for<NF>([&](auto fc) {
+      constexpr int f = decltype(fc)::value;
+      if constexpr (f + LOOK < NF) F[(f + LOOK) % (LOOK + 1)] = rdF(std::integral_constant<int, f + LOOK>{});
+      constexpr int younger = (NF - 1 - f < LOOK ? NF - 1 - f : LOOK) * 2;
+      wb_lgkm<younger>();
+      const bf16x8w Ff = F[f % (LOOK + 1)];
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        const int j = f - s;
+        if (j < 0 || j >= TAPS) continue;
+#pragma unroll
+        for (int io = 0; io < 2; ++io)
+          acc[io][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[s][io], Ff, acc[io][j], 0, 0, 0);
+      }
+    });
+  };
+
+  // ring: ST - 1 bands issued ahead; per band this wave's pieces waited for (counted vmcnt), one
+  // raw barrier (every wave's pieces landed AND every wave finished the band whose slot the
+  // refill overwrites: its reads were waited for inside compute), refill, MFMAs.  The loop is
+  // unrolled by the ring depth so that each band's slot -- and with it every fragment address
+  // -- is a compile-time offset.
+  static_assert(ST == 3, "the unrolled ring below");
+  for (int i = 0; i < ST - 1 && i < nbs; ++i) issue(i, i);
+  auto band = [&](auto slot_c, int i) {
+    constexpr int SL = decltype(slot_c)::value;
+    const int ahead = nbs - 1 - i < ST - 2 ? nbs - 1 - i : ST - 2;
+    vm(ahead);
+    __builtin_amdgcn_s_barrier();
+    if (i + ST - 1 < nbs) issue(i + ST - 1, (SL + ST - 1) % ST);
+    compute(slot_c);
+  };
+  int i = 0;
+  for (; i + 3 <= nbs; i += 3) {
+    band(std::integral_constant<int, 0>{}, i);
+    band(std::integral_constant<int, 1>{}, i + 1);
+    band(std::integral_constant<int, 2>{}, i + 2);
+  }
+  if (i < nbs) band(std::integral_constant<int, 0>{}, i);
+  if (i + 1 < nbs) band(std::integral_constant<int, 1>{}, i + 1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // epilogue: four 16-row slices of the tile through LDS in the dw layout ([o][c][j]), stored
+  // as f32x4 rows (Z == 1: added into dw; else written to this split's slab)
+  float* Q = reinterpret_cast<float*>(smem);
+  const int64_t Kp = (int64_t)a.Cin * TAPS;
+  const int ncol = (a.Cin - c0 < BC ? a.Cin - c0 : BC) * TAPS;  // valid floats per row
+  float* dst_base = a.Z == 1 ? a.dw : a.slab + (int64_t)z * a.Cout * Kp;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (wo == (k >> 1)) {
+      const int io = k & 1;
+#pragma unroll
+      for (int j = 0; j < TAPS; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Q[(4 * g + r) * QLD + (wc * 16 + r16) * TAPS + j] = acc[io][j][r];
+    }
+    __syncthreads();
+    constexpr int V = BC * TAPS / 4;
+    for (int e = tid; e < 16 * V; e += NT) {
+      const int row = e / V, v4 = e - row * V;
+      const int o = o0 + 16 * k + row;
+      if (o >= a.Cout || 4 * v4 >= ncol) continue;
+      const f32x4 v = ld4(Q + row * QLD + 4 * v4);
+      float* d = dst_base + (int64_t)o * Kp + (int64_t)c0 * TAPS + 4 * v4;
+      if (a.Z == 1) st4(d, ld4(d) + v);
+      else st4(d, v);
+    }
+    __syncthreads();
+  }
+}
+
+// kNotEligible: the caller uses the split-K kernels
 int conv_wgrad_band_launch(const void* dy, int64_t ldy, const void* x, int64_t ldx, float* dw,
                            float* db, int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out,
                            int taps, int pad, const int64_t* lens, hipStream_t st) {
   const int S = 2, BR = 32 * S;
-  if (!(taps == 3 || taps == 5 || taps == 9)) return -1;
-  if (pad < 0 || pad > taps - 1) return -1;
+  if (!(taps == 3 || taps == 5 || taps == 9)) return kNotEligible;
+  if (pad < 0 || pad > taps - 1) return kNotEligible;
   if (c_in % 8 || c_out % 8 || ldx % 8 || ldy % 8 || ((uintptr_t)dy & 15) || ((uintptr_t)x & 15))
-    return -1;
-  if (seq_len % BR || rows % seq_len || rows / BR > (1 << 15)) return -1;
-  if (c_in < 32 || c_out < 32) return -1;
+    return kNotEligible;
+  if (seq_len % BR || rows % seq_len || rows / BR > (1 << 15)) return kNotEligible;
+  if (c_in < 32 || c_out < 32) return kNotEligible;
   // taps 3 / 5 with 64-multiple channels (PostNet 512, variance predictors) stay on the split-K
   // halo kernel: step 6.91 vs 6.98 ms with the band kernel there (profiles/r4_ab_experiments.txt)
   if (g_tune[FS2_TUNE_WGRAD_BAND] != 4 && taps != 9 && c_in % 64 == 0 && c_out % 64 == 0 &&
       seq_len % 64 == 0)
-    return -1;
+    return kNotEligible;
   const int to = (int)((c_out + 31) / 32), tc = (int)((c_in + 31) / 32);
   // grids under half the CUs keep the split-K kernels (the variance predictors' 256 x 256 k=3
   // convs at T = 128: 64 tiles), unless those would be the tap-major kernel (C % 64 != 0: the
   // PostNet's 80-channel convs, 48 tiles -- 26 vs 47 us alone, on 48 CUs)
   const bool halo_ok = c_in % 64 == 0 && c_out % 64 == 0 && seq_len % 64 == 0;
   const int min_tiles = g_tune[FS2_TUNE_WGRAD_BAND] == 3 ? 128 : halo_ok ? 128 : 32;
-  if (to * tc < min_tiles) return -1;
+  if (to * tc < min_tiles) return kNotEligible;
   // f32x4 read-modify-writes of dw: rows of c_in * taps floats, tile columns 32 * taps
-  if (((uintptr_t)dw & 15) || (c_in * taps) % 4) return -1;
+  if (((uintptr_t)dw & 15) || (c_in * taps) % 4) return kNotEligible;
   WgradBand a{(const u16*)dy, ldy, (const u16*)x, ldx, dw, db, rows, seq_len, (int)c_in,
               (int)c_out, pad, to, tc, lens};
   const unsigned grid = (unsigned)(to * tc);
@@ -789,6 +1130,73 @@ int wgrad_k1_multi_launch(const int64_t* jobs, int n, int64_t rows, int64_t seq_
   else wgrad_k1_multi<4><<<(unsigned)begin, 512, 0, st>>>(m);
   wgrad_k1_multi_reduce<<<(unsigned)((ub + bb + 255) / 256), 256, 0, st>>>(red);
   return launch_status("fs2_conv_wgrad_k1_multi");
+}
+
+// ---------------------------------------------------------------- wide-tile launcher
+// split count: about 256 blocks, >= 4 bands per split (FS2_TUNE_WGRAD_WIDE > 1 forces it);
+// 0 = not eligible
+int conv_wgrad_wide_splits(int64_t rows, int64_t c_in, int64_t c_out, int taps) {
+  const int v = g_tune[FS2_TUNE_WGRAD_WIDE];
+  if (v < 0) return 0;
+  if (!(taps == 3 || taps == 5 || taps == 9)) return 0;
+  // default: the channel counts that are not 64-multiples (the PostNet's 80-channel convs:
+  // 97.5 -> 36 us alone against the band kernel).  On the 64-multiple shapes it was neutral to
+  // slower alone and 0.54 ms/step slower in the step (its 163-VGPR waves, two per SIMD, leave
+  // no room for the concurrent data gradient's 244-VGPR waves; profiles/r5_wide_ab.txt)
+  if (v == 0 && c_in % 64 == 0 && c_out % 64 == 0) return 0;
+  if (rows % 64 || rows / 64 > (1 << 15) || rows < 256) return 0;
+  if (c_in % 8 || c_out % 8 || (c_in * taps) % 4) return 0;
+  const int64_t tiles = ((c_out + 63) / 64) * ((c_in + 63) / 64);
+  const int64_t nb = rows / 64;
+  int64_t z = g_tune[FS2_TUNE_WGRAD_WIDE] > 1 ? g_tune[FS2_TUNE_WGRAD_WIDE] : (256 + tiles / 2) / tiles;
+  if (z > nb / 4) z = nb / 4;
+  if (z > 64) z = 64;
+  return (int)(z < 1 ? 1 : z);
+}
+
+// slab workspace (floats) the wide kernel needs at this shape (0 when it needs none)
+int64_t conv_wgrad_wide_ws_floats(int64_t rows, int64_t c_in, int64_t c_out, int taps) {
+  const int z = conv_wgrad_wide_splits(rows, c_in, c_out, taps);
+  if (z <= 1) return 0;
+  return (int64_t)z * c_out * (c_in * taps + 1);
+}
+
+// kNotEligible: the caller uses the other kernels
+int conv_wgrad_wide_launch(const void* dy, int64_t ldy, const void* x, int64_t ldx, float* dw,
+                           float* db, int64_t rows, int64_t seq_len, int64_t c_in, int64_t c_out,
+                           int taps, int pad, const int64_t* lens, float* ws, hipStream_t st) {
+  const int Z = conv_wgrad_wide_splits(rows, c_in, c_out, taps);
+  if (Z < 1 || seq_len <= 0 || seq_len % 64 || rows % seq_len) return kNotEligible;
+  if (lens && rows / 64 > WIDE_MAXB) return kNotEligible;
+  if (pad < 0 || pad > taps - 1) return kNotEligible;
+  if (ldx % 8 || ldy % 8 || ((uintptr_t)dy & 15) || ((uintptr_t)x & 15) || ((uintptr_t)dw & 15))
+    return kNotEligible;
+  if (Z > 1 && (ws == nullptr || ((uintptr_t)ws & 15))) return kNotEligible;
+  const int to = (int)((c_out + 63) / 64), tc = (int)((c_in + 63) / 64);
+  const int64_t Kp = c_in * taps;
+  float* bslab = (Z > 1 && db) ? ws + (int64_t)Z * c_out * Kp : nullptr;
+  WgradWide a{(const u16*)dy, ldy, (const u16*)x, ldx, dw, db, Z > 1 ? ws : nullptr, bslab,
+              rows, seq_len, (int)c_in, (int)c_out, pad, to, tc, Z, lens};
+  const unsigned grid = (unsigned)(to * tc * Z + (db ? Z * to : 0));
+  if (taps == 9) conv_wgrad_wide<9, 3><<<grid, 512, 0, st>>>(a);
+  else if (taps == 5) conv_wgrad_wide<5, 3><<<grid, 512, 0, st>>>(a);
+  else conv_wgrad_wide<3, 3><<<grid, 512, 0, st>>>(a);
+  if (Z > 1) {
+    K1Red red{};
+    red.n = 1;
+    red.slab[0] = ws;
+    red.bslab[0] = bslab;
+    red.dw[0] = dw;
+    red.db[0] = db;
+    red.splits[0] = Z;
+    red.u_begin[0] = 0;
+    red.u_begin[1] = c_out * Kp / 4;
+    red.b_begin[0] = 0;
+    red.b_begin[1] = db ? c_out : 0;
+    const int64_t n = red.u_begin[1] + red.b_begin[1];
+    wgrad_k1_multi_reduce<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(red);
+  }
+  return launch_status("fs2_conv_wgrad(bf16, wide)");
 }
 
 }  // namespace fs2

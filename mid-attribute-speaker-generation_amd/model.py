@@ -20,8 +20,8 @@ Parameters live in one flat fp32 buffer (``ParamArena``), laid out in reverse ba
 order so gradient buckets complete front-to-back; kernels accumulate weight gradients
 straight into the flat gradient buffer (``param.grad`` are views of it).
 """
+import ctypes
 import math
-import os
 
 import numpy as np
 import torch
@@ -111,13 +111,6 @@ def sinusoid_table(n_position, d_hid):
 # ----------------------------------------------------------------------------- runtime state
 
 
-# FS2_SERIAL_WGRAD_TAPS="9" (A/B): weight gradients of these kernel widths run on the main
-# stream, serially after the data gradient, instead of concurrently on the side stream
-_SERIAL_TAPS = frozenset(int(t) for t in os.environ.get("FS2_SERIAL_WGRAD_TAPS", "").split(",") if t)
-# FS2_WGRAD_AFTER_DGRAD: 1 = a Conv1d's (taps > 1) side-stream weight gradient is issued after
-# its own data gradient, so the two do not share the CUs (the data gradient then runs alone and
-# the weight gradient beside the lighter ops that follow it); 0 = issued before it (concurrent)
-WGRAD_AFTER_DGRAD = os.environ.get("FS2_WGRAD_AFTER_DGRAD", "0") == "1"
 
 
 class StepCtx:
@@ -166,7 +159,7 @@ class StepCtx:
                 self.k1 = (key, [], lens)
             self.k1[1].append((dy, x, dw, db, c_in, c_out))
             return
-        if self.side is None or taps in _SERIAL_TAPS:
+        if self.side is None:
             return K.conv_wgrad(dy, x, dw, rows, seq_len, c_in, c_out, taps, pad, db=db,
                                 lens=lens)
         ws = self._side_ws(K.lib.fs2_conv_wgrad_ws_bytes(rows, c_in, c_out, taps), dy.device)
@@ -203,14 +196,17 @@ class StepCtx:
             self.hook(params)
 
 
-# the FFT block's three k = 1 weight gradients (w_2, fc, QKV) as one grouped launch at the end
-# of its backward (fs2_conv_wgrad_k1_multi); FS2_GROUP_K1=0: one launch each (A/B)
-GROUP_K1 = os.environ.get("FS2_GROUP_K1", "1") != "0"
 # bf16 path: FFT-block post-LayerNorms fused into the fc / w_2 GEMM epilogues (fs2_conv_gemm_ln)
-FUSE_LN = os.environ.get("FS2_FUSE_LN", "1") != "0"  # step-level A/B switch
+# on decoder-sized grids; the bitwise tests compare against the two-launch form by clearing it
+FUSE_LN = True
 FUSE_LN_MIN_ROWS = 16384
 # ... and each block's QKV data gradient carries the previous block's LN2 backward
-FUSE_LN_BWD = os.environ.get("FS2_FUSE_LN_BWD", "1") != "0"
+FUSE_LN_BWD = True
+# bf16 path: each FFT block's forward / backward is ONE call into the library
+# (fs2_fft_block_fwd / _bwd issue its kernels and stream waits from C, in the order of
+# FFTBlock.fwd / .bwd below: bitwise the same results, a fifth of the host time); the tests
+# compare it against the per-kernel path by clearing it
+C_BLOCKS = True
 
 
 def _t(f, t):
@@ -388,6 +384,32 @@ class FFTBlock(nn.Module):
         _conv_prep(f.w_1, cdt, jobs)
         _conv_prep(f.w_2, cdt, jobs)
 
+    def cdesc(self):
+        """The block's fs2_fft_block_* descriptor (include/fs2hip.h, FS2_FB_*): geometry, the
+        compute-layout weights, biases, LayerNorm affines and gradient views, as a host int64
+        table (cached: the compute-layout buffers and the gradient arena persist)."""
+        a, f = self.slf_attn, self.pos_ffn
+        q = self._qkv_holder
+        key = (q._w_fwd.data_ptr(), f.w_1._w_fwd.data_ptr(), _g(f.w_1.weight).data_ptr(),
+               f.w_1.weight.data_ptr(), self.site)
+        d = self.__dict__.get("_cdesc")
+        if d is not None and d[0] == key:
+            return d[1]
+        P = lambda t: t.data_ptr()
+        w = [self.d, a.n_head, a.d_k, f.w_1.c_out, f.w_1.k, f.w_1.padding, self.site,
+             P(q._w_fwd), P(q._w_bwd), P(self._qkv_b), P(a.fc._w_fwd), P(a.fc._w_bwd), P(a.fc.bias),
+             P(f.w_1._w_fwd), P(f.w_1._w_bwd), P(f.w_1.bias), P(f.w_2._w_fwd), P(f.w_2._w_bwd),
+             P(f.w_2.bias), P(a.layer_norm.weight), P(a.layer_norm.bias), P(f.layer_norm.weight),
+             P(f.layer_norm.bias), P(self._qkv_gw), P(self._qkv_gb), P(_g(a.fc.weight)),
+             P(_g(a.fc.bias)), P(_g(f.w_1.weight)), P(_g(f.w_1.bias)), P(_g(f.w_2.weight)),
+             P(_g(f.w_2.bias)), P(_g(a.layer_norm.weight)), P(_g(a.layer_norm.bias)),
+             P(_g(f.layer_norm.weight)), P(_g(f.layer_norm.bias))]
+        if f.w_2.k != 1:
+            raise RuntimeError("fs2_fft_block_*: w_2 must be a 1x1 conv (SubLayers.py:78-83)")
+        arr = (ctypes.c_int64 * len(w))(*w)
+        self._cdesc = (key, arr)
+        return arr
+
     def fwd(self, x, x_t, lens, B, T, ctx):
         a, f = self.slf_attn, self.pos_ffn
         M, d = x.shape
@@ -458,17 +480,13 @@ class FFTBlock(nn.Module):
                                   dbias_in=_g(w2.bias))
         dy2_c = _t(dy2, dy2_t)
         ctx.wgrad(dy2_c, h, _g(w2.weight), M, T, w2.c_in, d, w2.k, w2.padding, lens=lens,
-                  group=GROUP_K1)
+                  group=True)
         dh = K.conv_gemm(dy2_c, w2._w_bwd, M, T, d, w2.c_in, w2.k, w2.padding,
                          flags=K.EPI_RELU_MASK_AUX, aux=h, out_dtype=cdt, lens=lens)
-        if not WGRAD_AFTER_DGRAD:
-            ctx.wgrad(dh, x1_c, _g(w1.weight), M, T, d, w1.c_out, w1.k, w1.padding,
-                      db=_g(w1.bias), lens=lens)
+        ctx.wgrad(dh, x1_c, _g(w1.weight), M, T, d, w1.c_out, w1.k, w1.padding,
+                  db=_g(w1.bias), lens=lens)
         K.conv_gemm(dh, w1._w_bwd, M, T, w1.c_out, d, w1.k, w1.padding, flags=K.EPI_ADD_AUX,
                     aux=dx1, out=dx1, lens=lens)
-        if WGRAD_AFTER_DGRAD:
-            ctx.wgrad(dh, x1_c, _g(w1.weight), M, T, d, w1.c_out, w1.k, w1.padding,
-                      db=_g(w1.bias), lens=lens)
         # LN1 -> fc -> attention -> QKV
         dx = torch.empty((M, d), dtype=torch.float32, device=x_c.device)
         dy1, dy1_t = K.ln_bwd(xh1, rs1, ln1.weight, ln1.bias, _g(ln1.weight), _g(ln1.bias),
@@ -477,11 +495,11 @@ class FFTBlock(nn.Module):
                               dbias_in=_g(a.fc.bias))
         dy1_c = _t(dy1, dy1_t)
         hd = a.n_head * a.d_k
-        ctx.wgrad(dy1_c, o, _g(a.fc.weight), M, T, hd, d, 1, 0, lens=lens, group=GROUP_K1)
+        ctx.wgrad(dy1_c, o, _g(a.fc.weight), M, T, hd, d, 1, 0, lens=lens, group=True)
         do = K.conv_gemm(dy1_c, a.fc._w_bwd, M, T, d, hd, 1, 0, out_dtype=cdt, lens=lens)
         dqkv = K.attn_bwd(qkv, o, do, lse, lens, B, T, a.n_head, a.d_k, 1.0 / math.sqrt(a.d_k))
         ctx.wgrad(dqkv, x_c, self._qkv_gw, M, T, d, n3, 1, 0, db=self._qkv_gb, lens=lens,
-                  group=GROUP_K1)
+                  group=True)
         ctx.flush()
         if prev is not None:
             pb, ps = prev
@@ -494,6 +512,86 @@ class FFTBlock(nn.Module):
         K.conv_gemm(dqkv, q._w_bwd, M, T, n3, d, 1, 0, flags=K.EPI_ADD_AUX, aux=dx, out=dx,
                     lens=lens)
         return dx
+
+
+def _c_blocks(ctx, d):
+    return C_BLOCKS and ctx.copy is not None and ctx.cdt == torch.bfloat16 and d == 256
+
+
+def _stack_fwd_c(layers, x, x_t, lens, B, T, ctx):
+    """Forward through a stack of FFT blocks, one fs2_fft_block_fwd call per block; each block's
+    activations live in one region (saved for the backward).  Returns the last block's output,
+    its bf16 copy and the per-block saved tuples."""
+    M, d = x.shape
+    fuse = FUSE_LN and M >= FUSE_LN_MIN_ROWS
+    saved = []
+    xp, xtp, x_keep = x.data_ptr(), x_t.data_ptr(), x_t
+    lp = 0 if lens is None else lens.data_ptr()
+    stream = K.stream()
+    acts = []
+    for layer in layers:
+        desc = layer.cdesc()
+        p = ctx.p(layer.slf_attn.p)
+        act = torch.empty(K.lib.fs2_fft_block_act_bytes(desc, M, B, T, int(fuse)),
+                          dtype=torch.uint8, device=x.device)
+        K.lib.fs2_fft_block_fwd(desc, xp, xtp, act.data_ptr(), M, B, T, lp, p,
+                                ctx.seed.data_ptr() if p > 0 else None, int(fuse), stream)
+        saved.append(("C", act, xtp, x_keep, fuse, p))
+        o2 = K.lib.fs2_fft_block_act_offset(desc, M, B, T, int(fuse), 0)
+        o2t = K.lib.fs2_fft_block_act_offset(desc, M, B, T, int(fuse), 1)
+        xp, xtp, x_keep = act.data_ptr() + o2, act.data_ptr() + o2t, act
+        acts.append((act, o2, o2t))
+    act, o2, o2t = acts[-1]
+    out = act[o2:o2 + M * d * 4].view(torch.float32).view(M, d)
+    out_t = act[o2t:o2t + M * d * 2].view(torch.bfloat16).view(M, d)
+    return out, out_t, saved
+
+
+def _stack_bwd_c(layers, saved, dx, ctx, lens, B, T):
+    """Backward through a stack of FFT blocks, one fs2_fft_block_bwd call per block (the
+    previous block's LN2 backward in each QKV data-gradient epilogue on decoder-sized grids, as
+    _stack_bwd)."""
+    layers, saved = list(reversed(layers)), list(reversed(saved))
+    M, d = dx.shape
+    ctx.flush()
+    lp = 0 if lens is None else lens.data_ptr()
+    side = ctx.side.cuda_stream if ctx.side is not None else None
+    stream = K.stream()
+    carry = None
+    dev = dx.device
+    for i, (layer, s) in enumerate(zip(layers, saved)):
+        _, act, xtp, x_keep, fuse, p = s
+        desc = layer.cdesc()
+        fuse_bwd = FUSE_LN_BWD and M >= FUSE_LN_MIN_ROWS and i + 1 < len(layers)
+        tmp = torch.empty(K.lib.fs2_fft_block_tmp_bytes(desc, M, B, T), dtype=torch.uint8, device=dev)
+        ws = ctx._side_ws(K.lib.fs2_fft_block_side_ws_bytes(desc, M), dev) if side is not None else \
+            K.ws(K.lib.fs2_fft_block_side_ws_bytes(desc, M), dev)
+        dxo = torch.empty((M, d), dtype=torch.float32, device=dev)
+        pdesc = pact = pdy2 = pdx1 = None
+        pfuse, pp = 0, 0.0
+        if fuse_bwd:
+            ps = saved[i + 1]
+            pdesc, pact, pfuse, pp = layers[i + 1].cdesc(), ps[1].data_ptr(), int(ps[4]), ps[5]
+            pdy2 = torch.empty((M, d), dtype=torch.bfloat16, device=dev)
+            pdx1 = torch.empty((M, d), dtype=torch.float32, device=dev)
+        need_seed = p > 0 or (fuse_bwd and pp > 0)
+        K.lib.fs2_fft_block_bwd(
+            desc, act.data_ptr(), xtp, int(fuse), p,
+            dx.data_ptr() if carry is None else None,
+            carry[0].data_ptr() if carry is not None else None,
+            carry[1].data_ptr() if carry is not None else None,
+            pdesc, pact, pfuse, pp, tmp.data_ptr(), dxo.data_ptr(),
+            None if pdy2 is None else pdy2.data_ptr(), None if pdx1 is None else pdx1.data_ptr(),
+            M, B, T, lp, ctx.seed.data_ptr() if need_seed else None, ws.data_ptr(), ws.numel() * 4,
+            stream, side)
+        # read by the side stream's weight gradients after this call: kept until the join
+        ctx.keep.append((tmp, act, x_keep, carry))
+        ctx.notify(fft_param_order(layer))
+        if fuse_bwd:
+            carry, dx = (pdy2, pdx1), None
+        else:
+            carry, dx = None, dxo
+    return dx
 
 
 def _stack_bwd(layers, saved, dx, ctx):
@@ -714,17 +812,13 @@ class PostNet(nn.Module):
             dz, dz_t = K.bn_bwd(d, z, mean, rstd, bn.weight, bn.bias, _g(bn.weight), _g(bn.bias),
                                 i < n - 1, p, ctx.seed, self.site + i, copy=ctx.copy)
             dz_c = _t(dz, dz_t)
-            if not WGRAD_AFTER_DGRAD:
-                ctx.wgrad(dz_c, a_c, _g(conv.weight), M, T, conv.c_in, conv.c_out, conv.k,
-                          conv.padding, db=_g(conv.bias))
+            ctx.wgrad(dz_c, a_c, _g(conv.weight), M, T, conv.c_in, conv.c_out, conv.k,
+                      conv.padding, db=_g(conv.bias))
             if i > 0:
                 d = K.conv_gemm(dz_c, conv._w_bwd, M, T, conv.c_out, conv.c_in, conv.k, conv.padding)
             else:
                 K.conv_gemm(dz_c, conv._w_bwd, M, T, conv.c_out, conv.c_in, conv.k, conv.padding,
                             flags=K.EPI_ADD_AUX, aux=dx_acc, out=dx_acc)
-            if WGRAD_AFTER_DGRAD:
-                ctx.wgrad(dz_c, a_c, _g(conv.weight), M, T, conv.c_in, conv.c_out, conv.k,
-                          conv.padding, db=_g(conv.bias))
 
 
 # ----------------------------------------------------------------------------- GMM head
@@ -864,18 +958,25 @@ class EncoderFn(torch.autograd.Function):
     def forward(fctx, token, enc, texts, accents, lens, B, T, ctx):
         x, x_t = K.encoder_embed(texts, accents, enc.src_word_emb.weight, enc.src_accent_emb.weight,
                                  enc.position_enc, B, T, enc.d, copy=ctx.copy)
-        saved = []
-        for layer in enc.layer_stack:
-            x, x_t, s = layer.fwd(x, x_t, lens, B, T, ctx)
-            saved.append(s)
+        if _c_blocks(ctx, enc.d) and x_t is not None:
+            x, x_t, saved = _stack_fwd_c(enc.layer_stack, x, x_t, lens, B, T, ctx)
+        else:
+            saved = []
+            for layer in enc.layer_stack:
+                x, x_t, s = layer.fwd(x, x_t, lens, B, T, ctx)
+                saved.append(s)
         fctx.enc, fctx.saved, fctx.ids, fctx.ctx = enc, saved, (texts, accents), ctx
+        fctx.geom = (lens, B, T)
         return x
 
     @staticmethod
     def backward(fctx, dx):
         enc = fctx.enc
         dx = dx.contiguous()
-        dx = _stack_bwd(enc.layer_stack, fctx.saved, dx, fctx.ctx)
+        if fctx.saved and isinstance(fctx.saved[0][0], str):
+            dx = _stack_bwd_c(enc.layer_stack, fctx.saved, dx, fctx.ctx, *fctx.geom)
+        else:
+            dx = _stack_bwd(enc.layer_stack, fctx.saved, dx, fctx.ctx)
         texts, accents = fctx.ids
         K.embedding_bwd(dx, texts, _g(enc.src_word_emb.weight), 0)
         K.embedding_bwd(dx, accents, _g(enc.src_accent_emb.weight), 0)
@@ -939,11 +1040,15 @@ class DecoderFn(torch.autograd.Function):
     def forward(fctx, token, x, x_t, dec, lens, B, T, ctx):
         fctx.set_materialize_grads(False)  # the compute-copy side output gets no zero gradient
         x_t = x_t if x_t.numel() else None
-        saved = []
-        for layer in dec.layer_stack:
-            x, x_t, s = layer.fwd(x, x_t, lens, B, T, ctx)
-            saved.append(s)
+        if _c_blocks(ctx, x.shape[1]) and x_t is not None:
+            x, x_t, saved = _stack_fwd_c(dec.layer_stack, x, x_t, lens, B, T, ctx)
+        else:
+            saved = []
+            for layer in dec.layer_stack:
+                x, x_t, s = layer.fwd(x, x_t, lens, B, T, ctx)
+                saved.append(s)
         fctx.dec, fctx.saved, fctx.ctx = dec, saved, ctx
+        fctx.geom, fctx.xshape, fctx.xdev = (lens, B, T), tuple(x.shape), x.device
         side = x_t if x_t is not None else torch.empty(0, device=x.device)
         fctx.mark_non_differentiable(side)
         return x, side
@@ -951,9 +1056,12 @@ class DecoderFn(torch.autograd.Function):
     @staticmethod
     def backward(fctx, dx, _):
         if dx is None:
-            dx = K.zeros(fctx.saved[0][0].shape, fctx.saved[0][0].device)
+            dx = K.zeros(fctx.xshape, fctx.xdev)
         dx = dx.contiguous()
-        dx = _stack_bwd(fctx.dec.layer_stack, fctx.saved, dx, fctx.ctx)
+        if fctx.saved and isinstance(fctx.saved[0][0], str):
+            dx = _stack_bwd_c(fctx.dec.layer_stack, fctx.saved, dx, fctx.ctx, *fctx.geom)
+        else:
+            dx = _stack_bwd(fctx.dec.layer_stack, fctx.saved, dx, fctx.ctx)
         fctx.saved = None
         return None, dx, None, None, None, None, None, None
 

@@ -95,6 +95,36 @@ def init_data_parallel(device, **kwargs):
     dist.init_process_group("nccl", device_id=device, **kwargs)
 
 
+class CollectiveModel:
+    """Stand-in collectives for pricing the data-parallel step at ``ranks`` ranks on ONE GPU
+    (measurement only: ``scripts/dp_collective_model.py``, ``profiles/r5_dp_collective_model.txt``).
+
+    A bucket's ring all-reduce of S bytes is replaced by ``fs2_collective_standin`` on the stream
+    the real collective would be issued from: ``blocks`` workgroups (RCCL's channels) that read
+    and write back 2 (n - 1) / n * S bytes of the bucket (values unchanged) over
+    2 (n - 1) / n * S / busbw + latency -- the collective's CU occupancy, HBM traffic and
+    duration, without the interconnect.  The step's 3-float all-reduce of the loss
+    denominators becomes a one-workgroup stand-in of ``latency_us`` on the main stream, and
+    the denominators stay local, so the step's values are the single-GPU step's."""
+
+    def __init__(self, ranks=8, busbw_gbs=300.0, blocks=32, latency_us=12.0):
+        self.ranks, self.busbw, self.blocks, self.lat = int(ranks), float(busbw_gbs), int(blocks), float(latency_us)
+
+    def wire_bytes(self, nbytes):
+        return 2.0 * (self.ranks - 1) / self.ranks * nbytes
+
+    def duration_ns(self, nbytes):
+        return int((self.wire_bytes(nbytes) / (self.busbw * 1e9) + self.lat * 1e-6) * 1e9)
+
+    def all_reduce(self, t):
+        nb = t.numel() * t.element_size()
+        K.lib.fs2_collective_standin(K.ptr(t), t.numel(), int(2 * self.wire_bytes(nb)),
+                                     self.blocks, self.duration_ns(nb), K.stream())
+
+    def small(self, t):
+        K.lib.fs2_collective_standin(K.ptr(t), t.numel(), 0, 1, int(self.lat * 1e3), K.stream())
+
+
 class GradBuckets:
     """Bucketed, backward-overlapped all-reduce of the arena's flat gradient buffer."""
 
@@ -126,6 +156,7 @@ class GradBuckets:
         # process (profiles/r3_ab_experiments.txt: separate / high-priority communication
         # streams measured 1.04-2.8x slower steps)
         self.producers = None
+        self.standin = None  # CollectiveModel.all_reduce: stand-in collectives (no process group)
         self.log = None  # optional list: bucket launches are appended (tests)
         del index
         self.reset()
@@ -142,6 +173,9 @@ class GradBuckets:
         cur = torch.cuda.current_stream() if self.arena.grad.is_cuda else None
         prods = [st for st in (self.producers() if self.producers else ()) if st is not None]
         if cur is None or not prods:
+            if self.standin is not None:
+                self.standin(self.arena.grad[s:e])
+                return
             self.works.append(dist.all_reduce(self.arena.grad[s:e], group=self.group,
                                               async_op=True))
             return
@@ -156,8 +190,11 @@ class GradBuckets:
                 issue.wait_event(ev)
         self._issue = issue
         with torch.cuda.stream(issue):
-            self.works.append(dist.all_reduce(self.arena.grad[s:e], group=self.group,
-                                              async_op=True))
+            if self.standin is not None:
+                self.standin(self.arena.grad[s:e])
+            else:
+                self.works.append(dist.all_reduce(self.arena.grad[s:e], group=self.group,
+                                                  async_op=True))
 
     def ready(self, params):
         for p in params:
@@ -196,7 +233,8 @@ class Trainer:
     """
 
     def __init__(self, model, preprocess_config, model_config, train_config, current_step=0,
-                 process_group=None, bucket_bytes=32 << 20, graph=False, data_parallel=None):
+                 process_group=None, bucket_bytes=32 << 20, graph=False, data_parallel=None,
+                 collective_model=None, comm_stream=False):
         self.model = model
         self.graph_mode = bool(graph)
         self._graph = None
@@ -218,10 +256,22 @@ class Trainer:
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
         self.dp = self.world > 1 if data_parallel is None else bool(data_parallel)
-        if self.dp and not dist.is_initialized():
+        self.cm = collective_model
+        if self.cm is not None:  # the data-parallel step with stand-in collectives
+            self.dp = True
+        if self.dp and self.cm is None and not dist.is_initialized():
             raise ValueError("data_parallel needs an initialised process group")
         self.buckets = None
-        if self.dp:
+        if self.cm is not None:
+            arena = model.arena()
+            self.buckets = GradBuckets(arena, None, bucket_bytes)
+            self.buckets.standin = self.cm.all_reduce
+            # comm_stream: the alternative schedule -- each bucket's collective on a stream of
+            # its own, event-gated on the main stream and on the weight-gradient stream
+            cs = torch.cuda.Stream() if comm_stream else None
+            self.buckets.producers = (lambda: (model._side, cs)) if cs is not None else (lambda: (model._side,))
+            model._hooks["grad"] = self.buckets.ready
+        elif self.dp:
             from .model import stream_reservation_problem
             problem = stream_reservation_problem(model.encoder.position_enc.device)
             if problem is not None:
@@ -239,7 +289,10 @@ class Trainer:
         T_dec = min(int(batch[8]), self.model.decoder.max_seq_len)
         counts = K.dp_counts(batch[4].contiguous().long(), batch[7].contiguous().long(),
                              int(batch[5]), T_dec, self.model.mel_linear.out_features)
-        dist.all_reduce(counts, group=self.pg)
+        if self.cm is not None:
+            self.cm.small(counts)  # its latency; the counts stay local
+        else:
+            dist.all_reduce(counts, group=self.pg)
         return counts
 
     def _shape_key(self, batch):

@@ -8,6 +8,8 @@ PKG = importlib.import_module("mid-attribute-speaker-generation_amd")
 M = importlib.import_module("mid-attribute-speaker-generation_amd.model")
 TR = importlib.import_module("mid-attribute-speaker-generation_amd.train")
 dev = torch.device("cuda", 0)
+if "--py" in sys.argv:  # the per-kernel host path (model.C_BLOCKS off) for the A/B
+    M.C_BLOCKS = False
 pp, mc, tc, path = PKG.config.load_configs("JVS-VCTK")
 model = M.FastSpeech2(pp, mc, path, device=dev, compute_dtype=torch.bfloat16)
 model.train()
@@ -43,3 +45,4 @@ g = np.array([[r["start"].elapsed_time(r[k]) for k in names] for r in gpu[2:]])
 hh = np.array([[(x - hr[0]) * 1e3 for x in hr[1:]] for hr in host[2:]])
 print("GPU  ms from step start:", "  ".join(f"{n} {v:.3f}" for n, v in zip(names, g.mean(0))))
 print("host ms from step start:", "  ".join(f"{n} {v:.3f}" for n, v in zip(names, hh.mean(0))))
+print(f"C blocks: {M.C_BLOCKS}; host enqueue {hh.mean(0)[-1]:.3f} ms, GPU {g.mean(0)[-1]:.3f} ms per step")

@@ -338,3 +338,45 @@ def test_data_parallel_warns_without_stream_reservation():
         r = torch.load(f"{out}/unres.pt")
     assert any("not reserved" in m for m in r["warned"]), r
     assert r["raised"] is not None and "not reserved" in r["raised"], r
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("comm", [False, True])
+def test_collective_model_step_equals_plain_step(comm):
+    """train.CollectiveModel (the one-GPU pricing of the N-rank collective schedule,
+    scripts/dp_collective_model.py): the data-parallel step with every bucket's all-reduce and the
+    denominators' all-reduce replaced by fs2_collective_standin -- issued from the weight-gradient
+    stream (comm=False) or a stream of its own (comm=True) -- leaves the gradients unchanged, so
+    two optimiser steps equal the plain step (to the fp32 rounding of the device-side loss
+    denominators, as in the one-rank RCCL test); every bucket is issued once per step."""
+    import sys
+    sys.path.insert(0, REPO)
+    pkg = importlib.import_module("mid-attribute-speaker-generation_amd")
+    M = importlib.import_module("mid-attribute-speaker-generation_amd.model")
+    tr = importlib.import_module("mid-attribute-speaker-generation_amd.train")
+    dev = torch.device("cuda", 0)
+    pp, mc, tc, path = pkg.config.load_configs("JVS-VCTK")
+    res = {}
+    for mode in ("plain", "model"):
+        torch.manual_seed(0)
+        model = M.FastSpeech2(pp, mc, path, device=dev, compute_dtype=torch.bfloat16)
+        model.train()
+        model.dropout = False
+        if mode == "plain":
+            t = tr.Trainer(model, pp, mc, tc)
+        else:
+            t = tr.Trainer(model, pp, mc, tc, collective_model=tr.CollectiveModel(
+                ranks=8, busbw_gbs=300.0, blocks=8, latency_us=5.0), bucket_bytes=16 << 20,
+                comm_stream=comm)
+            t.buckets.log = []
+        losses = [[float(x) for x in t.step(_shard(pkg, 0, dev, s))[0]] for s in range(2)]
+        torch.cuda.synchronize()
+        res[mode] = (losses, model.arena().flat.cpu(),
+                     list(t.buckets.log) if t.buckets is not None else None)
+    for a_, b_ in zip(res["model"][0], res["plain"][0]):
+        for x, y in zip(a_, b_):
+            assert abs(x - y) <= 1e-5 * max(abs(y), 1e-6), (a_, b_)
+    w, wp = res["model"][1], res["plain"][1]
+    assert (w - wp).abs().max().item() <= 1e-6 * wp.abs().max().item()
+    nb = len(t.buckets.sizes)
+    assert sorted(res["model"][2]) == sorted(list(range(nb)) * 2)

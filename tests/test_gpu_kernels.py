@@ -992,10 +992,13 @@ def test_convT_as_phase_conv():
                                             (2, 128, 80, 512, 5), (2, 128, 512, 80, 5)])
 def test_conv_wgrad_halo(B, T, cin, cout, k):
     """The Conv1d (taps 3/5/9) weight gradient with its fused bias gradient against fp32
-    autograd on the same bf16 data: FS2_TUNE_WGRAD_HALO 0 = the slab-free band kernel where the
-    32 x 32 output tiles fill the chip (else the split-K halo kernel), 1 = the split-K halo
-    kernel (C_in % 64 == 0, else tap-major), -1 = the tap-major kernel.  Partial o / c tiles,
-    determinism, accumulation into dw, and the padding-band skip under lens."""
+    autograd on the same bf16 data, every kernel: (FS2_TUNE_WGRAD_HALO, FS2_TUNE_WGRAD_WIDE)
+    (0, 0) = the default choice, (0, 1) = the wide-tile kernel wherever eligible (64 x 64 x taps
+    tiles, row splits + in-order reduce; T % 64 == 0), (0, -1) = the slab-free band kernel where
+    its 32 x 32 tiles fill the chip (else the split-K halo kernel), (0, 3) = the wide kernel with
+    3 forced splits, (1, 0) = the split-K
+    halo kernel (C_in % 64 == 0, else tap-major), (-1, 0) = the tap-major kernel.  Partial
+    o / c tiles, determinism, accumulation into dw, and the padding-band skip under lens."""
     pad = (k - 1) // 2
     x = bf(rnd(B * T, cin, seed=71))
     dy = bf(rnd(B * T, cout, seed=72))
@@ -1004,8 +1007,9 @@ def test_conv_wgrad_halo(B, T, cin, cout, k):
     ref_conv(xr, wr, None, B, T, pad).backward(dy.float())
     out = {}
     try:
-        for mode in (0, 1, -1):
-            K.lib.fs2_set_tuning(7, mode)  # FS2_TUNE_WGRAD_HALO
+        for mode in ((0, 0), (0, 1), (0, -1), (0, 3), (1, 0), (-1, 0)):
+            K.lib.fs2_set_tuning(7, mode[0])  # FS2_TUNE_WGRAD_HALO
+            K.lib.fs2_set_tuning(19, mode[1])  # FS2_TUNE_WGRAD_WIDE
             dw, db = torch.zeros_like(w), torch.zeros(cout, device=DEV)
             K.conv_wgrad(dy, x, dw, B * T, T, cin, cout, k, pad, db=db)
             out[mode] = (dw, db)
@@ -1013,15 +1017,18 @@ def test_conv_wgrad_halo(B, T, cin, cout, k):
             close(db, dy.float().sum(0), 1e-5)
     finally:
         K.lib.fs2_set_tuning(7, 0)
+        K.lib.fs2_set_tuning(19, 0)
     # fixed reduction order: a second run is bitwise equal; dw / db accumulate
-    dw2, db2 = out[0][0].clone(), out[0][1].clone()
+    dw2, db2 = out[(0, 0)][0].clone(), out[(0, 0)][1].clone()
     K.conv_wgrad(dy, x, dw2, B * T, T, cin, cout, k, pad, db=db2)
     dw3, db3 = torch.zeros_like(w), torch.zeros(cout, device=DEV)
     K.conv_wgrad(dy, x, dw3, B * T, T, cin, cout, k, pad, db=db3)
-    assert torch.equal(dw3, out[0][0]) and torch.equal(db3, out[0][1])
+    assert torch.equal(dw3, out[(0, 0)][0]) and torch.equal(db3, out[(0, 0)][1])
     close(dw2, 2 * wr.grad, 1e-5)
     close(db2, 2 * dy.float().sum(0), 1e-5)
-    # lens: zero dy rows past each length; the all-padding bands / k-tiles are skipped
+    # lens: zero dy rows past each length; the all-padding bands / k-tiles are skipped.  That
+    # changes which split / wave sums which rows, so the result equals the lens-free one to fp32
+    # rounding, not bitwise (reproducible per lens: fs2hip.h)
     lens = torch.tensor([T - (13 * u) % T for u in range(B)], device=DEV)
     padr = (torch.arange(T, device=DEV)[None] >= lens[:, None]).reshape(-1)
     dyz = dy * (~padr)[:, None]

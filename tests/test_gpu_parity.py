@@ -368,6 +368,35 @@ def test_fused_gemm_ln_step_bitwise():
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("min_rows", [0, 16384])
+def test_c_blocks_step_bitwise(min_rows):
+    """bf16: the FFT blocks issued from C (fs2_fft_block_fwd / _bwd, model.C_BLOCKS: one call per
+    block) give bitwise the weights, Adam moments, BatchNorm statistics and losses of the
+    per-kernel host path after 2 steps with dropout ON at ragged lengths -- with the post-LN
+    fusions on every block (min_rows 0: the fused forward epilogues and the carried LN2
+    backward) and with the unfused forms (the default threshold at SYN-8 x 32)."""
+    pp, mc, tc, path = PKG.config.load_configs("JVS-VCTK")
+    res = []
+    c_default = M.C_BLOCKS
+    for c_blocks in (False, True):
+        M.C_BLOCKS, M.FUSE_LN_MIN_ROWS = c_blocks, min_rows
+        try:
+            model = M.FastSpeech2(pp, mc, path, device=DEV, compute_dtype=torch.bfloat16)
+            PKG.seeded.load_seeded_(model)
+            model.train()
+            model.seed(25)
+            tr = T.Trainer(model, pp, mc, tc)
+            batch = PKG.data.to_device(PKG.data.syn_batch(8, 32, seed=8), DEV)
+            losses = [torch.stack(list(tr.step(batch)[0])).clone() for _ in range(2)]
+            torch.cuda.synchronize()
+            res.append((model.arena().flat.clone(), tr.opt.m.clone(), tr.opt.v.clone(),
+                        model.postnet.convolutions[1][1].running_mean.clone(), torch.stack(losses)))
+        finally:
+            M.C_BLOCKS, M.FUSE_LN_MIN_ROWS = c_default, 16384
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+
+
 def test_fused_gemm_ln_bwd_step():
     """bf16: each FFT block's QKV data gradient carrying the previous block's LN2 backward
     (fs2_conv_gemm_ln_bwd, model.FUSE_LN_BWD) against the two-launch form: one forward +

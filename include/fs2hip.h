@@ -272,7 +272,8 @@ int fs2_weight_prep_batch(int dtype, const int64_t* jobs, int n_jobs, int64_t n_
  *                          0 = the tap-register halo kernel where its grid fills the chip
  *                          (default: 4-wave 128 x 64 tiles at 3 blocks per CU, 128 x 128 at 2 for
  *                          c_out <= 256), -1 = off (the halo kernels above), 1 = force the
- *                          128 x 64 tiles, 3 = force 128 x 128
+ *                          128 x 64 tiles, 3 = force 128 x 128, 5 = 8-wave 256 x 128 tiles at
+ *                          one block per CU (T and rows % 256 == 0)
  *   FS2_TUNE_WGRAD_BAND    band weight gradient (taps 9, and taps 3 / 5 whose channels are not
  *                          64-multiples): 0 = 4 waves per block with 2-slot rings (default),
  *                          1 = 4 waves with 4-slot rings, 2 = 8 waves, 2-slot, 3 = default blocks
@@ -338,6 +339,62 @@ int fs2_fft_block_bwd(const int64_t* blk, void* act, const void* x_t, int fuse_l
                       void* tmp, float* dx, void* prev_dy2_t, float* prev_dx1, int64_t rows,
                       int64_t batch, int64_t seq_len, const int64_t* lens, const uint64_t* seed,
                       float* side_ws, int64_t side_ws_bytes, void* stream, void* side_stream);
+
+/* ---------------------------------------------------------------- mel head per call
+ * model/fastspeech2.py:91-93 (mel_linear, then postnet(output) + output; PostNet
+ * transformer/Layers.py:67-137: Conv1d(k) + BatchNorm1d (batch statistics, running update,
+ * num_batches_tracked), tanh on all but the last, dropout) and its backward, bf16, issued from C
+ * in the order of model.MelHeadFn / PostNet (bitwise those).  `mh` is a host int64 table of
+ * FS2_MH_WORDS words: geometry, mel_linear's bf16 compute-layout weights, fp32 bias and
+ * gradient buffers, then FS2_MHL_WORDS words per PostNet layer.                             */
+enum { FS2_MH_NMEL = 0, FS2_MH_DIN, FS2_MH_DIM, FS2_MH_TAPS, FS2_MH_PAD, FS2_MH_LAYERS, FS2_MH_SITE,
+       FS2_MH_LIN_WF, FS2_MH_LIN_WB, FS2_MH_LIN_B, FS2_MH_GLIN_W, FS2_MH_GLIN_B, FS2_MH_LAYER0 };
+enum { FS2_MHL_W_F = 0, FS2_MHL_W_B, FS2_MHL_B, FS2_MHL_BN_G, FS2_MHL_BN_B, FS2_MHL_BN_RM,
+       FS2_MHL_BN_RV, FS2_MHL_BN_NBT, FS2_MHL_GW, FS2_MHL_GB, FS2_MHL_GBN_G, FS2_MHL_GBN_B,
+       FS2_MHL_WORDS };
+enum { FS2_MH_MAX_LAYERS = 8, FS2_MH_WORDS = FS2_MH_LAYER0 + FS2_MH_MAX_LAYERS * FS2_MHL_WORDS };
+enum { FS2_MHA_OUT = 0, FS2_MHA_POST = 1 };
+/* Forward: x_t (rows, d_in) bf16 decoder output -> act (fs2_mel_head_act_bytes) holding the
+ * mel_linear output (FS2_MHA_OUT) and postnet(out) + out (FS2_MHA_POST), fp32 (rows, n_mel),
+ * byte offsets from fs2_mel_head_act_offset.  Backward from d_out and / or d_post (either may be
+ * NULL, not both): dx (rows, d_in) fp32 is written; tmp: fs2_mel_head_tmp_bytes; weight
+ * gradients on side_stream with side_ws (>= fs2_mel_head_side_ws_bytes), reading act / tmp /
+ * x_t after the call returns: keep them until that stream is joined.                       */
+int64_t fs2_mel_head_act_bytes(const int64_t* mh, int64_t rows);
+int64_t fs2_mel_head_act_offset(const int64_t* mh, int64_t rows, int which);
+int64_t fs2_mel_head_tmp_bytes(const int64_t* mh, int64_t rows);
+int64_t fs2_mel_head_side_ws_bytes(const int64_t* mh, int64_t rows);
+int fs2_mel_head_fwd(const int64_t* mh, const void* x_t, void* act, int64_t rows, int64_t seq_len,
+                     float p, const uint64_t* seed, void* stream);
+int fs2_mel_head_bwd(const int64_t* mh, void* act, const void* x_t, const float* d_out,
+                     const float* d_post, void* tmp, float* dx, int64_t rows, int64_t seq_len,
+                     float p, const uint64_t* seed, float* side_ws, int64_t side_ws_bytes,
+                     void* stream, void* side_stream);
+
+/* ---------------------------------------------------------------- variance predictor per call
+ * model/modules.py:197-250 (2 x (Conv1d(k) -> ReLU -> LayerNorm -> dropout) -> Linear(., 1),
+ * padded rows masked to 0) and its backward, bf16, in the order of model.VariancePredictor.fwd
+ * / .bwd (bitwise those).  `vp`: host int64 table of FS2_VP_WORDS words.  Forward: x_t (rows,
+ * d) bf16 -> act (fs2_variance_predictor_act_bytes) whose FS2_VPA_PRED tensor is the (rows,)
+ * fp32 prediction.  Backward from dpred (rows,) fp32: the input gradient is ADDED into dx_acc
+ * (rows, d) fp32; tmp / side_ws / side_stream as the mel head.                              */
+enum { FS2_VP_D = 0, FS2_VP_FILTER, FS2_VP_TAPS, FS2_VP_PAD1, FS2_VP_PAD2, FS2_VP_SITE,
+       FS2_VP_W1_F, FS2_VP_W1_B, FS2_VP_B1, FS2_VP_LN1_G, FS2_VP_LN1_B,
+       FS2_VP_W2_F, FS2_VP_W2_B, FS2_VP_B2, FS2_VP_LN2_G, FS2_VP_LN2_B, FS2_VP_LIN_W, FS2_VP_LIN_B,
+       FS2_VP_G1_W, FS2_VP_G1_B, FS2_VP_GLN1_G, FS2_VP_GLN1_B, FS2_VP_G2_W, FS2_VP_G2_B,
+       FS2_VP_GLN2_G, FS2_VP_GLN2_B, FS2_VP_GLIN_W, FS2_VP_GLIN_B, FS2_VP_WORDS };
+enum { FS2_VPA_PRED = 0 };
+int64_t fs2_variance_predictor_act_bytes(const int64_t* vp, int64_t rows);
+int64_t fs2_variance_predictor_act_offset(const int64_t* vp, int64_t rows, int which);
+int64_t fs2_variance_predictor_tmp_bytes(const int64_t* vp, int64_t rows);
+int64_t fs2_variance_predictor_side_ws_bytes(const int64_t* vp, int64_t rows);
+int fs2_variance_predictor_fwd(const int64_t* vp, const void* x_t, void* act, int64_t rows,
+                               int64_t seq_len, const int64_t* lens, float p, const uint64_t* seed,
+                               void* stream);
+int fs2_variance_predictor_bwd(const int64_t* vp, void* act, const void* x_t, const float* dpred,
+                               void* tmp, float* dx_acc, int64_t rows, int64_t seq_len,
+                               const int64_t* lens, float p, const uint64_t* seed, float* side_ws,
+                               int64_t side_ws_bytes, void* stream, void* side_stream);
 
 /* Stand-in for one gradient all-reduce of the data-parallel step, for pricing the collective
  * schedule at N ranks on one GPU (train.CollectiveModel; not on the training path):

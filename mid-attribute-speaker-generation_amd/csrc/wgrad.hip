@@ -43,7 +43,6 @@ typedef unsigned short u16;
 typedef __bf16 bf16x8w __attribute__((ext_vector_type(8)));
 typedef short s16x4w __attribute__((ext_vector_type(4)));
 
-static __device__ __attribute__((aligned(128))) uint4 g_wb_zero[8];  // zero source line
 
 struct WgradBand {
   const u16* dy;
@@ -88,24 +87,52 @@ FS2_DEV void wb_vm(int ahead) {  // at most `ahead` bands of N LDS-DMA instructi
 
 }  // namespace
 
+namespace {
+template <int N, typename Fn>
+FS2_DEV void ww_static_for(Fn&& fn) {
+  if constexpr (N > 0) {
+    ww_static_for<N - 1>(fn);
+    fn(std::integral_constant<int, N - 1>{});
+  }
+}
+// ds_read_b64_tr_b16 at a per-lane base + a compile-time byte offset (the instruction's
+// 16-bit immediate): every fragment address of a main loop is one of a few per-lane bases
+template <int OFF>
+FS2_DEV s16x4w ww_tr(uint32_t base) {
+  static_assert(OFF >= 0 && OFF < 65536, "ds offset field");
+  s16x4w r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(base), "n"(OFF));
+  return r;
+}
+FS2_DEV bf16x8w ww_cat(s16x4w lo, s16x4w hi) {
+  return __builtin_bit_cast(bf16x8w, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+}  // namespace
+
 template <int TAPS, int S, int ST, int W>
 __global__ __launch_bounds__(64 * W, W == 8 ? 1 : 2) void conv_wgrad_band(WgradBand a) {
   constexpr int BO = 32, BC = 32, BR = 32 * S, NT = 64 * W;
   constexpr int HR = BR + TAPS - 1, RS = (HR + S - 1) / S, NF = S + TAPS - 1;
-  constexpr int DPOS = BR, XPOS = (S * RS + 15) / 16 * 16;  // image positions (64 B each)
+  constexpr int PB = 64;                                     // bytes per image position
+  constexpr int DPOS = BR, XPOS = (S * RS + 15) / 16 * 16;  // image positions
   constexpr int NQD = DPOS / 16, NQX = XPOS / 16, NQ = NQD + NQX;  // LDS-DMA per band
-  constexpr int STAGE_E = (DPOS + XPOS) * 32;                     // bf16 per ring slot
-  constexpr int RING_B = W * ST * STAGE_E * 2;
+  constexpr int STAGE_B = (DPOS + XPOS) * PB;                     // bytes per ring slot
+  constexpr int RING_B = W * ST * STAGE_B;
+  static_assert(RING_B < 65536 + W * ST * STAGE_B, "offsets");
   constexpr int QLD = BC * TAPS + 4;  // fp32 row stride of a dW-layout partial tile
   constexpr int RED_B = (W / 2) * (BO * QLD * 4 + 2 * 64 * 16);  // W / 2 partial tiles + bias
   static_assert(TAPS * 16 * 64 <= BO * QLD, "native partial fits a region");
-  constexpr int SMEM_B = RING_B > RED_B ? RING_B : RED_B;
   constexpr int MAXB = 1024;
+  // the band list sits behind the ring, inside the reduction region (used after the main loop):
+  // 77 KB in all, two blocks per CU
+  constexpr int LIST_B = RING_B + 4 * MAXB + 64;
+  constexpr int SMEM_B = LIST_B > RED_B ? LIST_B : RED_B;
   constexpr int LOOK = 2;  // halo fragments read ahead of their MFMAs
-  static_assert(NQ * (ST - 2 > 0 ? ST - 2 : 1) <= 63 && ST <= 5, "vmcnt bookkeeping");
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[SMEM_B + 2 * MAXB + 64];
-  short* blist = reinterpret_cast<short*>(smem + SMEM_B);
-  int* wcnt = reinterpret_cast<int*>(smem + SMEM_B + 2 * MAXB);
+  static_assert(NQ * (ST - 2 > 0 ? ST - 2 : 1) <= 63 && ST == 2, "vmcnt bookkeeping / the unrolled ring");
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[SMEM_B];
+  short* blist = reinterpret_cast<short*>(smem + RING_B);          // band index
+  short* brem = reinterpret_cast<short*>(smem + RING_B + 2 * MAXB);  // its rows below the length
+  int* wcnt = reinterpret_cast<int*>(smem + RING_B + 4 * MAXB);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -118,19 +145,24 @@ __global__ __launch_bounds__(64 * W, W == 8 ? 1 : 2) void conv_wgrad_band(WgradB
   const int to = wg / a.tiles_c, tc = wg - to * a.tiles_c;
   const int o0 = to * BO, c0 = tc * BC;
 
-  // bands holding a real row, in row order (wave ballots + prefix popcounts)
+  // bands holding a real row, in row order, with their rows below the length (the launcher
+  // admits lens only with nb_all <= MAXB).  In LDS: a global load of lens in the main loop
+  // would make the compiler wait vmcnt(0) there, draining the LDS-DMA ring every band.
   const int nbu = (int)(a.T / BR);
   const int nb_all = (int)(a.M / BR);
-  const bool use_list = a.lens != nullptr && nb_all <= MAXB;
+  const bool use_list = a.lens != nullptr;
   int nb = nb_all;
   if (use_list) {
     int total = 0;
     for (int k0 = 0; k0 < nb_all; k0 += NT) {
       const int k = k0 + tid;
       bool v = false;
+      int rem = 0;
       if (k < nb_all) {
         const int b = k / nbu;
-        v = (int64_t)(k - b * nbu) * BR < a.lens[b];
+        const int64_t r = a.lens[b] - (int64_t)(k - b * nbu) * BR;
+        v = r > 0;
+        rem = r < BR ? (int)r : BR;
       }
       const uint64_t mask = __ballot(v);
       if (lane == 0) wcnt[wave] = __popcll(mask);
@@ -139,7 +171,10 @@ __global__ __launch_bounds__(64 * W, W == 8 ? 1 : 2) void conv_wgrad_band(WgradB
       for (int w = 0; w < wave; ++w) before += wcnt[w];
       const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
-      if (v) blist[before + below] = (short)k;
+      if (v) {
+        blist[before + below] = (short)k;
+        brem[before + below] = (short)rem;
+      }
       for (int w = 0; w < W; ++w) total += wcnt[w];
       __syncthreads();
     }
@@ -149,28 +184,33 @@ __global__ __launch_bounds__(64 * W, W == 8 ? 1 : 2) void conv_wgrad_band(WgradB
 
   // the 32-B halves of position P swap at (P >> 2) & 1 (16-B chunk index ^ 2)
   auto swz = [](int P) { return ((P >> 2) & 1) << 1; };
-  const u16* zero = reinterpret_cast<const u16*>(g_wb_zero);
-  const int lpos = lane >> 2, lch = lane & 3;
+  // LDS-DMA through buffer descriptors: dy from row 0, x from row -pad; the band's first row
+  // rides in the scalar offset
+  const auto dy_rs = buf_rsrc(a.dy, a.M * a.ldy * 2);
+  const auto x_rs = buf_rsrc(a.x - (int64_t)a.pad * a.ldx, (a.M + a.pad) * a.ldx * 2);
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) unsigned char*)smem;
+  unsigned char* ring = smem + wave * ST * STAGE_B;
 
   auto issue = [&](int i, int slot) {
-    const int k = __builtin_amdgcn_readfirstlane(use_list ? (int)blist[wave + W * i] : wave + W * i);
+    const int kk = wave + W * i;
+    const int k = __builtin_amdgcn_readfirstlane(use_list ? (int)blist[kk] : kk);
+    const int rem = __builtin_amdgcn_readfirstlane(use_list ? (int)brem[kk] : BR);
     const int b = k / nbu, t0 = (k - b * nbu) * BR;
-    const int64_t u0 = (int64_t)b * a.T;
-    int len = (int)a.T;
-    if (a.lens) {
-      const int64_t l = a.lens[b];
-      len = l < a.T ? (int)l : (int)a.T;
-    }
-    u16* Ds = reinterpret_cast<u16*>(smem) + (wave * ST + slot) * STAGE_E;
-    u16* Xs = Ds + DPOS * 32;
+    const int64_t r0 = (int64_t)b * a.T + t0;
+    unsigned char* St = ring + slot * STAGE_B;
+    // per-lane offsets recomputed here (an opaque lane id keeps them out of the registers
+    // held across the loop)
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const int lpos = ln >> 2, lch = ln & 3;
 #pragma unroll
     for (int qi = 0; qi < NQD; ++qi) {
       const int P = qi * 16 + lpos;
       const int h = (P & 31) * S + (P >> 5);
       const int col = o0 + ((lch ^ swz(P)) << 3);
-      const int t = t0 + h;
-      const u16* src = (t < len && col < a.Cout) ? a.dy + (u0 + t) * a.ldy + col : zero;
-      wb_glds16(src, Ds + qi * 16 * 32);
+      const bool ok = h < rem && col < a.Cout;
+      glds16_buf(dy_rs, St + qi * 16 * PB, ok ? (uint32_t)((h * a.ldy + col) * 2) : kOOB,
+                 (uint32_t)(r0 * a.ldy * 2));
     }
 #pragma unroll
     for (int qi = 0; qi < NQX; ++qi) {
@@ -179,8 +219,8 @@ __global__ __launch_bounds__(64 * W, W == 8 ? 1 : 2) void conv_wgrad_band(WgradB
       const int col = c0 + ((lch ^ swz(P)) << 3);
       const int t = t0 - a.pad + h;
       const bool ok = P < S * RS && h < HR && t >= 0 && t < (int)a.T && col < a.Cin;
-      const u16* src = ok ? a.x + (u0 + t) * a.ldx + col : zero;
-      wb_glds16(src, Xs + qi * 16 * 32);
+      glds16_buf(x_rs, St + (DPOS + qi * 16) * PB, ok ? (uint32_t)((h * a.ldx + col) * 2) : kOOB,
+                 (uint32_t)(r0 * a.ldx * 2));
     }
   };
 
@@ -197,40 +237,42 @@ __global__ __launch_bounds__(64 * W, W == 8 ? 1 : 2) void conv_wgrad_band(WgradB
 #pragma unroll
   for (int e = 0; e < 8; ++e) ones[e] = (__bf16)1.0f;
 
-  // fragment of 32 positions from pb, 16 columns at col0: positions pb + {4g+q} and + 16
-  auto frag = [&](const u16* img, int pb, int col0) -> bf16x8w {
+  // per-lane fragment bases: the fragment of 32 positions from pb (rows pb + 4g + q and + 16),
+  // 16 columns at col0, reads base(pb mod 8, col0) + (pb - pb mod 8) PB (+ 16 PB): the swizzle
+  // of position pb + L depends on pb only through pb mod 8
+  const int L = 4 * g + q;
+  auto fbase = [&](int r, int col0, int img) -> uint32_t {
     const int lc = (col0 >> 3) + (p >> 1);
-    const int R0 = pb + 4 * g + q, R1 = R0 + 16;
-    const s16x4w lo = wb_tr16(img + R0 * 32 + ((lc ^ swz(R0)) << 3) + ((p & 1) << 2));
-    const s16x4w hi = wb_tr16(img + R1 * 32 + ((lc ^ swz(R1)) << 3) + ((p & 1) << 2));
-    return __builtin_bit_cast(bf16x8w, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+    return lds0 + (uint32_t)(wave * ST * STAGE_B + img + (r + L) * PB + ((lc ^ swz(r + L)) << 4) +
+                             ((p & 1) << 3));
   };
+  uint32_t bA0 = fbase(0, 0, 0), bA1 = fbase(0, 16, 0);
+  uint32_t bF[8][2];
+#pragma unroll
+  for (int r = 0; r < 8; ++r)
+#pragma unroll
+    for (int ic = 0; ic < 2; ++ic) bF[r][ic] = fbase(r, ic * 16, DPOS * PB);
 
-  auto compute = [&](int slot) {
-    const u16* Ds = reinterpret_cast<const u16*>(smem) + (wave * ST + slot) * STAGE_E;
-    const u16* Xs = Ds + DPOS * 32;
+  auto compute = [&](auto slot_c) {
+    constexpr int SO = decltype(slot_c)::value * STAGE_B;
     bf16x8w A[S][2], F[LOOK + 1][2];
-#pragma unroll
-    for (int s = 0; s < S; ++s)
-#pragma unroll
-      for (int io = 0; io < 2; ++io) A[s][io] = frag(Ds, s * 32, io * 16);
-#pragma unroll
-    for (int f = 0; f < LOOK && f < NF; ++f)
-#pragma unroll
-      for (int ic = 0; ic < 2; ++ic) F[f][ic] = frag(Xs, (f % S) * RS + f / S, ic * 16);
-#pragma unroll
-    for (int f = 0; f < NF; ++f) {
-      if (f + LOOK < NF) {
-#pragma unroll
-        for (int ic = 0; ic < 2; ++ic)
-          F[(f + LOOK) % (LOOK + 1)][ic] = frag(Xs, ((f + LOOK) % S) * RS + (f + LOOK) / S, ic * 16);
-      }
-      // wait for the reads up to F[f]: the younger ones (F[f + 1 .. f + LOOK]) may stay in flight
-      const int younger = (NF - 1 - f < LOOK ? NF - 1 - f : LOOK) * 4;
-      if (younger >= 8) wb_lgkm<8>();
-      else if (younger == 4) wb_lgkm<4>();
-      else wb_lgkm<0>();
-      const bf16x8w* Ff = F[f % (LOOK + 1)];
+    ww_static_for<S>([&](auto sc) {
+      constexpr int s = decltype(sc)::value;
+      A[s][0] = ww_cat(ww_tr<SO + s * 32 * PB>(bA0), ww_tr<SO + (s * 32 + 16) * PB>(bA0));
+      A[s][1] = ww_cat(ww_tr<SO + s * 32 * PB>(bA1), ww_tr<SO + (s * 32 + 16) * PB>(bA1));
+    });
+    auto rdF = [&](auto fc, bf16x8w (&dst)[2]) {
+      constexpr int f = decltype(fc)::value;
+      constexpr int pb = (f % S) * RS + f / S, r = pb & 7, off = SO + (pb - r) * PB;
+      dst[0] = ww_cat(ww_tr<off>(bF[r][0]), ww_tr<off + 16 * PB>(bF[r][0]));
+      dst[1] = ww_cat(ww_tr<off>(bF[r][1]), ww_tr<off + 16 * PB>(bF[r][1]));
+    };
+    ww_static_for<LOOK>([&](auto fc) { rdF(fc, F[decltype(fc)::value]); });
+    ww_static_for<NF>([&](auto fc) {
+      constexpr int f = decltype(fc)::value;
+      if constexpr (f + LOOK < NF) rdF(std::integral_constant<int, f + LOOK>{}, F[(f + LOOK) % (LOOK + 1)]);
+      constexpr int younger = (NF - 1 - f < LOOK ? NF - 1 - f : LOOK) * 4;
+      wb_lgkm<younger>();
 #pragma unroll
       for (int s = 0; s < S; ++s) {
         const int j = f - s;
@@ -239,23 +281,34 @@ __global__ __launch_bounds__(64 * W, W == 8 ? 1 : 2) void conv_wgrad_band(WgradB
         for (int io = 0; io < 2; ++io)
 #pragma unroll
           for (int ic = 0; ic < 2; ++ic)
-            acc[j][io][ic] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[s][io], Ff[ic], acc[j][io][ic],
-                                                                     0, 0, 0);
+            acc[j][io][ic] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[s][io], F[f % (LOOK + 1)][ic],
+                                                                     acc[j][io][ic], 0, 0, 0);
         if (j == 0 && do_bias) {
 #pragma unroll
           for (int io = 0; io < 2; ++io)
             accb[io] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[s][io], ones, accb[io], 0, 0, 0);
         }
       }
-    }
+    });
   };
 
-  for (int i = 0; i < ST - 1 && i < nbw; ++i) issue(i, i);
+  // per-wave 2-slot ring, no barrier: wait for this wave's band i (counted vmcnt), refill the
+  // other slot with band i + 1, compute band i; the fragment bases step to the other slot
+  // after each band (one add per base)
+  if (nbw > 0) issue(0, 0);
+  int dslot = STAGE_B;
   for (int i = 0; i < nbw; ++i) {
-    const int ahead = nbw - 1 - i < ST - 2 ? nbw - 1 - i : ST - 2;
-    wb_vm<NQ>(ahead);
-    if (i + ST - 1 < nbw) issue(i + ST - 1, (i + ST - 1) % ST);
-    compute(i % ST);
+    wb_vm<NQ>(0);
+    if (i + 1 < nbw) issue(i + 1, (i + 1) & 1);
+    compute(std::integral_constant<int, 0>{});
+    bA0 += dslot;
+    bA1 += dslot;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      bF[r][0] += dslot;
+      bF[r][1] += dslot;
+    }
+    dslot = -dslot;
   }
 
   // fixed-order cross-wave sum, a tree through LDS: waves [h, 2h) write their partials, waves
@@ -375,24 +428,6 @@ struct WgradWide {
   const int64_t* lens;
 };
 
-namespace {
-template <int N, typename Fn>
-FS2_DEV void ww_static_for(Fn&& fn) {
-  if constexpr (N > 0) {
-    ww_static_for<N - 1>(fn);
-    fn(std::integral_constant<int, N - 1>{});
-  }
-}
-// ds_read_b64_tr_b16 at a per-lane base + a compile-time byte offset (the instruction's
-// 16-bit immediate): every fragment address of the main loop is one of a few per-lane bases
-template <int OFF>
-FS2_DEV s16x4w ww_tr(uint32_t base) {
-  static_assert(OFF >= 0 && OFF < 65536, "ds offset field");
-  s16x4w r;
-  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(base), "n"(OFF));
-  return r;
-}
-}  // namespace
 
 template <int TAPS, int ST>
 __global__ __launch_bounds__(512, 4) void conv_wgrad_wide(WgradWide a) {
@@ -684,6 +719,7 @@ int conv_wgrad_band_launch(const void* dy, int64_t ldy, const void* x, int64_t l
   if (c_in % 8 || c_out % 8 || ldx % 8 || ldy % 8 || ((uintptr_t)dy & 15) || ((uintptr_t)x & 15))
     return kNotEligible;
   if (seq_len % BR || rows % seq_len || rows / BR > (1 << 15)) return kNotEligible;
+  if (lens && rows / BR > 1024) return kNotEligible;  // the kernel's LDS band list
   if (c_in < 32 || c_out < 32) return kNotEligible;
   // taps 3 / 5 with 64-multiple channels (PostNet 512, variance predictors) stay on the split-K
   // halo kernel: step 6.91 vs 6.98 ms with the band kernel there (profiles/r4_ab_experiments.txt)
@@ -702,19 +738,11 @@ int conv_wgrad_band_launch(const void* dy, int64_t ldy, const void* x, int64_t l
   WgradBand a{(const u16*)dy, ldy, (const u16*)x, ldx, dw, db, rows, seq_len, (int)c_in,
               (int)c_out, pad, to, tc, lens};
   const unsigned grid = (unsigned)(to * tc);
-  // variant (FS2_TUNE_WGRAD_BAND): 0 = 4 waves x 2-slot rings (default), 1 = 4 waves x 4-slot
-  // rings, 2 = 8 waves x 2-slot rings.  Alone the 8-wave blocks are the fastest (decoder k=9
-  // 98 vs 133 us), but their 160 KB of LDS per CU starve the main-stream kernels they run
-  // beside: step 7.61 vs 7.07 ms (profiles/r4_ab_experiments.txt)
-  const int v = g_tune[FS2_TUNE_WGRAD_BAND];
-#define FS2_WB(T_)                                                         \
-  if (v == 1) conv_wgrad_band<T_, 2, 4, 4><<<grid, 256, 0, st>>>(a);       \
-  else if (v == 2) conv_wgrad_band<T_, 2, 2, 8><<<grid, 512, 0, st>>>(a);  \
-  else conv_wgrad_band<T_, 2, 2, 4><<<grid, 256, 0, st>>>(a);
-  if (taps == 9) { FS2_WB(9) }
-  else if (taps == 5) { FS2_WB(5) }
-  else { FS2_WB(3) }
-#undef FS2_WB
+  // (4-slot rings and 8-wave blocks measured slower in the step and were removed in round 5:
+  // profiles/r4_ab_experiments.txt)
+  if (taps == 9) conv_wgrad_band<9, 2, 2, 4><<<grid, 256, 0, st>>>(a);
+  else if (taps == 5) conv_wgrad_band<5, 2, 2, 4><<<grid, 256, 0, st>>>(a);
+  else conv_wgrad_band<3, 2, 2, 4><<<grid, 256, 0, st>>>(a);
   return launch_status("fs2_conv_wgrad(bf16, band)");
 }
 

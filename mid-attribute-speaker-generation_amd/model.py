@@ -207,6 +207,10 @@ FUSE_LN_BWD = True
 # FFTBlock.fwd / .bwd below: bitwise the same results, a fifth of the host time); the tests
 # compare it against the per-kernel path by clearing it
 C_BLOCKS = True
+# fs2_mel_head_* descriptor geometry (include/fs2hip.h: FS2_MH_LAYER0 + FS2_MH_MAX_LAYERS x
+# FS2_MHL_WORDS words)
+MH_MAX_LAYERS = 8
+MH_WORDS = 12 + MH_MAX_LAYERS * 12
 
 
 def _t(f, t):
@@ -672,7 +676,33 @@ class VariancePredictor(nn.Module):
         _conv_prep(self.conv_layer.conv1d_1.conv, cdt, jobs)
         _conv_prep(self.conv_layer.conv1d_2.conv, cdt, jobs)
 
+    def cdesc(self):
+        """fs2_variance_predictor_* descriptor (include/fs2hip.h, FS2_VP_*), cached as
+        FFTBlock.cdesc."""
+        c = self.conv_layer
+        c1, c2 = c.conv1d_1.conv, c.conv1d_2.conv
+        ln1, ln2, lin = c.layer_norm_1, c.layer_norm_2, self.linear_layer
+        key = (c1._w_fwd.data_ptr(), c2._w_fwd.data_ptr(), _g(c1.weight).data_ptr(),
+               c1.weight.data_ptr(), self.site)
+        d = self.__dict__.get("_cdesc")
+        if d is not None and d[0] == key:
+            return d[1]
+        P = lambda t: t.data_ptr()
+        w = [c1.c_in, c1.c_out, c1.k, c1.padding, c2.padding, self.site,
+             P(c1._w_fwd), P(c1._w_bwd), P(c1.bias), P(ln1.weight), P(ln1.bias),
+             P(c2._w_fwd), P(c2._w_bwd), P(c2.bias), P(ln2.weight), P(ln2.bias), P(lin.weight),
+             P(lin.bias), P(_g(c1.weight)), P(_g(c1.bias)), P(_g(ln1.weight)), P(_g(ln1.bias)),
+             P(_g(c2.weight)), P(_g(c2.bias)), P(_g(ln2.weight)), P(_g(ln2.bias)),
+             P(_g(lin.weight)), P(_g(lin.bias))]
+        if c2.c_in != c1.c_out or c2.k != c1.k or lin.out_features != 1:
+            raise RuntimeError("fs2_variance_predictor_*: unexpected geometry (modules.py:197-250)")
+        arr = (ctypes.c_int64 * len(w))(*w)
+        self._cdesc = (key, arr)
+        return arr
+
     def fwd(self, x, x_t, lens, B, T, ctx):
+        if _c_blocks(ctx, x.shape[1]) and x_t is not None:
+            return self._fwd_c(x_t, lens, B, T, ctx)
         c = self.conv_layer
         c1, c2 = c.conv1d_1.conv, c.conv1d_2.conv
         M = x.shape[0]
@@ -692,8 +722,42 @@ class VariancePredictor(nn.Module):
         saved = (x_c, h1, u1_c, h2, xh1, rs1, xh2, rs2, p, ctx, lens, T)
         return pred.view(B, T), saved
 
+    def _fwd_c(self, x_t, lens, B, T, ctx):
+        """One fs2_variance_predictor_fwd call (bitwise the per-kernel path below)."""
+        desc = self.cdesc()
+        M = x_t.shape[0]
+        p = ctx.p(self.p)
+        act = torch.empty(K.lib.fs2_variance_predictor_act_bytes(desc, M), dtype=torch.uint8,
+                          device=x_t.device)
+        K.lib.fs2_variance_predictor_fwd(desc, x_t.data_ptr(), act.data_ptr(), M, T,
+                                         0 if lens is None else lens.data_ptr(), p,
+                                         ctx.seed.data_ptr() if p > 0 else None, K.stream())
+        o = K.lib.fs2_variance_predictor_act_offset(desc, M, 0)
+        pred = act[o:o + M * 4].view(torch.float32)
+        return pred.view(B, T), ("C", act, x_t, lens, T, p, ctx)
+
+    def _bwd_c(self, dpred, saved, dx_acc):
+        _, act, x_t, lens, T, p, ctx = saved
+        desc = self.cdesc()
+        M = x_t.shape[0]
+        dev = x_t.device
+        dpred = dpred.contiguous()
+        tmp = torch.empty(K.lib.fs2_variance_predictor_tmp_bytes(desc, M), dtype=torch.uint8,
+                          device=dev)
+        need = K.lib.fs2_variance_predictor_side_ws_bytes(desc, M)
+        side = ctx.side.cuda_stream if ctx.side is not None else None
+        ws = ctx._side_ws(need, dev) if side is not None else K.ws(need, dev)
+        K.lib.fs2_variance_predictor_bwd(desc, act.data_ptr(), x_t.data_ptr(), dpred.data_ptr(),
+                                         tmp.data_ptr(), dx_acc.data_ptr(), M, T,
+                                         0 if lens is None else lens.data_ptr(), p,
+                                         ctx.seed.data_ptr() if p > 0 else None, ws.data_ptr(),
+                                         ws.numel() * 4, K.stream(), side)
+        ctx.keep.append((tmp, act, x_t))  # read by the side stream until the join
+
     def bwd(self, dpred, saved, dx_acc):
         """Backward; the input gradient is *added* into ``dx_acc`` (fp32, in place)."""
+        if isinstance(saved[0], str):
+            return self._bwd_c(dpred, saved, dx_acc)
         x_c, h1, u1_c, h2, xh1, rs1, xh2, rs2, p, ctx, lens, T = saved
         c = self.conv_layer
         c1, c2 = c.conv1d_1.conv, c.conv1d_2.conv
@@ -757,6 +821,32 @@ class PostNet(nn.Module):
     def prep(self, cdt, jobs=None):
         for layer in self.convolutions:
             _conv_prep(layer[0].conv, cdt, jobs)
+
+    def mel_head_desc(self, lin):
+        """fs2_mel_head_* descriptor (include/fs2hip.h, FS2_MH_* / FS2_MHL_*) of mel_linear
+        ``lin`` followed by this PostNet, cached as FFTBlock.cdesc."""
+        c0 = self.convolutions[0][0].conv
+        key = (lin._w_fwd.data_ptr(), c0._w_fwd.data_ptr(), _g(c0.weight).data_ptr(),
+               c0.weight.data_ptr(), _g(lin.weight).data_ptr(), self.site)
+        d = self.__dict__.get("_cdesc")
+        if d is not None and d[0] == key:
+            return d[1]
+        P = lambda t: t.data_ptr()
+        n = len(self.convolutions)
+        if n > MH_MAX_LAYERS:
+            raise RuntimeError(f"fs2_mel_head_*: at most {MH_MAX_LAYERS} PostNet layers")
+        w = [lin.out_features, lin.in_features, c0.c_out, c0.k, c0.padding, n, self.site,
+             P(lin._w_fwd), P(lin._w_bwd), P(lin.bias), P(_g(lin.weight)), P(_g(lin.bias))]
+        for conv, bn in ((layer[0].conv, layer[1]) for layer in self.convolutions):
+            if conv.k != c0.k or conv.padding != c0.padding:
+                raise RuntimeError("fs2_mel_head_*: PostNet convs of one kernel size")
+            w += [P(conv._w_fwd), P(conv._w_bwd), P(conv.bias), P(bn.weight), P(bn.bias),
+                  P(bn.running_mean), P(bn.running_var), P(bn.num_batches_tracked),
+                  P(_g(conv.weight)), P(_g(conv.bias)), P(_g(bn.weight)), P(_g(bn.bias))]
+        w += [0] * (MH_WORDS - len(w))
+        arr = (ctypes.c_int64 * len(w))(*w)
+        self._cdesc = (key, arr)
+        return arr
 
     def fwd(self, x, x_t, B, T, ctx):
         """x: (M, n_mel) mel_linear output; returns postnet(x) + x."""
@@ -1074,6 +1164,21 @@ class MelHeadFn(torch.autograd.Function):
         lin = m.mel_linear
         M = x.shape[0]
         x_c = x_t if x_t.numel() else x
+        if _c_blocks(ctx, x.shape[1]) and x_t.numel() and m.postnet.training:
+            # one fs2_mel_head_fwd call: mel_linear + PostNet (bitwise the path below)
+            desc = m.postnet.mel_head_desc(lin)
+            p = ctx.p(0.5)
+            act = torch.empty(K.lib.fs2_mel_head_act_bytes(desc, M), dtype=torch.uint8,
+                              device=x.device)
+            K.lib.fs2_mel_head_fwd(desc, x_c.data_ptr(), act.data_ptr(), M, T, p,
+                                   ctx.seed.data_ptr() if p > 0 else None, K.stream())
+            n_mel = lin.out_features
+            o = K.lib.fs2_mel_head_act_offset(desc, M, 0)
+            po = K.lib.fs2_mel_head_act_offset(desc, M, 1)
+            out = act[o:o + M * n_mel * 4].view(torch.float32)
+            post = act[po:po + M * n_mel * 4].view(torch.float32)
+            fctx.m, fctx.saved = m, ("C", act, x_c, p, B, T, ctx)
+            return out.view(B, T, -1), post.view(B, T, -1)
         out = K.conv_gemm(x_c, lin._w_fwd, M, T, lin.in_features, lin.out_features, 1, 0,
                           bias=lin.bias)
         out_t = K.cast_bf16(out) if ctx.copy is not None else None
@@ -1084,6 +1189,8 @@ class MelHeadFn(torch.autograd.Function):
     @staticmethod
     def backward(fctx, d_out, d_post):
         m = fctx.m
+        if isinstance(fctx.saved[0], str):
+            return MelHeadFn._backward_c(fctx, d_out, d_post)
         x_c, s, B, T, ctx = fctx.saved
         lin = m.mel_linear
         M = x_c.shape[0]
@@ -1099,6 +1206,35 @@ class MelHeadFn(torch.autograd.Function):
         dm_c = K.cast_bf16(dm) if ctx.copy is not None else dm
         ctx.wgrad(dm_c, x_c, _g(lin.weight), M, T, lin.in_features, n_mel, 1, 0, db=_g(lin.bias))
         dx = K.conv_gemm(dm_c, lin._w_bwd, M, T, n_mel, lin.in_features, 1, 0)
+        ctx.notify([lin.weight, lin.bias])
+        fctx.saved = None
+        return None, dx, None, None, None, None, None
+
+    @staticmethod
+    def _backward_c(fctx, d_out, d_post):
+        m = fctx.m
+        _, act, x_c, p, B, T, ctx = fctx.saved
+        lin = m.mel_linear
+        M = x_c.shape[0]
+        n_mel = lin.out_features
+        dev = x_c.device
+        d_out = d_out.contiguous().view(M, n_mel) if d_out is not None else None
+        d_post = d_post.contiguous().view(M, n_mel) if d_post is not None else None
+        if d_out is None and d_post is None:
+            d_out = K.zeros((M, n_mel), dev)
+        desc = m.postnet.mel_head_desc(lin)
+        tmp = torch.empty(K.lib.fs2_mel_head_tmp_bytes(desc, M), dtype=torch.uint8, device=dev)
+        need = K.lib.fs2_mel_head_side_ws_bytes(desc, M)
+        side = ctx.side.cuda_stream if ctx.side is not None else None
+        ws = ctx._side_ws(need, dev) if side is not None else K.ws(need, dev)
+        dx = torch.empty((M, lin.in_features), dtype=torch.float32, device=dev)
+        P = lambda t: None if t is None else t.data_ptr()
+        K.lib.fs2_mel_head_bwd(desc, act.data_ptr(), x_c.data_ptr(), P(d_out), P(d_post),
+                               tmp.data_ptr(), dx.data_ptr(), M, T, p,
+                               ctx.seed.data_ptr() if p > 0 else None,
+                               ws.data_ptr(), ws.numel() * 4, K.stream(), side)
+        ctx.keep.append((tmp, act, x_c))  # read by the side stream until the join
+        ctx.notify(postnet_param_order(m.postnet))
         ctx.notify([lin.weight, lin.bias])
         fctx.saved = None
         return None, dx, None, None, None, None, None

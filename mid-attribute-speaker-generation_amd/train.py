@@ -99,16 +99,21 @@ class CollectiveModel:
     """Stand-in collectives for pricing the data-parallel step at ``ranks`` ranks on ONE GPU
     (measurement only: ``scripts/dp_collective_model.py``, ``profiles/r5_dp_collective_model.txt``).
 
-    A bucket's ring all-reduce of S bytes is replaced by ``fs2_collective_standin`` on the stream
-    the real collective would be issued from: ``blocks`` workgroups (RCCL's channels) that read
-    and write back 2 (n - 1) / n * S bytes of the bucket (values unchanged) over
-    2 (n - 1) / n * S / busbw + latency -- the collective's CU occupancy, HBM traffic and
-    duration, without the interconnect.  The step's 3-float all-reduce of the loss
-    denominators becomes a one-workgroup stand-in of ``latency_us`` on the main stream, and
-    the denominators stay local, so the step's values are the single-GPU step's."""
+    A bucket's ring all-reduce of S bytes is replaced by ``fs2_collective_standin``:
+    ``blocks`` workgroups (RCCL's channels) that read and write back 2 (n - 1) / n * S bytes of
+    the bucket (values unchanged) over 2 (n - 1) / n * S / busbw + latency -- the collective's
+    CU occupancy, HBM traffic and duration, without the interconnect.  Like ProcessGroupNCCL,
+    which runs a collective on its own stream after that stream waits on the issuing stream,
+    the stand-in runs on a stream of its own gated by an event of the issuing stream
+    (``inline=True``: on the issuing stream itself, so later work there queues behind it).  The
+    step's 3-float all-reduce of the loss denominators becomes a one-workgroup stand-in of
+    ``latency_us`` on the main stream, and the denominators stay local, so the step's values are
+    the single-GPU step's."""
 
-    def __init__(self, ranks=8, busbw_gbs=300.0, blocks=32, latency_us=12.0):
+    def __init__(self, ranks=8, busbw_gbs=300.0, blocks=32, latency_us=12.0, inline=False):
         self.ranks, self.busbw, self.blocks, self.lat = int(ranks), float(busbw_gbs), int(blocks), float(latency_us)
+        self.inline = bool(inline)
+        self.stream = None
 
     def wire_bytes(self, nbytes):
         return 2.0 * (self.ranks - 1) / self.ranks * nbytes
@@ -118,8 +123,21 @@ class CollectiveModel:
 
     def all_reduce(self, t):
         nb = t.numel() * t.element_size()
-        K.lib.fs2_collective_standin(K.ptr(t), t.numel(), int(2 * self.wire_bytes(nb)),
-                                     self.blocks, self.duration_ns(nb), K.stream())
+        if self.inline:
+            K.lib.fs2_collective_standin(K.ptr(t), t.numel(), int(2 * self.wire_bytes(nb)),
+                                         self.blocks, self.duration_ns(nb), K.stream())
+            return
+        if self.stream is None:
+            self.stream = torch.cuda.Stream()
+        self.stream.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(self.stream):
+            K.lib.fs2_collective_standin(K.ptr(t), t.numel(), int(2 * self.wire_bytes(nb)),
+                                         self.blocks, self.duration_ns(nb), K.stream())
+
+    def join(self):
+        """The current stream waits for every stand-in collective issued so far (work.wait())."""
+        if self.stream is not None:
+            torch.cuda.current_stream().wait_stream(self.stream)
 
     def small(self, t):
         K.lib.fs2_collective_standin(K.ptr(t), t.numel(), 0, 1, int(self.lat * 1e3), K.stream())
@@ -156,7 +174,7 @@ class GradBuckets:
         # process (profiles/r3_ab_experiments.txt: separate / high-priority communication
         # streams measured 1.04-2.8x slower steps)
         self.producers = None
-        self.standin = None  # CollectiveModel.all_reduce: stand-in collectives (no process group)
+        self.standin = None  # a CollectiveModel: stand-in collectives (no process group)
         self.log = None  # optional list: bucket launches are appended (tests)
         del index
         self.reset()
@@ -174,7 +192,7 @@ class GradBuckets:
         prods = [st for st in (self.producers() if self.producers else ()) if st is not None]
         if cur is None or not prods:
             if self.standin is not None:
-                self.standin(self.arena.grad[s:e])
+                self.standin.all_reduce(self.arena.grad[s:e])
                 return
             self.works.append(dist.all_reduce(self.arena.grad[s:e], group=self.group,
                                               async_op=True))
@@ -191,7 +209,7 @@ class GradBuckets:
         self._issue = issue
         with torch.cuda.stream(issue):
             if self.standin is not None:
-                self.standin(self.arena.grad[s:e])
+                self.standin.all_reduce(self.arena.grad[s:e])
             else:
                 self.works.append(dist.all_reduce(self.arena.grad[s:e], group=self.group,
                                                   async_op=True))
@@ -209,6 +227,8 @@ class GradBuckets:
             self.next += 1
         for w in self.works:
             w.wait()  # stream-ordered: the clip/Adam kernels queue behind the collectives
+        if self.standin is not None:
+            self.standin.join()
         if getattr(self, "_issue", None) is not None:
             torch.cuda.current_stream().wait_stream(self._issue)
             self._issue = None
@@ -265,9 +285,9 @@ class Trainer:
         if self.cm is not None:
             arena = model.arena()
             self.buckets = GradBuckets(arena, None, bucket_bytes)
-            self.buckets.standin = self.cm.all_reduce
-            # comm_stream: the alternative schedule -- each bucket's collective on a stream of
-            # its own, event-gated on the main stream and on the weight-gradient stream
+            self.buckets.standin = self.cm
+            # comm_stream: issue each bucket from a stream of its own, event-gated on the main
+            # stream and on the weight-gradient stream (default: from the weight-gradient stream)
             cs = torch.cuda.Stream() if comm_stream else None
             self.buckets.producers = (lambda: (model._side, cs)) if cs is not None else (lambda: (model._side,))
             model._hooks["grad"] = self.buckets.ready

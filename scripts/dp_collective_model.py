@@ -3,8 +3,11 @@ with every bucket's all-reduce replaced by a stand-in on the stream the real col
 issued from (train.CollectiveModel -> fs2_collective_standin: RCCL-like CU occupancy, HBM
 traffic 2 (n-1)/n S read + written, paced to 2 (n-1)/n S / busbw + latency).  Schedules:
   side      the default: each bucket issued from the weight-gradient stream, event-gated on
-            the main stream, as soon as its parameters are final
-  comm      a stream of its own per the collective, event-gated on main + side streams
+            the main stream, as soon as its parameters are final; the collective then runs on
+            a stream of its own gated on the issuing stream (as ProcessGroupNCCL does)
+  comm      issued from a stream of its own, event-gated on the main + weight-gradient streams
+  inline    what if the collective ran ON the issuing (weight-gradient) stream: every later
+            weight gradient queues behind it
   bucket=B  bucket size B MB (default 32; 139 = one bucket after the backward: no overlap)
 Interleaved rounds in one process; prints ms/step per variant and the predicted N-rank
 throughput (N x valid frames / step).
@@ -49,12 +52,14 @@ def main():
     for bk in (16, 64, 160):
         variants.append((f"side   bucket={bk:<3d} busbw={bw0:.0f}", dict(bw=bw0, bucket=bk, comm=False)))
     variants.append((f"comm   bucket=32  busbw={bw0:.0f}", dict(bw=bw0, bucket=32, comm=True)))
+    variants.append((f"inline bucket=32  busbw={bw0:.0f}", dict(bw=bw0, bucket=32, comm=False, inline=True)))
 
     def trainer(cfg):
         model._hooks["grad"] = None
         if cfg is None:
             return TR.Trainer(model, pp, mc, tc)
-        cm = TR.CollectiveModel(ranks=args.ranks, busbw_gbs=cfg["bw"], blocks=args.blocks)
+        cm = TR.CollectiveModel(ranks=args.ranks, busbw_gbs=cfg["bw"], blocks=args.blocks,
+                                inline=cfg.get("inline", False))
         return TR.Trainer(model, pp, mc, tc, collective_model=cm,
                           bucket_bytes=cfg["bucket"] << 20, comm_stream=cfg["comm"])
 

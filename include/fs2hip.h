@@ -272,8 +272,7 @@ int fs2_weight_prep_batch(int dtype, const int64_t* jobs, int n_jobs, int64_t n_
  *                          0 = the tap-register halo kernel where its grid fills the chip
  *                          (default: 4-wave 128 x 64 tiles at 3 blocks per CU, 128 x 128 at 2 for
  *                          c_out <= 256), -1 = off (the halo kernels above), 1 = force the
- *                          128 x 64 tiles, 3 = force 128 x 128, 5 = 8-wave 256 x 128 tiles at
- *                          one block per CU (T and rows % 256 == 0)
+ *                          128 x 64 tiles, 3 = force 128 x 128
  *   FS2_TUNE_WGRAD_BAND    band weight gradient (taps 9, and taps 3 / 5 whose channels are not
  *                          64-multiples): 0 = 4 waves per block with 2-slot rings (default),
  *                          1 = 4 waves with 4-slot rings, 2 = 8 waves, 2-slot, 3 = default blocks

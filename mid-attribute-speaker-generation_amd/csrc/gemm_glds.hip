@@ -2257,15 +2257,13 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
     const int cu = cu_count();
     const int64_t t4 = (rows / 128) * ((c_out + 63) / 64);
     const bool ok4 = seq_len % 128 == 0 && rows % 128 == 0 && rows % seq_len == 0;
-    const bool ok8 = seq_len % 256 == 0 && rows % 256 == 0 && rows % seq_len == 0;
     int pick = 0;
     if (trk == 1) pick = ok4 ? 4 : 0;                  // force 128 x 64
     else if (trk == 3) pick = ok4 ? 3 : 0;             // force 128 x 128
-    else if (trk == 5) pick = ok8 ? 5 : 0;             // A/B: 8-wave 256 x 128, one block per CU
     else if (ok4 && c_out <= 256 && t4 >= 3 * cu) pick = 3;
     else if (ok4 && t4 >= 3 * cu) pick = 4;
     if (pick) {
-      a.tiles_m = (int)(rows / (pick == 5 ? 256 : 128));
+      a.tiles_m = (int)(rows / 128);
       const bool n64 = pick == 4;
       a.tiles_n = (int)((c_out + (n64 ? 63 : 127)) / (n64 ? 64 : 128));
       // tile group: the n-tiles whose weight slice (~1.25 MB) an XCD's resident blocks share in
@@ -2279,10 +2277,7 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
         a.group = gr < 1 ? 1 : gr > a.tiles_n ? a.tiles_n : gr;
       }
       const unsigned grid = (unsigned)(a.tiles_m * a.tiles_n);
-      if (pick == 5) {
-        if (taps == 9) conv_gemm_tapreg<256, 128, 4, 2, 4, 9, 2, 1><<<grid, 512, 0, st>>>(a);
-        else conv_gemm_tapreg<256, 128, 4, 2, 4, 5, 2, 1><<<grid, 512, 0, st>>>(a);
-      } else if (pick == 3) {  // 4-wave 128 x 128 tiles, 2 blocks per CU
+      if (pick == 3) {  // 4-wave 128 x 128 tiles, 2 blocks per CU
         if (taps == 9) conv_gemm_tapreg<128, 128, 2, 2, 4, 9, 2, 2><<<grid, 256, 0, st>>>(a);
         else conv_gemm_tapreg<128, 128, 2, 2, 4, 5, 2, 2><<<grid, 256, 0, st>>>(a);
       } else {

@@ -1,4 +1,8 @@
-"""cProfile of the host side of eager steps (where the Python enqueue time goes)."""
+"""Host-side (enqueue) profile of the eager training step: cProfile over 20 steps after
+warm-up, top functions by own time.  The GPU runs behind the host (the step is GPU-bound),
+so this is the Python + ctypes + launch cost the host pays per step.
+
+    python scripts/host_profile.py [--py]      (--py: per-kernel issue, model.C_BLOCKS off)"""
 import cProfile
 import importlib
 import os
@@ -11,19 +15,24 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 PKG = importlib.import_module("mid-attribute-speaker-generation_amd")
 M = importlib.import_module("mid-attribute-speaker-generation_amd.model")
 TR = importlib.import_module("mid-attribute-speaker-generation_amd.train")
+dev = torch.device("cuda", 0)
+if "--py" in sys.argv:
+    M.C_BLOCKS = False
 pp, mc, tc, path = PKG.config.load_configs("JVS-VCTK")
-model = M.FastSpeech2(pp, mc, path, device="cuda:0", compute_dtype=torch.bfloat16)
+model = M.FastSpeech2(pp, mc, path, device=dev, compute_dtype=torch.bfloat16)
 model.train()
 tr = TR.Trainer(model, pp, mc, tc)
-batch = PKG.data.to_device(PKG.data.syn_batch(48, 128, seed=0), "cuda:0")
-for _ in range(3):
+batch = PKG.data.to_device(PKG.data.syn_batch(48, 128, seed=0), dev)
+for _ in range(5):
     tr.step(batch)
 torch.cuda.synchronize()
+N = 20
 pr = cProfile.Profile()
 pr.enable()
-for _ in range(10):
+for _ in range(N):
     tr.step(batch)
 pr.disable()
 torch.cuda.synchronize()
 st = pstats.Stats(pr)
-st.sort_stats("tottime").print_stats(28)
+print(f"total host time per step: {st.total_tt / N * 1e3:.3f} ms (cProfile adds its own overhead)")
+st.sort_stats("tottime").print_stats(45)

@@ -274,9 +274,8 @@ int fs2_weight_prep_batch(int dtype, const int64_t* jobs, int n_jobs, int64_t n_
  *                          c_out <= 256), -1 = off (the halo kernels above), 1 = force the
  *                          128 x 64 tiles, 3 = force 128 x 128
  *   FS2_TUNE_WGRAD_BAND    band weight gradient (taps 9, and taps 3 / 5 whose channels are not
- *                          64-multiples): 0 = 4 waves per block with 2-slot rings (default),
- *                          1 = 4 waves with 4-slot rings, 2 = 8 waves, 2-slot, 3 = default blocks
- *                          only on grids of >= 128 tiles, 4 = band kernel for taps 3 / 5 too
+ *                          64-multiples): 0 = default, 3 = only on grids of >= 128 tiles,
+ *                          4 = the band kernel for taps 3 / 5 with 64-multiple channels too
  *   FS2_TUNE_ATTN_XCD      LDS-DMA attention kernels: 0 = the blocks of one (utterance, head) on
  *                          one XCD (K / V reuse in its L2; default), -1 = the launch grid's order
  *   FS2_TUNE_WGRAD_K1M_STAGES  grouped k = 1 weight gradient LDS ring: 0 = 4 slots, 2 / 3 slots

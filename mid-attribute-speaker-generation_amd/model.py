@@ -518,6 +518,20 @@ class FFTBlock(nn.Module):
         return dx
 
 
+_SIZE_MEMO = {}
+
+
+def _csize(name, desc, ngeo, *args):
+    """Memoised size / offset query of a per-module C entry (``fs2_*_bytes`` / ``_offset``):
+    they depend only on the descriptor's leading geometry words and the call's sizes, and a
+    ctypes call costs microseconds of host time per block and step."""
+    key = (name, tuple(desc[:ngeo]), args)
+    v = _SIZE_MEMO.get(key)
+    if v is None:
+        v = _SIZE_MEMO[key] = getattr(K.lib, name)(desc, *args)
+    return v
+
+
 def _c_blocks(ctx, d):
     return C_BLOCKS and ctx.copy is not None and ctx.cdt == torch.bfloat16 and d == 256
 
@@ -536,13 +550,13 @@ def _stack_fwd_c(layers, x, x_t, lens, B, T, ctx):
     for layer in layers:
         desc = layer.cdesc()
         p = ctx.p(layer.slf_attn.p)
-        act = torch.empty(K.lib.fs2_fft_block_act_bytes(desc, M, B, T, int(fuse)),
+        act = torch.empty(_csize('fs2_fft_block_act_bytes', desc, 7, M, B, T, int(fuse)),
                           dtype=torch.uint8, device=x.device)
         K.lib.fs2_fft_block_fwd(desc, xp, xtp, act.data_ptr(), M, B, T, lp, p,
                                 ctx.seed.data_ptr() if p > 0 else None, int(fuse), stream)
         saved.append(("C", act, xtp, x_keep, fuse, p))
-        o2 = K.lib.fs2_fft_block_act_offset(desc, M, B, T, int(fuse), 0)
-        o2t = K.lib.fs2_fft_block_act_offset(desc, M, B, T, int(fuse), 1)
+        o2 = _csize('fs2_fft_block_act_offset', desc, 7, M, B, T, int(fuse), 0)
+        o2t = _csize('fs2_fft_block_act_offset', desc, 7, M, B, T, int(fuse), 1)
         xp, xtp, x_keep = act.data_ptr() + o2, act.data_ptr() + o2t, act
         acts.append((act, o2, o2t))
     act, o2, o2t = acts[-1]
@@ -567,9 +581,9 @@ def _stack_bwd_c(layers, saved, dx, ctx, lens, B, T):
         _, act, xtp, x_keep, fuse, p = s
         desc = layer.cdesc()
         fuse_bwd = FUSE_LN_BWD and M >= FUSE_LN_MIN_ROWS and i + 1 < len(layers)
-        tmp = torch.empty(K.lib.fs2_fft_block_tmp_bytes(desc, M, B, T), dtype=torch.uint8, device=dev)
-        ws = ctx._side_ws(K.lib.fs2_fft_block_side_ws_bytes(desc, M), dev) if side is not None else \
-            K.ws(K.lib.fs2_fft_block_side_ws_bytes(desc, M), dev)
+        tmp = torch.empty(_csize('fs2_fft_block_tmp_bytes', desc, 7, M, B, T), dtype=torch.uint8, device=dev)
+        ws = ctx._side_ws(_csize('fs2_fft_block_side_ws_bytes', desc, 7, M), dev) if side is not None else \
+            K.ws(_csize('fs2_fft_block_side_ws_bytes', desc, 7, M), dev)
         dxo = torch.empty((M, d), dtype=torch.float32, device=dev)
         pdesc = pact = pdy2 = pdx1 = None
         pfuse, pp = 0, 0.0
@@ -727,12 +741,12 @@ class VariancePredictor(nn.Module):
         desc = self.cdesc()
         M = x_t.shape[0]
         p = ctx.p(self.p)
-        act = torch.empty(K.lib.fs2_variance_predictor_act_bytes(desc, M), dtype=torch.uint8,
+        act = torch.empty(_csize('fs2_variance_predictor_act_bytes', desc, 6, M), dtype=torch.uint8,
                           device=x_t.device)
         K.lib.fs2_variance_predictor_fwd(desc, x_t.data_ptr(), act.data_ptr(), M, T,
                                          0 if lens is None else lens.data_ptr(), p,
                                          ctx.seed.data_ptr() if p > 0 else None, K.stream())
-        o = K.lib.fs2_variance_predictor_act_offset(desc, M, 0)
+        o = _csize('fs2_variance_predictor_act_offset', desc, 6, M, 0)
         pred = act[o:o + M * 4].view(torch.float32)
         return pred.view(B, T), ("C", act, x_t, lens, T, p, ctx)
 
@@ -742,9 +756,9 @@ class VariancePredictor(nn.Module):
         M = x_t.shape[0]
         dev = x_t.device
         dpred = dpred.contiguous()
-        tmp = torch.empty(K.lib.fs2_variance_predictor_tmp_bytes(desc, M), dtype=torch.uint8,
+        tmp = torch.empty(_csize('fs2_variance_predictor_tmp_bytes', desc, 6, M), dtype=torch.uint8,
                           device=dev)
-        need = K.lib.fs2_variance_predictor_side_ws_bytes(desc, M)
+        need = _csize('fs2_variance_predictor_side_ws_bytes', desc, 6, M)
         side = ctx.side.cuda_stream if ctx.side is not None else None
         ws = ctx._side_ws(need, dev) if side is not None else K.ws(need, dev)
         K.lib.fs2_variance_predictor_bwd(desc, act.data_ptr(), x_t.data_ptr(), dpred.data_ptr(),
@@ -975,7 +989,8 @@ class ParamArena:
     def zero_grad(self):
         K.fill_(self.grad, 0.0)
         for p in self.params:
-            p.grad = p._fs2_grad
+            if p.grad is not p._fs2_grad:  # (setting .grad costs microseconds per parameter)
+                p.grad = p._fs2_grad
 
 
 def fft_param_order(b):
@@ -1168,13 +1183,13 @@ class MelHeadFn(torch.autograd.Function):
             # one fs2_mel_head_fwd call: mel_linear + PostNet (bitwise the path below)
             desc = m.postnet.mel_head_desc(lin)
             p = ctx.p(0.5)
-            act = torch.empty(K.lib.fs2_mel_head_act_bytes(desc, M), dtype=torch.uint8,
+            act = torch.empty(_csize('fs2_mel_head_act_bytes', desc, 7, M), dtype=torch.uint8,
                               device=x.device)
             K.lib.fs2_mel_head_fwd(desc, x_c.data_ptr(), act.data_ptr(), M, T, p,
                                    ctx.seed.data_ptr() if p > 0 else None, K.stream())
             n_mel = lin.out_features
-            o = K.lib.fs2_mel_head_act_offset(desc, M, 0)
-            po = K.lib.fs2_mel_head_act_offset(desc, M, 1)
+            o = _csize('fs2_mel_head_act_offset', desc, 7, M, 0)
+            po = _csize('fs2_mel_head_act_offset', desc, 7, M, 1)
             out = act[o:o + M * n_mel * 4].view(torch.float32)
             post = act[po:po + M * n_mel * 4].view(torch.float32)
             fctx.m, fctx.saved = m, ("C", act, x_c, p, B, T, ctx)
@@ -1223,8 +1238,8 @@ class MelHeadFn(torch.autograd.Function):
         if d_out is None and d_post is None:
             d_out = K.zeros((M, n_mel), dev)
         desc = m.postnet.mel_head_desc(lin)
-        tmp = torch.empty(K.lib.fs2_mel_head_tmp_bytes(desc, M), dtype=torch.uint8, device=dev)
-        need = K.lib.fs2_mel_head_side_ws_bytes(desc, M)
+        tmp = torch.empty(_csize('fs2_mel_head_tmp_bytes', desc, 7, M), dtype=torch.uint8, device=dev)
+        need = _csize('fs2_mel_head_side_ws_bytes', desc, 7, M)
         side = ctx.side.cuda_stream if ctx.side is not None else None
         ws = ctx._side_ws(need, dev) if side is not None else K.ws(need, dev)
         dx = torch.empty((M, lin.in_features), dtype=torch.float32, device=dev)

@@ -191,9 +191,10 @@ class StepCtx:
             self.keep.clear()
 
     def notify(self, params):
-        """Tell the gradient hook that these parameters' gradients are final."""
+        """Tell the gradient hook that these parameters' gradients are final (``params``: a
+        list, or a callable returning it -- built only when a hook is installed)."""
         if self.hook is not None:
-            self.hook(params)
+            self.hook(params() if callable(params) else params)
 
 
 # bf16 path: FFT-block post-LayerNorms fused into the fc / w_2 GEMM epilogues (fs2_conv_gemm_ln)
@@ -223,11 +224,17 @@ def _g(p):
     return p._fs2_grad
 
 
+# Bumped whenever a compute-weight buffer or the parameter arena is (re)allocated: the C-entry
+# descriptors (FFTBlock.cdesc, ...) hold raw pointers and are rebuilt when it moves
+_GEN = [0]
+
+
 def _buf(holder, name, n, dtype, device):
     t = getattr(holder, name, None)
     if t is None or t.numel() != n or t.dtype != dtype:
         t = torch.empty(n, dtype=dtype, device=device)
         setattr(holder, name, t)
+        _GEN[0] += 1
     return t
 
 
@@ -392,13 +399,12 @@ class FFTBlock(nn.Module):
         """The block's fs2_fft_block_* descriptor (include/fs2hip.h, FS2_FB_*): geometry, the
         compute-layout weights, biases, LayerNorm affines and gradient views, as a host int64
         table (cached: the compute-layout buffers and the gradient arena persist)."""
-        a, f = self.slf_attn, self.pos_ffn
-        q = self._qkv_holder
-        key = (q._w_fwd.data_ptr(), f.w_1._w_fwd.data_ptr(), _g(f.w_1.weight).data_ptr(),
-               f.w_1.weight.data_ptr(), self.site)
+        key = (_GEN[0], self.site)
         d = self.__dict__.get("_cdesc")
         if d is not None and d[0] == key:
             return d[1]
+        a, f = self.slf_attn, self.pos_ffn
+        q = self._qkv_holder
         P = lambda t: t.data_ptr()
         w = [self.d, a.n_head, a.d_k, f.w_1.c_out, f.w_1.k, f.w_1.padding, self.site,
              P(q._w_fwd), P(q._w_bwd), P(self._qkv_b), P(a.fc._w_fwd), P(a.fc._w_bwd), P(a.fc.bias),
@@ -604,7 +610,7 @@ def _stack_bwd_c(layers, saved, dx, ctx, lens, B, T):
             stream, side)
         # read by the side stream's weight gradients after this call: kept until the join
         ctx.keep.append((tmp, act, x_keep, carry))
-        ctx.notify(fft_param_order(layer))
+        ctx.notify(lambda: fft_param_order(layer))
         if fuse_bwd:
             carry, dx = (pdy2, pdx1), None
         else:
@@ -623,7 +629,7 @@ def _stack_bwd(layers, saved, dx, ctx):
         fuse = (FUSE_LN_BWD and ctx.copy is not None and d == 256 and M >= FUSE_LN_MIN_ROWS and
                 i + 1 < len(layers))
         out = layer.bwd(dx, s, ln2_done=carry, prev=(layers[i + 1], saved[i + 1]) if fuse else None)
-        ctx.notify(fft_param_order(layer))
+        ctx.notify(lambda: fft_param_order(layer))
         if fuse:
             carry, dx = out, None
         else:
@@ -693,14 +699,13 @@ class VariancePredictor(nn.Module):
     def cdesc(self):
         """fs2_variance_predictor_* descriptor (include/fs2hip.h, FS2_VP_*), cached as
         FFTBlock.cdesc."""
-        c = self.conv_layer
-        c1, c2 = c.conv1d_1.conv, c.conv1d_2.conv
-        ln1, ln2, lin = c.layer_norm_1, c.layer_norm_2, self.linear_layer
-        key = (c1._w_fwd.data_ptr(), c2._w_fwd.data_ptr(), _g(c1.weight).data_ptr(),
-               c1.weight.data_ptr(), self.site)
+        key = (_GEN[0], self.site)
         d = self.__dict__.get("_cdesc")
         if d is not None and d[0] == key:
             return d[1]
+        c = self.conv_layer
+        c1, c2 = c.conv1d_1.conv, c.conv1d_2.conv
+        ln1, ln2, lin = c.layer_norm_1, c.layer_norm_2, self.linear_layer
         P = lambda t: t.data_ptr()
         w = [c1.c_in, c1.c_out, c1.k, c1.padding, c2.padding, self.site,
              P(c1._w_fwd), P(c1._w_bwd), P(c1.bias), P(ln1.weight), P(ln1.bias),
@@ -839,12 +844,11 @@ class PostNet(nn.Module):
     def mel_head_desc(self, lin):
         """fs2_mel_head_* descriptor (include/fs2hip.h, FS2_MH_* / FS2_MHL_*) of mel_linear
         ``lin`` followed by this PostNet, cached as FFTBlock.cdesc."""
-        c0 = self.convolutions[0][0].conv
-        key = (lin._w_fwd.data_ptr(), c0._w_fwd.data_ptr(), _g(c0.weight).data_ptr(),
-               c0.weight.data_ptr(), _g(lin.weight).data_ptr(), self.site)
+        key = (_GEN[0], self.site, id(lin))
         d = self.__dict__.get("_cdesc")
         if d is not None and d[0] == key:
             return d[1]
+        c0 = self.convolutions[0][0].conv
         P = lambda t: t.data_ptr()
         n = len(self.convolutions)
         if n > MH_MAX_LAYERS:
@@ -977,6 +981,7 @@ class ParamArena:
         self.flat = torch.zeros(n, dtype=torch.float32, device=device)
         self.grad = torch.zeros(n, dtype=torch.float32, device=device)
         self.offsets = offs
+        _GEN[0] += 1
         with torch.no_grad():
             for p, o in zip(self.params, offs):
                 v = self.flat[o:o + p.numel()]
@@ -1086,7 +1091,7 @@ class EncoderFn(torch.autograd.Function):
         K.embedding_bwd(dx, texts, _g(enc.src_word_emb.weight), 0)
         K.embedding_bwd(dx, accents, _g(enc.src_accent_emb.weight), 0)
         fctx.ctx.join()  # last block of the backward: every weight gradient is final after this
-        fctx.ctx.notify([enc.src_accent_emb.weight, enc.src_word_emb.weight])
+        fctx.ctx.notify(lambda: [enc.src_accent_emb.weight, enc.src_word_emb.weight])
         fctx.saved = None
         return (None,) * 8
 
@@ -1126,16 +1131,16 @@ class VarianceAdaptorFn(torch.autograd.Function):
         K.bucket_embed_bwd(dx, idx_e, _g(va.energy_embedding.weight))
         if d_e is not None:
             va.energy_predictor.bwd(d_e, s_e, dx)
-        ctx.notify([va.energy_embedding.weight] + vp_param_order(va.energy_predictor))
+        ctx.notify(lambda: [va.energy_embedding.weight] + vp_param_order(va.energy_predictor))
         K.bucket_embed_bwd(dx, idx_p, _g(va.pitch_embedding.weight))
         if d_p is not None:
             va.pitch_predictor.bwd(d_p, s_p, dx)
-        ctx.notify([va.pitch_embedding.weight] + vp_param_order(va.pitch_predictor))
+        ctx.notify(lambda: [va.pitch_embedding.weight] + vp_param_order(va.pitch_predictor))
         if d_logd is not None:
             va.duration_predictor.bwd(d_logd, s_d, dx)
-        ctx.notify(vp_param_order(va.duration_predictor))
+        ctx.notify(lambda: vp_param_order(va.duration_predictor))
         K.rowvec_add_bwd(dx, speakers, _g(m.speaker_emb.weight), B, Ts)
-        ctx.notify([m.speaker_emb.weight])
+        ctx.notify(lambda: [m.speaker_emb.weight])
         fctx.saved = None
         return (None, dx) + (None,) * 10
 
@@ -1217,11 +1222,11 @@ class MelHeadFn(torch.autograd.Function):
             m.postnet.bwd(d_post, s, dm)
         else:
             dm = d_out
-        ctx.notify(postnet_param_order(m.postnet))
+        ctx.notify(lambda: postnet_param_order(m.postnet))
         dm_c = K.cast_bf16(dm) if ctx.copy is not None else dm
         ctx.wgrad(dm_c, x_c, _g(lin.weight), M, T, lin.in_features, n_mel, 1, 0, db=_g(lin.bias))
         dx = K.conv_gemm(dm_c, lin._w_bwd, M, T, n_mel, lin.in_features, 1, 0)
-        ctx.notify([lin.weight, lin.bias])
+        ctx.notify(lambda: [lin.weight, lin.bias])
         fctx.saved = None
         return None, dx, None, None, None, None, None
 
@@ -1249,8 +1254,8 @@ class MelHeadFn(torch.autograd.Function):
                                ctx.seed.data_ptr() if p > 0 else None,
                                ws.data_ptr(), ws.numel() * 4, K.stream(), side)
         ctx.keep.append((tmp, act, x_c))  # read by the side stream until the join
-        ctx.notify(postnet_param_order(m.postnet))
-        ctx.notify([lin.weight, lin.bias])
+        ctx.notify(lambda: postnet_param_order(m.postnet))
+        ctx.notify(lambda: [lin.weight, lin.bias])
         fctx.saved = None
         return None, dx, None, None, None, None, None
 
@@ -1303,6 +1308,7 @@ class FastSpeech2(nn.Module):
     # -- plumbing ---------------------------------------------------------------------
     def _apply(self, fn, *args, **kwargs):
         r = super()._apply(fn, *args, **kwargs)
+        _GEN[0] += 1
         self._arena = None  # parameters were re-materialised: rebuild the flat views lazily
         self._prep = None
         return r

@@ -726,7 +726,9 @@ def main():
                           "parallelism": f"dp{world}",
                           "use_clf": bool(args.use_clf),
                           "execution": "hip-graph replay" if use_graph else "eager",
-                          "host_issue": ("one C-ABI call per FFT block (fs2_fft_block_fwd / _bwd)"
+                          "host_issue": ("one C-ABI call per FFT block, mel head and variance "
+                                         "predictor (fs2_fft_block_* / fs2_mel_head_* / "
+                                         "fs2_variance_predictor_*)"
                                          if M.C_BLOCKS else "one C-ABI call per kernel"),
                           **({"data_parallel": "one-rank RCCL group (FS2_DP1)"} if dp1 else {})},
                "roofline": roof, "step_roofline": step_roof}

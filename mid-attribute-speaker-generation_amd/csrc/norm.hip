@@ -389,7 +389,17 @@ __global__ __launch_bounds__(1024) void bn_stats_final(const float* psum, const 
   if (nbt && col == 0) nbt[0] += 1;
 }
 
-FS2_DEV f32x4 tanh4(f32x4 v) { return f32x4{tanhf(v.x), tanhf(v.y), tanhf(v.z), tanhf(v.w)}; }
+// tanh(x) = 1 - 2 / (exp(2x) + 1) on v_exp_f32 / v_rcp_f32: absolute error ~3e-7 (|tanh| <= 1;
+// saturates to +-1 through exp's overflow / underflow), against the libm tanhf's ~30-instruction
+// branchy path -- the PostNet BatchNorm kernels evaluate it on every element (forward, and
+// again in both backward passes for the derivative 1 - t^2)
+FS2_DEV float tanh_fast(float x) {
+  const float e = __builtin_amdgcn_exp2f(x * 2.8853900817779268f);  // exp(2x) = 2^(2x log2 e)
+  return 1.f - 2.f * __builtin_amdgcn_rcpf(e + 1.f);
+}
+FS2_DEV f32x4 tanh4(f32x4 v) {
+  return f32x4{tanh_fast(v.x), tanh_fast(v.y), tanh_fast(v.z), tanh_fast(v.w)};
+}
 
 
 // out = act(BN(z)) * dropout (+ res), 8 consecutive elements (same row) per lane

@@ -9,7 +9,7 @@ Data parallel: one process per GPU, batch sharded by utterance.
 * Each rank normalises its masked means by the *global* valid counts and the GMM term by
   the global batch (one 3-float all-reduce of device-side counts before the forward, no host
   sync), so the summed gradient equals the 1-process gradient of the global batch.
-* Gradients are all-reduced (sum) over RCCL in ~32 MB buckets of the flat fp32 gradient
+* Gradients are all-reduced (sum) over RCCL in ~16 MB buckets of the flat fp32 gradient
   buffer.  The buffer is laid out in reverse backward order, every block's backward reports
   its parameters as final (``StepCtx.notify``), and a bucket's all-reduce is launched as soon
   as all of its parameters are final, so communication overlaps the rest of the backward.
@@ -146,7 +146,7 @@ class CollectiveModel:
 class GradBuckets:
     """Bucketed, backward-overlapped all-reduce of the arena's flat gradient buffer."""
 
-    def __init__(self, arena, group=None, bucket_bytes=32 << 20):
+    def __init__(self, arena, group=None, bucket_bytes=16 << 20):
         self.arena, self.group = arena, group
         index = {id(p): i for i, p in enumerate(arena.params)}
         buckets, cur, size = [], [], 0
@@ -253,7 +253,7 @@ class Trainer:
     """
 
     def __init__(self, model, preprocess_config, model_config, train_config, current_step=0,
-                 process_group=None, bucket_bytes=32 << 20, graph=False, data_parallel=None,
+                 process_group=None, bucket_bytes=16 << 20, graph=False, data_parallel=None,
                  collective_model=None, comm_stream=False):
         self.model = model
         self.graph_mode = bool(graph)

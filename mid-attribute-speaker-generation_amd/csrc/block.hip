@@ -110,7 +110,7 @@ ActLayout act_layout(const Blk& b, int64_t rows, int64_t batch, int64_t T, int f
 
 // the backward's temporaries
 struct TmpLayout {
-  int64_t dx1, dy2_t, dh, dy1_t, dout, dqkv, ws, ws_bytes, total;
+  int64_t dx1, dy2_t, dh, dy1_t, dout, dqkv, ws, ws_bytes, ln_ws[3], ln_ws_bytes, total;
 };
 TmpLayout tmp_layout(const Blk& b, int64_t rows, int64_t batch, int64_t T) {
   TmpLayout L;
@@ -129,6 +129,10 @@ TmpLayout tmp_layout(const Blk& b, int64_t rows, int64_t batch, int64_t T) {
   const int64_t w1 = fs2_ln_bwd_ws_bytes(rows, (int)b.d), w2 = fs2_attn_bwd_ws_bytes(batch, T, (int)b.heads);
   L.ws_bytes = al(w1 > w2 ? w1 : w2);
   L.ws = take(L.ws_bytes);
+  // the LayerNorm backwards' column partials (LN2, LN1, the previous block's LN2), reduced into
+  // the parameter gradients on the side stream after the call returns: a region each
+  L.ln_ws_bytes = al(w1);
+  for (int i = 0; i < 3; ++i) L.ln_ws[i] = take(L.ln_ws_bytes);
   L.total = o;
   return L;
 }
@@ -274,9 +278,17 @@ int fs2_fft_block_bwd(const int64_t* blk, void* act, const void* x_t, int fuse_l
     void* d2 = at<void>(tmp, W.dy2_t);
     FS2_TRY(fs2_ln_bwd(FS2_BF16, dx2, nullptr, nullptr, xh2, rs2, b.ln2_g, b.ln2_b, lens, T, rows,
                        (int)b.d, p, 0.f, sd, (uint64_t)(b.site + 1), 0, nullptr, nullptr, d2, dx1, 0,
-                       b.gln2_g, b.gln2_b, nullptr, nullptr, b.g2_b, ws, W.ws_bytes, stream));
+                       nullptr, nullptr, nullptr, nullptr, nullptr, at<float>(tmp, W.ln_ws[0]),
+                       W.ln_ws_bytes, stream));
     dy2_t = d2;
   }
+  // a LayerNorm backward's parameter gradients (dgamma, dbeta, the fused bias gradient): the
+  // column reduction of its partials, off the main chain on the side stream (called after a
+  // stream_wait that orders it behind the partials)
+  auto ln_final = [&](int slot, float* dg, float* db, float* dbias) {
+    return fs2_ln_bwd_final(rows, (int)b.d, at<float>(tmp, W.ln_ws[slot]), 0, dg, db, nullptr,
+                            nullptr, dbias, side);
+  };
   // grouped k = 1 weight gradients (w_2, fc, QKV), issued together at the end of the block
   int64_t jobs[24] = {(int64_t)(uintptr_t)dy2_t, b.d, (int64_t)(uintptr_t)h, b.dinner,
                       (int64_t)(uintptr_t)b.g2_w, 0, b.dinner, b.d};
@@ -286,6 +298,7 @@ int fs2_fft_block_bwd(const int64_t* blk, void* act, const void* x_t, int fuse_l
                         nullptr, FS2_EPI_RELU_MASK_AUX | FS2_EPI_OUT_BF16 | FS2_EPI_AUX_BF16, h,
                         b.dinner, stream));
   if (side != stream) FS2_TRY(fs2_stream_wait(side, stream));
+  if (!carry_dy2_t) FS2_TRY(ln_final(0, b.gln2_g, b.gln2_b, b.g2_b));
   FS2_TRY(fs2_conv_wgrad(FS2_BF16, dh, b.dinner, x1_t, b.d, b.g1_w, b.g1_b, rows, T, b.d, b.dinner,
                          (int)b.taps, (int)b.pad, lens, side_ws, side_ws_bytes, side));
   FS2_TRY(fs2_conv_gemm(FS2_BF16, dh, b.dinner, b.w1_b, dx1, b.d, rows, T, b.dinner, b.d, (int)b.taps,
@@ -293,8 +306,9 @@ int fs2_fft_block_bwd(const int64_t* blk, void* act, const void* x_t, int fuse_l
   // LN1 -> fc -> attention -> QKV
   void* dy1_t = at<void>(tmp, W.dy1_t);
   FS2_TRY(fs2_ln_bwd(FS2_BF16, dx1, nullptr, nullptr, xh1, rs1, b.ln1_g, b.ln1_b, lens, T, rows,
-                     (int)b.d, p, 0.f, sd, (uint64_t)b.site, 0, nullptr, nullptr, dy1_t, dx, 0, b.gln1_g,
-                     b.gln1_b, nullptr, nullptr, b.gfc_b, ws, W.ws_bytes, stream));
+                     (int)b.d, p, 0.f, sd, (uint64_t)b.site, 0, nullptr, nullptr, dy1_t, dx, 0, nullptr,
+                     nullptr, nullptr, nullptr, nullptr, at<float>(tmp, W.ln_ws[1]), W.ln_ws_bytes,
+                     stream));
   const int64_t j2[8] = {(int64_t)(uintptr_t)dy1_t, b.d, (int64_t)(uintptr_t)o, b.hd,
                          (int64_t)(uintptr_t)b.gfc_w, 0, b.hd, b.d};
   memcpy(jobs + 8, j2, sizeof j2);
@@ -309,16 +323,20 @@ int fs2_fft_block_bwd(const int64_t* blk, void* act, const void* x_t, int fuse_l
                          (int64_t)(uintptr_t)b.gq_w, (int64_t)(uintptr_t)b.gq_b, b.d, b.n3};
   memcpy(jobs + 16, j3, sizeof j3);
   if (side != stream) FS2_TRY(fs2_stream_wait(side, stream));
+  FS2_TRY(ln_final(1, b.gln1_g, b.gln1_b, b.gfc_b));
   FS2_TRY(fs2_conv_wgrad_k1_multi(FS2_BF16, jobs, 3, rows, T, lens, side_ws, side_ws_bytes, side));
   if (prev_blk) {
     // the previous block's FFN post-LN backward in this block's QKV data-gradient epilogue
     const Blk pb = unpack(prev_blk);
     const ActLayout PL = act_layout(pb, rows, batch, seq_len, prev_fuse_ln);
-    return fs2_conv_gemm_ln_bwd(dqkv, b.n3, b.wq_b, rows, T, b.n3, b.d, 1, 0, lens, dx,
-                                at<float>(prev_act, PL.xh2), at<float>(prev_act, PL.rs2), pb.ln2_g,
-                                pb.gln2_g, pb.gln2_b, pb.g2_b, prev_p, prev_p > 0.f ? seed : nullptr,
-                                (uint64_t)(pb.site + 1), prev_dx1, 0, prev_dy2_t, ws, W.ws_bytes,
-                                stream);
+    FS2_TRY(fs2_conv_gemm_ln_bwd(dqkv, b.n3, b.wq_b, rows, T, b.n3, b.d, 1, 0, lens, dx,
+                                 at<float>(prev_act, PL.xh2), at<float>(prev_act, PL.rs2), pb.ln2_g,
+                                 nullptr, nullptr, nullptr, prev_p, prev_p > 0.f ? seed : nullptr,
+                                 (uint64_t)(pb.site + 1), prev_dx1, 0, prev_dy2_t,
+                                 at<float>(tmp, W.ln_ws[2]), W.ln_ws_bytes, stream));
+    if (side != stream) FS2_TRY(fs2_stream_wait(side, stream));
+    return fs2_ln_bwd_final(rows, (int)pb.d, at<float>(tmp, W.ln_ws[2]), 0, pb.gln2_g, pb.gln2_b,
+                            nullptr, nullptr, pb.g2_b, side);
   }
   return fs2_conv_gemm(FS2_BF16, dqkv, b.n3, b.wq_b, dx, b.d, rows, T, b.n3, b.d, 1, 0, lens, nullptr,
                        FS2_EPI_ADD_AUX, dx, b.d, stream);

@@ -214,8 +214,10 @@ VpAct vp_act(const Vp& v, int64_t rows) {
   return A;
 }
 
+// backward temporaries; the two LayerNorm backwards' column partials each have a region (their
+// reductions into the parameter gradients run later, on the side stream)
 struct VpTmp {
-  int64_t dh2_t, du1, dh1_t, ws, ws_bytes, total;
+  int64_t dh2_t, du1, dh1_t, ws[2], ws_bytes, total;
 };
 VpTmp vp_tmp(const Vp& v, int64_t rows) {
   VpTmp W;
@@ -224,7 +226,8 @@ VpTmp vp_tmp(const Vp& v, int64_t rows) {
   W.du1 = take(rows * v.filt * 4);
   W.dh1_t = take(rows * v.filt * 2);
   W.ws_bytes = al(fs2_ln_bwd_ws_bytes(rows, (int)v.filt));
-  W.ws = take(W.ws_bytes);
+  W.ws[0] = take(W.ws_bytes);
+  W.ws[1] = take(W.ws_bytes);
   W.total = take.o;
   return W;
 }
@@ -439,15 +442,19 @@ int fs2_variance_predictor_bwd(const int64_t* vp, void* act, const void* x_t, co
   const int64_t T = seq_len;
   const uint64_t* sd = p > 0.f ? seed : nullptr;
   void* side = side_stream ? side_stream : stream;
-  float* ws = at<float>(tmp, W.ws);
+  float* ws2 = at<float>(tmp, W.ws[0]);
+  float* ws1 = at<float>(tmp, W.ws[1]);
   const void* u1_t = at<void>(act, A.u1_t);
-  // LN2 (+ Linear, masked; ReLU mask; conv2 bias gradient) backward
+  // LN2 (+ Linear, masked; ReLU mask; conv2 bias gradient) backward; its parameter gradients
+  // (LN2 affine, Linear, conv2 bias) reduced on the side stream
   void* dh2_t = at<void>(tmp, W.dh2_t);
   FS2_TRY(fs2_ln_bwd(FS2_BF16, nullptr, dpred, v.lin_w, at<float>(act, A.xh2), at<float>(act, A.rs2),
                      v.ln2_g, v.ln2_b, lens, T, rows, (int)v.filt, 0.f, p, sd, 0,
                      (uint64_t)(v.site + 1), at<float>(act, A.h2), nullptr, dh2_t, nullptr, 1,
-                     v.gln2_g, v.gln2_b, v.glin_w, v.glin_b, v.g2_b, ws, W.ws_bytes, stream));
+                     nullptr, nullptr, nullptr, nullptr, nullptr, ws2, W.ws_bytes, stream));
   if (side != stream) FS2_TRY(fs2_stream_wait(side, stream));
+  FS2_TRY(fs2_ln_bwd_final(rows, (int)v.filt, ws2, 1, v.gln2_g, v.gln2_b, v.glin_w, v.glin_b, v.g2_b,
+                           side));
   FS2_TRY(fs2_conv_wgrad(FS2_BF16, dh2_t, v.filt, u1_t, v.filt, v.g2_w, nullptr, rows, T, v.filt,
                          v.filt, (int)v.taps, (int)v.pad2, nullptr, side_ws, side_ws_bytes, side));
   float* du1 = at<float>(tmp, W.du1);
@@ -457,9 +464,11 @@ int fs2_variance_predictor_bwd(const int64_t* vp, void* act, const void* x_t, co
   void* dh1_t = at<void>(tmp, W.dh1_t);
   FS2_TRY(fs2_ln_bwd(FS2_BF16, du1, nullptr, nullptr, at<float>(act, A.xh1), at<float>(act, A.rs1),
                      v.ln1_g, v.ln1_b, nullptr, 1, rows, (int)v.filt, 0.f, p, sd, 0, (uint64_t)v.site,
-                     at<float>(act, A.h1), nullptr, dh1_t, nullptr, 1, v.gln1_g, v.gln1_b, nullptr,
-                     nullptr, v.g1_b, ws, W.ws_bytes, stream));
+                     at<float>(act, A.h1), nullptr, dh1_t, nullptr, 1, nullptr, nullptr, nullptr,
+                     nullptr, nullptr, ws1, W.ws_bytes, stream));
   if (side != stream) FS2_TRY(fs2_stream_wait(side, stream));
+  FS2_TRY(fs2_ln_bwd_final(rows, (int)v.filt, ws1, 0, v.gln1_g, v.gln1_b, nullptr, nullptr, v.g1_b,
+                           side));
   FS2_TRY(fs2_conv_wgrad(FS2_BF16, dh1_t, v.filt, x_t, v.d, v.g1_w, nullptr, rows, T, v.d, v.filt,
                          (int)v.taps, (int)v.pad1, nullptr, side_ws, side_ws_bytes, side));
   return fs2_conv_gemm(FS2_BF16, dh1_t, v.filt, v.w1_b, dx_acc, v.d, rows, T, v.filt, v.d,

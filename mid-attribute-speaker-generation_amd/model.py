@@ -208,6 +208,8 @@ FUSE_LN_BWD = True
 # FFTBlock.fwd / .bwd below: bitwise the same results, a fifth of the host time); the tests
 # compare it against the per-kernel path by clearing it
 C_BLOCKS = True
+# pitch predictor forward on the side stream beside the duration / energy predictors (A/B)
+VA_SIDE = True
 # fs2_mel_head_* descriptor geometry (include/fs2hip.h: FS2_MH_LAYER0 + FS2_MH_MAX_LAYERS x
 # FS2_MHL_WORDS words)
 MH_MAX_LAYERS = 8
@@ -719,9 +721,11 @@ class VariancePredictor(nn.Module):
         self._cdesc = (key, arr)
         return arr
 
-    def fwd(self, x, x_t, lens, B, T, ctx):
+    def fwd(self, x, x_t, lens, B, T, ctx, stream=None):
+        """``stream`` (raw handle): the C-ABI path issues on it instead of the current stream
+        (the caller orders it); the per-kernel path always runs on the current stream."""
         if _c_blocks(ctx, x.shape[1]) and x_t is not None:
-            return self._fwd_c(x_t, lens, B, T, ctx)
+            return self._fwd_c(x_t, lens, B, T, ctx, stream)
         c = self.conv_layer
         c1, c2 = c.conv1d_1.conv, c.conv1d_2.conv
         M = x.shape[0]
@@ -741,8 +745,9 @@ class VariancePredictor(nn.Module):
         saved = (x_c, h1, u1_c, h2, xh1, rs1, xh2, rs2, p, ctx, lens, T)
         return pred.view(B, T), saved
 
-    def _fwd_c(self, x_t, lens, B, T, ctx):
-        """One fs2_variance_predictor_fwd call (bitwise the per-kernel path below)."""
+    def _fwd_c(self, x_t, lens, B, T, ctx, stream=None):
+        """One fs2_variance_predictor_fwd call (bitwise the per-kernel path below); its
+        activations are allocated on the current stream whatever stream computes them."""
         desc = self.cdesc()
         M = x_t.shape[0]
         p = ctx.p(self.p)
@@ -750,7 +755,8 @@ class VariancePredictor(nn.Module):
                           device=x_t.device)
         K.lib.fs2_variance_predictor_fwd(desc, x_t.data_ptr(), act.data_ptr(), M, T,
                                          0 if lens is None else lens.data_ptr(), p,
-                                         ctx.seed.data_ptr() if p > 0 else None, K.stream())
+                                         ctx.seed.data_ptr() if p > 0 else None,
+                                         K.stream() if stream is None else stream)
         o = _csize('fs2_variance_predictor_act_offset', desc, 6, M, 0)
         pred = act[o:o + M * 4].view(torch.float32)
         return pred.view(B, T), ("C", act, x_t, lens, T, p, ctx)
@@ -1104,8 +1110,15 @@ class VarianceAdaptorFn(torch.autograd.Function):
         fctx.set_materialize_grads(False)  # unused outputs' gradients stay None (no zero fills)
         va = m.variance_adaptor
         x0, x0_t = K.rowvec_add(enc_out, speakers, m.speaker_emb.weight, B, Ts, copy=ctx.copy)
+        # the three predictors are independent under teacher forcing (the energy predictor's
+        # input adds the pitch *target*'s embedding): the pitch predictor runs on the side
+        # stream -- idle in the forward once the weights are prepared -- beside the duration and
+        # energy predictors, joined before the LengthRegulator (C-ABI path; same results)
+        side = ctx.side.cuda_stream if ctx.side is not None and VA_SIDE else None
+        if side is not None:
+            K.lib.fs2_stream_wait(side, K.stream())
+        p, s_p = va.pitch_predictor.fwd(x0, x0_t, src_lens, B, Ts, ctx, stream=side)
         log_d, s_d = va.duration_predictor.fwd(x0, x0_t, src_lens, B, Ts, ctx)
-        p, s_p = va.pitch_predictor.fwd(x0, x0_t, src_lens, B, Ts, ctx)
         x1, x1_t, idx_p = K.bucket_embed(x0, p_t.contiguous().view(-1), va.pitch_bins,
                                          va.pitch_embedding.weight, copy=ctx.copy)
         e, s_e = va.energy_predictor.fwd(x1, x1_t, src_lens, B, Ts, ctx)
@@ -1113,6 +1126,8 @@ class VarianceAdaptorFn(torch.autograd.Function):
                                       va.energy_embedding.weight)
         cum, mel_len = K.lr_index(d_t.contiguous())
         x_lr, x_lr_t = K.lr_expand(x2, cum, T_dec, posenc=m.decoder.position_enc, copy=ctx.copy)
+        if side is not None:
+            K.lib.fs2_stream_wait(K.stream(), side)
         fctx.m, fctx.saved = m, (s_d, s_p, s_e, idx_p, idx_e, cum, speakers, B, Ts, T_dec, ctx)
         side = x_lr_t if x_lr_t is not None else torch.empty(0, device=x_lr.device)
         fctx.mark_non_differentiable(mel_len, side)

@@ -1,0 +1,14 @@
+#!/bin/bash
+# round 5: pitch predictor forward on the side stream (model.VA_SIDE) -- same-box step A/B and
+# forward phase
+set -u
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+o=gpurun_out/va; mkdir -p $o
+for r in 1 2 3; do
+  for v in 1 0; do
+    timeout -k 10 200 python -u scripts/bench_ab.py model.VA_SIDE=$v -- --steps 30 --warmup 5 --no-cpu-baseline --no-f32 --no-traffic > $o/ab.log 2>&1 || { tail -20 $o/ab.log; exit 1; }
+    echo "[VA_SIDE=$v] $(tail -1 $o/ab.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"])')"
+  done
+done
+timeout -k 10 300 python -u scripts/step_phases.py > $o/phases.log 2>&1 || { tail -20 $o/phases.log; exit 1; }
+grep -E "C blocks|ms from" $o/phases.log

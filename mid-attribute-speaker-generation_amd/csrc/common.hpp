@@ -41,23 +41,6 @@ struct ColsumJob {
   int64_t nparts, cols;
   float* out;
 };
-// s = sum over p = p0, p0 + step, ... < n of x[p * ld] in p order, the first N loads issued
-// together (a runtime-count loop unrolled by the compiler runs short counts one load at a time);
-// missing terms add +0, which leaves the in-order sum unchanged bitwise
-template <int N>
-FS2_DEV float strided_sum(const float* x, int64_t p0, int64_t step, int64_t n, int64_t ld) {
-  float v[N];
-#pragma unroll
-  for (int i = 0; i < N; ++i) {
-    const int64_t p = p0 + i * step;
-    v[i] = p < n ? x[p * ld] : 0.f;
-  }
-  float s = 0.f;
-#pragma unroll
-  for (int i = 0; i < N; ++i) s += v[i];
-  for (int64_t p = p0 + N * step; p < n; p += step) s += x[p * ld];
-  return s;
-}
 struct ColsumJobs {
   ColsumJob job[6];
   int n, acc;

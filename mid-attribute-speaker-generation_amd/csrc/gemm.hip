@@ -319,7 +319,10 @@ __global__ __launch_bounds__(1024) void colsum_final(const float* part, int64_t 
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int64_t c = (int64_t)blockIdx.x * 64 + tx;
   float s = 0.f;
-  if (c < cols) s = strided_sum<16>(part + c, ty, 16, nparts, cols);
+  if (c < cols) {
+#pragma unroll 4
+    for (int64_t p = ty; p < nparts; p += 16) s += part[p * cols + c];
+  }
   red[ty][tx] = s;
   __syncthreads();
   if (ty == 0 && c < cols) {
@@ -332,7 +335,7 @@ __global__ __launch_bounds__(1024) void colsum_final(const float* part, int64_t 
 
 // Several independent finals in one launch (blockIdx.y = job), each as colsum_final.
 // 16 columns x 64 row groups per block: each thread sums every 64th partial row of its column
-// (a dozen loads for the LN backward's 768 partial rows, all in flight), then a fixed-order
+// (a dozen loads for the LN backward's 768 partial rows, four in flight), then a fixed-order
 // LDS tree over the 64 groups.  Deterministic; the blocks of all jobs run in one launch.
 __global__ __launch_bounds__(1024) void colsum_final_multi(ColsumJobs jobs) {
   __shared__ float red[64][17];
@@ -341,7 +344,10 @@ __global__ __launch_bounds__(1024) void colsum_final_multi(ColsumJobs jobs) {
   const int64_t c = (int64_t)blockIdx.x * 16 + tx;
   if ((int64_t)blockIdx.x * 16 >= jb.cols) return;  // block-uniform
   float s = 0.f;
-  if (c < jb.cols) s = strided_sum<16>(jb.part + c, ty, 64, jb.nparts, jb.cols);
+  if (c < jb.cols) {
+#pragma unroll 4
+    for (int64_t p = ty; p < jb.nparts; p += 64) s += jb.part[p * jb.cols + c];
+  }
   red[ty][tx] = s;
   __syncthreads();
 #pragma unroll

@@ -286,12 +286,15 @@ __global__ __launch_bounds__(LN_BWD_WAVES * 64) void ln_bwd_f32(LnBwd a) {
 // ------------------------------------------------------------------ BatchNorm
 constexpr int BN_ROWS = 64;  // rows per partial block: 1,536 blocks at 24,576 rows (latency-bound at 64)
 
-// in-order column sum of partial rows: 32 columns x 32 part lanes per block, 16 loads in flight
+// in-order column sum of partial rows: 32 columns x 32 part lanes per block, 8 loads in flight
 // per lane (the 64 x 16 layout with 4 took 24 dependent rounds at the PostNet's 384 parts)
 FS2_DEV float col_reduce(const float* part, int64_t nparts, int64_t c, int64_t col, int tx, int ty,
                          float (*red)[33]) {
   float s = 0.f;
-  if (col < c) s = strided_sum<16>(part + col, ty, 32, nparts, c);
+  if (col < c) {
+#pragma unroll 8
+    for (int64_t p = ty; p < nparts; p += 32) s += part[p * c + col];
+  }
   red[ty][tx] = s;
   __syncthreads();
   float t = 0.f;
@@ -364,25 +367,13 @@ __global__ __launch_bounds__(1024) void bn_stats_final(const float* psum, const 
   const float mu = mu_s[tx];
   float q = 0.f;
   if (col < c) {
-    // the first 16 partial rows' loads issued together (the PostNet's 384 parts: 12 per lane)
-    constexpr int N = 16;
-    float ps[N], pq[N];
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-      const int64_t p = ty + 32 * i;
-      ps[i] = p < nparts ? psum[p * c + col] : 0.f;
-      pq[i] = p < nparts ? pm2[p * c + col] : 0.f;
-    }
-    auto term = [&](int64_t p, float sp, float m2) {
+#pragma unroll 8
+    for (int64_t p = ty; p < nparts; p += 32) {
       const int64_t left = rows - p * BN_ROWS;
       const float n = (float)(left < BN_ROWS ? left : BN_ROWS);
-      const float d = sp / n - mu;
-      q += m2 + n * d * d;
-    };
-#pragma unroll
-    for (int i = 0; i < N; ++i)
-      if (ty + 32 * i < nparts) term(ty + 32 * i, ps[i], pq[i]);
-    for (int64_t p = ty + 32 * N; p < nparts; p += 32) term(p, psum[p * c + col], pm2[p * c + col]);
+      const float d = psum[p * c + col] / n - mu;
+      q += pm2[p * c + col] + n * d * d;
+    }
   }
   red[ty][tx] = q;
   __syncthreads();
@@ -556,8 +547,11 @@ FS2_DEV void col_reduce2(const float* pa, const float* pb, int64_t nparts, int64
                          int tx, int ty, float (*red)[2][33], float& sa, float& sb) {
   float a = 0.f, b = 0.f;
   if (col < c) {
-    a = strided_sum<24>(pa + col, ty, 32, nparts, c);
-    b = strided_sum<24>(pb + col, ty, 32, nparts, c);
+#pragma unroll 8
+    for (int64_t p = ty; p < nparts; p += 32) {
+      a += pa[p * c + col];
+      b += pb[p * c + col];
+    }
   }
   red[ty][0][tx] = a;
   red[ty][1][tx] = b;

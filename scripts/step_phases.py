@@ -10,6 +10,23 @@ TR = importlib.import_module("mid-attribute-speaker-generation_amd.train")
 dev = torch.device("cuda", 0)
 if "--py" in sys.argv:  # the per-kernel host path (model.C_BLOCKS off) for the A/B
     M.C_BLOCKS = False
+# --modules: HIP events on the main stream around each autograd block's forward and backward
+# (encoder, variance adaptor, decoder, mel head): where the step's main-stream time goes
+MODS = {}
+if "--modules" in sys.argv:
+    for nm in ("EncoderFn", "VarianceAdaptorFn", "DecoderFn", "MelHeadFn"):
+        cls = getattr(M, nm)
+        for ph in ("forward", "backward"):
+            f = getattr(cls, ph)
+
+            def wrap(*a, _f=f, _k=f"{nm[:-2]}.{ph[:3]}"):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                r = _f(*a)
+                e1.record()
+                MODS.setdefault(_k, []).append((e0, e1))
+                return r
+            setattr(cls, ph, staticmethod(wrap))
 pp, mc, tc, path = PKG.config.load_configs("JVS-VCTK")
 model = M.FastSpeech2(pp, mc, path, device=dev, compute_dtype=torch.bfloat16)
 model.train()
@@ -46,3 +63,8 @@ hh = np.array([[(x - hr[0]) * 1e3 for x in hr[1:]] for hr in host[2:]])
 print("GPU  ms from step start:", "  ".join(f"{n} {v:.3f}" for n, v in zip(names, g.mean(0))))
 print("host ms from step start:", "  ".join(f"{n} {v:.3f}" for n, v in zip(names, hh.mean(0))))
 print(f"C blocks: {M.C_BLOCKS}; host enqueue {hh.mean(0)[-1]:.3f} ms, GPU {g.mean(0)[-1]:.3f} ms per step")
+if MODS:
+    torch.cuda.synchronize()
+    for k, v in MODS.items():
+        t = [a.elapsed_time(b) for a, b in v[-10:]]
+        print(f"  {k:24s} {np.mean(t):.3f} ms (main stream, last {len(t)} steps)")

@@ -293,6 +293,35 @@ def test_embeddings():
     assert m.cpu().tolist() == (torch.arange(11)[None] >= torch.tensor([3, 0, 11])[:, None]).tolist()
 
 
+@pytest.mark.parametrize("n,n_table", [(6144, 429), (5000, 5), (2049, 256), (6144, 1)])
+def test_embedding_bwd_chunks(n, n_table):
+    """The scatter-add of the embedding / bucket-embedding backward over several 1,024-row chunks,
+    a ragged last chunk, table sizes that are not a multiple of the 8 ids a block lists, and a
+    skewed id distribution (half the rows on one id): against a float64 index_add, padding row
+    untouched, accumulation into the table, and bitwise repeatable."""
+    g = torch.Generator(device="cpu").manual_seed(n + n_table)
+    ids = torch.randint(0, n_table, (n,), generator=g)
+    ids[::2] = min(7, n_table - 1)
+    ids = ids.to(DEV)
+    dout = rnd(n, 256, seed=11)
+    base = rnd(n_table, 256, seed=12)
+    ref = base.double().index_add(0, ids, dout.double())
+    pad = 0 if n_table > 1 else -1
+    if pad == 0:
+        ref[0] = base[0].double()
+    outs = []
+    for _ in range(2):
+        t = base.clone()
+        K.embedding_bwd(dout, ids, t, pad)
+        outs.append(t)
+    close(outs[0], ref, 1e-5)
+    assert torch.equal(outs[0], outs[1])
+    t32 = base.clone()
+    K.bucket_embed_bwd(dout, ids.to(torch.int32), t32)
+    ref32 = base.double().index_add(0, ids, dout.double())
+    close(t32, ref32, 1e-5)
+
+
 def test_grad_norm_adam():
     n = 10_003
     g = rnd(n, seed=1)

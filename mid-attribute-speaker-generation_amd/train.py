@@ -29,18 +29,41 @@ from .loss import FastSpeech2Loss, SpeakerMetaEncLoss
 from .optimizer import ScheduledOptim
 
 
-def clf_backward(model, batch, clf, perm, step, total_step, lambd=1.0):
+def clf_backward(model, batch, clf, perm, step, total_step, lambd=1.0, group=None):
     """The ``--use_clf`` branch of ``train.py:168-197``: a second forward with the speakers
     (and their metadata) shuffled by ``perm`` (the reference draws it with
     ``random.sample``), the predicted mel cut into 150-frame chunks, the language
     discriminator on every chunk, and ``dloss * coef(step / total_step) / len(langs) *
     lambd`` back-propagated into the model.  ``clf = (SpeechEmbedder, GE2ELoss)``.  Returns
-    ``(dloss, cross-lingual chunk count, chunk count)``."""
+    ``(dloss, cross-lingual chunk count, chunk count)``.
+
+    ``group`` (data parallel, equal shards): the reference shuffles its whole
+    (``nn.DataParallel``) batch, so ``perm`` permutes the global batch of ``world x B``
+    utterances, the same on every rank.  Every rank's speakers and metadata are all-gathered
+    (B ints and B metadata rows per rank), a rank takes its rows of the shuffled global batch,
+    and the loss is divided by the global chunk count (the BCE term sums over chunks, so the
+    summed all-reduce of the ranks' gradients is the global batch's).  The returned dloss and
+    counts are the global sums."""
     from . import ge2e
     disc, dLoss = clf
-    idx = torch.as_tensor(perm, device=batch[2].device)
-    speakers = batch[2].index_select(0, idx)  # (B,) ids: the gather of train.py:172
-    meta = batch[12].index_select(0, idx)
+    dev = batch[2].device
+    idx = torch.as_tensor(perm, device=dev)
+    if group is None:
+        speakers = batch[2].index_select(0, idx)  # (B,) ids: the gather of train.py:172
+        meta = batch[12].index_select(0, idx)
+    else:
+        world, rank = dist.get_world_size(group), dist.get_rank(group)
+        B = batch[2].shape[0]
+        if idx.numel() != world * B:
+            raise ValueError(f"use_clf with data parallelism: perm must permute the global batch "
+                             f"({world} x {B} utterances), got {idx.numel()}")
+        spk = [torch.empty_like(batch[2]) for _ in range(world)]
+        dist.all_gather(spk, batch[2].contiguous(), group=group)
+        mt = [torch.empty_like(batch[12]) for _ in range(world)]
+        dist.all_gather(mt, batch[12].contiguous(), group=group)
+        mine = idx[rank * B:(rank + 1) * B]
+        speakers = torch.cat(spk).index_select(0, mine)
+        meta = torch.cat(mt).index_select(0, mine)
     output = model(speakers, *batch[3:12], accents=batch[13], speaker_meta=meta)
     chunks, rep = ge2e.chunk_mels(output[0])
     langs = ge2e.chunk_langs(meta, rep)
@@ -48,13 +71,20 @@ def clf_backward(model, batch, clf, perm, step, total_step, lambd=1.0):
     out_r = disc(chunks)
     _, _, dloss = dLoss(out_r["embeddings"].view(chunks.shape[0], 1, -1),
                         out_r["da_lang_logits"], langs, reduction="sum")
-    scale = ge2e.da_coefficient(step, total_step) / langs.shape[0] * lambd
-    (dloss * scale).backward()
-    return dloss, (langs != langs_original).sum(), langs.shape[0]
+    cross = (langs != langs_original).sum()
+    n = langs.shape[0]
+    if group is None:
+        scale = ge2e.da_coefficient(step, total_step) / n * lambd
+        (dloss * scale).backward()
+        return dloss, cross, n
+    stats = torch.stack([torch.tensor(float(n), device=dev), cross.float(), dloss.detach()])
+    dist.all_reduce(stats, group=group)  # global chunk count, cross-lingual chunks, dloss
+    (dloss * (ge2e.da_coefficient(step, total_step) * lambd / stats[0])).backward()
+    return stats[2], stats[1].long(), int(stats[0].item())
 
 
 def train_step(model, optimizer, Loss, eLoss, batch, grad_clip_thresh=1.0, grad_sync=None,
-               clf=None, clf_args=None, grad_acc_step=1, update=True):
+               clf=None, clf_args=None, grad_acc_step=1, update=True, clf_group=None):
     """One batch of ``train.py:138-206`` -> (losses, eloss, grad norm, output).
 
     Both losses are back-propagated divided by ``grad_acc_step`` (``train.py:159,165``);
@@ -68,7 +98,7 @@ def train_step(model, optimizer, Loss, eLoss, batch, grad_clip_thresh=1.0, grad_
     (losses[0] / grad_acc_step if grad_acc_step != 1 else losses[0]).backward()
     eloss = eLoss(output[-1], output[-2])
     (-eloss / grad_acc_step if grad_acc_step != 1 else -eloss).backward()
-    clf_out = clf_backward(model, batch, clf, *clf_args) if clf is not None else None
+    clf_out = clf_backward(model, batch, clf, *clf_args, group=clf_group) if clf is not None else None
     gnorm = None
     if update:
         if grad_sync is not None:
@@ -348,15 +378,26 @@ class Trainer:
         """One batch (``train.py:137-206``); the optimiser steps when the batch counter is a
         multiple of ``grad_acc_step`` (the returned grad norm is None on the other batches).
         ``clf=(SpeechEmbedder, GE2ELoss)`` with ``clf_args=(perm, step, total_step, lambd)``
-        adds the ``--use_clf`` branch (eager, single process)."""
+        adds the ``--use_clf`` branch (eager; under data parallelism ``perm`` permutes the
+        global batch and this step's gradient buckets go out after the clf backward)."""
         update = self.batch_step % self.grad_acc == 0
         self.batch_step += 1
         acc = dict(grad_acc_step=self.grad_acc, update=update)
         if clf is not None:
-            if self.dp:
-                raise NotImplementedError("use_clf with data parallelism")
+            if not self.dp:
+                return train_step(self.model, self.opt, self.Loss, self.eLoss, batch, self.clip,
+                                  clf=clf, clf_args=clf_args, **acc)
+            # data parallel: the clf backward adds to every parameter's gradient after the main
+            # backward has released the buckets, so this step's buckets all go out in finish(),
+            # after it (no overlap); perm permutes the global batch (clf_backward)
+            glob = self._global_denominators(batch)
+            self.Loss.denoms = glob[0:2]
+            self.eLoss.denom = glob[2:3]
+            self.model._hooks["grad"] = None
             return train_step(self.model, self.opt, self.Loss, self.eLoss, batch, self.clip,
-                              clf=clf, clf_args=clf_args, **acc)
+                              grad_sync=self.buckets.finish, clf=clf, clf_args=clf_args,
+                              clf_group=None if self.cm is not None else
+                              (self.pg if self.pg is not None else dist.group.WORLD), **acc)
         if self.graph_mode and not self.dp and self.grad_acc == 1:
             return self._graph_step(batch)
         if self.dp:

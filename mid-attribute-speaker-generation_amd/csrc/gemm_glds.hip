@@ -2070,8 +2070,26 @@ static void launch_nt(GldsArgs a, bool tapaligned, bool voc, hipStream_t st) {
 // summed by halo_splitk_reduce.  The partials live in one process-wide buffer, grown outside
 // graph capture only (a too-small buffer during capture falls back to the unsplit launch), so
 // an eager step and its captured replay take the same decomposition (bitwise-equal results).
-// A launch from a different stream than the previous user first drains that stream; the
+// Stream order between users: every eager split launch pair records one event of ours after
+// its reduce (halo_splitk_done) and the next eager user's stream waits on it on the device, so
+// the choice never depends on another stream's handle.  (The round-4 form synchronised the
+// previous user's stream from the host and fell back to the unsplit launch when that failed --
+// as it did once the stream was destroyed, e.g. a test's warm-up stream: later steps in the
+// process then computed the same convs unsplit, a different fp32 summation order.)  The
 // launches of one captured graph all come from its capture stream.
+static std::mutex g_splitk_mu;
+static hipEvent_t g_splitk_ev = nullptr;
+static bool g_splitk_recorded = false;
+static hipStream_t g_splitk_last = nullptr;  // the stream of that event (same stream: no wait)
+static void halo_splitk_done(hipStream_t st) {
+  std::lock_guard<std::mutex> lock(g_splitk_mu);
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return;
+  if (g_splitk_ev && hipEventRecord(g_splitk_ev, st) == hipSuccess) {
+    g_splitk_recorded = true;
+    g_splitk_last = st;
+  }
+}
 static int halo_splitk(GldsArgs& a, unsigned grid, bool voc, bool hx64, hipStream_t st) {
   const int knob = g_tune[FS2_TUNE_HALO_SPLITK];
   const int ncb = a.Cin / 64;
@@ -2081,16 +2099,23 @@ static int halo_splitk(GldsArgs& a, unsigned grid, bool voc, bool hx64, hipStrea
   int kz = knob > 0 ? knob : (grid < 512 && ncb >= 8 ? (int)((768 + grid - 1) / grid) : 1);
   if (kz > ncb / 4) kz = ncb / 4;
   if (kz < 2) return 1;
-  static std::mutex mu;
   static float* buf = nullptr;
   static size_t cap = 0;
-  static hipStream_t last = nullptr;
   const size_t need = (size_t)kz * (size_t)a.M * (size_t)a.N * sizeof(float);
-  std::lock_guard<std::mutex> lock(mu);
+  std::lock_guard<std::mutex> lock(g_splitk_mu);
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(st, &cs) != hipSuccess) return 1;
   const bool capturing = cs != hipStreamCaptureStatusNone;
-  if (!capturing && last && last != st && hipStreamSynchronize(last) != hipSuccess) return 1;
+  if (!capturing) {
+    if (!g_splitk_ev && hipEventCreateWithFlags(&g_splitk_ev, hipEventDisableTiming) != hipSuccess) {
+      g_splitk_ev = nullptr;
+      return 1;
+    }
+    // the previous eager user's reduce has read the buffer before this stream writes it
+    if (g_splitk_recorded && st != g_splitk_last &&
+        hipStreamWaitEvent(st, g_splitk_ev, 0) != hipSuccess)
+      return 1;
+  }
   if (cap < need) {
     if (capturing) return 1;
     if (buf) {
@@ -2104,7 +2129,6 @@ static int halo_splitk(GldsArgs& a, unsigned grid, bool voc, bool hx64, hipStrea
     buf = static_cast<float*>(p);
     cap = need;
   }
-  if (!capturing) last = st;
   a.slab = buf;
   return kz;
 }
@@ -2331,6 +2355,7 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
           const int64_t n8 = rows * (c_out / 8);
           halo_splitk_reduce<128><<<(unsigned)((n8 + 255) / 256 < 2048 ? (n8 + 255) / 256 : 2048),
                                     256, 0, st>>>(a);
+          halo_splitk_done(st);
         } else {
           FS2_HALO2(128, 128)
         }
@@ -2344,6 +2369,7 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
           const int64_t n8 = rows * (c_out / 8);
           halo_splitk_reduce<128><<<(unsigned)((n8 + 255) / 256 < 2048 ? (n8 + 255) / 256 : 2048),
                                     256, 0, st>>>(a);
+          halo_splitk_done(st);
         } else {
           FS2_HALO2(128, 64)
         }
@@ -2362,12 +2388,14 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
           const int64_t n8 = rows * (c_out / 8);
           halo_splitk_reduce<128><<<(unsigned)((n8 + 255) / 256 < 2048 ? (n8 + 255) / 256 : 2048),
                                     256, 0, st>>>(a2);
+          halo_splitk_done(st);
         } else if (kz > 1) {
           a.kz = kz;
           conv_gemm_halo<64, 64, 2, 16, false, 4, true><<<grid * kz, 256, 0, st>>>(a);
           const int64_t n8 = rows * (c_out / 8);
           halo_splitk_reduce<64><<<(unsigned)((n8 + 255) / 256 < 2048 ? (n8 + 255) / 256 : 2048),
                                    256, 0, st>>>(a);
+          halo_splitk_done(st);
         } else {
           FS2_HALO2(64, 64)
         }

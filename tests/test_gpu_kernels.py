@@ -914,6 +914,30 @@ def test_conv_gemm_bf16_halo_splitk(B, T, cin, cout, k, flags):
         K.lib.fs2_set_tuning(8, 0)
 
 
+def test_conv_gemm_bf16_halo_splitk_streams():
+    """The split-K launches share one partials buffer: a launch on another stream is ordered
+    behind the previous user's reduce on the device (an event of the library's), and the split
+    decomposition -- hence the fp32 summation order -- does not depend on which streams ran
+    before or whether they still exist: the default-stream result is bitwise the same before
+    and after split launches on other, since released, streams."""
+    B, T, cin, cout, k = 48, 128, 1024, 256, 9
+    x = bf(rnd(B * T, cin, seed=61))
+    w = bf(rnd(cout, cin, k, scale=1 / math.sqrt(cin * k), seed=62)).float()
+    wf = torch.empty(cout * cin * k, device=DEV, dtype=torch.bfloat16)
+    K.weight_prep(w, cout, cin, k, wf, None)
+    run = lambda: K.conv_gemm(x, wf, B * T, T, cin, cout, k, 4)
+    want = run()
+    for _ in range(3):
+        s = torch.cuda.Stream()
+        with torch.cuda.stream(s):
+            other = run()
+        s.synchronize()
+        assert torch.equal(other, want)
+        del s
+        assert torch.equal(run(), want)
+    torch.cuda.synchronize()
+
+
 @pytest.mark.parametrize("M,c", [(333, 8), (97, 24), (65, 4096), (32, 512), (2, 80)])
 def test_batchnorm_widths(M, c):
     """BatchNorm forward/backward at the edges of the backward partials' lane layout (c / 8

@@ -598,12 +598,15 @@ def main():
         disc = G.SpeechEmbedder(device=dev)
         PKG.seeded.load_seeded_(disc)
         clf = (disc, G.GE2ELoss(dev))
-        rnd = random.Random(1234 + rank)
+        # under data parallelism the shuffle is one permutation of the global batch, drawn with
+        # the same seed on every rank (train.clf_backward gathers the speakers it indexes)
+        rnd = random.Random(1234)
         counter = [0]
+        n_perm = world * args.batch
 
         def clf_kw():  # train.py:171 draws the shuffle with random.sample each step
             counter[0] += 1
-            return {"clf": clf, "clf_args": (rnd.sample(range(args.batch), args.batch),
+            return {"clf": clf, "clf_args": (rnd.sample(range(n_perm), n_perm),
                                              counter[0], tc["step"]["total_step"],
                                              float(tc.get("lambda", 1)))}
     batch_np = PKG.data.syn_batch(args.batch, args.src_len, seed=rank)

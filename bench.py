@@ -497,6 +497,9 @@ def cpu_baseline(batch_np, steps=3):
 def build_trainer(M, TR, dtype, dev, rank, graph=False, data_parallel=None):
     pp, mc, tc, path = PKG.config.load_configs("JVS-VCTK")
     cdt = {"f32": torch.float32, "bf16": torch.bfloat16}[dtype]
+    # the random init draws from torch's global generator: seed it so final_loss reproduces
+    # across runs (data parallel: rank 0's weights are broadcast at the first step anyway)
+    torch.manual_seed(1234)
     model = M.FastSpeech2(pp, mc, path, device=dev, compute_dtype=cdt)
     model.train()
     model.seed(1234 + rank)

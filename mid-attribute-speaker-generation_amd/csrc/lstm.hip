@@ -82,6 +82,32 @@ FS2_DEV void lstm_mfma_share2(const float* ap0, const float* ap1, const float* b
   }
 }
 
+// two A tiles x two B tiles (sequence tiles): every A load feeds two B columns
+template <int GT>
+FS2_DEV void lstm_mfma_share22(const float* ap0, const float* ap1, const float* bp0,
+                               const float* bp1, bool bv0, bool bv1, int kb, int kper,
+                               f32x4m (&c)[2][2][2]) {
+  for (int k = kb; k < kb + kper; k += 16 * GT) {
+    float4 a0[GT], a1[GT], b0[GT], b1[GT];
+#pragma unroll
+    for (int g = 0; g < GT; ++g) {
+      a0[g] = *reinterpret_cast<const float4*>(ap0 + k + 16 * g);
+      a1[g] = *reinterpret_cast<const float4*>(ap1 + k + 16 * g);
+      b0[g] = *reinterpret_cast<const float4*>(bp0 + k + 16 * g);
+      b1[g] = *reinterpret_cast<const float4*>(bp1 + k + 16 * g);
+    }
+#pragma unroll
+    for (int g = 0; g < GT; ++g) {
+      if (!bv0) b0[g] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (!bv1) b1[g] = make_float4(0.f, 0.f, 0.f, 0.f);
+      mfma_k16(a0[g], b0[g], c[0][0][0], c[0][0][1]);
+      mfma_k16(a1[g], b0[g], c[1][0][0], c[1][0][1]);
+      mfma_k16(a0[g], b1[g], c[0][1][0], c[0][1][1]);
+      mfma_k16(a1[g], b1[g], c[1][1][0], c[1][1][1]);
+    }
+  }
+}
+
 constexpr int LSTM_FWD_WAVES = 8;  // split-K ways of the forward tile (K = H)
 constexpr int LSTM_FWD_GT = 2;     // 16-k groups per trip (H / 8 = 32 k per wave at H = 256)
 constexpr int LSTM_BWD_WAVES = 8;  // split-K ways of the backward tile (K = 4H)
@@ -225,23 +251,25 @@ struct LstmStackFwd {
   int N, T, H, L, s;
 };
 
-// 4 waves, 8 hidden units (two 16-gate-row A tiles sharing the h loads) x 16 sequences:
-// layer 0 splits the recurrent K = H 4 ways; layers >= 1 give the input product (K = H) to
-// waves 0-1 and the recurrent one to waves 2-3
+// 4 waves, 8 hidden units (two 16-gate-row A tiles) x 32 sequences (two 16-sequence B tiles;
+// every weight load feeds both): layer 0 splits the recurrent K = H 4 ways; layers >= 1 give
+// the input product (K = H) to waves 0-1 and the recurrent one to waves 2-3.  Each output's
+// k order and partial-sum order are those of one 16-sequence tile.
 __global__ __launch_bounds__(256) void lstm_stack_fwd_step(LstmStackFwd a) {
-  __shared__ float red[4][2][4][64];
+  __shared__ float red[4][2][2][4][64];
   const int l = blockIdx.z, t = a.s - l;
   if (t < 0 || t >= a.T) return;  // block-uniform
   const int N = a.N, T = a.T, H = a.H;
   const int64_t rows = (int64_t)N * T;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int u0 = blockIdx.x * 8, n0 = blockIdx.y * 16;
+  const int u0 = blockIdx.x * 8, n0 = blockIdx.y * 32;
   float* h_l = a.h + l * rows * H;
   float* c_l = a.c + l * rows * H;
-  // epilogue thread (waves 0-1) -> (tile ut, sequence nn, unit uu)
-  const int ut = (threadIdx.x >> 6) & 1, uu = threadIdx.x & 3, nn = (threadIdx.x >> 2) & 15;
-  const int ne = n0 + nn, u = u0 + ut * 4 + uu;
-  const bool epi = threadIdx.x < 128 && ne < N;
+  // epilogue thread -> (sequence tile st, unit tile ut, sequence nn, unit uu)
+  const int ut = (threadIdx.x >> 6) & 1, st = threadIdx.x >> 7, uu = threadIdx.x & 3,
+            nn = (threadIdx.x >> 2) & 15;
+  const int ne = n0 + st * 16 + nn, u = u0 + ut * 4 + uu;
+  const bool epi = ne < N;
   const int64_t row = (int64_t)(epi ? ne : 0) * T + t;
   float z[4], cp = 0.f;
   if (epi) {
@@ -252,44 +280,49 @@ __global__ __launch_bounds__(256) void lstm_stack_fwd_step(LstmStackFwd a) {
   }
   const int kq = lane >> 4, r = lane & 15;
   const int m_row = (r & 3) * H + u0 + (r >> 2);  // gate row of tile 0 (tile 1: + 4)
-  const int n = n0 + r;
-  const bool nv = n < N;
-  const int64_t nrow = (int64_t)(nv ? n : 0) * T;
-  f32x4m c[2][2] = {{{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}},
-                    {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}}};
+  const int nA = n0 + r, nB = n0 + 16 + r;
+  const bool nvA = nA < N, nvB = nB < N;
+  const int64_t nrowA = (int64_t)(nvA ? nA : 0) * T, nrowB = (int64_t)(nvB ? nB : 0) * T;
+  f32x4m c[2][2][2];
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y) c[x][y][0] = c[x][y][1] = f32x4m{0.f, 0.f, 0.f, 0.f};
   const float* w = nullptr;
-  const float* bp = nullptr;
-  int kb = 0, kper = 0;
+  const float* hb = nullptr;  // h rows of the operand (this layer at t - 1, or the one below at t)
+  int dt = 0, kb = 0, kper = 0;
   if (l == 0) {
     if (t > 0) {
-      w = a.w_hh;
-      bp = h_l + (nrow + t - 1) * H;
+      w = a.w_hh, hb = h_l, dt = -1;
       kb = wave * (H / 4), kper = H / 4;
     }
   } else if (wave < 2) {
     w = a.w_ih_up + (int64_t)(l - 1) * 4 * H * H;
-    bp = a.h + (l - 1) * rows * H + (nrow + t) * H;
+    hb = a.h + (l - 1) * rows * H, dt = 0;
     kb = wave * (H / 2), kper = H / 2;
   } else if (t > 0) {
     w = a.w_hh + (int64_t)l * 4 * H * H;
-    bp = h_l + (nrow + t - 1) * H;
+    hb = h_l, dt = -1;
     kb = (wave - 2) * (H / 2), kper = H / 2;
   }
   if (w) {
     const float* ap0 = w + (int64_t)m_row * H + 4 * kq;
-    lstm_mfma_share2<4>(ap0, ap0 + 4 * H, bp + 4 * kq, nv, kb, kper, c);
+    lstm_mfma_share22<4>(ap0, ap0 + 4 * H, hb + (nrowA + t + dt) * H + 4 * kq,
+                         hb + (nrowB + t + dt) * H + 4 * kq, nvA, nvB, kb, kper, c);
   }
 #pragma unroll
   for (int x = 0; x < 2; ++x)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) red[wave][x][i][lane] = c[x][0][i] + c[x][1][i];
+    for (int y = 0; y < 2; ++y)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) red[wave][x][y][i][lane] = c[x][y][0][i] + c[x][y][1][i];
   __syncthreads();
   if (!epi) return;
 #pragma unroll
   for (int gi = 0; gi < 4; ++gi) {
     float acc = 0.f;
 #pragma unroll
-    for (int wv = 0; wv < 4; ++wv) acc += red[wv][ut][gi][uu * 16 + nn];
+    for (int wv = 0; wv < 4; ++wv) acc += red[wv][ut][st][gi][uu * 16 + nn];
     z[gi] += acc;
   }
   const float i = sigm(z[0]), f = sigm(z[1]), gg = tanhf(z[2]), o = sigm(z[3]);
@@ -570,7 +603,7 @@ int fs2_lstm_stack_fwd(const float* x, int64_t n_seq, int64_t steps, int64_t c_i
                          FS2_EPI_BIAS, nullptr, 0, stream);
   if (rc) return rc;
   hipStream_t st = as_stream(stream);
-  const dim3 grid((unsigned)(hidden / 8), (unsigned)((n_seq + 15) / 16), (unsigned)layers);
+  const dim3 grid((unsigned)(hidden / 8), (unsigned)((n_seq + 31) / 32), (unsigned)layers);
   LstmStackFwd a{gx, w_ih_up, w_hh, bias, h_all, c_all, act, (int)n_seq, (int)steps,
                  (int)hidden, layers, 0};
   for (int s = 0; s < (int)steps + layers - 1; ++s) {

@@ -44,6 +44,19 @@ def seeded(module, prefix):
 # (softmax is invariant to a per-query constant shift) and conv biases followed by
 # training-mode BatchNorm (the batch mean removes them).  They are checked against the
 # scale of their layer's weight gradient instead of their own (noise) scale.
+def _arena_diff(model, a, b):
+    """Names (and max |diff|) of the parameters whose sections of two arena-layout flat
+    buffers differ: the message of a failed bitwise step comparison."""
+    ar = model.arena()
+    names = {id(p): n for n, p in model.named_parameters()}
+    out = []
+    for p, o in zip(ar.params, ar.offsets):
+        x, y = a[o:o + p.numel()], b[o:o + p.numel()]
+        if not torch.equal(x, y):
+            out.append(f"{names.get(id(p), '?')} {float((x - y).abs().max()):.3e}")
+    return "; ".join(out[:12]) + (f" (+{len(out) - 12} more)" if len(out) > 12 else "")
+
+
 def _structural_zero(name):
     return name.endswith("slf_attn.w_ks.bias") or ("postnet" in name or name.startswith("pn.")
                                                      or "convolutions" in name) and name.endswith(".0.conv.bias")
@@ -364,8 +377,8 @@ def test_fused_gemm_ln_step_bitwise():
             res.append((model.arena().flat.clone(), tr.opt.m.clone(), torch.stack(losses)))
         finally:
             M.FUSE_LN, M.FUSE_LN_MIN_ROWS, M.FUSE_LN_BWD = True, 16384, True
-    for a, b in zip(*res):
-        assert torch.equal(a, b)
+    for i, (a, b) in enumerate(zip(*res)):
+        assert torch.equal(a, b), (i, _arena_diff(model, a, b) if i < 2 else (a - b).abs().max())
 
 
 @pytest.mark.parametrize("min_rows", [0, 16384])
@@ -393,8 +406,8 @@ def test_c_blocks_step_bitwise(min_rows):
                         model.postnet.convolutions[1][1].running_mean.clone(), torch.stack(losses)))
         finally:
             M.C_BLOCKS, M.FUSE_LN_MIN_ROWS = c_default, 16384
-    for a, b in zip(*res):
-        assert torch.equal(a, b)
+    for i, (a, b) in enumerate(zip(*res)):
+        assert torch.equal(a, b), (i, _arena_diff(model, a, b) if i < 3 else (a - b).abs().max())
 
 
 def test_fused_gemm_ln_bwd_step():

@@ -693,6 +693,20 @@ int fs2_fill_from(float* x, int64_t n, const float* src, float scale, const floa
                   void* stream);
 int fs2_add(float* out, const float* a, const float* b, int64_t n, void* stream); /* out = a + b */
 
+/* ---------------------------------------------------------------- debug: stale-read poisoning
+ * Not part of the reference's surface: a harness for the bitwise-determinism tests
+ * (tests/test_stale_reads.py).  fs2_debug_poison(byte), byte in [0, 255] (or the FS2_POISON
+ * environment variable, read once): every workspace an entry point receives and the library's
+ * reused split-K partials are filled with that byte before each use; -1 turns it off (the
+ * default).  fs2_debug_alloc / fs2_debug_free have the
+ * signatures of torch.cuda.memory.CUDAPluggableAllocator: no caching, every device allocation
+ * filled with the poison byte (0xff when off) at allocation, every free after a device drain.
+ * With both, a kernel that reads memory nothing wrote this step reads the poison, so its
+ * results depend on the byte instead of on what ran earlier in the process.               */
+int fs2_debug_poison(int byte);
+void* fs2_debug_alloc(int64_t size, int device, void* stream);
+void fs2_debug_free(void* ptr, int64_t size, int device, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -24,6 +24,8 @@ _CT = {
     "float": ctypes.c_float,
     "double": ctypes.c_double,
     "const char*": ctypes.c_char_p,
+    "void*": ctypes.c_void_p,
+    "void": None,
 }
 
 
@@ -33,7 +35,7 @@ def parse_header(path=HEADER):
         src = f.read()
     src = re.sub(r"/\*.*?\*/", " ", src, flags=re.S)
     out = {}
-    for m in re.finditer(r"(const char\*|int64_t|int)\s+(fs2_\w+)\s*\(([^)]*)\)\s*;", src):
+    for m in re.finditer(r"(const char\*|int64_t|int|void\*|void)\s+(fs2_\w+)\s*\(([^)]*)\)\s*;", src):
         ret, name, args = m.group(1), m.group(2), m.group(3).strip()
         argtypes = []
         if args and args != "void":

@@ -1,6 +1,7 @@
 // Error reporting and small utility entry points of the C-ABI.
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 #include "common.hpp"
 
@@ -51,6 +52,21 @@ __global__ void fill_from_kernel(float* x, int64_t n, const float* src, float sc
     x[i] = v;
 }
 
+static int g_poison = -2;  // -2: FS2_POISON not read yet
+
+int poison_byte() {
+  if (g_poison == -2) {
+    const char* e = getenv("FS2_POISON");
+    g_poison = (e && *e) ? (atoi(e) & 0xff) : -1;
+  }
+  return g_poison;
+}
+
+void poison(void* p, int64_t bytes, hipStream_t st) {
+  const int b = poison_byte();
+  if (b >= 0 && p && bytes > 0) (void)hipMemsetAsync(p, b, (size_t)bytes, st);
+}
+
 static unsigned grid_for(int64_t n) {
   int64_t b = (n + 255) / 256;
   if (b > 8192) b = 8192;
@@ -96,6 +112,34 @@ int fs2_stream_wait(void* waiter, void* signaler) {
     return FS2_ERR_LAUNCH;
   }
   return FS2_OK;
+}
+
+int fs2_debug_poison(int byte) {
+  g_poison = byte < 0 ? -1 : (byte & 0xff);
+  return FS2_OK;
+}
+
+// torch.cuda.memory.CUDAPluggableAllocator pair: no caching, every block filled with the poison
+// byte (0xff when poisoning is off) at allocation; a free waits for the device to drain first
+void* fs2_debug_alloc(int64_t size, int device, void* stream) {
+  (void)device;
+  (void)stream;
+  void* p = nullptr;
+  if (hipMalloc(&p, size > 0 ? (size_t)size : 1) != hipSuccess) return nullptr;
+  const int b = poison_byte();
+  if (size > 0 && hipMemset(p, b >= 0 ? b : 0xff, (size_t)size) != hipSuccess) {
+    (void)hipFree(p);
+    return nullptr;
+  }
+  return p;
+}
+
+void fs2_debug_free(void* p, int64_t size, int device, void* stream) {
+  (void)size;
+  (void)device;
+  (void)stream;
+  (void)hipDeviceSynchronize();
+  (void)hipFree(p);
 }
 
 int fs2_fill(float* x, int64_t n, float value, void* stream) {

@@ -347,6 +347,7 @@ int fs2_attn_bwd(int dtype, const void* qkv, const void* o, const void* d_o, con
   FS2_CHECK_ARG(ws_bytes >= fs2_attn_bwd_ws_bytes(batch, seq_len, heads),
                 "fs2_attn_bwd: workspace too small");
   if (batch == 0) return FS2_OK;
+  poison(ws, ws_bytes, as_stream(stream));
   if (dtype == FS2_BF16)
     return attn_bwd_bf16_launch(qkv, o, d_o, lse, d_qkv, lens, batch, seq_len, heads, scale, ws,
                                 as_stream(stream));

@@ -24,6 +24,13 @@ extern int g_tune[FS2_TUNE_COUNT];  // fs2_set_tuning knobs (abi.hip)
 void set_error(const char* fmt, ...);
 int launch_status(const char* what);
 
+// Stale-read poisoning (debug, off by default; fs2_debug_poison / FS2_POISON, abi.hip): the
+// byte every caller workspace and the library's own reused scratch is filled with before each
+// use, or -1.  A kernel that reads scratch it has not written then reads the poison, so two
+// runs with different bytes differ instead of depending on what ran before in the process.
+int poison_byte();
+void poison(void* p, int64_t bytes, hipStream_t st);
+
 #define FS2_CHECK_ARG(cond, ...)                     \
   do {                                               \
     if (!(cond)) {                                   \

@@ -342,6 +342,7 @@ int fs2_embedding_bwd(const float* dout, const int64_t* ids, int64_t n, int d, i
   FS2_CHECK_ARG(ws_bytes >= fs2_embedding_bwd_ws_bytes(n, d, n_table),
                 "fs2_embedding_bwd: workspace too small");
   if (n == 0 || n_table == 0) return FS2_OK;
+  poison(ws, ws_bytes, as_stream(stream));
   return index_add_launch<int64_t>(dout, ids, n, d, padding_idx, dtable, n_table, ws,
                                    as_stream(stream));
 }
@@ -389,6 +390,7 @@ int fs2_bucket_embed_bwd(const float* dout, const int32_t* idx, int64_t rows, in
   FS2_CHECK_ARG(ws_bytes >= fs2_embedding_bwd_ws_bytes(rows, d, n_table),
                 "fs2_bucket_embed_bwd: workspace too small");
   if (rows == 0 || n_table == 0) return FS2_OK;
+  poison(ws, ws_bytes, as_stream(stream));
   return index_add_launch<int32_t>(dout, idx, rows, d, -1, dtable, n_table, ws, as_stream(stream));
 }
 

@@ -489,6 +489,7 @@ int fs2_conv_gemm_ln_bwd(const void* x, int64_t ldx, const void* wk, int64_t row
   FS2_CHECK_ARG(!(p_in > 0.f) || seed, "fs2_conv_gemm_ln_bwd: dropout without seed");
   FS2_CHECK_ARG(ws_bytes >= fs2_ln_bwd_ws_bytes(rows, 256), "fs2_conv_gemm_ln_bwd: workspace too small");
   if (rows == 0) return FS2_OK;
+  poison(ws, ws_bytes, as_stream(stream));
   int rc = conv_gemm_lnbwd_glds_launch(x, ldx, wk, rows, seq_len, c_in, taps, pad, lens, aux, xhat,
                                        rstd, gamma, p_in, seed, site_in, dres, dres_add, dy_t, ws,
                                        as_stream(stream));
@@ -555,6 +556,7 @@ int fs2_conv_wgrad(int dtype, const void* dy, int64_t ldy, const void* x, int64_
     FS2_CHECK_ARG(ws_bytes >= fs2_conv_wgrad_ws_bytes(rows, c_in, c_out, taps),
                   "fs2_conv_wgrad: workspace too small");
     if (rows == 0) return FS2_OK;
+    poison(ws, ws_bytes, as_stream(stream));
     const int S = wgrad_splits(rows, c_in, c_out, taps);
     if (taps == 1 && !g_tune[FS2_TUNE_LEGACY_GEMM] && g_tune[FS2_TUNE_WGRAD_K1] == 0) {
       // k = 1: the grouped split-K kernel with one job (128 x 128 tiles, one reduce)
@@ -591,6 +593,7 @@ int fs2_conv_wgrad(int dtype, const void* dy, int64_t ldy, const void* x, int64_
   FS2_CHECK_ARG(ws_bytes >= fs2_conv_wgrad_ws_bytes(rows, c_in, c_out, taps),
                 "fs2_conv_wgrad: workspace too small");
   if (rows == 0) return FS2_OK;
+  poison(ws, ws_bytes, as_stream(stream));
   const int S = wgrad_splits(rows, c_in, c_out, taps);
   int64_t rps = (rows + S - 1) / S;
   rps = (rps + BK - 1) / BK * BK;
@@ -624,6 +627,7 @@ int fs2_conv_wgrad_k1_multi(int dtype, const int64_t* jobs, int n_jobs, int64_t 
                 "fs2_conv_wgrad_k1_multi: workspace too small");
   FS2_CHECK_ARG(seq_len > 0 && rows % seq_len == 0, "fs2_conv_wgrad_k1_multi: rows must be batch x seq_len");
   if (rows == 0) return FS2_OK;
+  poison(ws, ws_bytes, as_stream(stream));
   if (dtype == FS2_BF16 && !g_tune[FS2_TUNE_LEGACY_GEMM])
     return wgrad_k1_multi_launch(jobs, n_jobs, rows, seq_len, lens, ws, as_stream(stream));
   for (int j = 0; j < n_jobs; ++j) {
@@ -643,6 +647,7 @@ int64_t fs2_colsum_ws_bytes(int64_t rows, int64_t cols) {
 int fs2_colsum(int dtype, const void* x, int64_t ldx, int64_t rows, int64_t cols, float* out,
                int accumulate, float* ws, int64_t ws_bytes, void* stream) {
   FS2_CHECK_ARG(ws_bytes >= fs2_colsum_ws_bytes(rows, cols), "fs2_colsum: workspace too small");
+  poison(ws, ws_bytes, as_stream(stream));
   if (rows == 0) {
     if (!accumulate) (void)hipMemsetAsync(out, 0, cols * 4, as_stream(stream));
     return FS2_OK;

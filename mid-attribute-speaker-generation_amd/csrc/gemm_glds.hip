@@ -2067,30 +2067,32 @@ static void launch_nt(GldsArgs a, bool tapaligned, bool voc, hipStream_t st) {
 // long channel loop (the encoder's k=9 data gradient: 384 tiles, 16 channel blocks x 9 taps
 // each) leaves CUs with one block and the rest with two; splitting the channel blocks kz ways
 // fills the chip and halves each block's serial loop, at the cost of kz fp32 partial products
-// summed by halo_splitk_reduce.  The partials live in one process-wide buffer, grown outside
-// graph capture only (a too-small buffer during capture falls back to the unsplit launch), so
-// an eager step and its captured replay take the same decomposition (bitwise-equal results).
-// Stream order between users: every eager split launch pair records one event of ours after
-// its reduce (halo_splitk_done) and the next eager user's stream waits on it on the device, so
-// the choice never depends on another stream's handle.  (The round-4 form synchronised the
-// previous user's stream from the host and fell back to the unsplit launch when that failed --
-// as it did once the stream was destroyed, e.g. a test's warm-up stream: later steps in the
-// process then computed the same convs unsplit, a different fp32 summation order.)  The
-// launches of one captured graph all come from its capture stream.
+// summed by halo_splitk_reduce.
+//
+// The decomposition is a function of the shape alone (halo_splitk_count): no stream, capture
+// or allocation state can change it, so every call of a shape sums in one fp32 order.  The
+// partials live in process-wide buffers (halo_splitk_slab), one for eager calls and one for
+// calls recorded into a graph (a replay must not share scratch with eager work on another
+// stream); both grow together, outside capture only.  Any failure to provide them -- a capture
+// needing more than an earlier eager call sized, an event or allocation error -- is an error
+// of the call, never a silent switch to the unsplit launch.  (Rounds 4 / 5 fell back to the
+// unsplit kernel, a different summation order, on such failures: a process-history-dependent
+// result.)  Stream order between eager users: each eager split launch pair records one event
+// after its reduce (halo_splitk_done) and the next eager user's stream always waits on it.
+// A graph buffer is never freed while a graph may still replay it (retired on growth).
 static std::mutex g_splitk_mu;
 static hipEvent_t g_splitk_ev = nullptr;
 static bool g_splitk_recorded = false;
-static hipStream_t g_splitk_last = nullptr;  // the stream of that event (same stream: no wait)
+static float* g_slab[2] = {nullptr, nullptr};  // [0] eager calls, [1] captured calls
+static size_t g_slab_cap = 0;
+static bool g_slab_captured = false;  // g_slab[1] is referenced by a captured graph
 static void halo_splitk_done(hipStream_t st) {
   std::lock_guard<std::mutex> lock(g_splitk_mu);
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return;
-  if (g_splitk_ev && hipEventRecord(g_splitk_ev, st) == hipSuccess) {
-    g_splitk_recorded = true;
-    g_splitk_last = st;
-  }
+  if (g_splitk_ev && hipEventRecord(g_splitk_ev, st) == hipSuccess) g_splitk_recorded = true;
 }
-static int halo_splitk(GldsArgs& a, unsigned grid, bool voc, bool hx64, hipStream_t st) {
+static int halo_splitk_count(const GldsArgs& a, unsigned grid, bool voc, bool hx64) {
   const int knob = g_tune[FS2_TUNE_HALO_SPLITK];
   const int ncb = a.Cin / 64;
   const int keep = FS2_EPI_BIAS | FS2_EPI_RELU | FS2_EPI_ADD_AUX | FS2_EPI_RELU_MASK_AUX |
@@ -2098,39 +2100,60 @@ static int halo_splitk(GldsArgs& a, unsigned grid, bool voc, bool hx64, hipStrea
   if (knob == -1 || voc || hx64 || !a.vec || (a.flags & ~keep) || a.N % 8) return 1;
   int kz = knob > 0 ? knob : (grid < 512 && ncb >= 8 ? (int)((768 + grid - 1) / grid) : 1);
   if (kz > ncb / 4) kz = ncb / 4;
-  if (kz < 2) return 1;
-  static float* buf = nullptr;
-  static size_t cap = 0;
+  return kz < 2 ? 1 : kz;
+}
+static int halo_splitk_slab(GldsArgs& a, int kz, hipStream_t st) {
   const size_t need = (size_t)kz * (size_t)a.M * (size_t)a.N * sizeof(float);
   std::lock_guard<std::mutex> lock(g_splitk_mu);
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(st, &cs) != hipSuccess) return 1;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess) {
+    set_error("fs2_conv_gemm: split-K: stream capture query failed");
+    return FS2_ERR_LAUNCH;
+  }
   const bool capturing = cs != hipStreamCaptureStatusNone;
-  if (!capturing) {
+  if (capturing) {
+    if (g_slab_cap < need) {
+      set_error("fs2_conv_gemm: split-K partials of %zu bytes needed during graph capture; run the "
+                "same shapes eagerly once before capturing (%zu bytes sized)", need, g_slab_cap);
+      return FS2_ERR_LAUNCH;
+    }
+    g_slab_captured = true;
+    a.slab = g_slab[1];
+  } else {
     if (!g_splitk_ev && hipEventCreateWithFlags(&g_splitk_ev, hipEventDisableTiming) != hipSuccess) {
       g_splitk_ev = nullptr;
-      return 1;
+      set_error("fs2_conv_gemm: split-K: event creation failed");
+      return FS2_ERR_LAUNCH;
     }
     // the previous eager user's reduce has read the buffer before this stream writes it
-    if (g_splitk_recorded && st != g_splitk_last &&
-        hipStreamWaitEvent(st, g_splitk_ev, 0) != hipSuccess)
-      return 1;
-  }
-  if (cap < need) {
-    if (capturing) return 1;
-    if (buf) {
-      if (hipDeviceSynchronize() != hipSuccess) return 1;
-      (void)hipFree(buf);
-      buf = nullptr;
-      cap = 0;
+    if (g_splitk_recorded && hipStreamWaitEvent(st, g_splitk_ev, 0) != hipSuccess) {
+      set_error("fs2_conv_gemm: split-K: stream wait failed");
+      return FS2_ERR_LAUNCH;
     }
-    void* p = nullptr;
-    if (hipMalloc(&p, need) != hipSuccess) return 1;
-    buf = static_cast<float*>(p);
-    cap = need;
+    if (g_slab_cap < need) {
+      if (hipDeviceSynchronize() != hipSuccess) {
+        set_error("fs2_conv_gemm: split-K: device synchronisation failed");
+        return FS2_ERR_LAUNCH;
+      }
+      (void)hipFree(g_slab[0]);
+      if (!g_slab_captured) (void)hipFree(g_slab[1]);  // else retired: a graph may replay it
+      g_slab[0] = g_slab[1] = nullptr;
+      g_slab_cap = 0;
+      g_slab_captured = false;
+      void *p0 = nullptr, *p1 = nullptr;
+      if (hipMalloc(&p0, need) != hipSuccess || hipMalloc(&p1, need) != hipSuccess) {
+        (void)hipFree(p0);
+        set_error("fs2_conv_gemm: split-K: hipMalloc of %zu bytes failed", need);
+        return FS2_ERR_LAUNCH;
+      }
+      g_slab[0] = static_cast<float*>(p0);
+      g_slab[1] = static_cast<float*>(p1);
+      g_slab_cap = need;
+    }
+    a.slab = g_slab[0];
   }
-  a.slab = buf;
-  return kz;
+  poison(a.slab, (int64_t)need, st);
+  return FS2_OK;
 }
 
 // n-tiles per tile group of the halo kernels (FS2_TUNE_NT_GROUP; default: all of them)
@@ -2348,8 +2371,9 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
   else conv_gemm_halo<BM_, BN_, 2, 16, false, 4, true><<<grid, 256, 0, st>>>(a);
     {
       if (halo_wide && halo_bm == 128) {
-        const int kz = g_tune[FS2_TUNE_HALO_SPLITK] > 0 ? halo_splitk(a, grid, voc, hx64, st) : 1;
+        const int kz = g_tune[FS2_TUNE_HALO_SPLITK] > 0 ? halo_splitk_count(a, grid, voc, hx64) : 1;
         if (kz > 1) {  // forced split of 128x128 tiles (experiments)
+          if (int rc = halo_splitk_slab(a, kz, st)) return rc;
           a.kz = kz;
           conv_gemm_halo<128, 128, 2, 16, false><<<grid * kz, 256, 0, st>>>(a);
           const int64_t n8 = rows * (c_out / 8);
@@ -2362,8 +2386,9 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
       } else if (halo_wide) { FS2_HALO2(64, 128) }
       else if (halo_bm == 128) {
         // a forced split count (FS2_TUNE_HALO_SPLITK > 0) also applies to full 128x64 grids
-        const int kz = g_tune[FS2_TUNE_HALO_SPLITK] > 0 ? halo_splitk(a, grid, voc, hx64, st) : 1;
+        const int kz = g_tune[FS2_TUNE_HALO_SPLITK] > 0 ? halo_splitk_count(a, grid, voc, hx64) : 1;
         if (kz > 1) {
+          if (int rc = halo_splitk_slab(a, kz, st)) return rc;
           a.kz = kz;
           conv_gemm_halo<128, 64, 2, 16, false, 4, true><<<grid * kz, 256, 0, st>>>(a);
           const int64_t n8 = rows * (c_out / 8);
@@ -2380,9 +2405,10 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
         a2.tiles_m = (int)((rows + 127) / 128);
         const unsigned grid2 = (unsigned)(a2.tiles_m * a2.tiles_n);
         const int kz2 = seq_len % 128 == 0 && g_tune[FS2_TUNE_HALO_SPLITK] != -2
-                            ? halo_splitk(a2, grid2, voc, hx64, st) : 1;
-        const int kz = kz2 > 1 ? 1 : halo_splitk(a, grid, voc, hx64, st);
+                            ? halo_splitk_count(a2, grid2, voc, hx64) : 1;
+        const int kz = kz2 > 1 ? 1 : halo_splitk_count(a, grid, voc, hx64);
         if (kz2 > 1) {
+          if (int rc = halo_splitk_slab(a2, kz2, st)) return rc;
           a2.kz = kz2;
           conv_gemm_halo<128, 64, 2, 16, false, 4, true><<<grid2 * kz2, 256, 0, st>>>(a2);
           const int64_t n8 = rows * (c_out / 8);
@@ -2390,6 +2416,7 @@ int conv_gemm_glds_launch(const void* x, int64_t ldx, const void* wk, void* y, i
                                     256, 0, st>>>(a2);
           halo_splitk_done(st);
         } else if (kz > 1) {
+          if (int rc = halo_splitk_slab(a, kz, st)) return rc;
           a.kz = kz;
           conv_gemm_halo<64, 64, 2, 16, false, 4, true><<<grid * kz, 256, 0, st>>>(a);
           const int64_t n8 = rows * (c_out / 8);

@@ -408,6 +408,7 @@ int fs2_fs2loss_fwd(const float* mel_out, const float* post_out, const float* me
   FS2_CHECK_ARG(tgt_len >= mel_len, "fs2_fs2loss_fwd: target shorter than prediction");
   FS2_CHECK_ARG(ws_bytes >= fs2_fs2loss_ws_bytes(batch, mel_len), "fs2_fs2loss_fwd: workspace too small");
   hipStream_t st = as_stream(stream);
+  poison(ws, ws_bytes, st);
   const int64_t np = loss_parts(batch, mel_len);
   fs2loss_partial<<<(unsigned)np, 256, 0, st>>>(mel_out, post_out, mel_tgt, tgt_len, p_pred, e_pred,
                                                 logd_pred, p_tgt, e_tgt, d_tgt, src_pad, mel_pad,

@@ -138,6 +138,7 @@ int fs2_grad_norm(const float* g, int64_t n, float max_norm, float* norm_coef, f
   FS2_CHECK_ARG(ws_bytes >= fs2_grad_norm_ws_bytes(n), "fs2_grad_norm: workspace too small");
   FS2_CHECK_ARG(((uintptr_t)g & 15) == 0, "fs2_grad_norm: gradient buffer must be 16-B aligned");
   hipStream_t st = as_stream(stream);
+  poison(ws, ws_bytes, st);
   sumsq_partial<<<GN_BLOCKS, 256, 0, st>>>(g, n, ws);
   norm_final<<<1, 1024, 0, st>>>(ws, GN_BLOCKS, max_norm, norm_coef);
   return launch_status("fs2_grad_norm");

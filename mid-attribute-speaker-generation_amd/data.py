@@ -88,5 +88,26 @@ def to_device(batch, device):
             t(accents).long().to(device))
 
 
+def pad_batch(batch, max_src_len, max_mel_len):
+    """A device batch padded on the right to ``max_src_len`` phonemes / ``max_mel_len`` frames
+    (zeros, as ``collate_fn``'s ``pad_1D`` / ``pad_2D`` pad the whole batch,
+    ``dataset.py:133-140``, ``utils/tools.py:329-360``); the lengths are unchanged.  Used
+    for a data-parallel shard whose own maxima are below the global batch's (see
+    ``train.Trainer``)."""
+    b = list(batch)
+    ds, dm = int(max_src_len) - int(b[5]), int(max_mel_len) - int(b[8])
+    if ds < 0 or dm < 0:
+        raise ValueError("pad_batch: target lengths below the batch's own")
+    F = torch.nn.functional
+    if ds:
+        for i in (3, 9, 10, 11, 13):  # texts, pitches, energies, durations, accents
+            b[i] = F.pad(b[i], (0, ds))
+        b[5] = int(max_src_len)
+    if dm:
+        b[6] = F.pad(b[6], (0, 0, 0, dm))  # mels (B, T, n_mel)
+        b[8] = int(max_mel_len)
+    return tuple(b)
+
+
 def valid_frames(batch):
     return int(np.asarray(batch[7] if not torch.is_tensor(batch[7]) else batch[7].cpu()).sum())

@@ -304,6 +304,7 @@ class Trainer:
             warnings.warn("Trainer(graph=True) with grad_acc_step > 1 runs eager steps "
                           "(HIP-graph replay captures whole optimiser steps only)", stacklevel=2)
         self.pg = process_group
+        self._host_pg = None
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
         self.dp = self.world > 1 if data_parallel is None else bool(data_parallel)
         self.cm = collective_model
@@ -334,6 +335,32 @@ class Trainer:
             self.buckets = GradBuckets(arena, process_group, bucket_bytes)
             self.buckets.producers = lambda: (model._side,)
             model._hooks["grad"] = self.buckets.ready
+            # host-side group for the ranks' shard lengths (_agree_lengths): gloo on CPU ints,
+            # so agreeing on them never waits for the GPU
+            if "gloo" in str(dist.get_backend(process_group)):
+                self._host_pg = process_group
+            else:
+                ranks = None if process_group is None else dist.get_process_group_ranks(process_group)
+                self._host_pg = dist.new_group(ranks=ranks, backend="gloo")
+
+    def _agree_lengths(self, batch):
+        """``nn.DataParallel`` semantics for the shards' padded lengths.  The reference collates
+        the global batch (``dataset.py:133-140``) and ``nn.DataParallel`` (``train.py:67-68``)
+        hands every replica its rows of it together with the global ``max_src_len`` /
+        ``max_mel_len``.  Those lengths are visible in the outputs: the PostNet BatchNorm
+        statistics run over every padded frame, the variance predictors' convs read the padded
+        phoneme rows (which carry the speaker embedding), and the ``--use_clf`` chunking cuts the
+        padded mel into ``max_mel_len // 150 + 1`` chunks.  So each rank pads its shard to the
+        ranks' maxima (one host-side all-reduce of two ints, no GPU sync) before the step."""
+        if self.cm is not None or self._host_pg is None:
+            return batch
+        t = torch.tensor([int(batch[5]), int(batch[8])], dtype=torch.int64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self._host_pg)
+        ts, tm = int(t[0]), int(t[1])
+        if ts == int(batch[5]) and tm == int(batch[8]):
+            return batch
+        from .data import pad_batch
+        return pad_batch(batch, ts, tm)
 
     def _global_denominators(self, batch):
         T_dec = min(int(batch[8]), self.model.decoder.max_seq_len)
@@ -382,6 +409,8 @@ class Trainer:
         global batch and this step's gradient buckets go out after the clf backward)."""
         update = self.batch_step % self.grad_acc == 0
         self.batch_step += 1
+        if self.dp:
+            batch = self._agree_lengths(batch)
         acc = dict(grad_acc_step=self.grad_acc, update=update)
         if clf is not None:
             if not self.dp:

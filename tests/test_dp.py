@@ -58,6 +58,36 @@ def _bucket_worker(rank, world, port, out):
     dist.destroy_process_group()
 
 
+def _lengths_worker(rank, world, port, out):
+    import types
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    pkg = importlib.import_module("mid-attribute-speaker-generation_amd")
+    tr = importlib.import_module("mid-attribute-speaker-generation_amd.train")
+    fake = types.SimpleNamespace(cm=None, _host_pg=dist.group.WORLD)
+    b = pkg.data.to_device(pkg.data.syn_batch(8, (40, 32)[rank], seed=10 + rank), "cpu")
+    got = tr.Trainer._agree_lengths(fake, b)
+    torch.save([x for x in got[2:] if torch.is_tensor(x) or isinstance(x, int)], f"{out}/len{rank}.pt")
+    dist.destroy_process_group()
+
+
+def test_data_parallel_shard_lengths_agree_gloo_cpu():
+    """Trainer._agree_lengths on 2 gloo ranks (CPU): shards of 40 / 32 phonemes (160 / 128
+    frames) both come out padded to the global maxima, as DataParallel replicas of the
+    reference's collated batch are (dataset.py:133-140, train.py:67-68); the longer shard is
+    unchanged."""
+    pkg = importlib.import_module("mid-attribute-speaker-generation_amd")
+    with tempfile.TemporaryDirectory() as out:
+        mp.spawn(_lengths_worker, args=(2, _port(), out), nprocs=2, join=True)
+        for rank, ts in enumerate((40, 32)):
+            got = torch.load(f"{out}/len{rank}.pt")
+            want = pkg.data.to_device(_pad_np(pkg.data.syn_batch(8, ts, seed=10 + rank), 40, 160), "cpu")
+            want = [x for x in want[2:] if torch.is_tensor(x) or isinstance(x, int)]
+            assert len(got) == len(want)
+            for g, w in zip(got, want):
+                assert (g == w) if isinstance(w, int) else (g.shape == w.shape and torch.equal(g, w))
+
+
 def test_grad_buckets_gloo_cpu():
     with tempfile.TemporaryDirectory() as out:
         mp.spawn(_bucket_worker, args=(2, _port(), out), nprocs=2, join=True)
@@ -394,7 +424,30 @@ def _clf_pair(dev):
     return d, G.GE2ELoss(dev)
 
 
-def _clf_worker(rank, world, port, out):
+def _pad_np(b, ts, tm):
+    """A numpy syn_batch padded on the right to ts phonemes / tm frames with zeros (the global
+    batch's collate, dataset.py:133-140) -- independent of data.pad_batch."""
+    b = list(b)
+    ds, dm = ts - b[5], tm - b[8]
+    for i in (3, 9, 10, 11, 13):
+        b[i] = np.pad(b[i], ((0, 0), (0, ds)))
+    b[6] = np.pad(b[6], ((0, 0), (0, dm), (0, 0)))
+    b[5], b[8] = ts, tm
+    return tuple(b)
+
+
+def _clf_shard(pkg, rank, dev, ts=None, pad=False):
+    """Rank's shard: the equal-length default (_shard), or syn_batch(8, ts[rank]) -- padded to
+    the ranks' maxima when ``pad`` (what a replica of the reference's DataParallel receives)."""
+    if ts is None:
+        return _shard(pkg, rank, dev, 0)
+    b = pkg.data.syn_batch(8, ts[rank], seed=10 + rank)
+    if pad:
+        b = _pad_np(b, max(ts), 4 * max(ts))
+    return pkg.data.to_device(b, dev)
+
+
+def _clf_worker(rank, world, port, out, ts=None):
     import sys
     sys.path.insert(0, REPO)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -421,7 +474,7 @@ def _clf_worker(rank, world, port, out):
 
     t.opt.clip_grad_norm_ = capture
     for s in range(2):
-        r = t.step(_shard(pkg, rank, dev, 0), clf=clf, clf_args=(_CLF_PERM, 4 + s, 10, 1.0))
+        r = t.step(_clf_shard(pkg, rank, dev, ts), clf=clf, clf_args=(_CLF_PERM, 4 + s, 10, 1.0))
         dl.append((float(r[4][0]), int(r[4][1]), int(r[4][2])))
         globs.append(torch.cat([t.Loss.denoms, t.eLoss.denom]).cpu())
     torch.save({"g": grads, "glob": globs, "dl": dl, "w": model.arena().flat.cpu()},
@@ -429,7 +482,7 @@ def _clf_worker(rank, world, port, out):
     dist.destroy_process_group()
 
 
-def _emulate_clf(globs):
+def _emulate_clf(globs, ts=None):
     """One process, both shards per step, as _emulate, plus the clf branch per shard with the
     speakers / metadata of the permuted global batch and the global chunk count."""
     pkg = importlib.import_module("mid-attribute-speaker-generation_amd")
@@ -443,7 +496,7 @@ def _emulate_clf(globs):
     model.train()
     t = tr.Trainer(model, pp, mc, tc)
     disc, dLoss = _clf_pair("cuda:0")
-    shards = [_shard(pkg, r, "cuda:0", 0) for r in range(2)]
+    shards = [_clf_shard(pkg, r, "cuda:0", ts, pad=True) for r in range(2)]
     gspk = torch.cat([b[2] for b in shards])
     gmeta = torch.cat([b[12] for b in shards])
     perm = torch.as_tensor(_CLF_PERM, device="cuda:0")
@@ -481,19 +534,27 @@ def _emulate_clf(globs):
 
 
 @pytest.mark.gpu
-def test_data_parallel_use_clf_matches_emulation():
+@pytest.mark.parametrize("ts", [None, (40, 32)])
+def test_data_parallel_use_clf_matches_emulation(ts):
     """``--use_clf`` under data parallelism (Trainer.step, 2 ranks on gloo, both on cuda:0):
     the global permutation of speakers / metadata across the ranks, the global chunk count, and
     the buckets all-reduced after the clf backward give the gradients, discriminator losses
     and weights of one process running both shards (sums of per-shard gradients; the emulation
-    accumulates both shards in one buffer, so fp32 summation order differs: 1e-5)."""
+    accumulates both shards in one buffer, so fp32 summation order differs: 1e-5).
+    ``ts = (40, 32)``: shards of different lengths (160 vs 128 frames, so 2 vs 1 chunks of
+    150 each on their own).  The reference's DataParallel replicas all see the global batch's
+    max lengths, so the emulation runs each shard padded to 40 phonemes / 160 frames -- the
+    PostNet statistics, the predictors' padded rows and the chunk count (2 per utterance) all
+    follow from it -- and the ranks must agree on them (Trainer._agree_lengths)."""
     with tempfile.TemporaryDirectory() as out:
-        mp.spawn(_clf_worker, args=(2, _port(), out), nprocs=2, join=True)
+        mp.spawn(_clf_worker, args=(2, _port(), out, ts), nprocs=2, join=True)
         r0, r1 = torch.load(f"{out}/clf0.pt"), torch.load(f"{out}/clf1.pt")
         for g0, g1 in zip(r0["g"], r1["g"]):
             assert torch.equal(g0, g1)
         assert r0["dl"] == r1["dl"] and r0["dl"][0][2] % 16 == 0  # 16 utterances x chunks each
-        grads, dls, w = _emulate_clf(r0["glob"])
+        if ts is not None:
+            assert r0["dl"][0][2] == 16 * (4 * max(ts) // 150 + 1)
+        grads, dls, w = _emulate_clf(r0["glob"], ts)
         # step 0 from the same weights: the gradients to fp32 summation order.  Step 1 starts
         # from weights one Adam step apart, and Adam's m / sqrt(v) turns the summation-order
         # noise of near-zero gradients into updates of up to lr: looser there

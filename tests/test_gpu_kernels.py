@@ -958,6 +958,22 @@ def test_batchnorm_widths(M, c):
     close(db, br.grad)
 
 
+def test_batchnorm_tanh_relative_near_zero():
+    """The PostNet's tanh (BatchNorm epilogue) in RELATIVE terms near 0, where an absolute
+    error of ~3e-7 would be a large relative one: gamma spreads the normalised values over
+    |y| in [1e-9, 2] on a log scale, against torch.tanh of the same fp32 pre-activation."""
+    M, c = 4096, 64
+    z = rnd(M, c, seed=31)
+    g = torch.logspace(-9, 0.3, c, device=DEV)
+    b = torch.zeros(c, device=DEV)
+    out, _, mean, rstd = K.bn_fwd(z, g, b, None, None, True, 0.0, 1, 2)
+    y = (z - mean) * rstd * g  # the kernel's own statistics: only the tanh is under test
+    ref = torch.tanh(y.double())
+    rel = ((out.double() - ref).abs() / ref.abs().clamp_min(1e-30))
+    big = y.abs() >= 1e-12  # below that the pre-activation itself is at fp32's denormal edge
+    assert rel[big].max().item() <= 5e-6, f"max relative error {rel[big].max().item():.3e}"
+
+
 @pytest.mark.parametrize("c,act", [(512, True), (80, False)])
 def test_batchnorm_dropout(c, act):
     """PostNet BatchNorm with dropout (p = 0.5): keep-rate of the 16-bit Philox draws, and the

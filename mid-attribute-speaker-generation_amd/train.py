@@ -304,7 +304,8 @@ class Trainer:
             warnings.warn("Trainer(graph=True) with grad_acc_step > 1 runs eager steps "
                           "(HIP-graph replay captures whole optimiser steps only)", stacklevel=2)
         self.pg = process_group
-        self._host_pg = None
+        self._agree = False  # data-parallel shards padded to the ranks' maxima (_agree_lengths)
+        self._host_pg = None  # its group (None: the default group, when that is gloo)
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
         self.dp = self.world > 1 if data_parallel is None else bool(data_parallel)
         self.cm = collective_model
@@ -337,6 +338,7 @@ class Trainer:
             model._hooks["grad"] = self.buckets.ready
             # host-side group for the ranks' shard lengths (_agree_lengths): gloo on CPU ints,
             # so agreeing on them never waits for the GPU
+            self._agree = True
             if "gloo" in str(dist.get_backend(process_group)):
                 self._host_pg = process_group
             else:
@@ -352,7 +354,7 @@ class Trainer:
         phoneme rows (which carry the speaker embedding), and the ``--use_clf`` chunking cuts the
         padded mel into ``max_mel_len // 150 + 1`` chunks.  So each rank pads its shard to the
         ranks' maxima (one host-side all-reduce of two ints, no GPU sync) before the step."""
-        if self.cm is not None or self._host_pg is None:
+        if not self._agree:
             return batch
         t = torch.tensor([int(batch[5]), int(batch[8])], dtype=torch.int64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self._host_pg)

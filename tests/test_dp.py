@@ -64,7 +64,9 @@ def _lengths_worker(rank, world, port, out):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     pkg = importlib.import_module("mid-attribute-speaker-generation_amd")
     tr = importlib.import_module("mid-attribute-speaker-generation_amd.train")
-    fake = types.SimpleNamespace(cm=None, _host_pg=dist.group.WORLD)
+    # the state Trainer(data_parallel) leaves on a gloo default group: _host_pg None (the
+    # default group), which round 6's first version took for "no group" and skipped
+    fake = types.SimpleNamespace(cm=None, _agree=True, _host_pg=None)
     b = pkg.data.to_device(pkg.data.syn_batch(8, (40, 32)[rank], seed=10 + rank), "cpu")
     got = tr.Trainer._agree_lengths(fake, b)
     torch.save([x for x in got[2:] if torch.is_tensor(x) or isinstance(x, int)], f"{out}/len{rank}.pt")

@@ -698,14 +698,31 @@ int fs2_add(float* out, const float* a, const float* b, int64_t n, void* stream)
  * (tests/test_stale_reads.py).  fs2_debug_poison(byte), byte in [0, 255] (or the FS2_POISON
  * environment variable, read once): every workspace an entry point receives and the library's
  * reused split-K partials are filled with that byte before each use; -1 turns it off (the
- * default).  fs2_debug_alloc / fs2_debug_free have the
- * signatures of torch.cuda.memory.CUDAPluggableAllocator: no caching, every device allocation
- * filled with the poison byte (0xff when off) at allocation, every free after a device drain.
- * With both, a kernel that reads memory nothing wrote this step reads the poison, so its
- * results depend on the byte instead of on what ran earlier in the process.               */
+ * default).  fs2_debug_alloc / fs2_debug_free have the signatures of
+ * torch.cuda.memory.CUDAPluggableAllocator: no caching and no device synchronisation; a block
+ * is filled with the poison byte (0xff when off) at allocation (done before the call returns)
+ * and again on its stream at its free, and freed blocks are quarantined (not reused) until 6 GB of them pile up.  With both, a
+ * kernel that reads memory nothing wrote this step, or memory freed before it ran, reads the
+ * poison, so its results depend on the byte instead of on what ran earlier in the process.
+ * With poisoning on, every fs2_stream_wait also fills the LDS of every CU with the byte on the
+ * waiting stream (one 160 KiB block per CU), so a kernel reading LDS it did not write reads it.
+ * fs2_debug_race(delay_us, main_stream, mode): mode 0 -- every stream other than main_stream
+ * is held back delay_us after each fs2_stream_wait it receives (a one-lane sleep kernel), so
+ * side-stream work trails the main stream and a buffer freed or overwritten on the main stream
+ * before a side-stream reader ran is poisoned by then; mode 1 -- the main stream is held back
+ * after each event a side stream waits on, so a side-stream read of a main-stream result that
+ * was not waited for reads stale data.  Either way a missing ordering or lifetime guard fails
+ * deterministically.  Mode 2 -- a seeded random schedule: at each wait the waiter and the
+ * signaler are each held back with probability 1/2 by a random 0..delay_us (an LCG from seed),
+ * so one seed replays one interleaving.  delay_us 0: off.  fs2_debug_lds_dma_oob(src, out, stream): one wave
+ * LDS-DMAs 16 B per lane from src (64 x 16 B) into LDS pre-filled with 0xAB bytes, lanes 32-63
+ * at an out-of-range offset, and copies the 1 KiB image to out (the padding-row contract of
+ * every LDS-DMA kernel: out-of-range lanes land zeros).                                      */
 int fs2_debug_poison(int byte);
 void* fs2_debug_alloc(int64_t size, int device, void* stream);
 void fs2_debug_free(void* ptr, int64_t size, int device, void* stream);
+int fs2_debug_race(int delay_us, void* main_stream, int mode, int seed);
+int fs2_debug_lds_dma_oob(const float* src, void* out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -3,6 +3,9 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <mutex>
+#include <vector>
+
 #include "common.hpp"
 
 namespace fs2 {
@@ -74,6 +77,28 @@ static unsigned grid_for(int64_t n) {
   return (unsigned)b;
 }
 
+// LDS poisoning (with fs2_debug_poison): one 160 KiB block per CU fills its LDS with the poison
+// byte, so a kernel that reads LDS it did not write in its own launch reads the byte instead of
+// what the CU's previous kernel left there
+__global__ __launch_bounds__(256) void lds_fill_kernel(uint32_t word) {
+  extern __shared__ uint32_t lds_all[];
+  for (int i = threadIdx.x; i < 163840 / 4; i += 256) lds_all[i] = word;
+  __syncthreads();
+  if (lds_all[(threadIdx.x * 37) % (163840 / 4)] == 0x12345678u && word == 1u) lds_all[0] = 0;
+}
+void lds_poison(hipStream_t st) {
+  const int b = poison_byte();
+  if (b < 0) return;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)lds_fill_kernel,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+    attr = true;
+  }
+  const uint32_t w = 0x01010101u * (uint32_t)b;
+  lds_fill_kernel<<<512, 256, 163840, st>>>(w);
+}
+
 }  // namespace fs2
 
 using namespace fs2;
@@ -88,6 +113,31 @@ int fs2_set_tuning(int knob, int value) {
   FS2_CHECK_ARG(knob >= 0 && knob < FS2_TUNE_COUNT, "fs2_set_tuning: unknown knob %d", knob);
   g_tune[knob] = value;
   return FS2_OK;
+}
+
+// race mode (fs2_debug_race): mode 0 holds every stream other than `main` back this long after
+// each cross-stream wait it receives, so it trails the main stream; mode 1 holds the main stream
+// back after each event a non-main stream waits on, so the main stream trails instead.
+static int g_race_us = 0;
+static int g_race_mode = 0;
+static void* g_race_main = nullptr;
+static uint64_t g_race_rng = 0;
+
+__global__ void delay_kernel(uint64_t ticks) {
+  const uint64_t t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(64);
+}
+
+static int race_delay(void* st, int us) {
+  static uint64_t per_us = 0;
+  if (!per_us) {
+    int khz = 0;
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, 0) != hipSuccess || khz <= 0)
+      khz = 100000;  // the 100 MHz constant clock
+    per_us = (uint64_t)khz / 1000;
+  }
+  delay_kernel<<<1, 1, 0, as_stream(st)>>>((uint64_t)us * per_us);
+  return launch_status("fs2_debug_race delay");
 }
 
 // Cross-stream ordering without host objects: a ring of timing-free events; a wait binds to
@@ -111,7 +161,51 @@ int fs2_stream_wait(void* waiter, void* signaler) {
     set_error("fs2_stream_wait: event record/wait failed");
     return FS2_ERR_LAUNCH;
   }
+  lds_poison(as_stream(waiter));
+  if (g_race_us > 0) {
+    if (g_race_mode == 0 && waiter != g_race_main) return race_delay(waiter, g_race_us);
+    if (g_race_mode == 1 && signaler == g_race_main && waiter != g_race_main)
+      return race_delay(signaler, g_race_us);
+    if (g_race_mode == 2) {  // seeded random schedule: either side may be held back
+      for (void* st : {waiter, signaler}) {
+        g_race_rng = g_race_rng * 6364136223846793005ull + 1442695040888963407ull;
+        const uint32_t r = (uint32_t)(g_race_rng >> 33);
+        if (r & 1) {
+          const int rc = race_delay(st, (int)((r >> 1) % (uint32_t)g_race_us));
+          if (rc) return rc;
+        }
+      }
+    }
+  }
   return FS2_OK;
+}
+
+int fs2_debug_race(int delay_us, void* main_stream, int mode, int seed) {
+  FS2_CHECK_ARG(mode >= 0 && mode <= 2,
+                "fs2_debug_race: mode 0 (side trails), 1 (main trails) or 2 (seeded random)");
+  g_race_us = delay_us > 0 ? delay_us : 0;
+  g_race_mode = mode;
+  g_race_main = main_stream;
+  g_race_rng = 0x9E3779B97F4A7C15ull ^ (uint64_t)(uint32_t)seed;
+  return FS2_OK;
+}
+
+// LDS-DMA of an out-of-range buffer offset: what lands in LDS (one wave; out[i], i < 64 * 4,
+// the dwords of 16 B per lane after the LDS was filled with 0xAB bytes)
+__global__ void lds_dma_oob_kernel(const float* src, uint32_t* out) {
+  __shared__ __attribute__((aligned(16))) uint32_t img[64 * 4];
+  for (int i = threadIdx.x; i < 64 * 4; i += 64) img[i] = 0xABABABABu;
+  __syncthreads();
+  const auto r = buf_rsrc(src, 64 * 16);
+  const uint32_t voff = threadIdx.x < 32 ? threadIdx.x * 16u : kOOB;
+  glds16_buf(r, img, voff, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int i = threadIdx.x; i < 64 * 4; i += 64) out[i] = img[i];
+}
+int fs2_debug_lds_dma_oob(const float* src, void* out, void* stream) {
+  lds_dma_oob_kernel<<<1, 64, 0, as_stream(stream)>>>(src, (uint32_t*)out);
+  return launch_status("fs2_debug_lds_dma_oob");
 }
 
 int fs2_debug_poison(int byte) {
@@ -119,15 +213,37 @@ int fs2_debug_poison(int byte) {
   return FS2_OK;
 }
 
-// torch.cuda.memory.CUDAPluggableAllocator pair: no caching, every block filled with the poison
-// byte (0xff when poisoning is off) at allocation; a free waits for the device to drain first
+// torch.cuda.memory.CUDAPluggableAllocator pair: no caching and no device synchronisation.  A
+// block is filled with the poison byte (0xff when poisoning is off) at allocation (complete
+// before the call returns) and again on its stream at its free; freed blocks are quarantined (never handed out again) until the
+// quarantine passes kQuarantineBytes, then drained after a device synchronisation.  A read of
+// a block after its free -- another stream still using it, unordered against the free --
+// therefore sees the poison instead of whatever reused the memory.
+static std::mutex g_dbg_mu;
+static std::vector<void*> g_quarantine;
+static size_t g_quarantine_bytes = 0;
+static constexpr size_t kQuarantineBytes = size_t(6) << 30;
+
 void* fs2_debug_alloc(int64_t size, int device, void* stream) {
   (void)device;
-  (void)stream;
   void* p = nullptr;
-  if (hipMalloc(&p, size > 0 ? (size_t)size : 1) != hipSuccess) return nullptr;
+  if (hipMalloc(&p, size > 0 ? (size_t)size : 1) != hipSuccess) {
+    std::lock_guard<std::mutex> lock(g_dbg_mu);  // drain the quarantine and try once more
+    (void)hipDeviceSynchronize();
+    for (void* q : g_quarantine) (void)hipFree(q);
+    g_quarantine.clear();
+    g_quarantine_bytes = 0;
+    if (hipMalloc(&p, size > 0 ? (size_t)size : 1) != hipSuccess) return nullptr;
+  }
+  // fresh memory: filled on a stream of our own and waited for here, so the fill precedes every
+  // later use on any stream without ordering it behind (or draining) the work already queued on
+  // the allocating stream -- which the race modes hold back on purpose
+  (void)stream;
+  static hipStream_t fill_st = nullptr;
+  if (!fill_st && hipStreamCreateWithFlags(&fill_st, hipStreamNonBlocking) != hipSuccess) fill_st = nullptr;
   const int b = poison_byte();
-  if (size > 0 && hipMemset(p, b >= 0 ? b : 0xff, (size_t)size) != hipSuccess) {
+  if (size > 0 && (!fill_st || hipMemsetAsync(p, b >= 0 ? b : 0xff, (size_t)size, fill_st) != hipSuccess ||
+                   hipStreamSynchronize(fill_st) != hipSuccess)) {
     (void)hipFree(p);
     return nullptr;
   }
@@ -135,11 +251,18 @@ void* fs2_debug_alloc(int64_t size, int device, void* stream) {
 }
 
 void fs2_debug_free(void* p, int64_t size, int device, void* stream) {
-  (void)size;
   (void)device;
-  (void)stream;
-  (void)hipDeviceSynchronize();
-  (void)hipFree(p);
+  const int b = poison_byte();
+  if (size > 0) (void)hipMemsetAsync(p, b >= 0 ? b : 0xff, (size_t)size, as_stream(stream));
+  std::lock_guard<std::mutex> lock(g_dbg_mu);
+  g_quarantine.push_back(p);
+  g_quarantine_bytes += size > 0 ? (size_t)size : 1;
+  if (g_quarantine_bytes > kQuarantineBytes) {
+    (void)hipDeviceSynchronize();
+    for (void* q : g_quarantine) (void)hipFree(q);
+    g_quarantine.clear();
+    g_quarantine_bytes = 0;
+  }
 }
 
 int fs2_fill(float* x, int64_t n, float value, void* stream) {

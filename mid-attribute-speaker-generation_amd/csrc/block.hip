@@ -191,6 +191,7 @@ int fs2_fft_block_fwd(const int64_t* blk, const float* x, const void* x_t, void*
   const int64_t T = seq_len;
   const uint64_t* sd = p > 0.f ? seed : nullptr;
   FS2_CHECK_ARG(!(p > 0.f) || seed, "fs2_fft_block_fwd: dropout without seed");
+  lds_poison(as_stream(stream));
   void* qkv = at<void>(act, L.qkv);
   void* o = at<void>(act, L.o);
   float* lse = at<float>(act, L.lse);
@@ -258,6 +259,7 @@ int fs2_fft_block_bwd(const int64_t* blk, void* act, const void* x_t, int fuse_l
   void* side = side_stream ? side_stream : stream;
   FS2_CHECK_ARG(side_ws && side_ws_bytes >= fs2_fft_block_side_ws_bytes(blk, rows),
                 "fs2_fft_block_bwd: side-stream workspace too small");
+  lds_poison(as_stream(stream));
   const void* qkv = at<void>(act, L.qkv);
   const void* o = at<void>(act, L.o);
   const float* lse = at<float>(act, L.lse);

@@ -30,6 +30,8 @@ int launch_status(const char* what);
 // runs with different bytes differ instead of depending on what ran before in the process.
 int poison_byte();
 void poison(void* p, int64_t bytes, hipStream_t st);
+// ... and the LDS of every CU filled with it on `st` (no-op when poisoning is off)
+void lds_poison(hipStream_t st);
 
 #define FS2_CHECK_ARG(cond, ...)                     \
   do {                                               \

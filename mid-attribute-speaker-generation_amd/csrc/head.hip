@@ -280,6 +280,7 @@ int fs2_mel_head_fwd(const int64_t* mh, const void* x_t, void* act, int64_t rows
   const MhAct A = mh_act(m, rows);
   const int64_t T = seq_len;
   const uint64_t* sd = p > 0.f ? seed : nullptr;
+  lds_poison(as_stream(stream));
   float* ws = at<float>(act, A.ws);
   // mel_linear (fastspeech2.py:91) and its bf16 copy: the PostNet's input and residual
   float* out = at<float>(act, A.out);
@@ -319,6 +320,7 @@ int fs2_mel_head_bwd(const int64_t* mh, void* act, const void* x_t, const float*
   FS2_CHECK_ARG(!(p > 0.f) || seed, "fs2_mel_head_bwd: dropout without seed");
   FS2_CHECK_ARG(side_ws && side_ws_bytes >= fs2_mel_head_side_ws_bytes(mh, rows),
                 "fs2_mel_head_bwd: side-stream workspace too small");
+  lds_poison(as_stream(stream));
   const MhAct A = mh_act(m, rows);
   const MhTmp W = mh_tmp(m, rows);
   const int64_t T = seq_len;
@@ -408,6 +410,7 @@ int fs2_variance_predictor_fwd(const int64_t* vp, const void* x_t, void* act, in
   const VpAct A = vp_act(v, rows);
   const int64_t T = seq_len;
   const uint64_t* sd = p > 0.f ? seed : nullptr;
+  lds_poison(as_stream(stream));
   float* h1 = at<float>(act, A.h1);
   void* u1_t = at<void>(act, A.u1_t);
   float* h2 = at<float>(act, A.h2);
@@ -436,6 +439,7 @@ int fs2_variance_predictor_bwd(const int64_t* vp, void* act, const void* x_t, co
   FS2_CHECK_ARG(!(p > 0.f) || seed, "fs2_variance_predictor_bwd: dropout without seed");
   FS2_CHECK_ARG(side_ws && side_ws_bytes >= fs2_variance_predictor_side_ws_bytes(vp, rows),
                 "fs2_variance_predictor_bwd: side-stream workspace too small");
+  lds_poison(as_stream(stream));
   const Vp v = unpack_vp(vp);
   const VpAct A = vp_act(v, rows);
   const VpTmp W = vp_tmp(v, rows);

@@ -3,12 +3,14 @@
 Every device allocation of the process comes from the library's debug allocator
 (``fs2_debug_alloc``: no caching, each block filled with the poison byte) and every
 workspace / split-K scratch the library reuses is re-filled with the byte before each use
-(``fs2_debug_poison``).  A kernel that reads memory nothing wrote this step therefore reads
-the byte: runs with two different bytes give different results instead of results that
+(``fs2_debug_poison``); a freed block is poisoned again on its stream and never reused.
+With ``--race`` the side streams trail the main stream by that many microseconds after every
+cross-stream wait.  A kernel that reads memory nothing wrote this step, or memory freed before
+it ran, therefore reads the byte: runs with two different bytes give different results instead of results that
 depend on what ran earlier in the process.  ``tests/test_stale_reads.py`` compares them.
 
     python tests/stale_probe.py --poison 0 --out a.pt [--dtype bf16|f32] [--path c|kernel]
-        [--fuse 0|1] [--batch 8x32] [--seed 25]
+        [--fuse 0|1] [--batch 8x32] [--seed 25] [--race US [--race-mode 0|1]]
 
 Writes {"grads": {name: tensor}, "losses1": ..., "flat": ..., "m": ..., "v": ...,
 "bn": ..., "losses2": ...}: the parameter gradients of one forward + backward
@@ -34,17 +36,48 @@ def main(argv=None):
     ap.add_argument("--batch", default="8x32")
     ap.add_argument("--seed", type=int, default=25)
     ap.add_argument("--no-side", action="store_true", help="weight gradients on the main stream")
+    ap.add_argument("--drop-keep", action="store_true",
+                    help="detector self-check: StepCtx.keep forgets what it is given, so the "
+                         "side stream's operands may be freed before it reads them")
+    ap.add_argument("--race-mode", type=int, default=0,
+                    help="0: side streams trail the main stream; 1: the main stream trails")
+    ap.add_argument("--race", type=int, default=0,
+                    help="hold every non-main stream back this many us after each cross-stream "
+                         "wait (fs2_debug_race): a side-stream read of a buffer the main stream "
+                         "freed before it then reads the poison")
+    ap.add_argument("--plain", action="store_true",
+                    help="no poisoning and torch's caching allocator (a repeat-run baseline)")
     a = ap.parse_args(argv)
 
-    os.environ["FS2_POISON"] = str(a.poison)
+    if not a.plain:
+        os.environ["FS2_POISON"] = str(a.poison)
     import torch
     sys.path.insert(0, REPO)
     lib_mod = importlib.import_module(PKG_NAME + "._lib")
-    alloc = torch.cuda.memory.CUDAPluggableAllocator(lib_mod.LIB_PATH, "fs2_debug_alloc",
-                                                      "fs2_debug_free")
-    torch.cuda.memory.change_current_allocator(alloc)
-    lib_mod.lib.fs2_debug_poison(a.poison)
+    if not a.plain:
+        alloc = torch.cuda.memory.CUDAPluggableAllocator(lib_mod.LIB_PATH, "fs2_debug_alloc",
+                                                          "fs2_debug_free")
+        torch.cuda.memory.change_current_allocator(alloc)
+        lib_mod.lib.fs2_debug_poison(a.poison)
+    if a.race:
+        lib_mod.lib.fs2_debug_race(a.race, torch.cuda.current_stream().cuda_stream, a.race_mode, 0)
 
+    if a.drop_keep:
+        M = importlib.import_module(PKG_NAME + ".model")
+
+        class _Forget(list):
+            def append(self, x):
+                pass
+
+            def extend(self, x):
+                pass
+
+        init = M.StepCtx.__init__
+
+        def _init(self, *args, **kw):
+            init(self, *args, **kw)
+            self.keep = _Forget()
+        M.StepCtx.__init__ = _init
     out = run_config(dtype=a.dtype, path=a.path, fuse=a.fuse, batch=a.batch, seed=a.seed,
                      side=not a.no_side)
     torch.save(out, a.out)

@@ -1150,3 +1150,18 @@ def test_wgrad_k1_multi(B, T, lens_on, dt):
         assert torch.equal(j[2], w1)
         if j[3] is not None:
             assert torch.equal(j[3], b1)
+
+
+@pytest.mark.gpu
+def test_lds_dma_out_of_range_lanes_land_zeros():
+    """The padding-row contract of every LDS-DMA kernel (conv_wgrad_band, the halo / tap-register
+    GEMMs, attention): a buffer LDS-DMA at an out-of-range offset writes zeros into LDS rather
+    than leaving what was there (the LDS is pre-filled with 0xAB bytes, lanes 32-63 out of
+    range).  If it left the old bytes, padded rows would carry whatever the CU's previous kernel
+    left in LDS -- a result that depends on process history."""
+    src = torch.arange(64 * 4, dtype=torch.float32, device=DEV) + 1.0
+    out = torch.empty(64 * 4, dtype=torch.int32, device=DEV)
+    K.lib.fs2_debug_lds_dma_oob(src.data_ptr(), out.data_ptr(), K.stream())
+    got = out.cpu()
+    assert torch.equal(got[:128], src[:128].cpu().view(torch.int32))
+    assert int((got[128:] != 0).sum()) == 0, got[128:].tolist()[:8]

@@ -5,8 +5,11 @@ the same process: a kernel read memory that nothing had written in the step, so 
 followed the allocator's history.  ``tests/stale_probe.py`` runs a step in a fresh process
 with every device allocation, every workspace and the split-K scratch filled with one byte
 (the library's debug allocator and ``fs2_debug_poison``); a stale read then sees that byte.
-Two processes with different bytes must produce bitwise the same gradients, weights, Adam
-moments, BatchNorm statistics and losses.
+A freed block is poisoned on its stream and quarantined, and in the race cases every stream but
+the main one trails it by 20 ms after each cross-stream wait (``fs2_debug_race``), so a
+side-stream read of a buffer freed on the main stream sees the byte too.  Two processes with
+different bytes must produce bitwise the same gradients, weights, Adam moments, BatchNorm
+statistics and losses.
 """
 import os
 import subprocess
@@ -31,9 +34,31 @@ def _probe(tmp, byte, *args):
     return torch.load(out, weights_only=True)
 
 
-@pytest.mark.parametrize("args", [(), ("--dtype", "f32")], ids=["bf16-c", "f32"])
+# race: the weight-gradient (side) stream held back 20 ms after every wait on the main stream,
+# longer than the host takes to reach the end of the step at SYN-8 x 32, so a buffer the main
+# stream frees (and poisons) while a side-stream kernel still has to read it is poisoned by then
+# race-mode 1 holds the main stream back instead (a side-stream read of a main-stream result it
+# did not wait for reads stale data); fuse 0: the post-LN GEMM fusions on every block
+@pytest.mark.parametrize("args", [(), ("--dtype", "f32"), ("--race", "20000"),
+                                  ("--race", "20000", "--path", "kernel"),
+                                  ("--race", "20000", "--race-mode", "1"),
+                                  ("--race", "20000", "--race-mode", "1", "--path", "kernel"),
+                                  ("--race", "20000", "--fuse", "0"),
+                                  ("--race", "20000", "--race-mode", "1", "--fuse", "0")],
+                         ids=["bf16-c", "f32", "bf16-c-race", "bf16-kernel-race", "bf16-c-lag",
+                              "bf16-kernel-lag", "bf16-c-fused-race", "bf16-c-fused-lag"])
 def test_step_independent_of_stale_memory(tmp_path, args):
     a = _probe(str(tmp_path), 0, *args)
     b = _probe(str(tmp_path), 63, *args)
     d = stale_probe.diff(a, b)
-    assert not d, "results depend on unwritten memory:\n" + "\n".join(d[:20])
+    assert not d, ("results depend on unwritten memory:\n" + "\n".join(d[:12]) +
+                   f"\n{len(d)} entries: " + "; ".join(x.split(":")[0] for x in d))
+
+
+def test_race_detector_catches_a_missing_lifetime_guard(tmp_path):
+    """The detector itself: with StepCtx.keep forgetting its tensors (the side stream's operands
+    may then be freed, poisoned and reused before it reads them) the side-trailing race mode
+    must see the poison byte in the results."""
+    a = _probe(str(tmp_path), 0, "--race", "20000", "--drop-keep")
+    b = _probe(str(tmp_path), 63, "--race", "20000", "--drop-keep")
+    assert stale_probe.diff(a, b), "the race mode did not expose a dropped lifetime guard"

@@ -717,12 +717,22 @@ int fs2_add(float* out, const float* a, const float* b, int64_t n, void* stream)
  * so one seed replays one interleaving.  delay_us 0: off.  fs2_debug_lds_dma_oob(src, out, stream): one wave
  * LDS-DMAs 16 B per lane from src (64 x 16 B) into LDS pre-filled with 0xAB bytes, lanes 32-63
  * at an out-of-range offset, and copies the 1 KiB image to out (the padding-row contract of
- * every LDS-DMA kernel: out-of-range lanes land zeros).                                      */
+ * every LDS-DMA kernel: out-of-range lanes land zeros).  fs2_debug_snap(buf, cap): the variance
+ * predictor backward appends copies of its intermediates (dh2, the LN2 partials, du1, dh1, the
+ * LN1 partials), in stream order, to buf; fs2_debug_snap_used() is the byte count so far
+ * (cap + 1 after an overflow); buf NULL turns it off.  fs2_debug_coherence(x, n, rounds,
+ * blocks, bad, stream): per round, `blocks` blocks read the n uint32 of x, one block writes
+ * x[i] = tag + i, and `blocks` blocks read x again, adding to bad[block] the elements that
+ * are not tag + i (bad: blocks + 1 uint32, zeroed by the caller) -- a stale line in some
+ * XCD's L2 after a kernel boundary on one stream shows up as a nonzero count.             */
 int fs2_debug_poison(int byte);
 void* fs2_debug_alloc(int64_t size, int device, void* stream);
 void fs2_debug_free(void* ptr, int64_t size, int device, void* stream);
 int fs2_debug_race(int delay_us, void* main_stream, int mode, int seed);
 int fs2_debug_lds_dma_oob(const float* src, void* out, void* stream);
+int fs2_debug_snap(void* buf, int64_t cap);
+int fs2_debug_coherence(void* x, int64_t n, int rounds, int blocks, void* bad, void* stream);
+int64_t fs2_debug_snap_used(void);
 
 #ifdef __cplusplus
 }

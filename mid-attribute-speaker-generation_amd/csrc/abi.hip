@@ -99,6 +99,27 @@ void lds_poison(hipStream_t st) {
   lds_fill_kernel<<<512, 256, 163840, st>>>(w);
 }
 
+// debug snapshots (fs2_debug_snap): copies of intermediate buffers appended, in stream order,
+// to one caller-owned device buffer; nothing is copied while no buffer is set
+__global__ void snap_copy_kernel(const unsigned char* src, unsigned char* dst, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    dst[i] = src[i];
+}
+static unsigned char* g_snap = nullptr;
+static int64_t g_snap_cap = 0, g_snap_used = 0;
+void snap(const void* p, int64_t bytes, hipStream_t st) {
+  if (!g_snap || !p || bytes <= 0) return;
+  if (g_snap_used + bytes > g_snap_cap) {
+    g_snap_used = g_snap_cap + 1;  // overflow: reported by fs2_debug_snap_used
+    return;
+  }
+  // a kernel, not hipMemcpyAsync: the copy must see memory exactly as the next kernel would
+  snap_copy_kernel<<<grid_for((bytes + 3) / 4), 256, 0, st>>>(
+      static_cast<const unsigned char*>(p), g_snap + g_snap_used, bytes);
+  g_snap_used += bytes;
+}
+
 }  // namespace fs2
 
 using namespace fs2;
@@ -179,6 +200,41 @@ int fs2_stream_wait(void* waiter, void* signaler) {
   }
   return FS2_OK;
 }
+
+// cross-XCD visibility probe (fs2_debug_coherence): every block reads all of x (so every XCD's
+// L2 may hold its lines), then ONE block writes x[i] = tag + i, then every block reads x again
+// and counts the elements that are not tag + i; three launches on one stream
+__global__ void coh_read_kernel(const uint32_t* x, int64_t n, uint32_t tag, uint32_t* bad) {
+  uint32_t acc = 0, nbad = 0;
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+    const uint32_t v = x[i];
+    acc += v;
+    if (tag && v != tag + (uint32_t)i) ++nbad;
+  }
+  if (tag && nbad) bad[blockIdx.x] += nbad;
+  if (acc == 0x9e3779b9u && !tag) bad[gridDim.x] = acc;  // keep the loads
+}
+__global__ void coh_write_kernel(uint32_t* x, int64_t n, uint32_t tag) {
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) x[i] = tag + (uint32_t)i;
+}
+int fs2_debug_coherence(void* x, int64_t n, int rounds, int blocks, void* bad, void* stream) {
+  hipStream_t st = as_stream(stream);
+  for (int r = 1; r <= rounds; ++r) {
+    coh_read_kernel<<<blocks, 256, 0, st>>>((const uint32_t*)x, n, 0u, (uint32_t*)bad);
+    coh_write_kernel<<<1, 256, 0, st>>>((uint32_t*)x, n, 0x1000000u * (uint32_t)r);
+    coh_read_kernel<<<blocks, 256, 0, st>>>((const uint32_t*)x, n, 0x1000000u * (uint32_t)r,
+                                            (uint32_t*)bad);
+  }
+  return launch_status("fs2_debug_coherence");
+}
+
+int fs2_debug_snap(void* buf, int64_t cap) {
+  g_snap = static_cast<unsigned char*>(buf);
+  g_snap_cap = buf ? cap : 0;
+  g_snap_used = 0;
+  return FS2_OK;
+}
+int64_t fs2_debug_snap_used(void) { return g_snap_used; }
 
 int fs2_debug_race(int delay_us, void* main_stream, int mode, int seed) {
   FS2_CHECK_ARG(mode >= 0 && mode <= 2,

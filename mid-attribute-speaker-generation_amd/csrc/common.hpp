@@ -32,6 +32,8 @@ int poison_byte();
 void poison(void* p, int64_t bytes, hipStream_t st);
 // ... and the LDS of every CU filled with it on `st` (no-op when poisoning is off)
 void lds_poison(hipStream_t st);
+// debug: append a copy of [p, p + bytes) to the snapshot buffer on `st` (fs2_debug_snap)
+void snap(const void* p, int64_t bytes, hipStream_t st);
 
 #define FS2_CHECK_ARG(cond, ...)                     \
   do {                                               \

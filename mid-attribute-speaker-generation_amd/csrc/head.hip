@@ -452,10 +452,24 @@ int fs2_variance_predictor_bwd(const int64_t* vp, void* act, const void* x_t, co
   // LN2 (+ Linear, masked; ReLU mask; conv2 bias gradient) backward; its parameter gradients
   // (LN2 affine, Linear, conv2 bias) reduced on the side stream
   void* dh2_t = at<void>(tmp, W.dh2_t);
+  // debug snapshots (fs2_debug_snap): the LN2 backward's inputs before and after it runs
+  auto snap_in = [&]() {
+    snap(dpred, rows * 4, as_stream(stream));
+    snap(at<float>(act, A.xh2), rows * v.filt * 4, as_stream(stream));
+    snap(at<float>(act, A.rs2), rows * 4, as_stream(stream));
+    snap(at<float>(act, A.h2), rows * v.filt * 4, as_stream(stream));
+    snap(v.lin_w, v.filt * 4, as_stream(stream));
+    snap(v.ln2_g, v.filt * 4, as_stream(stream));
+    snap(v.ln2_b, v.filt * 4, as_stream(stream));
+  };
+  snap_in();
   FS2_TRY(fs2_ln_bwd(FS2_BF16, nullptr, dpred, v.lin_w, at<float>(act, A.xh2), at<float>(act, A.rs2),
                      v.ln2_g, v.ln2_b, lens, T, rows, (int)v.filt, 0.f, p, sd, 0,
                      (uint64_t)(v.site + 1), at<float>(act, A.h2), nullptr, dh2_t, nullptr, 1,
                      nullptr, nullptr, nullptr, nullptr, nullptr, ws2, W.ws_bytes, stream));
+  snap_in();
+  snap(dh2_t, rows * v.filt * 2, as_stream(stream));
+  snap(ws2, W.ws_bytes, as_stream(stream));
   if (side != stream) FS2_TRY(fs2_stream_wait(side, stream));
   FS2_TRY(fs2_ln_bwd_final(rows, (int)v.filt, ws2, 1, v.gln2_g, v.gln2_b, v.glin_w, v.glin_b, v.g2_b,
                            side));
@@ -470,6 +484,9 @@ int fs2_variance_predictor_bwd(const int64_t* vp, void* act, const void* x_t, co
                      v.ln1_g, v.ln1_b, nullptr, 1, rows, (int)v.filt, 0.f, p, sd, 0, (uint64_t)v.site,
                      at<float>(act, A.h1), nullptr, dh1_t, nullptr, 1, nullptr, nullptr, nullptr,
                      nullptr, nullptr, ws1, W.ws_bytes, stream));
+  snap(du1, rows * v.filt * 4, as_stream(stream));
+  snap(dh1_t, rows * v.filt * 2, as_stream(stream));
+  snap(ws1, W.ws_bytes, as_stream(stream));
   if (side != stream) FS2_TRY(fs2_stream_wait(side, stream));
   FS2_TRY(fs2_ln_bwd_final(rows, (int)v.filt, ws1, 0, v.gln1_g, v.gln1_b, nullptr, nullptr, v.g1_b,
                            side));

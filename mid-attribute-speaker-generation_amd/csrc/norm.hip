@@ -160,8 +160,10 @@ __global__ __launch_bounds__(LN_BWD_WAVES * 64) void ln_bwd_f32(LnBwd a) {
   float RS[IT], RD[IT];
   bool LIVE[IT];
   const bool dres_rd = a.dres && a.dres_add;
-#pragma unroll
-  for (int it = 0; it < IT; ++it) {
+  // the row loads of iteration `it` (issued for all iterations up front, except with DDOT:
+  // there each row is loaded right before it is reduced -- see DESIGN.md section 4,
+  // "intermittent LayerNorm-backward rows")
+  auto load_row = [&](int it) {
     const int64_t r = rbeg + 2 * (wave + LN_BWD_WAVES * it) + half;
     LIVE[it] = r < a.rows && !row_padded(a.lens, a.T, r);
     XH[it][0] = XH[it][1] = DU[it][0] = DU[it][1] = DR[it][0] = DR[it][1] = zz;
@@ -182,9 +184,14 @@ __global__ __launch_bounds__(LN_BWD_WAVES * 64) void ln_bwd_f32(LnBwd a) {
         DU[it][1] = ld4(a.dout + e0 + 4);
       }
     }
+  };
+  if constexpr (!DDOT) {
+#pragma unroll
+    for (int it = 0; it < IT; ++it) load_row(it);
   }
 #pragma unroll
   for (int it = 0; it < IT; ++it) {
+    if constexpr (DDOT) load_row(it);
     const int64_t r = rbeg + 2 * (wave + LN_BWD_WAVES * it) + half;
     if (r >= a.rows) break;
     const int64_t e0 = r * LN_D + c8;

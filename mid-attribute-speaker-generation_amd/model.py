@@ -113,6 +113,29 @@ def sinusoid_table(n_position, d_hid):
 
 
 
+# Debug (tests/stale_probe.py --guard): every region handed to a C entry point (activations,
+# temporaries, the side-stream workspace) gets a guard tail filled with a pattern and is kept;
+# check_guards() names each region whose tail a kernel wrote (an out-of-bounds write).
+_GUARD = {"on": False, "regions": []}
+_GUARD_BYTES = 1 << 16
+
+
+def _region(nbytes, device, label):
+    nbytes = int(nbytes)
+    if not _GUARD["on"]:
+        return torch.empty(nbytes, dtype=torch.uint8, device=device)
+    t = torch.empty(nbytes + _GUARD_BYTES, dtype=torch.uint8, device=device)
+    t[nbytes:].fill_(0x5A)
+    _GUARD["regions"].append((t, nbytes, label))
+    return t[:nbytes]
+
+
+def check_guards():
+    """Labels of the guarded regions whose guard tail was overwritten (synchronises)."""
+    torch.cuda.synchronize()
+    return [f"{label} ({n} B)" for t, n, label in _GUARD["regions"] if bool((t[n:] != 0x5A).any())]
+
+
 class StepCtx:
     """Per-forward state: compute dtype of the GEMM operands, one Philox seed per step (one
     site id per dropout call, assigned at construction)."""
@@ -141,7 +164,7 @@ class StepCtx:
             if torch.cuda.is_current_stream_capturing():
                 raise RuntimeError("weight-gradient workspace must be sized before capture")
             K.lib.fs2_stream_wait(K.stream(), self.side.cuda_stream)  # old buffer drained
-            ws = self.ws_cache["wgrad"] = torch.empty(need, dtype=torch.float32, device=device)
+            ws = self.ws_cache["wgrad"] = _region(need * 4, device, "side_ws").view(torch.float32)
         return ws
 
     def wgrad(self, dy, x, dw, rows, seq_len, c_in, c_out, taps, pad, db=None, lens=None,
@@ -558,8 +581,8 @@ def _stack_fwd_c(layers, x, x_t, lens, B, T, ctx):
     for layer in layers:
         desc = layer.cdesc()
         p = ctx.p(layer.slf_attn.p)
-        act = torch.empty(_csize('fs2_fft_block_act_bytes', desc, 7, M, B, T, int(fuse)),
-                          dtype=torch.uint8, device=x.device)
+        act = _region(_csize('fs2_fft_block_act_bytes', desc, 7, M, B, T, int(fuse)), x.device,
+                      "fft_block act")
         K.lib.fs2_fft_block_fwd(desc, xp, xtp, act.data_ptr(), M, B, T, lp, p,
                                 ctx.seed.data_ptr() if p > 0 else None, int(fuse), stream)
         saved.append(("C", act, xtp, x_keep, fuse, p))
@@ -589,7 +612,7 @@ def _stack_bwd_c(layers, saved, dx, ctx, lens, B, T):
         _, act, xtp, x_keep, fuse, p = s
         desc = layer.cdesc()
         fuse_bwd = FUSE_LN_BWD and M >= FUSE_LN_MIN_ROWS and i + 1 < len(layers)
-        tmp = torch.empty(_csize('fs2_fft_block_tmp_bytes', desc, 7, M, B, T), dtype=torch.uint8, device=dev)
+        tmp = _region(_csize('fs2_fft_block_tmp_bytes', desc, 7, M, B, T), dev, "fft_block tmp")
         ws = ctx._side_ws(_csize('fs2_fft_block_side_ws_bytes', desc, 7, M), dev) if side is not None else \
             K.ws(_csize('fs2_fft_block_side_ws_bytes', desc, 7, M), dev)
         dxo = torch.empty((M, d), dtype=torch.float32, device=dev)
@@ -751,8 +774,8 @@ class VariancePredictor(nn.Module):
         desc = self.cdesc()
         M = x_t.shape[0]
         p = ctx.p(self.p)
-        act = torch.empty(_csize('fs2_variance_predictor_act_bytes', desc, 6, M), dtype=torch.uint8,
-                          device=x_t.device)
+        act = _region(_csize('fs2_variance_predictor_act_bytes', desc, 6, M), x_t.device,
+                      f"predictor {self.site} act")
         K.lib.fs2_variance_predictor_fwd(desc, x_t.data_ptr(), act.data_ptr(), M, T,
                                          0 if lens is None else lens.data_ptr(), p,
                                          ctx.seed.data_ptr() if p > 0 else None,
@@ -764,11 +787,17 @@ class VariancePredictor(nn.Module):
     def _bwd_c(self, dpred, saved, dx_acc):
         _, act, x_t, lens, T, p, ctx = saved
         desc = self.cdesc()
+        if _GUARD["on"]:  # debug: the inputs this backward reads, in stream order
+            c = self.conv_layer
+            _GUARD.setdefault("snap", []).append(
+                (self.site, [t.detach().clone() for t in (self.linear_layer.weight, self.linear_layer.bias,
+                                                          c.layer_norm_2.weight, c.layer_norm_2.bias,
+                                                          dpred, act, x_t)]))
         M = x_t.shape[0]
         dev = x_t.device
         dpred = dpred.contiguous()
-        tmp = torch.empty(_csize('fs2_variance_predictor_tmp_bytes', desc, 6, M), dtype=torch.uint8,
-                          device=dev)
+        tmp = _region(_csize('fs2_variance_predictor_tmp_bytes', desc, 6, M), dev,
+                      f"predictor {self.site} tmp")
         need = _csize('fs2_variance_predictor_side_ws_bytes', desc, 6, M)
         side = ctx.side.cuda_stream if ctx.side is not None else None
         ws = ctx._side_ws(need, dev) if side is not None else K.ws(need, dev)
@@ -1203,8 +1232,7 @@ class MelHeadFn(torch.autograd.Function):
             # one fs2_mel_head_fwd call: mel_linear + PostNet (bitwise the path below)
             desc = m.postnet.mel_head_desc(lin)
             p = ctx.p(0.5)
-            act = torch.empty(_csize('fs2_mel_head_act_bytes', desc, 7, M), dtype=torch.uint8,
-                              device=x.device)
+            act = _region(_csize('fs2_mel_head_act_bytes', desc, 7, M), x.device, "mel_head act")
             K.lib.fs2_mel_head_fwd(desc, x_c.data_ptr(), act.data_ptr(), M, T, p,
                                    ctx.seed.data_ptr() if p > 0 else None, K.stream())
             n_mel = lin.out_features
@@ -1258,7 +1286,7 @@ class MelHeadFn(torch.autograd.Function):
         if d_out is None and d_post is None:
             d_out = K.zeros((M, n_mel), dev)
         desc = m.postnet.mel_head_desc(lin)
-        tmp = torch.empty(_csize('fs2_mel_head_tmp_bytes', desc, 7, M), dtype=torch.uint8, device=dev)
+        tmp = _region(_csize('fs2_mel_head_tmp_bytes', desc, 7, M), dev, "mel_head tmp")
         need = _csize('fs2_mel_head_side_ws_bytes', desc, 7, M)
         side = ctx.side.cuda_stream if ctx.side is not None else None
         ws = ctx._side_ws(need, dev) if side is not None else K.ws(need, dev)

@@ -123,8 +123,21 @@ def run_config(dtype="bf16", path="c", fuse=-1, batch="8x32", seed=25, side=True
                         if hasattr(p, "_fs2_grad")}
         del model, tr, losses
         model, tr = fresh()
-        l2 = [torch.stack(list(tr.step(b)[0])).detach().clone() for _ in range(2)]
+        steps_g, steps_w = [], []
+        clip = tr.opt.clip_grad_norm_
+
+        def capture(max_norm):  # each step's gradients as the clip sees them
+            model.join_side()
+            steps_g.append(model.arena().grad.detach().clone())
+            return clip(max_norm)
+        tr.opt.clip_grad_norm_ = capture
+        l2 = []
+        for _ in range(2):
+            l2.append(torch.stack(list(tr.step(b)[0])).detach().clone())
+            steps_w.append(model.arena().flat.detach().clone())
         torch.cuda.synchronize()
+        out["step_grads"] = [g.cpu() for g in steps_g]
+        out["step_flat"] = [w.cpu() for w in steps_w]
         out["losses2"] = torch.stack(l2).cpu()
         out["flat"] = model.arena().flat.cpu()
         out["m"] = tr.opt.m.cpu()
@@ -156,7 +169,19 @@ def diff(a, b):
     if not torch.equal(a["losses1"], b["losses1"]):
         msgs.append(f"losses1 {a['losses1'].tolist()} vs {b['losses1'].tolist()}")
     if not torch.equal(a["losses2"], b["losses2"]):
-        msgs.append(f"losses2 {a['losses2'][-1].tolist()} vs {b['losses2'][-1].tolist()}")
+        msgs.append(f"losses2 {a['losses2'].tolist()} vs {b['losses2'].tolist()}")
+    for i, (ga, gb) in enumerate(zip(a.get("step_grads", []), b.get("step_grads", []))):
+        if not torch.equal(ga, gb):
+            bad = [n for n, o, c in a["names"] if not torch.equal(ga[o:o + c], gb[o:o + c])]
+            first = [n for n, o, c in a["names"] if n in bad]
+            worst = max(((float((ga[o:o + c] - gb[o:o + c]).abs().max()), n) for n, o, c in a["names"]
+                         if n in bad), default=(0.0, ""))
+            msgs.append(f"step {i + 1} gradients: {len(bad)} parameters differ (max |diff| {worst[0]:.3e} "
+                        f"in {worst[1]}): {', '.join(first)}")
+    for i, (wa, wb) in enumerate(zip(a.get("step_flat", []), b.get("step_flat", []))):
+        if not torch.equal(wa, wb):
+            bad = [n for n, o, c in a["names"] if not torch.equal(wa[o:o + c], wb[o:o + c])]
+            msgs.append(f"weights after step {i + 1}: {len(bad)} parameters differ: {', '.join(bad[:12])}")
     for k in ("flat", "m", "v"):
         if not torch.equal(a[k], b[k]):
             bad = [n for n, o, c in a["names"] if not torch.equal(a[k][o:o + c], b[k][o:o + c])]

@@ -49,7 +49,7 @@ def _bucket_worker(rank, world, port, out):
         for p, o in zip(arena.params, arena.offsets):
             arena.grad[o:o + p.numel()] = (rank + 1) * (step + 1) * torch.arange(p.numel()).float()
         order = list(range(len(sizes)))
-        if rank == 1:
+        if rank % 2 == 1:
             order = order[::-1]  # completion order may differ across ranks within a step
         for i in order:
             gb.ready([arena.params[i]])
@@ -90,16 +90,21 @@ def test_data_parallel_shard_lengths_agree_gloo_cpu():
                 assert (g == w) if isinstance(w, int) else (g.shape == w.shape and torch.equal(g, w))
 
 
-def test_grad_buckets_gloo_cpu():
+@pytest.mark.parametrize("world", [2, 4])
+def test_grad_buckets_gloo_cpu(world):
+    """GradBuckets on `world` gloo ranks (CPU): every rank ends each step with the sum of the
+    ranks' gradients, whatever order its parameters became ready in (odd ranks reverse it)."""
     with tempfile.TemporaryDirectory() as out:
-        mp.spawn(_bucket_worker, args=(2, _port(), out), nprocs=2, join=True)
+        mp.spawn(_bucket_worker, args=(world, _port(), out), nprocs=world, join=True)
         for step in range(2):
-            g0, g1 = torch.load(f"{out}/r0_s{step}.pt"), torch.load(f"{out}/r1_s{step}.pt")
-            assert torch.equal(g0, g1)
+            gs = [torch.load(f"{out}/r{r}_s{step}.pt") for r in range(world)]
+            for g in gs[1:]:
+                assert torch.equal(gs[0], g)
             arena = _FakeArena([7, 1000, 33, 5000, 12, 4096, 3])
+            scale = world * (world + 1) // 2  # sum over ranks of (rank + 1)
             for p, o in zip(arena.params, arena.offsets):
-                want = 3 * (step + 1) * torch.arange(p.numel()).float()
-                assert torch.equal(g0[o:o + p.numel()], want)
+                want = scale * (step + 1) * torch.arange(p.numel()).float()
+                assert torch.equal(gs[0][o:o + p.numel()], want)
 
 
 def _shard(pkg, rank, dev, micro=0):

@@ -231,7 +231,7 @@ FUSE_LN_BWD = True
 # FFTBlock.fwd / .bwd below: bitwise the same results, a fifth of the host time); the tests
 # compare it against the per-kernel path by clearing it
 C_BLOCKS = True
-# pitch predictor forward on the side stream beside the duration / energy predictors (A/B)
+# pitch and duration predictor forwards on the side stream beside the energy predictor (A/B)
 VA_SIDE = True
 # fs2_mel_head_* descriptor geometry (include/fs2hip.h: FS2_MH_LAYER0 + FS2_MH_MAX_LAYERS x
 # FS2_MHL_WORDS words)
@@ -1140,14 +1140,15 @@ class VarianceAdaptorFn(torch.autograd.Function):
         va = m.variance_adaptor
         x0, x0_t = K.rowvec_add(enc_out, speakers, m.speaker_emb.weight, B, Ts, copy=ctx.copy)
         # the three predictors are independent under teacher forcing (the energy predictor's
-        # input adds the pitch *target*'s embedding): the pitch predictor runs on the side
-        # stream -- idle in the forward once the weights are prepared -- beside the duration and
-        # energy predictors, joined before the LengthRegulator (C-ABI path; same results)
+        # input adds the pitch *target*'s embedding, the LengthRegulator uses the duration
+        # *targets*): the pitch and duration predictors run on the side stream -- idle in the
+        # forward once the weights are prepared -- beside the energy predictor, the embeddings
+        # and the LengthRegulator, joined after them (C-ABI path; same results)
         side = ctx.side.cuda_stream if ctx.side is not None and VA_SIDE else None
         if side is not None:
             K.lib.fs2_stream_wait(side, K.stream())
         p, s_p = va.pitch_predictor.fwd(x0, x0_t, src_lens, B, Ts, ctx, stream=side)
-        log_d, s_d = va.duration_predictor.fwd(x0, x0_t, src_lens, B, Ts, ctx)
+        log_d, s_d = va.duration_predictor.fwd(x0, x0_t, src_lens, B, Ts, ctx, stream=side)
         x1, x1_t, idx_p = K.bucket_embed(x0, p_t.contiguous().view(-1), va.pitch_bins,
                                          va.pitch_embedding.weight, copy=ctx.copy)
         e, s_e = va.energy_predictor.fwd(x1, x1_t, src_lens, B, Ts, ctx)

@@ -296,7 +296,11 @@ void* fs2_debug_alloc(int64_t size, int device, void* stream) {
   // the allocating stream -- which the race modes hold back on purpose
   (void)stream;
   static hipStream_t fill_st = nullptr;
-  if (!fill_st && hipStreamCreateWithFlags(&fill_st, hipStreamNonBlocking) != hipSuccess) fill_st = nullptr;
+  {
+    std::lock_guard<std::mutex> lock(g_dbg_mu);  // the allocator is called from several threads
+    if (!fill_st && hipStreamCreateWithFlags(&fill_st, hipStreamNonBlocking) != hipSuccess)
+      fill_st = nullptr;
+  }
   const int b = poison_byte();
   if (size > 0 && (!fill_st || hipMemsetAsync(p, b >= 0 ? b : 0xff, (size_t)size, fill_st) != hipSuccess ||
                    hipStreamSynchronize(fill_st) != hipSuccess)) {

@@ -324,9 +324,15 @@ int fs2_fft_block_bwd(const int64_t* blk, void* act, const void* x_t, int fuse_l
   const int64_t j3[8] = {(int64_t)(uintptr_t)dqkv, b.n3, (int64_t)(uintptr_t)x_t, b.d,
                          (int64_t)(uintptr_t)b.gq_w, (int64_t)(uintptr_t)b.gq_b, b.d, b.n3};
   memcpy(jobs + 16, j3, sizeof j3);
-  if (side != stream) FS2_TRY(fs2_stream_wait(side, stream));
-  FS2_TRY(ln_final(1, b.gln1_g, b.gln1_b, b.gfc_b));
-  FS2_TRY(fs2_conv_wgrad_k1_multi(FS2_BF16, jobs, 3, rows, T, lens, side_ws, side_ws_bytes, side));
+  // the grouped k = 1 weight gradients and the LN1 parameter reduction go to the side stream
+  // after the QKV data gradient is issued, not before it: the w_2 data gradient of the next
+  // block then runs beside the band weight gradient rather than beside the grouped k = 1
+  // kernel (same kernels and per-buffer order; -0.04 ms/step same-box, profiles/r6_k1_late_ab.txt)
+  auto k1_side = [&]() -> int {
+    if (side != stream) FS2_TRY(fs2_stream_wait(side, stream));
+    FS2_TRY(ln_final(1, b.gln1_g, b.gln1_b, b.gfc_b));
+    return fs2_conv_wgrad_k1_multi(FS2_BF16, jobs, 3, rows, T, lens, side_ws, side_ws_bytes, side);
+  };
   if (prev_blk) {
     // the previous block's FFN post-LN backward in this block's QKV data-gradient epilogue
     const Blk pb = unpack(prev_blk);
@@ -336,12 +342,13 @@ int fs2_fft_block_bwd(const int64_t* blk, void* act, const void* x_t, int fuse_l
                                  nullptr, nullptr, nullptr, prev_p, prev_p > 0.f ? seed : nullptr,
                                  (uint64_t)(pb.site + 1), prev_dx1, 0, prev_dy2_t,
                                  at<float>(tmp, W.ln_ws[2]), W.ln_ws_bytes, stream));
-    if (side != stream) FS2_TRY(fs2_stream_wait(side, stream));
+    FS2_TRY(k1_side());
     return fs2_ln_bwd_final(rows, (int)pb.d, at<float>(tmp, W.ln_ws[2]), 0, pb.gln2_g, pb.gln2_b,
                             nullptr, nullptr, pb.g2_b, side);
   }
-  return fs2_conv_gemm(FS2_BF16, dqkv, b.n3, b.wq_b, dx, b.d, rows, T, b.n3, b.d, 1, 0, lens, nullptr,
-                       FS2_EPI_ADD_AUX, dx, b.d, stream);
+  FS2_TRY(fs2_conv_gemm(FS2_BF16, dqkv, b.n3, b.wq_b, dx, b.d, rows, T, b.n3, b.d, 1, 0, lens, nullptr,
+                        FS2_EPI_ADD_AUX, dx, b.d, stream));
+  return k1_side();
 }
 
 }  // extern "C"

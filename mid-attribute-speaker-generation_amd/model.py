@@ -150,6 +150,7 @@ class StepCtx:
         self.ws_cache = None  # dict holding the side stream's shared split-K workspace
         self.keep = []  # operands read by side-stream work, released at the next join
         self.k1 = None  # held-back grouped k = 1 weight gradients: (key, jobs, lens)
+        self.after_first = None  # issued after the encoder's first block (prep_weights)
 
     def p(self, p):
         return float(p) if self.drop else 0.0
@@ -567,10 +568,11 @@ def _c_blocks(ctx, d):
     return C_BLOCKS and ctx.copy is not None and ctx.cdt == torch.bfloat16 and d == 256
 
 
-def _stack_fwd_c(layers, x, x_t, lens, B, T, ctx):
+def _stack_fwd_c(layers, x, x_t, lens, B, T, ctx, after_first=None):
     """Forward through a stack of FFT blocks, one fs2_fft_block_fwd call per block; each block's
-    activations live in one region (saved for the backward).  Returns the last block's output,
-    its bf16 copy and the per-block saved tuples."""
+    activations live in one region (saved for the backward); ``after_first`` is called once the
+    first block is issued.  Returns the last block's output, its bf16 copy and the per-block
+    saved tuples."""
     M, d = x.shape
     fuse = FUSE_LN and M >= FUSE_LN_MIN_ROWS
     saved = []
@@ -585,6 +587,9 @@ def _stack_fwd_c(layers, x, x_t, lens, B, T, ctx):
                       "fft_block act")
         K.lib.fs2_fft_block_fwd(desc, xp, xtp, act.data_ptr(), M, B, T, lp, p,
                                 ctx.seed.data_ptr() if p > 0 else None, int(fuse), stream)
+        if after_first is not None:
+            after_first()
+            after_first = None
         saved.append(("C", act, xtp, x_keep, fuse, p))
         o2 = _csize('fs2_fft_block_act_offset', desc, 7, M, B, T, int(fuse), 0)
         o2t = _csize('fs2_fft_block_act_offset', desc, 7, M, B, T, int(fuse), 1)
@@ -1103,13 +1108,19 @@ class EncoderFn(torch.autograd.Function):
     def forward(fctx, token, enc, texts, accents, lens, B, T, ctx):
         x, x_t = K.encoder_embed(texts, accents, enc.src_word_emb.weight, enc.src_accent_emb.weight,
                                  enc.position_enc, B, T, enc.d, copy=ctx.copy)
+        after_first, ctx.after_first = ctx.after_first, None
         if _c_blocks(ctx, enc.d) and x_t is not None:
-            x, x_t, saved = _stack_fwd_c(enc.layer_stack, x, x_t, lens, B, T, ctx)
+            x, x_t, saved = _stack_fwd_c(enc.layer_stack, x, x_t, lens, B, T, ctx, after_first)
         else:
             saved = []
             for layer in enc.layer_stack:
                 x, x_t, s = layer.fwd(x, x_t, lens, B, T, ctx)
                 saved.append(s)
+                if after_first is not None:
+                    after_first()
+                    after_first = None
+        if not enc.layer_stack and after_first is not None:
+            after_first()
         fctx.enc, fctx.saved, fctx.ids, fctx.ctx = enc, saved, (texts, accents), ctx
         fctx.geom = (lens, B, T)
         return x
@@ -1397,15 +1408,20 @@ class FastSpeech2(nn.Module):
 
     def prep_weights(self, side=None):
         """Re-lay out (and cast) every weight for the GEMMs, batched launches; the job tables
-        (pointers into the arena and the compute-weight buffers) are built once.  With a side
-        stream the encoder's weights are prepared on the current stream and everything after
-        them (variance predictors, decoder, PostNet, mel head) on ``side``, under the
-        encoder's forward; the caller joins ``side`` before the first of those layers."""
+        (pointers into the arena and the compute-weight buffers) are built once.  Without a side
+        stream everything is prepared on the current stream.  With one, only the first encoder
+        block's weights are prepared on the current stream; the other encoder blocks' follow on
+        ``side`` under the first block's forward, and everything after them (variance predictors,
+        decoder, PostNet, mel head) under the rest of the encoder.  Returns None, or (with
+        ``side``) the callable the encoder calls once its first block is issued: the current
+        stream waits for the other encoder blocks' weights there, and the rest is issued on
+        ``side`` after that wait point; the caller joins ``side`` before the first of those
+        layers."""
         cdt = self.compute_dtype
         if self._prep is None or self._prep[0] != cdt:
-            enc_jobs, rest = [], []
-            for b in self.encoder.layer_stack:
-                b.prep(cdt, enc_jobs)
+            first, enc_jobs, rest = [], [], []
+            for i, b in enumerate(self.encoder.layer_stack):
+                b.prep(cdt, first if i == 0 else enc_jobs)
             va = self.variance_adaptor
             for v in (va.duration_predictor, va.pitch_predictor, va.energy_predictor):
                 v.prep(cdt, rest)
@@ -1424,14 +1440,27 @@ class FastSpeech2(nn.Module):
                     first += n
                 t = torch.tensor(rows, dtype=torch.int64).to(self._arena.flat.device)
                 return t, len(rows), first
-            self._prep = (cdt, table(enc_jobs), table(rest))
-        cdt, (t0, n0, k0), (t1, n1, k1) = self._prep
-        K.lib.fs2_weight_prep_batch(K.code(cdt), K.ptr(t0), n0, k0, K.stream())
+            self._prep = (cdt, table(first), table(enc_jobs) if enc_jobs else None, table(rest),
+                          table(enc_jobs + rest))
+        cdt, t_first, t_enc, t_rest, t_all = self._prep
+        code = K.code(cdt)
+
+        def run(t, stream):
+            K.lib.fs2_weight_prep_batch(code, K.ptr(t[0]), t[1], t[2], stream)
         if side is None:
-            K.lib.fs2_weight_prep_batch(K.code(cdt), K.ptr(t1), n1, k1, K.stream())
-        else:
-            K.lib.fs2_stream_wait(side.cuda_stream, K.stream())
-            K.lib.fs2_weight_prep_batch(K.code(cdt), K.ptr(t1), n1, k1, side.cuda_stream)
+            run(t_first, K.stream())
+            run(t_all, K.stream())
+            return None
+        run(t_first, K.stream())
+        K.lib.fs2_stream_wait(side.cuda_stream, K.stream())
+        if t_enc is not None:
+            run(t_enc, side.cuda_stream)
+
+        def after_first_block():
+            if t_enc is not None:
+                K.lib.fs2_stream_wait(K.stream(), side.cuda_stream)
+            run(t_rest, side.cuda_stream)
+        return after_first_block
 
     # -- forward ----------------------------------------------------------------------
     def forward(self, speakers, texts, src_lens, max_src_len, mels=None, mel_lens=None,
@@ -1450,7 +1479,7 @@ class FastSpeech2(nn.Module):
                                        e_control, d_control, accents, speaker_meta=speaker_meta)
         self.arena()
         side = self.side_stream() if self.training else None
-        self.prep_weights(side)  # A/B: 8.171 -> 8.152 ms against one launch on the main stream
+        after_first = self.prep_weights(side)
         seed = self._step_seed() if (self.training and self.dropout) else 0
         ctx = StepCtx(seed, self.training, self.dropout, self.compute_dtype)
         ctx.hook = self._hooks["grad"]
@@ -1467,6 +1496,7 @@ class FastSpeech2(nn.Module):
         mel_masks = K.length_mask(mel_lens, T_dec)
 
         tok = self._token
+        ctx.after_first = after_first  # the encoder calls it after issuing its first block
         enc = EncoderFn.apply(tok, self.encoder, texts.contiguous(), accents.contiguous(), src_lens,
                               B, Ts, ctx)
         speaker_emb_s = K.embedding_fwd(speakers.contiguous(), self.speaker_emb.weight)

@@ -1,5 +1,6 @@
 """Per-phase GPU (HIP events) and host (enqueue) time of one training step, no profiler:
-forward | losses | main backward | GMM speaker loss fwd+bwd | side-stream drain | clip + Adam."""
+forward | GMM speaker loss fwd+bwd | losses | main backward | side-stream drain | clip + Adam
+(train_step's order)."""
 import importlib, os, sys, time
 import numpy as np
 import torch
@@ -36,7 +37,7 @@ for _ in range(5):
     tr.step(batch)
 torch.cuda.synchronize()
 E = lambda: torch.cuda.Event(enable_timing=True)
-names = ("fwd", "loss", "bwd", "eloss", "side", "end")
+names = ("fwd", "eloss", "loss", "bwd", "side", "end")
 gpu, host = [], []
 for it in range(12):
     ev = {k: E() for k in ("start",) + names}
@@ -44,13 +45,13 @@ for it in range(12):
     ev["start"].record()
     output = model(*(batch[2:12]), accents=batch[13], speaker_meta=batch[12])
     ev["fwd"].record(); h.append(time.perf_counter())
+    eloss = tr.eLoss(output[-1], output[-2])  # train_step's order: the GMM loss first
+    (-eloss).backward()
+    ev["eloss"].record(); h.append(time.perf_counter())
     losses = tr.Loss(batch[:12], output[:-2])
     ev["loss"].record(); h.append(time.perf_counter())
     losses[0].backward()
     ev["bwd"].record(); h.append(time.perf_counter())
-    eloss = tr.eLoss(output[-1], output[-2])
-    (-eloss).backward()
-    ev["eloss"].record(); h.append(time.perf_counter())
     ev["side"].record(model.side_stream()); h.append(time.perf_counter())
     tr.opt.clip_grad_norm_(tr.clip)
     tr.opt.step_and_update_lr()
